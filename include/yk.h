@@ -1,0 +1,175 @@
+/*
+ * yk.h — C ABI of the MI355X-native detect-and-track hot path (libyk.so).
+ *
+ * The reference has no FFI: its hot path is two Python surfaces,
+ *   ultralytics.YOLO.__call__/predict        (ultralytics/engine/model.py:158-188, 498-557)
+ *   kalman.EnhancedMultiTargetTracker.update (kalman/enhanced_multi_target_tracker.py:42-132)
+ * driven per frame by kalman/aircraft_detection_tracking.py:88-131.  This header is the
+ * boundary the two Python shims of this package (and any other host: cgo, JNI, ctypes)
+ * bind.  Every entry point cites the reference interface it replaces.
+ *
+ * Conventions
+ *   - every call returns an int status (YK_OK = 0); yk_last_error() returns a
+ *     thread-local message for the last failing call on the calling thread.
+ *   - pointers named dev_* are device (HBM) pointers; host_* are host pointers.
+ *     Callers own host buffers; handles own their device buffers.
+ *   - `stream` is a hipStream_t passed as void* (NULL = the legacy default stream).
+ *     No call allocates or synchronises inside a *_step / yk_detect launch, so
+ *     those calls are hipGraph-capturable.
+ *   - a handle is bound to one GPU and is not re-entrant (mirrors the reference
+ *     predictor's threading.Lock, ultralytics/engine/predictor.py:149,304).
+ */
+#ifndef YK_H_
+#define YK_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define YK_ABI_VERSION 1
+
+enum yk_status {
+  YK_OK = 0,
+  YK_ERR_ARG = 1,      /* bad argument (reference: assert / ValueError)                */
+  YK_ERR_HIP = 2,      /* HIP runtime error                                           */
+  YK_ERR_CAPACITY = 3, /* a fixed capacity (max_tracks, max_dets) was exceeded         */
+  YK_ERR_STATE = 4     /* call out of order (e.g. detect before a model was loaded)     */
+};
+
+enum yk_dtype { YK_F32 = 0, YK_F64 = 1 };
+
+typedef struct yk_ctx yk_ctx;
+typedef struct yk_tracker yk_tracker;
+typedef struct yk_model yk_model;
+
+/* ------------------------------------------------------------------ common */
+int yk_abi_version(void);
+const char* yk_last_error(void);
+
+/* Bind a context to GPU `device` (reference: select_device, ultralytics/utils/torch_utils.py:134-245). */
+int yk_ctx_create(int device, yk_ctx** out);
+int yk_ctx_destroy(yk_ctx* ctx);
+
+/* ------------------------------------------------------------------ tracker
+ * Replaces kalman.EnhancedMultiTargetTracker (kalman/enhanced_multi_target_tracker.py:15-40)
+ * for `n_streams` independent video streams at once (one reference tracker object per stream).
+ */
+typedef struct {
+  int32_t max_lost_frames; /* reference default 450 (driver uses 150)            */
+  int32_t min_hits;        /* reference default 3   (driver uses 1)              */
+  double iou_threshold;    /* reference default 0.3 (driver uses 0.1)            */
+  int32_t max_tracks;      /* capacity of live tracks per stream (<= 2048)       */
+  int32_t max_dets;        /* capacity of detections per stream per frame (<= 1024) */
+} yk_tracker_cfg;
+
+/* Per-stream counters: EnhancedMultiTargetTracker.stats + frame_count/next_track_id
+ * (enhanced_multi_target_tracker.py:28-38). */
+typedef struct {
+  int64_t frame_count;
+  int64_t next_track_id;
+  int64_t total_tracks_created;
+  int64_t total_tracks_terminated;
+  int64_t current_active_tracks;
+  int64_t long_term_predictions;
+  int64_t successful_recoveries;
+  int64_t overflow; /* detections/tracks dropped because a capacity was hit (0 in parity runs) */
+} yk_tracker_stats;
+
+/* One output row = one reference get_track_info() dict
+ * (kalman/enhanced_aircraft_kalman_tracker.py:366-383). */
+#define YK_TRAJ_OUT 30
+typedef struct {
+  int32_t track_num;          /* track_id = "T%03d" % track_num                    */
+  int32_t status;             /* 0 = 'detected', 1 = 'predicted'                   */
+  int32_t age, hits, hit_streak, time_since_update; /* lost_frames == time_since_update */
+  int32_t traj_len;           /* number of valid points in traj (<= 30)            */
+  int32_t is_stable_motion;   /* stability_score > 0.5                             */
+  double bbox[4];             /* x1, y1, x2, y2                                    */
+  double confidence;
+  double velocity[2];         /* x[4:6]                                            */
+  double motion_confidence, speed, direction;
+  double traj[YK_TRAJ_OUT][2];/* last 30 trajectory centres, oldest first          */
+} yk_track_out;
+
+/* Full filter state of one live track (AircraftKalmanTracker attributes,
+ * kalman/enhanced_aircraft_kalman_tracker.py:32-101).  P is stored densely here. */
+#define YK_VEL_HIST 50
+#define YK_TRAJ_HIST 150
+typedef struct {
+  int32_t track_num, age, hits, hit_streak, time_since_update, is_lost, lost_frames;
+  int32_t vel_len, traj_len, max_lost_frames;
+  double x[8];
+  double P[64];
+  double velocity_avg[2], velocity_std[2], direction, speed, stability_score, prediction_confidence;
+  double vel_hist[YK_VEL_HIST][2];   /* oldest first */
+  double traj_hist[YK_TRAJ_HIST][2]; /* oldest first */
+} yk_track_state;
+
+int yk_tracker_create(yk_ctx* ctx, int n_streams, const yk_tracker_cfg* cfg, yk_tracker** out);
+int yk_tracker_destroy(yk_tracker* trk);
+/* Return every stream to the freshly-constructed state (frame_count 0, next id 1). */
+int yk_tracker_reset(yk_tracker* trk, void* stream);
+
+/* One EnhancedMultiTargetTracker.update() for every stream
+ * (enhanced_multi_target_tracker.py:42-132): batched predict, IoU cost matrix, greedy
+ * association, update / mark_as_lost / create / delete, get_track_info().
+ *   dev_dets   : n_streams x max_dets rows of `row_stride` elements of `dtype`,
+ *                each row [x1, y1, x2, y2, conf, ...]; YK_F32 reproduces the reference's
+ *                np.float32 detections bit for bit, YK_F64 python-float detections.
+ *   dev_counts : int32[n_streams] detections per stream (clamped to max_dets; the
+ *                excess is counted in stats.overflow).
+ * Results stay on the device (yk_tracker_outputs) until yk_tracker_download. */
+int yk_tracker_step(yk_tracker* trk, const void* dev_dets, int dtype, int row_stride,
+                    const int32_t* dev_counts, void* stream);
+
+/* Device views of the last step's results: rows[n_streams][max_tracks], counts[n_streams],
+ * stats[n_streams].  Valid until the next step. */
+int yk_tracker_outputs(yk_tracker* trk, yk_track_out** dev_rows, int32_t** dev_counts,
+                       yk_tracker_stats** dev_stats);
+
+/* Copy results to the host: counts and stats for every stream, then the live rows of
+ * each stream into host_rows[s * max_tracks ...].  Synchronises `stream`. */
+int yk_tracker_download(yk_tracker* trk, yk_track_out* host_rows, int32_t* host_counts,
+                        yk_tracker_stats* host_stats, void* stream);
+
+/* Snapshot the live tracks of one stream in list order (EnhancedMultiTargetTracker.trackers).
+ * host_states must hold max_tracks entries; *n_out receives the number written. */
+int yk_tracker_snapshot(yk_tracker* trk, int stream_index, yk_track_state* host_states,
+                        int32_t* n_out, void* stream);
+
+/* Device-side single-track operations on list position `pos` of stream `stream_index`,
+ * for the AircraftKalmanTracker object surface (kalman/enhanced_aircraft_kalman_tracker.py):
+ *   YK_OP_PREDICT      predict()                        (:184-203)  out5 <- box
+ *   YK_OP_UPDATE       update(in_box)                   (:249-297)  in_box dtype as in step
+ *   YK_OP_MARK_LOST    mark_as_lost()                   (:299-317)
+ *   YK_OP_INFO         get_track_info()                 (:335-383)  row_out (may predict: quirk A)
+ *   YK_OP_LONG_TERM    enhanced_long_term_predict(arg)  (:205-247)  out5 <- box, confidence
+ *   YK_OP_LOST_PRED    get_lost_prediction()            (:319-333)  out5 <- box, confidence
+ * host_in_box / host_out5 / host_row_out may be NULL when unused.  Synchronous. */
+enum yk_track_op_code {
+  YK_OP_PREDICT = 0,
+  YK_OP_UPDATE = 1,
+  YK_OP_MARK_LOST = 2,
+  YK_OP_INFO = 3,
+  YK_OP_LONG_TERM = 4,
+  YK_OP_LOST_PRED = 5
+};
+int yk_track_op(yk_tracker* trk, int stream_index, int pos, int op, int arg, const double* host_in_box,
+                int dtype, double* host_out5, yk_track_out* host_row_out, void* stream);
+
+/* sizeof() of the ABI structs, for bindings that mirror them (0: yk_tracker_cfg,
+ * 1: yk_tracker_stats, 2: yk_track_out, 3: yk_track_state); -1 for an unknown id. */
+int64_t yk_struct_size(int which);
+
+/* Append a new track created from a box (AircraftKalmanTracker.__init__, :23-101) to the
+ * end of stream `stream_index`'s list, with the given track number. Synchronous. */
+int yk_track_create(yk_tracker* trk, int stream_index, const double* host_bbox, int dtype,
+                    int32_t track_num, int32_t max_lost_frames, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* YK_H_ */

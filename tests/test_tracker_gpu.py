@@ -1,0 +1,149 @@
+"""GPU parity: the HIP tracker (libyk.so, csrc/tracker.hip) against the numpy oracle
+(oracle/tracker_ref.py) on seeded synthetic sequences.
+
+Bar (BASELINE.json north_star): track-ID / association decisions identical, box and
+Kalman-state floats within 1e-4 relative.  The test asserts a much tighter 1e-9: every
+value is computed with the reference's exact float32/float64 operation order, the only
+non-bitwise source being the device arctan2 (last-ulp; feeds direction/stability only).
+The oracle runs with stable tie-breaking (the kernel's documented rule)."""
+import numpy as np
+import pytest
+
+from conftest import pkg
+from oracle.tracker_ref import RefMultiTracker, RefTrack
+
+pytestmark = pytest.mark.gpu
+
+INT_KEYS = ("track_id", "status", "age", "hits", "hit_streak", "time_since_update", "lost_frames", "is_lost",
+            "is_stable_motion")
+FLOAT_KEYS = ("confidence", "motion_confidence", "speed", "direction")
+RTOL = 1e-9
+
+
+def _close(a, b, what):
+    a, b = np.asarray(a, dtype=np.float64), np.asarray(b, dtype=np.float64)
+    assert a.shape == b.shape, what
+    assert np.allclose(a, b, rtol=RTOL, atol=1e-9), f"{what}: {a} vs {b}"
+
+
+def compare_frame(ours, ref, where):
+    assert [o["track_id"] for o in ours] == [r["track_id"] for r in ref], where
+    for o, r in zip(ours, ref):
+        for k in INT_KEYS:
+            assert o[k] == r[k], f"{where} {o['track_id']} {k}: {o[k]} vs {r[k]}"
+        for k in FLOAT_KEYS:
+            _close(o[k], r[k], f"{where} {o['track_id']} {k}")
+        _close(o["bbox"], r["bbox"], f"{where} {o['track_id']} bbox")
+        _close(o["velocity"], r["velocity"], f"{where} {o['track_id']} velocity")
+        _close(np.array(o["trajectory"]).reshape(-1, 2), np.array(r["trajectory"], dtype=np.float64).reshape(-1, 2),
+               f"{where} {o['track_id']} trajectory")
+
+
+def run_pair(det_frames, max_lost=150, min_hits=1, thr=0.1):
+    yk = pkg()
+    ours = yk.EnhancedMultiTargetTracker(max_lost, min_hits, thr)
+    ref = RefMultiTracker(max_lost, min_hits, thr, stable_ties=True)
+    exact = total = 0
+    for t, dets in enumerate(det_frames):
+        a = ours.update(dets)
+        b = ref.update(dets)
+        compare_frame(a, b, f"frame {t}")
+        for o, r in zip(a, b):
+            total += 1
+            exact += bool(np.array_equal(o["bbox"], r["bbox"]))
+    assert ours.stats == ref.stats
+    assert ours.frame_count == ref.frame_count and ours.next_track_id == ref.next_track_id
+    return ours, ref, exact, total
+
+
+@pytest.mark.parametrize("seed,K", [(0, 16), (1, 64)])
+def test_tracker_matches_oracle_gt_sequences(seed, K):
+    yk = pkg()
+    sc = yk.synth.Scene(seed=seed, n_targets=K, n_frames=180)
+    frames = [sc.detections(t) for t in range(sc.T)]
+    ours, ref, exact, total = run_pair(frames)
+    assert total > 0
+    # boxes are computed with the reference's own rounding sequence: bitwise in practice
+    assert exact / total > 0.99
+
+
+def test_tracker_reference_defaults_and_float64_detections():
+    yk = pkg()
+    sc = yk.synth.Scene(seed=3, n_targets=12, n_frames=80)
+    frames = [[[float(v) for v in d] for d in sc.detections(t)] for t in range(sc.T)]  # python floats
+    run_pair(frames, max_lost=450, min_hits=3, thr=0.3)
+
+
+def test_tracker_deletion_boundary_and_empty_frames():
+    f = np.float32
+    det = [[f(100), f(100), f(110), f(108), f(0.9)]]
+    frames = [det, [[f(101), f(100), f(111), f(108), f(0.9)]]] + [[] for _ in range(160)] + [det]
+    ours, ref, _, _ = run_pair(frames)
+    assert ours.stats["total_tracks_terminated"] == 1
+
+
+def test_tracker_exact_ties_stable_order():
+    f = np.float32
+    # two identical detections over one track: exact IoU tie, lowest detection index wins
+    frames = [[[f(50), f(50), f(60), f(60), f(.9)]],
+              [[f(50), f(50), f(60), f(60), f(.9)], [f(50), f(50), f(60), f(60), f(.8)]]] * 3
+    run_pair(frames, thr=0.1)
+
+
+def test_tracker_many_tracks_and_streams():
+    yk = pkg()
+    S = 4
+    scenes = [yk.synth.Scene(seed=10 + s, n_targets=48 + 8 * s, n_frames=60) for s in range(S)]
+    ms = yk.MultiStreamTracker(S, 150, 1, 0.1, max_tracks=256, max_dets=128)
+    refs = [RefMultiTracker(150, 1, 0.1, stable_ties=True) for _ in range(S)]
+    for t in range(60):
+        per = [sc.detections(t) for sc in scenes]
+        ms.step_host(per)
+        rows, counts, stats = ms.download()
+        for s in range(S):
+            rb = refs[s].update(per[s])
+            ours = [yk.tracker._row_to_dict(r, yk.tracker.track_id_of(r["track_num"])) for r in rows[s, : counts[s]]]
+            compare_frame(ours, rb, f"stream {s} frame {t}")
+            assert int(stats[s]["total_tracks_created"]) == refs[s].stats["total_tracks_created"]
+
+
+def test_standalone_track_object_ops():
+    yk = pkg()
+    f = np.float32
+    b0 = [f(100), f(100), f(110), f(108)]
+    ours = yk.AircraftKalmanTracker(b0, track_id="A", max_lost_frames=150)
+    ref = RefTrack(b0, "A", 150)
+    for t in range(40):
+        _close(ours.predict(), ref.predict(), f"predict {t}")
+        if t % 5 != 4:
+            b = [f(100 + 1.5 * t), f(100 + 0.5 * t), f(110 + 1.5 * t), f(108 + 0.5 * t)]
+            ours.update(b)
+            ref.update(b)
+        else:
+            ours.mark_as_lost()
+            ref.mark_as_lost()
+        _close(ours.x, ref.x, f"x {t}")
+        _close(ours.P, ref.P, f"P {t}")
+        compare_frame([ours.get_track_info()], [ref.get_track_info()], f"info {t}")
+    for k in (1, 2, 7, 40):
+        a, ca = ours.enhanced_long_term_predict(k)
+        b, cb = ref.long_term_predict(k)
+        _close(a, b, f"long-term {k}")
+        _close(ca, cb, f"long-term conf {k}")
+
+
+def test_multi_tracker_views_and_statistics():
+    yk = pkg()
+    sc = yk.synth.Scene(seed=5, n_targets=8, n_frames=40)
+    ours = yk.EnhancedMultiTargetTracker(150, 1, 0.1)
+    ref = RefMultiTracker(150, 1, 0.1, stable_ties=True)
+    for t in range(40):
+        ours.update(sc.detections(t))
+        ref.update(sc.detections(t))
+    so, sr = ours.get_statistics(), ref.get_statistics()
+    assert so["tracker_details"] == [{**d, "confidence": pytest.approx(d["confidence"], rel=RTOL)} for d in sr["tracker_details"]]
+    assert [t.track_id for t in ours.trackers] == [t.track_id for t in ref.trackers]
+    for a, b in zip(ours.trackers, ref.trackers):
+        _close(a.x, b.x, "view x")
+        _close(a.P, b.P, "view P")
+        assert a.age == b.age and a.hits == b.hits

@@ -1,0 +1,145 @@
+"""ctypes binding of libyk.so (include/yk.h).
+
+torch is imported before the library is loaded so that libyk.so's libamdhip64.so.7
+resolves to torch's bundled HIP runtime: one runtime, one device context, and torch
+tensors' data_ptr() can be handed to yk calls directly.  There is no fallback: if the
+library is missing or fails to load, every product entry point raises YKError.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+import numpy as np
+import torch  # noqa: F401  (load order: torch's HIP runtime first)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("YK_LIB", os.path.join(_HERE, "libyk.so"))
+
+YK_OK, YK_ERR_ARG, YK_ERR_HIP, YK_ERR_CAPACITY, YK_ERR_STATE = 0, 1, 2, 3, 4
+YK_F32, YK_F64 = 0, 1
+OP_PREDICT, OP_UPDATE, OP_MARK_LOST, OP_INFO, OP_LONG_TERM, OP_LOST_PRED = range(6)
+TRAJ_OUT, VEL_HIST, TRAJ_HIST = 30, 50, 150
+
+
+class YKError(RuntimeError):
+    """A libyk.so call failed (message from yk_last_error())."""
+
+
+# ---------------------------------------------------------------- ABI structs
+class TrackerCfg(C.Structure):
+    _fields_ = [("max_lost_frames", C.c_int32), ("min_hits", C.c_int32), ("iou_threshold", C.c_double),
+                ("max_tracks", C.c_int32), ("max_dets", C.c_int32)]
+
+
+STATS_DTYPE = np.dtype([(k, np.int64) for k in (
+    "frame_count", "next_track_id", "total_tracks_created", "total_tracks_terminated",
+    "current_active_tracks", "long_term_predictions", "successful_recoveries", "overflow")])
+
+TRACK_OUT_DTYPE = np.dtype([
+    ("track_num", np.int32), ("status", np.int32), ("age", np.int32), ("hits", np.int32),
+    ("hit_streak", np.int32), ("time_since_update", np.int32), ("traj_len", np.int32),
+    ("is_stable_motion", np.int32), ("bbox", np.float64, (4,)), ("confidence", np.float64),
+    ("velocity", np.float64, (2,)), ("motion_confidence", np.float64), ("speed", np.float64),
+    ("direction", np.float64), ("traj", np.float64, (TRAJ_OUT, 2))], align=True)
+
+TRACK_STATE_DTYPE = np.dtype([
+    ("track_num", np.int32), ("age", np.int32), ("hits", np.int32), ("hit_streak", np.int32),
+    ("time_since_update", np.int32), ("is_lost", np.int32), ("lost_frames", np.int32),
+    ("vel_len", np.int32), ("traj_len", np.int32), ("max_lost_frames", np.int32),
+    ("x", np.float64, (8,)), ("P", np.float64, (8, 8)), ("velocity_avg", np.float64, (2,)),
+    ("velocity_std", np.float64, (2,)), ("direction", np.float64), ("speed", np.float64),
+    ("stability_score", np.float64), ("prediction_confidence", np.float64),
+    ("vel_hist", np.float64, (VEL_HIST, 2)), ("traj_hist", np.float64, (TRAJ_HIST, 2))], align=True)
+
+_vp = C.c_void_p
+_i32 = C.c_int32
+_SIGS = {
+    "yk_abi_version": ([], C.c_int),
+    "yk_last_error": ([], C.c_char_p),
+    "yk_struct_size": ([C.c_int], C.c_int64),
+    "yk_ctx_create": ([C.c_int, C.POINTER(_vp)], C.c_int),
+    "yk_ctx_destroy": ([_vp], C.c_int),
+    "yk_tracker_create": ([_vp, C.c_int, C.POINTER(TrackerCfg), C.POINTER(_vp)], C.c_int),
+    "yk_tracker_destroy": ([_vp], C.c_int),
+    "yk_tracker_reset": ([_vp, _vp], C.c_int),
+    "yk_tracker_step": ([_vp, _vp, C.c_int, C.c_int, _vp, _vp], C.c_int),
+    "yk_tracker_outputs": ([_vp, C.POINTER(_vp), C.POINTER(_vp), C.POINTER(_vp)], C.c_int),
+    "yk_tracker_download": ([_vp, _vp, _vp, _vp, _vp], C.c_int),
+    "yk_tracker_snapshot": ([_vp, C.c_int, _vp, C.POINTER(_i32), _vp], C.c_int),
+    "yk_track_op": ([_vp, C.c_int, C.c_int, C.c_int, C.c_int, _vp, C.c_int, _vp, _vp, _vp], C.c_int),
+    "yk_track_create": ([_vp, C.c_int, _vp, C.c_int, _i32, _i32, _vp], C.c_int),
+}
+
+_lock = threading.Lock()
+_lib = None
+
+
+def exported_symbols() -> list[str]:
+    return sorted(_SIGS)
+
+
+def lib() -> C.CDLL:
+    """Load libyk.so once (raises YKError if it is missing: there is no CPU fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise YKError(f"libyk.so not found at {LIB_PATH}: build it with `python __graft_entry__.py build` "
+                          "(or csrc/build.py); the HIP path has no CPU fallback")
+        try:
+            L = C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL)
+        except OSError as e:
+            raise YKError(f"failed to load {LIB_PATH}: {e}") from e
+        for name, (args, res) in _SIGS.items():
+            fn = getattr(L, name)
+            fn.argtypes = args
+            fn.restype = res
+        if L.yk_abi_version() != 1:
+            raise YKError("libyk.so ABI version mismatch")
+        sizes = {0: C.sizeof(TrackerCfg), 1: STATS_DTYPE.itemsize, 2: TRACK_OUT_DTYPE.itemsize,
+                 3: TRACK_STATE_DTYPE.itemsize}
+        for k, v in sizes.items():
+            if L.yk_struct_size(k) != v:
+                raise YKError(f"ABI struct {k} size mismatch: C {L.yk_struct_size(k)} vs python {v}")
+        _lib = L
+        return L
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc != YK_OK:
+        msg = lib().yk_last_error().decode(errors="replace")
+        raise YKError(f"{what or 'yk call'} failed (status {rc}): {msg}")
+
+
+def ptr(a) -> C.c_void_p:
+    """Raw pointer of a numpy array or torch tensor (None -> NULL)."""
+    if a is None:
+        return C.c_void_p(0)
+    if isinstance(a, torch.Tensor):
+        return C.c_void_p(a.data_ptr())
+    return C.c_void_p(a.ctypes.data)
+
+
+_ctx: dict[int, C.c_void_p] = {}
+
+
+def context(device: int = 0) -> C.c_void_p:
+    """Process-wide yk_ctx for a device (one context per GPU, like select_device)."""
+    if device in _ctx:
+        return _ctx[device]
+    if not torch.cuda.is_available():
+        raise YKError("no HIP device visible: the yk hot path runs only on an AMD GPU (no CPU fallback)")
+    torch.cuda.init()
+    h = C.c_void_p()
+    check(lib().yk_ctx_create(device, C.byref(h)), "yk_ctx_create")
+    _ctx[device] = h
+    return h
+
+
+def current_stream(device: int = 0) -> C.c_void_p:
+    return C.c_void_p(torch.cuda.current_stream(device).cuda_stream)

@@ -1,0 +1,1031 @@
+// Batched multi-stream Kalman tracker step for gfx950 (MI355X).
+//
+// One workgroup per video stream runs one complete
+// EnhancedMultiTargetTracker.update() (kalman/enhanced_multi_target_tracker.py:42-132):
+//   predict every live track            (kalman/enhanced_aircraft_kalman_tracker.py:184-203)
+//   IoU candidates, mixed f32/f64        (enhanced_multi_target_tracker.py:180-232)
+//   greedy association                   (enhanced_multi_target_tracker.py:234-270)
+//   update / mark_as_lost / create / delete / get_track_info
+//                                        (enhanced_aircraft_kalman_tracker.py:249-405)
+//
+// Filter structure.  F = I + unit(i,i+4), H = [I4 0], Q, R and the initial P are all
+// block-structured over the four (position_c, velocity_c) pairs, so P keeps exactly the
+// 16 entries P[c][c], P[c][c+4], P[c+4][c], P[c+4][c+4].  Each track is
+// therefore four independent 2x2 filters.  The arithmetic below reproduces numpy's
+// evaluation order and roundings (checked bitwise against oracle/tracker_ref.py):
+//   F@P@F.T + Q  -> pp' = ((p+b)+(a+v)) + q_p, pv' = a+v, vp' = b+v, vv' = v + q_v
+//   K = P H^T inv(S), inv(S) = diag(1/(p+R))
+//   (I-KH)@P     -> pp' = (1-Kp)*p, pv' = (1-Kp)*a, vp' = (-Kv*p)+b, vv' = (-Kv*a)+v  (unfused)
+// This file is compiled with -ffp-contract=off so no FMA contraction changes a rounding.
+//
+// Association is the sequential greedy match over candidates ordered by (IoU desc,
+// row-major pair index asc), computed in parallel as rounds of "locally dominant" pairs
+// (a pair that is the best free pair of both its detection row and its track column is
+// exactly the pair the sequential scan would accept).  Ties are thereby broken like a
+// stable argsort; numpy's default argsort is unstable on exact ties (SURVEY §7 hard parts).
+#include <climits>
+
+#include "yk_internal.h"
+
+namespace yk {
+namespace trk {
+
+constexpr int NT = 256;                 // threads per stream workgroup (4 waves)
+constexpr int NW = NT / 64;
+constexpr int VH = YK_VEL_HIST;         // velocity ring (deque maxlen=50)
+constexpr int TH = YK_TRAJ_HIST;        // trajectory ring (deque maxlen=150)
+constexpr int TOUT = YK_TRAJ_OUT;       // trajectory points exported per row
+constexpr double kPi = 3.141592653589793;  // np.pi
+
+struct Slot {
+  double x[8];
+  double P[16];  // per coordinate c: [4c+0]=P[c][c] [4c+1]=P[c][c+4] [4c+2]=P[c+4][c] [4c+3]=P[c+4][c+4]
+  double vavg[2], vstd[2], direction, speed, stability, pconf;
+  double vh[VH][2];
+  double vang[VH];  // arctan2(vy, vx) of each velocity entry, cached at push time
+  double th[TH][2];
+  int age, hits, hit_streak, tsu, is_lost, lost_frames, track_num, max_lost;
+  int vh_len, vh_head, th_len, th_head;
+};
+
+struct Hdr {
+  int n_tracks, n_free;
+  yk_tracker_stats st;
+};
+
+struct Dev {
+  Slot* slots;          // [S][T]
+  Hdr* hdr;             // [S]
+  int* order;           // [S][T] list position -> slot
+  int* free_stack;      // [S][T]
+  unsigned long long* cand_key;  // [S][C] IoU bits of candidate pairs
+  int* cand_flat;                // [S][C] row-major pair index d*n + t
+  yk_track_out* rows;   // [S][T]
+  int* counts;          // [S]
+  yk_tracker_stats* stats;  // [S]
+  int T, D, C;
+  int max_lost, min_hits;
+  double thr;
+};
+
+// ---------------------------------------------------------------- per-track math
+__device__ __forceinline__ void ring_push(double (*buf)[2], int cap, int& len, int& head, double a,
+                                          double b, int* pos_out = nullptr) {
+  int pos;
+  if (len < cap) {
+    pos = head + len;
+    if (pos >= cap) pos -= cap;
+    ++len;
+  } else {
+    pos = head;
+    head = (head + 1 == cap) ? 0 : head + 1;
+  }
+  buf[pos][0] = a;
+  buf[pos][1] = b;
+  if (pos_out) *pos_out = pos;
+}
+
+__device__ __forceinline__ void state_to_bbox(const double* s, double* b) {
+  // enhanced_aircraft_kalman_tracker.py:130-135
+  b[0] = s[0] - s[2] / 2.0;
+  b[1] = s[1] - s[3] / 2.0;
+  b[2] = s[0] + s[2] / 2.0;
+  b[3] = s[1] + s[3] / 2.0;
+}
+
+// bbox_to_state (kf.py:113-118) in the detection's own dtype, widened to f64.
+template <typename DT>
+__device__ __forceinline__ void bbox_to_state(const DT* b, double* z) {
+  DT cx = (b[0] + b[2]) / DT(2);
+  DT cy = (b[1] + b[3]) / DT(2);
+  DT w = b[2] - b[0];
+  DT h = b[3] - b[1];
+  z[0] = (double)cx;
+  z[1] = (double)cy;
+  z[2] = (double)w;
+  z[3] = (double)h;
+}
+
+__device__ void slot_init(Slot& s, const double* z, int track_num, int max_lost) {
+  // AircraftKalmanTracker.__init__ (kf.py:32-101)
+  for (int i = 0; i < 8; ++i) s.x[i] = 0.0;
+  for (int c = 0; c < 4; ++c) {
+    s.x[c] = z[c];
+    s.P[4 * c + 0] = 50.0;
+    s.P[4 * c + 1] = 0.0;
+    s.P[4 * c + 2] = 0.0;
+    s.P[4 * c + 3] = c < 2 ? 100.0 : 1.0;
+  }
+  s.vavg[0] = s.vavg[1] = s.vstd[0] = s.vstd[1] = 0.0;
+  s.direction = s.speed = s.stability = s.pconf = 0.0;
+  s.age = 0;
+  s.hits = 1;
+  s.hit_streak = 1;
+  s.tsu = 0;
+  s.is_lost = 0;
+  s.lost_frames = 0;
+  s.track_num = track_num;
+  s.max_lost = max_lost;
+  s.vh_len = s.vh_head = 0;
+  s.th_len = s.th_head = 0;
+  ring_push(s.th, TH, s.th_len, s.th_head, z[0], z[1]);
+}
+
+__device__ void kf_predict(Slot& s) {
+  // kf.py:192-201: x = F x ; P = F P F^T + Q
+  const double qp[4] = {0.1, 0.1, 0.01, 0.01};
+  const double qv[4] = {0.1, 0.1, 0.001, 0.001};
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    s.x[c] = s.x[c] + s.x[c + 4];
+    const double p = s.P[4 * c], a = s.P[4 * c + 1], b = s.P[4 * c + 2], v = s.P[4 * c + 3];
+    const double app = p + b, apv = a + v;  // rows of F@P
+    s.P[4 * c + 0] = (app + apv) + qp[c];
+    s.P[4 * c + 1] = apv + 0.0;
+    s.P[4 * c + 2] = (b + v) + 0.0;
+    s.P[4 * c + 3] = v + qv[c];
+  }
+  s.age += 1;
+  s.tsu += 1;
+  ring_push(s.th, TH, s.th_len, s.th_head, s.x[0], s.x[1]);
+}
+
+// numpy's pairwise summation for a contiguous 1-D float64 array of n <= 128 elements
+// (numpy/_core/src/umath/loops_utils.h.src, pairwise_sum), the add.reduce of np.std/np.mean.
+__device__ double np_pairwise_sum(const double* a, int n) {
+  if (n < 8) {
+    double r = 0.0;
+    for (int i = 0; i < n; ++i) r += a[i];
+    return r;
+  }
+  double r[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = a[j];
+  int i = 8;
+  for (; i < n - (n % 8); i += 8) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] += a[i + j];
+  }
+  double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+  for (; i < n; ++i) res += a[i];
+  return res;
+}
+
+__device__ void analyze_motion(Slot& s) {
+  // kf.py:137-182
+  const int n = s.vh_len;
+  if (n < 5) return;
+  double mean[2], sq[2];
+  for (int j = 0; j < 2; ++j) {  // np.mean(axis=0): sequential over rows
+    int idx = s.vh_head;
+    double acc = s.vh[idx][j];
+    for (int k = 1; k < n; ++k) {
+      idx = (idx + 1 == VH) ? 0 : idx + 1;
+      acc += s.vh[idx][j];
+    }
+    mean[j] = acc / (double)n;
+  }
+  for (int j = 0; j < 2; ++j) {  // np.std(axis=0), ddof=0
+    int idx = s.vh_head;
+    double d = s.vh[idx][j] - mean[j];
+    double acc = d * d;
+    for (int k = 1; k < n; ++k) {
+      idx = (idx + 1 == VH) ? 0 : idx + 1;
+      d = s.vh[idx][j] - mean[j];
+      acc += d * d;
+    }
+    sq[j] = sqrt(acc / (double)n);
+  }
+  s.vavg[0] = mean[0];
+  s.vavg[1] = mean[1];
+  s.vstd[0] = sq[0];
+  s.vstd[1] = sq[1];
+  s.speed = sqrt(mean[0] * mean[0] + mean[1] * mean[1]);
+  s.direction = atan2(mean[1], mean[0]);
+  const double speed_stab = 1.0 / (1.0 + ((0.0 + sq[0]) + sq[1]) / 2.0);
+  // _calculate_direction_consistency (kf.py:165-182); n >= 5 here, so the n<3 exit is dead
+  double dch[VH];
+  const int m = n - 1;
+  {
+    int idx = s.vh_head;
+    double prev = s.vang[idx];
+    for (int k = 0; k < m; ++k) {
+      idx = (idx + 1 == VH) ? 0 : idx + 1;
+      const double cur = s.vang[idx];
+      double c = cur - prev;
+      if (!(fabs(c) < kPi)) c = c - 2.0 * kPi * (c > 0.0 ? 1.0 : (c < 0.0 ? -1.0 : c));
+      dch[k] = c;
+      prev = cur;
+    }
+  }
+  const double dmean = np_pairwise_sum(dch, m) / (double)m;
+  for (int k = 0; k < m; ++k) {
+    const double d = dch[k] - dmean;
+    dch[k] = d * d;
+  }
+  const double dstd = sqrt(np_pairwise_sum(dch, m) / (double)m);
+  const double dir_cons = 1.0 / (1.0 + dstd * 10.0);
+  s.stability = (speed_stab + dir_cons) / 2.0;
+  const double frac = (double)n / 30.0;
+  s.pconf = s.stability * (1.0 < frac ? 1.0 : frac);
+}
+
+template <typename DT>
+__device__ void kf_update(Slot& s, const DT* box) {
+  // kf.py:249-297 (recovery print omitted; the count is kept by the caller)
+  s.tsu = 0;
+  s.hits += 1;
+  s.hit_streak += 1;
+  if (s.is_lost) {
+    s.is_lost = 0;
+    s.lost_frames = 0;
+  }
+  double z[4];
+  bbox_to_state<DT>(box, z);
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const double p = s.P[4 * c], a = s.P[4 * c + 1], b = s.P[4 * c + 2], v = s.P[4 * c + 3];
+    const double y = z[c] - s.x[c];
+    const double inv = 1.0 / (p + 10.0);
+    const double kp = p * inv, kv = b * inv;
+    s.x[c] = s.x[c] + kp * y;
+    s.x[c + 4] = s.x[c + 4] + kv * y;
+    const double ikh = 1.0 - kp, nkv = -kv;
+    s.P[4 * c + 0] = ikh * p;
+    s.P[4 * c + 1] = ikh * a;
+    s.P[4 * c + 2] = nkv * p + b;
+    s.P[4 * c + 3] = nkv * a + v;
+  }
+  int pos;
+  ring_push(s.vh, VH, s.vh_len, s.vh_head, s.x[4], s.x[5], &pos);
+  s.vang[pos] = atan2(s.x[5], s.x[4]);
+  ring_push(s.th, TH, s.th_len, s.th_head, s.x[0], s.x[1]);
+  analyze_motion(s);
+}
+
+__device__ __forceinline__ void mark_lost(Slot& s) {
+  // kf.py:299-317
+  if (!s.is_lost) {
+    s.is_lost = 1;
+    s.lost_frames = 0;
+  }
+  s.lost_frames += 1;
+  s.hit_streak = 0;
+}
+
+__device__ __forceinline__ bool should_delete(const Slot& s, int max_lost) {
+  // kf.py:385-405
+  if (s.tsu > max_lost) return true;
+  if (s.age < 5 && s.hit_streak == 0 && s.tsu > 15) return true;
+  if (s.age < 10 && s.hit_streak <= 1 && s.tsu > 30) return true;
+  return false;
+}
+
+// enhanced_long_term_predict(frames_ahead=k) (kf.py:205-247).  k <= 1 runs predict().
+__device__ void long_term_predict(Slot& s, int k, double* box, double& conf) {
+  if (k <= 1) {
+    kf_predict(s);
+    state_to_bbox(s.x, box);
+    conf = 1.0;
+    return;
+  }
+  // analyze_motion_pattern() is re-run by the reference here; the velocity history has
+  // not changed since the last update() (which ran it), so the cached statistics are
+  // identical to a recomputation.
+  double st[4];
+  if (s.pconf > 0.3) {
+    st[0] = s.x[0] + s.vavg[0] * (double)k;
+    st[1] = s.x[1] + s.vavg[1] * (double)k;
+    st[2] = s.x[2];
+    st[3] = s.x[3];
+    const double decay = 1.0 - (double)k / (double)s.max_lost;
+    conf = s.pconf * (decay > 0.1 ? decay : 0.1);
+  } else {
+    st[0] = s.x[0];
+    st[1] = s.x[1];
+    st[2] = s.x[2];
+    st[3] = s.x[3];
+    for (int r = 0; r < k; ++r)
+      for (int c = 0; c < 4; ++c) st[c] = st[c] + s.x[c + 4];
+    const double decay = 1.0 - (double)k / ((double)s.max_lost * 0.5);
+    conf = decay > 0.1 ? decay : 0.1;
+  }
+  state_to_bbox(st, box);
+}
+
+// get_lost_prediction (kf.py:319-333)
+__device__ void lost_prediction(Slot& s, double* box, double& conf) {
+  if (!s.is_lost) {
+    state_to_bbox(s.x, box);
+    conf = 1.0;
+    return;
+  }
+  long_term_predict(s, s.lost_frames, box, conf);
+}
+
+// get_track_info (kf.py:335-383) including quirk A (a second predict() on the first
+// lost frame, via get_lost_prediction -> enhanced_long_term_predict(1)).
+__device__ void track_info(Slot& s, yk_track_out& o) {
+  double box[4];
+  double conf;
+  int status;
+  if (s.tsu > 0) {
+    status = 1;
+    if (s.is_lost) {
+      lost_prediction(s, box, conf);
+    } else {  // short-loss branch; unreachable from update(), kept for parity
+      state_to_bbox(s.x, box);
+      const double decay = 1.0 - (double)s.tsu / 60.0;
+      conf = decay > 0.3 ? decay : 0.3;
+    }
+  } else {
+    status = 0;
+    state_to_bbox(s.x, box);
+    conf = 1.0;
+  }
+  o.track_num = s.track_num;
+  o.status = status;
+  o.age = s.age;
+  o.hits = s.hits;
+  o.hit_streak = s.hit_streak;
+  o.time_since_update = s.tsu;
+  o.is_stable_motion = s.stability > 0.5 ? 1 : 0;
+  for (int i = 0; i < 4; ++i) o.bbox[i] = box[i];
+  o.confidence = conf;
+  o.velocity[0] = s.x[4];
+  o.velocity[1] = s.x[5];
+  o.motion_confidence = s.pconf;
+  o.speed = s.speed;
+  o.direction = s.direction;
+  const int nt = s.th_len < TOUT ? s.th_len : TOUT;
+  o.traj_len = nt;
+  int idx = s.th_head + (s.th_len - nt);
+  if (idx >= TH) idx -= TH;
+  for (int k = 0; k < nt; ++k) {
+    o.traj[k][0] = s.th[idx][0];
+    o.traj[k][1] = s.th[idx][1];
+    idx = (idx + 1 == TH) ? 0 : idx + 1;
+  }
+  for (int k = nt; k < TOUT; ++k) o.traj[k][0] = o.traj[k][1] = 0.0;
+}
+
+// IoU of detection (DT) against a predicted track box (f64) with the reference's dtype
+// propagation (enhanced_multi_target_tracker.py:200-232): python max/min
+// return the winning object (ties -> the detection), f32-op-f32 stays f32.
+template <typename DT>
+__device__ double iou_mixed(const DT* d, const double* t) {
+  // each intersection coordinate: value as double + whether it is still a DT value
+  const bool tx1 = t[0] > (double)d[0];
+  const bool ty1 = t[1] > (double)d[1];
+  const bool tx2 = t[2] < (double)d[2];
+  const bool ty2 = t[3] < (double)d[3];
+  const double ix1 = tx1 ? t[0] : (double)d[0];
+  const double iy1 = ty1 ? t[1] : (double)d[1];
+  const double ix2 = tx2 ? t[2] : (double)d[2];
+  const double iy2 = ty2 ? t[3] : (double)d[3];
+  if (ix2 <= ix1 || iy2 <= iy1) return 0.0;
+  // width / height: DT arithmetic when both operands are detection values
+  const bool w_dt = !tx1 && !tx2, h_dt = !ty1 && !ty2;
+  const double w = w_dt ? (double)(DT)(d[2] - d[0]) : ix2 - ix1;
+  const double h = h_dt ? (double)(DT)(d[3] - d[1]) : iy2 - iy1;
+  const double inter = (w_dt && h_dt) ? (double)((DT)w * (DT)h) : w * h;
+  const DT area1 = (d[2] - d[0]) * (d[3] - d[1]);
+  const double area2 = (t[2] - t[0]) * (t[3] - t[1]);
+  const double uni = ((double)area1 + area2) - inter;
+  if (uni <= 0.0) return 0.0;
+  return inter / uni;
+}
+
+// ---------------------------------------------------------------- block helpers
+// Exclusive prefix count of `flag` over the workgroup; `total` gets the block total.
+__device__ __forceinline__ int block_scan(int flag, int* wsum, int& total) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const unsigned long long m = __ballot(flag);
+  const int pre = __popcll(m & ((1ull << lane) - 1ull));
+  if (lane == 0) wsum[w] = __popcll(m);
+  __syncthreads();
+  int base = 0, tot = 0;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) {
+    base += (i < w) ? wsum[i] : 0;
+    tot += wsum[i];
+  }
+  __syncthreads();
+  total = tot;
+  return base + pre;
+}
+
+struct Lds {
+  double* pb;                 // [T][4] predicted boxes by list position
+  double* det;                // [D][4] detection boxes (exact widening of DT)
+  int* det_match;             // [D] matched list position or -1
+  int* trk_match;             // [T] matched detection or -1
+  unsigned long long* row_max;  // [D]
+  unsigned long long* col_max;  // [T]
+  int* row_arg;               // [D]
+  int* col_arg;               // [T]
+  int* order_tmp;             // [T]
+  int* misc;                  // [16]
+};
+
+__host__ __device__ inline size_t lds_bytes(int T, int D) {
+  return (size_t)T * 32 + (size_t)D * 32 + (size_t)D * 4 + (size_t)T * 4 + (size_t)D * 8 +
+         (size_t)T * 8 + (size_t)D * 4 + (size_t)T * 4 + (size_t)T * 4 + 16 * 4;
+}
+
+__device__ Lds carve(char* base, int T, int D) {
+  Lds L;
+  L.pb = (double*)base;
+  base += (size_t)T * 32;
+  L.det = (double*)base;
+  base += (size_t)D * 32;
+  L.row_max = (unsigned long long*)base;
+  base += (size_t)D * 8;
+  L.col_max = (unsigned long long*)base;
+  base += (size_t)T * 8;
+  L.det_match = (int*)base;
+  base += (size_t)D * 4;
+  L.trk_match = (int*)base;
+  base += (size_t)T * 4;
+  L.row_arg = (int*)base;
+  base += (size_t)D * 4;
+  L.col_arg = (int*)base;
+  base += (size_t)T * 4;
+  L.order_tmp = (int*)base;
+  base += (size_t)T * 4;
+  L.misc = (int*)base;
+  return L;
+}
+
+enum { M_NCAND = 0, M_ACTIVE, M_RECOVER, M_LONGTERM, M_OVERFLOW, M_WSUM = 8 };
+
+// ---------------------------------------------------------------- the step kernel
+template <typename DT>
+__global__ void __launch_bounds__(NT) step_kernel(Dev g, const DT* __restrict__ dets, int row_stride,
+                                                  const int* __restrict__ counts) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int s = blockIdx.x, tid = threadIdx.x;
+  const int T = g.T;
+  Lds L = carve(smem, T, g.D);
+  Hdr& H = g.hdr[s];
+  Slot* slots = g.slots + (size_t)s * T;
+  int* order = g.order + (size_t)s * T;
+  int* fstack = g.free_stack + (size_t)s * T;
+  int* wsum = L.misc + M_WSUM;
+
+  int Draw = counts[s];
+  if (Draw < 0) Draw = 0;
+  const int D = Draw < g.D ? Draw : g.D;
+  const int n = H.n_tracks;
+  if (tid < 8) L.misc[tid] = 0;
+  // load detections (rows of row_stride elements; only x1..y2 are used by the tracker)
+  for (int i = tid; i < D * 4; i += NT) {
+    const int d = i >> 2, k = i & 3;
+    L.det[i] = (double)dets[((size_t)s * g.D + d) * row_stride + k];
+  }
+  for (int d = tid; d < D; d += NT) L.det_match[d] = -1;
+  for (int t = tid; t < n; t += NT) L.trk_match[t] = -1;
+  // Step 1: predict every live track (multi:55-58)
+  for (int i = tid; i < n; i += NT) {
+    Slot& sl = slots[order[i]];
+    kf_predict(sl);
+    state_to_bbox(sl.x, &L.pb[4 * i]);
+  }
+  __syncthreads();
+
+  // Step 2: association (multi:61-68, 134-178)
+  if (D > 0 && n > 0) {
+    unsigned long long* ckey = g.cand_key + (size_t)s * g.C;
+    int* cflat = g.cand_flat + (size_t)s * g.C;
+    const int npair = D * n;
+    for (int f = tid; f < npair; f += NT) {
+      const int d = f / n, t = f - d * n;
+      DT db[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) db[k] = (DT)L.det[4 * d + k];
+      const double v = iou_mixed<DT>(db, &L.pb[4 * t]);
+      if (v >= g.thr) {
+        const int c = atomicAdd(&L.misc[M_NCAND], 1);
+        if (c < g.C) {
+          ckey[c] = (unsigned long long)__double_as_longlong(v);
+          cflat[c] = f;
+        }
+      }
+    }
+    __syncthreads();
+    int nc = L.misc[M_NCAND];
+    if (nc > g.C) {
+      if (tid == 0) L.misc[M_OVERFLOW] += nc - g.C;
+      nc = g.C;
+    }
+    for (int round = 0; round <= D + 1; ++round) {
+      for (int d = tid; d < D; d += NT) {
+        L.row_max[d] = 0ull;
+        L.row_arg[d] = INT_MAX;
+      }
+      for (int t = tid; t < n; t += NT) {
+        L.col_max[t] = 0ull;
+        L.col_arg[t] = INT_MAX;
+      }
+      if (tid == 0) L.misc[M_ACTIVE] = 0;
+      __syncthreads();
+      int local_active = 0;
+      for (int c = tid; c < nc; c += NT) {
+        const int f = cflat[c], d = f / n, t = f - d * n;
+        if (L.det_match[d] < 0 && L.trk_match[t] < 0) {
+          const unsigned long long k = ckey[c];
+          atomicMax(&L.row_max[d], k);
+          atomicMax(&L.col_max[t], k);
+          ++local_active;
+        }
+      }
+      if (local_active) atomicAdd(&L.misc[M_ACTIVE], local_active);
+      __syncthreads();
+      if (L.misc[M_ACTIVE] == 0) break;
+      for (int c = tid; c < nc; c += NT) {
+        const int f = cflat[c], d = f / n, t = f - d * n;
+        if (L.det_match[d] < 0 && L.trk_match[t] < 0) {
+          const unsigned long long k = ckey[c];
+          if (k == L.row_max[d]) atomicMin(&L.row_arg[d], f);
+          if (k == L.col_max[t]) atomicMin(&L.col_arg[t], f);
+        }
+      }
+      __syncthreads();
+      for (int c = tid; c < nc; c += NT) {
+        const int f = cflat[c], d = f / n, t = f - d * n;
+        if (L.row_arg[d] == f && L.col_arg[t] == f) {
+          L.det_match[d] = t;
+          L.trk_match[t] = d;
+        }
+      }
+      __syncthreads();
+    }
+  }
+
+  // Steps 3-4: update matched tracks, mark the others lost (multi:71-89)
+  int recov = 0;
+  for (int i = tid; i < n; i += NT) {
+    Slot& sl = slots[order[i]];
+    const int d = L.trk_match[i];
+    if (d >= 0) {
+      DT db[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) db[k] = (DT)L.det[4 * d + k];
+      recov += sl.is_lost ? 1 : 0;
+      kf_update<DT>(sl, db);
+    } else {
+      mark_lost(sl);
+    }
+  }
+  if (recov) atomicAdd(&L.misc[M_RECOVER], recov);
+
+  // Step 5: new tracks for unmatched detections, ascending detection order (multi:92-101)
+  int n_new_total = 0;
+  const int next_num = (int)H.st.next_track_id;
+  const int nfree0 = H.n_free;
+  for (int base = 0; base < D; base += NT) {
+    const int d = base + tid;
+    const int flag = (d < D && L.det_match[d] < 0) ? 1 : 0;
+    int tot;
+    const int r = n_new_total + block_scan(flag, wsum, tot);
+    if (flag) {
+      const int pos = n + r;
+      if (pos < T && r < nfree0) {
+        const int slot = fstack[nfree0 - 1 - r];
+        DT db[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) db[k] = (DT)L.det[4 * d + k];
+        double z[4];
+        bbox_to_state<DT>(db, z);
+        slot_init(slots[slot], z, next_num + r, g.max_lost);
+        order[pos] = slot;
+      } else {
+        atomicAdd(&L.misc[M_OVERFLOW], 1);
+      }
+    }
+    n_new_total += tot;
+  }
+  int n_new = n_new_total;
+  if (n + n_new > T) n_new = T - n;
+  if (n_new > nfree0) n_new = nfree0;
+  __syncthreads();
+
+  // Step 6: delete (multi:104-113) with a stable compaction of the list
+  const int n_all = n + n_new;
+  int kept = 0, n_del = 0;
+  for (int base = 0; base < n_all; base += NT) {
+    const int i = base + tid;
+    int slot = -1, keep = 0;
+    if (i < n_all) {
+      slot = order[i];
+      keep = should_delete(slots[slot], g.max_lost) ? 0 : 1;
+    }
+    int tot;
+    const int r = kept + block_scan(keep, wsum, tot);
+    if (i < n_all) {
+      if (keep) L.order_tmp[r] = slot;
+    }
+    kept += tot;
+  }
+  n_del = n_all - kept;
+  __syncthreads();
+  // return deleted slots to the free stack: collect them in a second pass
+  {
+    const int nfree_after_pop = nfree0 - n_new;
+    int pushed = 0;
+    for (int base = 0; base < n_all; base += NT) {
+      const int i = base + tid;
+      int slot = -1, del = 0;
+      if (i < n_all) {
+        slot = order[i];
+        del = should_delete(slots[slot], g.max_lost) ? 1 : 0;
+      }
+      int tot;
+      const int r = pushed + block_scan(del, wsum, tot);
+      if (del) fstack[nfree_after_pop + r] = slot;
+      pushed += tot;
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < kept; i += NT) order[i] = L.order_tmp[i];
+  __syncthreads();
+
+  // Step 7: outputs in list order (multi:116-126), get_track_info may predict (quirk A)
+  const int fc = (int)H.st.frame_count + 1;
+  int nout = 0, lt = 0;
+  for (int base = 0; base < kept; base += NT) {
+    const int i = base + tid;
+    int q = 0;
+    Slot* sl = nullptr;
+    if (i < kept) {
+      sl = &slots[order[i]];
+      q = (sl->hit_streak >= g.min_hits || fc <= g.min_hits || sl->is_lost) ? 1 : 0;
+    }
+    int tot;
+    const int r = nout + block_scan(q, wsum, tot);
+    if (q) {
+      yk_track_out& o = g.rows[(size_t)s * T + r];
+      track_info(*sl, o);
+      if (o.status == 1 && o.time_since_update > 30) ++lt;
+    }
+    nout += tot;
+  }
+  if (lt) atomicAdd(&L.misc[M_LONGTERM], lt);
+  __syncthreads();
+  if (tid == 0) {
+    H.n_tracks = kept;
+    H.n_free = nfree0 - n_new + n_del;
+    H.st.frame_count = fc;
+    H.st.next_track_id += n_new;
+    H.st.total_tracks_created += n_new;
+    H.st.total_tracks_terminated += n_del;
+    H.st.current_active_tracks = kept;
+    H.st.long_term_predictions += L.misc[M_LONGTERM];
+    H.st.successful_recoveries += L.misc[M_RECOVER];
+    H.st.overflow += L.misc[M_OVERFLOW] + (Draw - D);
+    g.counts[s] = nout;
+    g.stats[s] = H.st;
+  }
+}
+
+__global__ void reset_kernel(Dev g, int S) {
+  const int s = blockIdx.x;
+  if (s >= S) return;
+  int* fstack = g.free_stack + (size_t)s * g.T;
+  for (int i = threadIdx.x; i < g.T; i += blockDim.x) fstack[i] = g.T - 1 - i;  // pops 0,1,2,...
+  if (threadIdx.x == 0) {
+    Hdr& H = g.hdr[s];
+    H.n_tracks = 0;
+    H.n_free = g.T;
+    H.st = yk_tracker_stats{};
+    H.st.next_track_id = 1;
+    g.counts[s] = 0;
+    g.stats[s] = H.st;
+  }
+}
+
+// Snapshot of the live tracks of stream s in list order (dense P, rings oldest first).
+__global__ void snapshot_kernel(Dev g, int s, yk_track_state* out) {
+  const int n = g.hdr[s].n_tracks;
+  const Slot* slots = g.slots + (size_t)s * g.T;
+  const int* order = g.order + (size_t)s * g.T;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const Slot& sl = slots[order[i]];
+    yk_track_state& o = out[i];
+    o.track_num = sl.track_num;
+    o.age = sl.age;
+    o.hits = sl.hits;
+    o.hit_streak = sl.hit_streak;
+    o.time_since_update = sl.tsu;
+    o.is_lost = sl.is_lost;
+    o.lost_frames = sl.lost_frames;
+    o.vel_len = sl.vh_len;
+    o.traj_len = sl.th_len;
+    o.max_lost_frames = sl.max_lost;
+    for (int k = 0; k < 8; ++k) o.x[k] = sl.x[k];
+    for (int k = 0; k < 64; ++k) o.P[k] = 0.0;
+    for (int c = 0; c < 4; ++c) {
+      o.P[c * 8 + c] = sl.P[4 * c + 0];
+      o.P[c * 8 + c + 4] = sl.P[4 * c + 1];
+      o.P[(c + 4) * 8 + c] = sl.P[4 * c + 2];
+      o.P[(c + 4) * 8 + c + 4] = sl.P[4 * c + 3];
+    }
+    o.velocity_avg[0] = sl.vavg[0];
+    o.velocity_avg[1] = sl.vavg[1];
+    o.velocity_std[0] = sl.vstd[0];
+    o.velocity_std[1] = sl.vstd[1];
+    o.direction = sl.direction;
+    o.speed = sl.speed;
+    o.stability_score = sl.stability;
+    o.prediction_confidence = sl.pconf;
+    int idx = sl.vh_head;
+    for (int k = 0; k < VH; ++k) {
+      const bool v = k < sl.vh_len;
+      o.vel_hist[k][0] = v ? sl.vh[idx][0] : 0.0;
+      o.vel_hist[k][1] = v ? sl.vh[idx][1] : 0.0;
+      idx = (idx + 1 == VH) ? 0 : idx + 1;
+    }
+    idx = sl.th_head;
+    for (int k = 0; k < TH; ++k) {
+      const bool v = k < sl.th_len;
+      o.traj_hist[k][0] = v ? sl.th[idx][0] : 0.0;
+      o.traj_hist[k][1] = v ? sl.th[idx][1] : 0.0;
+      idx = (idx + 1 == TH) ? 0 : idx + 1;
+    }
+  }
+}
+
+// Single-track object operations (AircraftKalmanTracker surface), one thread.
+template <typename DT>
+__global__ void track_op_kernel(Dev g, int s, int pos, int op, int arg, const double* in_box, double* out5,
+                                yk_track_out* out_row) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  Slot& sl = g.slots[(size_t)s * g.T + g.order[(size_t)s * g.T + pos]];
+  double conf = 1.0;
+  switch (op) {
+    case YK_OP_PREDICT:
+      kf_predict(sl);
+      state_to_bbox(sl.x, out5);
+      break;
+    case YK_OP_UPDATE: {
+      DT b[4];
+      for (int k = 0; k < 4; ++k) b[k] = (DT)in_box[k];
+      kf_update<DT>(sl, b);
+      break;
+    }
+    case YK_OP_MARK_LOST:
+      mark_lost(sl);
+      break;
+    case YK_OP_INFO:
+      track_info(sl, *out_row);
+      break;
+    case YK_OP_LONG_TERM:
+      long_term_predict(sl, arg, out5, conf);
+      break;
+    case YK_OP_LOST_PRED:
+      lost_prediction(sl, out5, conf);
+      break;
+  }
+  out5[4] = conf;
+}
+
+template <typename DT>
+__global__ void track_create_kernel(Dev g, int s, const double* in_box, int track_num, int max_lost,
+                                    int* status) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  Hdr& H = g.hdr[s];
+  if (H.n_tracks >= g.T || H.n_free <= 0) {
+    *status = 1;
+    return;
+  }
+  const int slot = g.free_stack[(size_t)s * g.T + H.n_free - 1];
+  H.n_free -= 1;
+  DT b[4];
+  for (int k = 0; k < 4; ++k) b[k] = (DT)in_box[k];
+  double z[4];
+  bbox_to_state<DT>(b, z);
+  slot_init(g.slots[(size_t)s * g.T + slot], z, track_num, max_lost);
+  g.order[(size_t)s * g.T + H.n_tracks] = slot;
+  H.n_tracks += 1;
+  *status = 0;
+}
+
+}  // namespace trk
+}  // namespace yk
+
+using yk::trk::Dev;
+
+struct yk_tracker {
+  yk_ctx* ctx;
+  int S;
+  yk_tracker_cfg cfg;
+  Dev dev;
+  size_t lds;
+  yk_track_state* d_snap;
+  yk_track_out* d_row1;
+  double* d_box;  // [8]: in[4], out[4]
+  int* d_status;
+};
+
+extern "C" {
+
+int yk_tracker_create(yk_ctx* ctx, int n_streams, const yk_tracker_cfg* cfg, yk_tracker** out) {
+  YK_CHECK_ARG(ctx && cfg && out, "yk_tracker_create: NULL argument");
+  YK_CHECK_ARG(n_streams >= 1 && n_streams <= 65535, "yk_tracker_create: n_streams out of range");
+  YK_CHECK_ARG(cfg->max_tracks >= 1 && cfg->max_tracks <= 2048, "yk_tracker_create: max_tracks must be in [1, 2048]");
+  YK_CHECK_ARG(cfg->max_dets >= 1 && cfg->max_dets <= 1024, "yk_tracker_create: max_dets must be in [1, 1024]");
+  YK_CHECK_ARG(cfg->max_lost_frames >= 0, "yk_tracker_create: max_lost_frames must be >= 0");
+  const size_t lds = yk::trk::lds_bytes(cfg->max_tracks, cfg->max_dets);
+  YK_CHECK_ARG(lds <= 160 * 1024, "yk_tracker_create: max_tracks x max_dets exceed the 160 KiB LDS budget");
+  yk::DeviceGuard guard(ctx->device);
+  auto* t = new yk_tracker{};
+  t->ctx = ctx;
+  t->S = n_streams;
+  t->cfg = *cfg;
+  t->lds = lds;
+  Dev& g = t->dev;
+  g.T = cfg->max_tracks;
+  g.D = cfg->max_dets;
+  g.C = cfg->max_tracks * cfg->max_dets;
+  g.max_lost = cfg->max_lost_frames;
+  g.min_hits = cfg->min_hits;
+  g.thr = cfg->iou_threshold;
+  const size_t S = n_streams, T = g.T;
+  hipError_t e = hipSuccess;
+  auto A = [&](void** p, size_t bytes) {
+    if (e == hipSuccess) e = hipMalloc(p, bytes);
+  };
+  A((void**)&g.slots, S * T * sizeof(yk::trk::Slot));
+  A((void**)&g.hdr, S * sizeof(yk::trk::Hdr));
+  A((void**)&g.order, S * T * sizeof(int));
+  A((void**)&g.free_stack, S * T * sizeof(int));
+  A((void**)&g.cand_key, S * (size_t)g.C * sizeof(unsigned long long));
+  A((void**)&g.cand_flat, S * (size_t)g.C * sizeof(int));
+  A((void**)&g.rows, S * T * sizeof(yk_track_out));
+  A((void**)&g.counts, S * sizeof(int));
+  A((void**)&g.stats, S * sizeof(yk_tracker_stats));
+  A((void**)&t->d_snap, T * sizeof(yk_track_state));
+  A((void**)&t->d_row1, sizeof(yk_track_out));
+  A((void**)&t->d_box, 16 * sizeof(double));
+  A((void**)&t->d_status, sizeof(int));
+  if (e != hipSuccess) {
+    yk::set_error(std::string("yk_tracker_create: hipMalloc failed: ") + hipGetErrorString(e));
+    yk_tracker_destroy(t);
+    return YK_ERR_HIP;
+  }
+  if (hipFuncSetAttribute((const void*)yk::trk::step_kernel<float>,
+                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess ||
+      hipFuncSetAttribute((const void*)yk::trk::step_kernel<double>,
+                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) {
+    (void)hipGetLastError();
+  }
+  int rc = yk_tracker_reset(t, nullptr);
+  if (rc != YK_OK) {
+    yk_tracker_destroy(t);
+    return rc;
+  }
+  YK_HIP(hipDeviceSynchronize());
+  *out = t;
+  return YK_OK;
+}
+
+int yk_tracker_destroy(yk_tracker* t) {
+  if (!t) return YK_OK;
+  yk::DeviceGuard guard(t->ctx->device);
+  Dev& g = t->dev;
+  void* ptrs[] = {g.slots, g.hdr, g.order, g.free_stack, g.cand_key, g.cand_flat, g.rows,
+                  g.counts, g.stats, t->d_snap, t->d_row1, t->d_box, t->d_status};
+  for (void* p : ptrs)
+    if (p) (void)hipFree(p);
+  delete t;
+  return YK_OK;
+}
+
+int yk_tracker_reset(yk_tracker* t, void* stream) {
+  YK_CHECK_ARG(t, "yk_tracker_reset: NULL tracker");
+  yk::DeviceGuard guard(t->ctx->device);
+  hipLaunchKernelGGL(yk::trk::reset_kernel, dim3(t->S), dim3(256), 0, (hipStream_t)stream, t->dev, t->S);
+  YK_HIP(hipGetLastError());
+  return YK_OK;
+}
+
+int yk_tracker_step(yk_tracker* t, const void* dets, int dtype, int row_stride, const int32_t* counts,
+                    void* stream) {
+  YK_CHECK_ARG(t && dets && counts, "yk_tracker_step: NULL argument");
+  YK_CHECK_ARG(row_stride >= 4, "yk_tracker_step: row_stride must be >= 4");
+  YK_CHECK_ARG(dtype == YK_F32 || dtype == YK_F64, "yk_tracker_step: dtype must be YK_F32 or YK_F64");
+  yk::DeviceGuard guard(t->ctx->device);
+  if (dtype == YK_F32)
+    hipLaunchKernelGGL(yk::trk::step_kernel<float>, dim3(t->S), dim3(yk::trk::NT), t->lds,
+                       (hipStream_t)stream, t->dev, (const float*)dets, row_stride, counts);
+  else
+    hipLaunchKernelGGL(yk::trk::step_kernel<double>, dim3(t->S), dim3(yk::trk::NT), t->lds,
+                       (hipStream_t)stream, t->dev, (const double*)dets, row_stride, counts);
+  YK_HIP(hipGetLastError());
+  return YK_OK;
+}
+
+int yk_tracker_outputs(yk_tracker* t, yk_track_out** rows, int32_t** counts, yk_tracker_stats** stats) {
+  YK_CHECK_ARG(t, "yk_tracker_outputs: NULL tracker");
+  if (rows) *rows = t->dev.rows;
+  if (counts) *counts = t->dev.counts;
+  if (stats) *stats = t->dev.stats;
+  return YK_OK;
+}
+
+int yk_tracker_download(yk_tracker* t, yk_track_out* host_rows, int32_t* host_counts,
+                        yk_tracker_stats* host_stats, void* stream) {
+  YK_CHECK_ARG(t && host_counts, "yk_tracker_download: NULL argument");
+  yk::DeviceGuard guard(t->ctx->device);
+  hipStream_t st = (hipStream_t)stream;
+  YK_HIP(hipMemcpyAsync(host_counts, t->dev.counts, t->S * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+  if (host_stats)
+    YK_HIP(hipMemcpyAsync(host_stats, t->dev.stats, t->S * sizeof(yk_tracker_stats),
+                          hipMemcpyDeviceToHost, st));
+  YK_HIP(hipStreamSynchronize(st));
+  if (host_rows) {
+    const size_t T = t->dev.T;
+    for (int s = 0; s < t->S; ++s) {
+      const int c = host_counts[s];
+      if (c > 0)
+        YK_HIP(hipMemcpyAsync(host_rows + s * T, t->dev.rows + s * T, c * sizeof(yk_track_out),
+                              hipMemcpyDeviceToHost, st));
+    }
+    YK_HIP(hipStreamSynchronize(st));
+  }
+  return YK_OK;
+}
+
+int yk_tracker_snapshot(yk_tracker* t, int s, yk_track_state* host_states, int32_t* n_out, void* stream) {
+  YK_CHECK_ARG(t && host_states && n_out, "yk_tracker_snapshot: NULL argument");
+  YK_CHECK_ARG(s >= 0 && s < t->S, "yk_tracker_snapshot: stream index out of range");
+  yk::DeviceGuard guard(t->ctx->device);
+  hipStream_t st = (hipStream_t)stream;
+  yk::trk::Hdr h;
+  YK_HIP(hipMemcpyAsync(&h, t->dev.hdr + s, sizeof(h), hipMemcpyDeviceToHost, st));
+  YK_HIP(hipStreamSynchronize(st));
+  *n_out = h.n_tracks;
+  if (h.n_tracks > 0) {
+    hipLaunchKernelGGL(yk::trk::snapshot_kernel, dim3((h.n_tracks + 63) / 64), dim3(64), 0, st, t->dev, s,
+                       t->d_snap);
+    YK_HIP(hipGetLastError());
+    YK_HIP(hipMemcpyAsync(host_states, t->d_snap, h.n_tracks * sizeof(yk_track_state),
+                          hipMemcpyDeviceToHost, st));
+    YK_HIP(hipStreamSynchronize(st));
+  }
+  return YK_OK;
+}
+
+int yk_track_op(yk_tracker* t, int s, int pos, int op, int arg, const double* in_box, int dtype, double* out5,
+                yk_track_out* out_row, void* stream) {
+  YK_CHECK_ARG(t, "yk_track_op: NULL tracker");
+  YK_CHECK_ARG(s >= 0 && s < t->S, "yk_track_op: stream index out of range");
+  YK_CHECK_ARG(op >= YK_OP_PREDICT && op <= YK_OP_LOST_PRED, "yk_track_op: unknown op");
+  YK_CHECK_ARG(op != YK_OP_UPDATE || in_box, "yk_track_op: update needs a box");
+  YK_CHECK_ARG(dtype == YK_F32 || dtype == YK_F64, "yk_track_op: bad dtype");
+  yk::DeviceGuard guard(t->ctx->device);
+  hipStream_t st = (hipStream_t)stream;
+  yk::trk::Hdr h;
+  YK_HIP(hipMemcpyAsync(&h, t->dev.hdr + s, sizeof(h), hipMemcpyDeviceToHost, st));
+  YK_HIP(hipStreamSynchronize(st));
+  YK_CHECK_ARG(pos >= 0 && pos < h.n_tracks, "yk_track_op: track position out of range");
+  if (in_box) YK_HIP(hipMemcpyAsync(t->d_box, in_box, 4 * sizeof(double), hipMemcpyHostToDevice, st));
+  if (dtype == YK_F32)
+    hipLaunchKernelGGL(yk::trk::track_op_kernel<float>, dim3(1), dim3(64), 0, st, t->dev, s, pos, op, arg,
+                       t->d_box, t->d_box + 4, t->d_row1);
+  else
+    hipLaunchKernelGGL(yk::trk::track_op_kernel<double>, dim3(1), dim3(64), 0, st, t->dev, s, pos, op, arg,
+                       t->d_box, t->d_box + 4, t->d_row1);
+  YK_HIP(hipGetLastError());
+  if (out5) YK_HIP(hipMemcpyAsync(out5, t->d_box + 4, 5 * sizeof(double), hipMemcpyDeviceToHost, st));
+  if (out_row) YK_HIP(hipMemcpyAsync(out_row, t->d_row1, sizeof(yk_track_out), hipMemcpyDeviceToHost, st));
+  YK_HIP(hipStreamSynchronize(st));
+  return YK_OK;
+}
+
+int yk_track_create(yk_tracker* t, int s, const double* box, int dtype, int32_t track_num, int32_t max_lost,
+                    void* stream) {
+  YK_CHECK_ARG(t && box, "yk_track_create: NULL argument");
+  YK_CHECK_ARG(s >= 0 && s < t->S, "yk_track_create: stream index out of range");
+  YK_CHECK_ARG(dtype == YK_F32 || dtype == YK_F64, "yk_track_create: bad dtype");
+  yk::DeviceGuard guard(t->ctx->device);
+  hipStream_t st = (hipStream_t)stream;
+  YK_HIP(hipMemcpyAsync(t->d_box, box, 4 * sizeof(double), hipMemcpyHostToDevice, st));
+  if (dtype == YK_F32)
+    hipLaunchKernelGGL(yk::trk::track_create_kernel<float>, dim3(1), dim3(64), 0, st, t->dev, s, t->d_box,
+                       track_num, max_lost, t->d_status);
+  else
+    hipLaunchKernelGGL(yk::trk::track_create_kernel<double>, dim3(1), dim3(64), 0, st, t->dev, s, t->d_box,
+                       track_num, max_lost, t->d_status);
+  YK_HIP(hipGetLastError());
+  int status = 0;
+  YK_HIP(hipMemcpyAsync(&status, t->d_status, sizeof(int), hipMemcpyDeviceToHost, st));
+  YK_HIP(hipStreamSynchronize(st));
+  if (status != 0) {
+    yk::set_error("yk_track_create: stream is at max_tracks capacity");
+    return YK_ERR_CAPACITY;
+  }
+  return YK_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,417 @@
+"""Device-backed mirror of the reference ``kalman`` package.
+
+Reference surface (kalman/__init__.py:28-33):
+  EnhancedMultiTargetTracker(max_lost_frames=450, min_hits=3, iou_threshold=0.3)
+      .update(detections) -> list[dict]           enhanced_multi_target_tracker.py:42-132
+      .get_statistics(), .stats, .trackers, .frame_count, .next_track_id
+  AircraftKalmanTracker / EnhancedAircraftKalmanTracker(initial_bbox, track_id=None,
+      max_lost_frames=450)                         enhanced_aircraft_kalman_tracker.py:7-408
+  MultiTargetTracker = EnhancedMultiTargetTracker
+
+All filter arithmetic, association and lifecycle run in libyk.so's HIP kernels
+(csrc/tracker.hip); this module only marshals detections in and dicts out.
+``MultiStreamTracker`` is the batched, device-resident fast path (one launch steps
+every stream) that the benchmark and the detector pipeline use.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import uuid
+from collections import deque
+
+import numpy as np
+import torch
+
+from . import _lib as L
+
+_STATUS = ("detected", "predicted")
+
+
+def _det_array(detections):
+    """Detections -> (array[D, 4], yk dtype).  np.float32 inputs (what the reference driver
+    passes, aircraft_detection_tracking.py:101-106) keep float32 semantics; python floats /
+    float64 arrays keep float64 semantics, exactly as the reference's arithmetic would."""
+    if isinstance(detections, torch.Tensor):
+        detections = detections.detach().cpu().numpy()
+    if isinstance(detections, np.ndarray):
+        a = detections
+        if a.size == 0:
+            return np.zeros((0, 4), np.float32), L.YK_F32
+        if a.ndim != 2 or a.shape[1] < 4:
+            raise ValueError(f"detections must be (N, >=4), got {a.shape}")
+        if a.dtype == np.float32:
+            return np.ascontiguousarray(a[:, :4]), L.YK_F32
+        return np.ascontiguousarray(a[:, :4], dtype=np.float64), L.YK_F64
+    dets = list(detections)
+    if not dets:
+        return np.zeros((0, 4), np.float32), L.YK_F32
+    first = dets[0][0]
+    if isinstance(first, np.float32) or (isinstance(first, np.ndarray) and first.dtype == np.float32):
+        return np.array([[d[0], d[1], d[2], d[3]] for d in dets], dtype=np.float32), L.YK_F32
+    return np.array([[d[0], d[1], d[2], d[3]] for d in dets], dtype=np.float64), L.YK_F64
+
+
+def _row_to_dict(r, track_id: str) -> dict:
+    """One yk_track_out row -> the reference get_track_info() dict
+    (enhanced_aircraft_kalman_tracker.py:366-383)."""
+    tsu = int(r["time_since_update"])
+    n = int(r["traj_len"])
+    tr = r["traj"][:n]
+    return {
+        "track_id": track_id,
+        "bbox": np.array(r["bbox"], dtype=np.float64),
+        "confidence": float(r["confidence"]),
+        "status": _STATUS[int(r["status"])],
+        "age": int(r["age"]),
+        "hits": int(r["hits"]),
+        "hit_streak": int(r["hit_streak"]),
+        "time_since_update": tsu,
+        "lost_frames": tsu,
+        "is_lost": tsu > 0,
+        "trajectory": [(float(a), float(b)) for a, b in tr],
+        "velocity": np.array(r["velocity"], dtype=np.float64),
+        "motion_confidence": float(r["motion_confidence"]),
+        "is_stable_motion": bool(r["is_stable_motion"]),
+        "speed": float(r["speed"]),
+        "direction": float(r["direction"]),
+    }
+
+
+def track_id_of(num: int) -> str:
+    return f"T{int(num):03d}"
+
+
+class MultiStreamTracker:
+    """``n_streams`` independent EnhancedMultiTargetTracker instances stepped by one
+    kernel launch (one workgroup per stream).  Detections and results stay in HBM."""
+
+    def __init__(self, n_streams: int = 1, max_lost_frames: int = 450, min_hits: int = 3,
+                 iou_threshold: float = 0.3, max_tracks: int = 1024, max_dets: int = 1024,
+                 device: int = 0):
+        self.n_streams, self.device = int(n_streams), int(device)
+        self.max_lost_frames, self.min_hits, self.iou_threshold = int(max_lost_frames), int(min_hits), float(iou_threshold)
+        self.max_tracks, self.max_dets = int(max_tracks), int(max_dets)
+        ctx = L.context(self.device)
+        cfg = L.TrackerCfg(self.max_lost_frames, self.min_hits, self.iou_threshold, self.max_tracks, self.max_dets)
+        h = C.c_void_p()
+        L.check(L.lib().yk_tracker_create(ctx, self.n_streams, C.byref(cfg), C.byref(h)), "yk_tracker_create")
+        self._h = h
+        S, T = self.n_streams, self.max_tracks
+        self.host_rows = np.zeros((S, T), dtype=L.TRACK_OUT_DTYPE)
+        self.host_counts = np.zeros(S, dtype=np.int32)
+        self.host_stats = np.zeros(S, dtype=L.STATS_DTYPE)
+        dev = torch.device("cuda", self.device)
+        self._dets = {L.YK_F32: torch.zeros((S, self.max_dets, 4), dtype=torch.float32, device=dev),
+                      L.YK_F64: torch.zeros((S, self.max_dets, 4), dtype=torch.float64, device=dev)}
+        self._counts = torch.zeros(S, dtype=torch.int32, device=dev)
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and L._lib is not None:
+            L.lib().yk_tracker_destroy(h)
+            self._h = None
+
+    @property
+    def handle(self) -> C.c_void_p:
+        return self._h
+
+    def reset(self):
+        L.check(L.lib().yk_tracker_reset(self._h, L.current_stream(self.device)), "yk_tracker_reset")
+
+    def step_device(self, dets: torch.Tensor, counts: torch.Tensor, stream=None):
+        """dets: device tensor [S, max_dets, stride] (float32 or float64); counts: int32 [S]."""
+        if dets.dim() != 3 or dets.shape[0] != self.n_streams or dets.shape[1] != self.max_dets or dets.shape[2] < 4:
+            raise ValueError(f"dets must be [{self.n_streams}, {self.max_dets}, >=4], got {tuple(dets.shape)}")
+        if not dets.is_contiguous() or not counts.is_contiguous() or counts.dtype != torch.int32:
+            raise ValueError("dets / counts must be contiguous; counts int32")
+        dt = {torch.float32: L.YK_F32, torch.float64: L.YK_F64}.get(dets.dtype)
+        if dt is None:
+            raise ValueError("dets dtype must be float32 or float64")
+        st = L.current_stream(self.device) if stream is None else C.c_void_p(stream)
+        L.check(L.lib().yk_tracker_step(self._h, L.ptr(dets), dt, int(dets.shape[2]), L.ptr(counts), st),
+                "yk_tracker_step")
+
+    def step_host(self, per_stream_dets):
+        """Host detections (one list/array per stream) -> step.  Returns nothing; call download()."""
+        arrs = [_det_array(d) for d in per_stream_dets]
+        if len(arrs) != self.n_streams:
+            raise ValueError("need one detection list per stream")
+        dts = {a[1] for a in arrs if len(a[0])}
+        dt = dts.pop() if len(dts) == 1 else (L.YK_F64 if dts else L.YK_F32)
+        buf = self._dets[dt]
+        npdt = np.float32 if dt == L.YK_F32 else np.float64
+        host = np.zeros((self.n_streams, self.max_dets, 4), npdt)
+        cnt = np.zeros(self.n_streams, np.int32)
+        for s, (a, _) in enumerate(arrs):
+            if len(a) > self.max_dets:
+                raise L.YKError(f"{len(a)} detections exceed max_dets={self.max_dets}")
+            host[s, :len(a)] = a
+            cnt[s] = len(a)
+        buf.copy_(torch.from_numpy(host))
+        self._counts.copy_(torch.from_numpy(cnt))
+        self.step_device(buf, self._counts)
+
+    def download(self):
+        st = L.current_stream(self.device)
+        L.check(L.lib().yk_tracker_download(self._h, L.ptr(self.host_rows), L.ptr(self.host_counts),
+                                            L.ptr(self.host_stats), st), "yk_tracker_download")
+        return self.host_rows, self.host_counts, self.host_stats
+
+    def device_outputs(self):
+        rows, counts, stats = C.c_void_p(), C.c_void_p(), C.c_void_p()
+        L.check(L.lib().yk_tracker_outputs(self._h, C.byref(rows), C.byref(counts), C.byref(stats)),
+                "yk_tracker_outputs")
+        return rows.value, counts.value, stats.value
+
+    def snapshot(self, stream_index: int = 0) -> np.ndarray:
+        out = np.zeros(self.max_tracks, dtype=L.TRACK_STATE_DTYPE)
+        n = C.c_int32()
+        L.check(L.lib().yk_tracker_snapshot(self._h, int(stream_index), L.ptr(out), C.byref(n),
+                                            L.current_stream(self.device)), "yk_tracker_snapshot")
+        return out[: n.value].copy()
+
+    def track_op(self, stream_index, pos, op, arg=0, box=None, dtype=L.YK_F64):
+        inb = None if box is None else np.ascontiguousarray(np.asarray(box, dtype=np.float64)[:4])
+        out5 = np.zeros(5, np.float64)
+        row = np.zeros(1, dtype=L.TRACK_OUT_DTYPE)
+        L.check(L.lib().yk_track_op(self._h, int(stream_index), int(pos), int(op), int(arg), L.ptr(inb), int(dtype),
+                                    L.ptr(out5), L.ptr(row), L.current_stream(self.device)), "yk_track_op")
+        return out5, row[0]
+
+    def create_track(self, stream_index, box, dtype, track_num, max_lost_frames):
+        b = np.ascontiguousarray(np.asarray(box, dtype=np.float64)[:4])
+        L.check(L.lib().yk_track_create(self._h, int(stream_index), L.ptr(b), int(dtype), int(track_num),
+                                        int(max_lost_frames), L.current_stream(self.device)), "yk_track_create")
+
+
+def _box_dtype(bbox):
+    a, _ = _det_array([list(bbox)[:4]])
+    return a[0], (L.YK_F32 if a.dtype == np.float32 else L.YK_F64)
+
+
+_F = np.eye(8)
+for _i in range(4):
+    _F[_i, _i + 4] = 1.0
+_H = np.hstack([np.eye(4), np.zeros((4, 4))])
+_Q = np.diag([0.1, 0.1, 0.01, 0.01, 0.1, 0.1, 0.001, 0.001])
+_R = np.eye(4) * 10.0
+
+
+class AircraftKalmanTracker:
+    """One track (enhanced_aircraft_kalman_tracker.py:7-408) whose state lives in HBM.
+
+    Constructed directly it owns a private one-track device tracker; obtained from
+    ``EnhancedMultiTargetTracker.trackers`` it is a live view of that tracker's track.
+    Every filter operation runs on the GPU (``yk_track_op``)."""
+
+    state_dim, measure_dim = 8, 4
+    F, H, Q, R = _F, _H, _Q, _R
+
+    def __init__(self, initial_bbox, track_id=None, max_lost_frames=450, *, device: int = 0):
+        self.track_id = track_id or str(uuid.uuid4())[:8]
+        self.max_lost_frames = int(max_lost_frames)
+        self._owner = MultiStreamTracker(1, max_lost_frames=self.max_lost_frames, min_hits=1, iou_threshold=0.3,
+                                         max_tracks=1, max_dets=1, device=device)
+        box, dt = _box_dtype(initial_bbox)
+        self._dtype = dt
+        self._owner.create_track(0, box, dt, -1, self.max_lost_frames)
+        self._num = None  # standalone: always list position 0
+        self._multi = None
+
+    @classmethod
+    def _view(cls, multi: "EnhancedMultiTargetTracker", num: int):
+        self = cls.__new__(cls)
+        self.track_id = track_id_of(num)
+        self.max_lost_frames = multi.max_lost_frames
+        self._owner = multi._core
+        self._dtype = L.YK_F32
+        self._num = int(num)
+        self._multi = multi
+        return self
+
+    # -- location / state ------------------------------------------------------
+    def _pos(self) -> int:
+        if self._num is None:
+            return 0
+        snap = self._multi._snapshot()
+        idx = np.nonzero(snap["track_num"] == self._num)[0]
+        if len(idx) == 0:
+            raise L.YKError(f"track {self.track_id} is no longer live")
+        return int(idx[0])
+
+    def _state(self):
+        snap = self._owner.snapshot(0) if self._num is None else self._multi._snapshot()
+        return snap[self._pos()]
+
+    def _touch(self):
+        if self._multi is not None:
+            self._multi._snap = None
+
+    @property
+    def x(self):
+        return self._state()["x"].copy()
+
+    @property
+    def P(self):
+        return self._state()["P"].copy()
+
+    def _int(name):  # noqa: N805
+        return property(lambda self: int(self._state()[name]))
+
+    age = _int("age")
+    hits = _int("hits")
+    hit_streak = _int("hit_streak")
+    time_since_update = _int("time_since_update")
+    lost_frames = _int("lost_frames")
+    del _int
+
+    @property
+    def is_lost(self):
+        return bool(self._state()["is_lost"])
+
+    @property
+    def velocity_history(self):
+        s = self._state()
+        return deque([s["vel_hist"][i].copy() for i in range(int(s["vel_len"]))], maxlen=50)
+
+    @property
+    def trajectory_history(self):
+        s = self._state()
+        return deque([tuple(map(float, s["traj_hist"][i])) for i in range(int(s["traj_len"]))], maxlen=150)
+
+    @property
+    def motion_analysis(self):
+        s = self._state()
+        return {"velocity_avg": s["velocity_avg"].copy(), "velocity_std": s["velocity_std"].copy(),
+                "direction": float(s["direction"]), "speed": float(s["speed"]),
+                "stability_score": float(s["stability_score"]),
+                "prediction_confidence": float(s["prediction_confidence"])}
+
+    # -- pure helpers (kf.py:103-135) -------------------------------------------
+    @staticmethod
+    def bbox_to_state(bbox):
+        x1, y1, x2, y2 = bbox
+        return np.array([(x1 + x2) / 2.0, (y1 + y2) / 2.0, x2 - x1, y2 - y1])
+
+    @staticmethod
+    def state_to_bbox(state):
+        cx, cy, w, h = state[:4]
+        return np.array([cx - w / 2.0, cy - h / 2.0, cx + w / 2.0, cy + h / 2.0])
+
+    # -- filter operations (all on the device) ---------------------------------
+    def predict(self):
+        out, _ = self._owner.track_op(0, self._pos(), L.OP_PREDICT)
+        self._touch()
+        return out[:4].copy()
+
+    def update(self, bbox):
+        box, dt = _box_dtype(bbox)
+        self._owner.track_op(0, self._pos(), L.OP_UPDATE, box=box, dtype=dt)
+        self._touch()
+
+    def mark_as_lost(self):
+        self._owner.track_op(0, self._pos(), L.OP_MARK_LOST)
+        self._touch()
+
+    def analyze_motion_pattern(self):
+        """The device recomputes the motion statistics inside every update(); the history
+        cannot change in between, so an explicit call has nothing left to do."""
+
+    def enhanced_long_term_predict(self, frames_ahead=1):
+        out, _ = self._owner.track_op(0, self._pos(), L.OP_LONG_TERM, arg=int(frames_ahead))
+        self._touch()
+        return out[:4].copy(), float(out[4])
+
+    def get_lost_prediction(self):
+        out, _ = self._owner.track_op(0, self._pos(), L.OP_LOST_PRED)
+        self._touch()
+        return out[:4].copy(), float(out[4])
+
+    def get_track_info(self):
+        _, row = self._owner.track_op(0, self._pos(), L.OP_INFO)
+        self._touch()
+        return _row_to_dict(row, self.track_id)
+
+    def should_delete(self, max_lost_frames):
+        s = self._state()
+        tsu, age, hs = int(s["time_since_update"]), int(s["age"]), int(s["hit_streak"])
+        if tsu > max_lost_frames:
+            return True
+        if age < 5 and hs == 0 and tsu > 15:
+            return True
+        return age < 10 and hs <= 1 and tsu > 30
+
+
+EnhancedAircraftKalmanTracker = AircraftKalmanTracker
+
+
+class EnhancedMultiTargetTracker:
+    """Drop-in for kalman.EnhancedMultiTargetTracker (enhanced_multi_target_tracker.py:4-304),
+    one stream, executed by the batched HIP tracker kernel."""
+
+    def __init__(self, max_lost_frames=450, min_hits=3, iou_threshold=0.3, *, max_tracks: int = 1024,
+                 max_dets: int = 1024, device: int = 0, verbose: bool = False):
+        self.max_lost_frames, self.min_hits, self.iou_threshold = max_lost_frames, min_hits, iou_threshold
+        self.verbose = verbose
+        self._core = MultiStreamTracker(1, max_lost_frames, min_hits, iou_threshold, max_tracks, max_dets, device)
+        self._stats = np.zeros(1, dtype=L.STATS_DTYPE)[0]
+        self._stats["next_track_id"] = 1
+        self._snap = None
+        if verbose:
+            print(f"增强版多目标跟踪器初始化完成 - 最大丢失容忍: {max_lost_frames}帧 ({max_lost_frames/30:.1f}秒)")
+
+    @property
+    def frame_count(self) -> int:
+        return int(self._stats["frame_count"])
+
+    @property
+    def next_track_id(self) -> int:
+        return int(self._stats["next_track_id"])
+
+    @property
+    def stats(self) -> dict:
+        s = self._stats
+        return {k: int(s[k]) for k in ("total_tracks_created", "total_tracks_terminated", "current_active_tracks",
+                                        "long_term_predictions", "successful_recoveries")}
+
+    def _snapshot(self):
+        if self._snap is None:
+            self._snap = self._core.snapshot(0)
+        return self._snap
+
+    @property
+    def trackers(self) -> list:
+        return [AircraftKalmanTracker._view(self, int(n)) for n in self._snapshot()["track_num"]]
+
+    def update(self, detections):
+        """One frame: list of [x1, y1, x2, y2, conf] -> list of track dicts."""
+        self._core.step_host([detections])
+        rows, counts, stats = self._core.download()
+        self._stats = stats[0].copy()
+        self._snap = None
+        if int(self._stats["overflow"]):
+            raise L.YKError(f"tracker capacity exceeded (max_tracks={self._core.max_tracks})")
+        out = [_row_to_dict(r, track_id_of(r["track_num"])) for r in rows[0, : int(counts[0])]]
+        if self.verbose and self.frame_count % 100 == 0:
+            self._print_statistics()
+        return out
+
+    def _print_statistics(self):
+        s = self.stats
+        print(f"\n=== 跟踪统计 (帧 {self.frame_count}) ===")
+        print(f"当前活跃轨迹: {s['current_active_tracks']}")
+        print(f"总创建轨迹: {s['total_tracks_created']}")
+        print(f"总终止轨迹: {s['total_tracks_terminated']}")
+        print(f"成功恢复次数: {s['successful_recoveries']}")
+        print(f"长期预测次数: {s['long_term_predictions']}")
+
+    def get_statistics(self):
+        snap = self._snapshot()
+        return {**self.stats, "frame_count": self.frame_count,
+                "tracker_details": [{"track_id": track_id_of(t["track_num"]), "age": int(t["age"]),
+                                     "hits": int(t["hits"]), "lost_frames": int(t["lost_frames"]),
+                                     "is_lost": bool(t["is_lost"]),
+                                     "confidence": float(t["prediction_confidence"])} for t in snap]}
+
+
+MultiTargetTracker = EnhancedMultiTargetTracker
