@@ -161,13 +161,102 @@ int yk_track_op(yk_tracker* trk, int stream_index, int pos, int op, int arg, con
                 int dtype, double* host_out5, yk_track_out* host_row_out, void* stream);
 
 /* sizeof() of the ABI structs, for bindings that mirror them (0: yk_tracker_cfg,
- * 1: yk_tracker_stats, 2: yk_track_out, 3: yk_track_state); -1 for an unknown id. */
+ * 1: yk_tracker_stats, 2: yk_track_out, 3: yk_track_state, 4: yk_view, 5: yk_op,
+ * 6: yk_model_desc); -1 for an unknown id. */
 int64_t yk_struct_size(int which);
 
 /* Append a new track created from a box (AircraftKalmanTracker.__init__, :23-101) to the
  * end of stream `stream_index`'s list, with the given track number. Synchronous. */
 int yk_track_create(yk_tracker* trk, int stream_index, const double* host_bbox, int dtype,
                     int32_t track_num, int32_t max_lost_frames, void* stream);
+
+
+/* ------------------------------------------------------------------ detector
+ * Replaces YOLO.predict() for the detection models this path uses
+ * (ultralytics/engine/model.py:498-557 -> engine/predictor.py:152-387): LetterBox +
+ * BGR->RGB + /255, the conv graph (nn/tasks.py:159-188), Detect decode (nn/modules/head.py
+ * :116-187), non_max_suppression + TorchNMS.nms (utils/nms.py:13-304) and scale/clip
+ * (utils/ops.py:105-184).  The host builds the program (parse_model rules + weight
+ * packing, see arch.py / model.py); the library executes it.
+ */
+enum yk_act_dtype { YK_ACT_BF16 = 0, YK_ACT_F32 = 1 };
+enum yk_op_kind {
+  YK_K_CONV_INPUT = 0, /* first conv, reads uint8 BGR frames (fused letterbox/RGB//255)    */
+  YK_K_CONV = 1,       /* implicit-GEMM conv (+bias, SiLU, residual, concat/upsample read)   */
+  YK_K_SPPF_POOL = 2,  /* SPPF's three chained 5x5 max-pools, written as concat slices     */
+  YK_K_DETECT = 3      /* Detect level: box/cls 1x1 + DFL + dist2bbox + sigmoid + threshold  */
+};
+
+typedef struct {
+  int32_t buf;      /* activation buffer index                                  */
+  int32_t c_off;    /* first channel of the view inside a pixel                 */
+  int32_t c_stride; /* channels per pixel of the buffer                         */
+  int32_t h, w;     /* stored spatial size                                      */
+  int32_t up;       /* log2 nearest-upsample factor applied on read (0 or 1)    */
+} yk_view;
+
+typedef struct {
+  int32_t kind;
+  int32_t ksize, stride, act; /* act: 0 none, 1 SiLU                                   */
+  int32_t n_src;
+  yk_view src[2];
+  int32_t src_ch[2];          /* physical channels of each source (multiples of 8)     */
+  yk_view dst;
+  int32_t cout;               /* physical output channels written                      */
+  int32_t has_res;
+  yk_view res;                /* residual added after the activation (Bottleneck add)  */
+  int32_t out_h, out_w;
+  int32_t k_steps, n_tiles;   /* packed weights: [n_tiles][k_steps][64 lanes][16 B]    */
+  int64_t w_off, b_off, t_off;/* blob offsets: packed weights, f32 bias, int32 K-chunk table */
+  /* YK_K_DETECT */
+  int32_t det_stride;         /* level stride in input pixels                           */
+  int32_t det_anchor_off;     /* index of this level's first anchor                     */
+  int32_t det_cls_off;        /* channel offset of the class features in src[0]         */
+  int32_t det_cls_ch;         /* class feature channels (physical)                      */
+  int64_t det_wc_off;         /* f32 [det_cls_ch] class 1x1 weights, then f32 bias      */
+} yk_op;
+
+typedef struct {
+  int32_t act_dtype;          /* yk_act_dtype                                           */
+  int32_t max_batch;
+  int32_t frame_h, frame_w;   /* original frame size, uint8 BGR HWC                      */
+  int32_t in_h, in_w;         /* letterboxed network input size                          */
+  int32_t pad_top, pad_left;  /* frame placement inside the input (LetterBox centring)  */
+  int32_t n_anchors, nc, max_det;
+  int32_t n_bufs;
+  const int64_t* buf_elems;   /* per-image element count of each activation buffer       */
+  int32_t n_ops;
+  const yk_op* ops;
+} yk_model_desc;
+
+int yk_model_create(yk_ctx* ctx, const yk_model_desc* desc, const void* host_blob, int64_t blob_bytes,
+                    yk_model** out);
+int yk_model_destroy(yk_model* m);
+
+/* One predict() over `batch` frames resident in HBM (dev_frames: batch x frame_h x frame_w x 3
+ * uint8 BGR).  Writes dev_dets[batch][max_det][6] = x1,y1,x2,y2,conf,cls (original-image pixels,
+ * like Results.boxes.data) and dev_counts[batch].  NULL outputs use the model's own buffers
+ * (yk_model_outputs).  conf/iou as in non_max_suppression (asserted in [0,1]). */
+int yk_detect(yk_model* m, const uint8_t* dev_frames, int batch, float conf, float iou, int max_det,
+              float* dev_dets, int32_t* dev_counts, void* stream);
+
+/* Capture yk_detect for a fixed (batch, conf, iou, max_det, frames, outputs) into a hipGraph
+ * and replay it: one graph launch per call (created on first use, cached per batch). */
+int yk_detect_graph(yk_model* m, const uint8_t* dev_frames, int batch, float conf, float iou, int max_det,
+                    float* dev_dets, int32_t* dev_counts, void* stream);
+
+int yk_model_outputs(yk_model* m, float** dev_dets, int32_t** dev_counts);
+
+/* Pre-NMS candidates of the last yk_detect: [max_batch][n_anchors] rows of
+ * {x1, y1, x2, y2, score, anchor_index (int32 bits)} in network-input pixels, unordered,
+ * counts per image (parity harnesses compare them to the oracle's Detect output). */
+int yk_model_candidates(yk_model* m, float** dev_cand, int32_t** dev_counts);
+
+/* Device pointer of activation buffer `buf` (debug / parity). */
+int yk_model_buffer(yk_model* m, int buf, void** dev_ptr);
+
+/* Synchronous device -> host copy (bindings without their own HIP runtime access). */
+int yk_memcpy_d2h(void* host_dst, const void* dev_src, int64_t bytes);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,150 @@
+"""GPU parity of the detector (libyk.so csrc/detector.hip) against the torch-CPU oracle
+(oracle/detector_ref.py) on synthetic 640x512 frames with seeded weights.
+
+fp32 build: the MFMA path is exact f32 (a different summation order than ATen), so
+activations agree to ~1e-5 relative and boxes/scores of the candidates and of the final
+detections to 1e-4 (the north-star float tolerance).  bf16 build (the production dtype):
+the detection sets must agree in size (+-15%) and 90% of the oracle's boxes must have a
+GPU box with IoU > 0.5 (bf16 rounding can move a cluster's top score to a neighbouring
+anchor 4 px away, IoU ~0.7 at the planted 96 px box size)."""
+import importlib
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import pkg
+from oracle import detector_ref as D
+
+pytestmark = pytest.mark.gpu
+
+
+def _mods():
+    P = pkg()
+    return P, importlib.import_module(P.__name__ + ".arch"), importlib.import_module(P.__name__ + ".weights"), \
+        importlib.import_module(P.__name__ + ".model")
+
+
+def layer_list(ar):
+    out = []
+    for Ly in ar.layers:
+        a = dict(Ly.args)
+        if Ly.kind == "C2f":
+            a["c"] = int(Ly.c2 * 0.5)
+        out.append((Ly.i, Ly.f, Ly.kind, a))
+    return out
+
+
+_CACHE = {}
+
+
+def setup(scale="s", dtype="fp32", B=2, frame_hw=(512, 640), seed=0, K=24):
+    key = (scale, dtype, B, frame_hw, seed, K)
+    if key in _CACHE:
+        return _CACHE[key]
+    P, A, W, M = _mods()
+    ar = A.parse_arch(A.load_model_dict(f"yolov8{scale}-small.yaml"))
+    sd = W.synthetic_state_dict(ar, seed)
+    ref = D.RefDetector(layer_list(ar), sd, A.detect_strides(ar))
+    sc = P.synth.Scene(seed=seed, n_targets=K, n_frames=B + 2, height=frame_hw[0], width=frame_hw[1])
+    frames = [sc.frame(t) for t in range(B)]
+    prog = M.Program(ar, sd, frame_hw[0], frame_hw[1], 640, B, dtype)
+    dm = M.DeviceModel(prog)
+    ft = torch.from_numpy(np.stack(frames)).cuda()
+    dets, counts = dm.detect(ft, 0.25, 0.7, 300)
+    torch.cuda.synchronize()
+    torch.set_num_threads(8)
+    im = D.preprocess(frames, 640)
+    y, _ = ref.forward(im, keep_all=True)
+    res = D.non_max_suppression(y, 0.25, 0.7, 300)
+    res = [D.scale_clip(p, im.shape[2:], frames[0].shape[:2]) for p in res]
+    out = dict(P=P, M=M, ar=ar, ref=ref, dm=dm, dets=dets.cpu(), counts=counts.cpu(), y=y, res=res, B=B)
+    _CACHE[key] = out
+    return out
+
+
+def rel_err(a, b):
+    a, b = torch.as_tensor(a, dtype=torch.float64), torch.as_tensor(b, dtype=torch.float64)
+    return float((a - b).abs().max() / max(float(b.abs().max()), 1e-30))
+
+
+@pytest.mark.parametrize("layer", [0, 1, 2, 4, 8, 9, 12, 15, 18, 21, 24])
+def test_fp32_layer_activations(layer):
+    s = setup()
+    ours = s["dm"].layer_nchw(layer, s["B"])
+    ref = s["ref"].outputs[layer]
+    assert ours.shape == ref.shape
+    assert rel_err(ours, ref) < 1e-4, rel_err(ours, ref)
+
+
+def _cand_map(cand, cnt, b):
+    c = cand[b, : cnt[b]]
+    idx = c[:, 5].view(np.int32)
+    return {int(i): row for i, row in zip(idx, c)}
+
+
+def test_fp32_candidates_match_detect_output():
+    s = setup()
+    cand, cnt = s["dm"].candidates(s["B"])
+    y = s["y"]
+    for b in range(s["B"]):
+        ours = _cand_map(cand, cnt, b)
+        sc = y[b, 4]
+        want = set(torch.nonzero(sc > 0.25).flatten().tolist())
+        near = set(torch.nonzero((sc - 0.25).abs() < 1e-5).flatten().tolist())
+        assert set(ours) ^ want <= near
+        assert len(want) > 0
+        box = y[b, :4].T
+        xyxy = torch.cat((box[:, :2] - box[:, 2:] / 2, box[:, :2] + box[:, 2:] / 2), 1)
+        for a in sorted(want & set(ours)):
+            r = ours[a]
+            np.testing.assert_allclose(r[:4], xyxy[a].numpy(), rtol=1e-4, atol=1e-3)
+            np.testing.assert_allclose(r[4], float(sc[a]), rtol=1e-4, atol=1e-6)
+
+
+def test_fp32_final_detections_match_oracle():
+    s = setup()
+    for b in range(s["B"]):
+        ref = s["res"][b]
+        n = int(s["counts"][b])
+        assert n == len(ref)
+        ours = s["dets"][b, :n]
+        np.testing.assert_allclose(ours[:, :4].numpy(), ref[:, :4].numpy(), rtol=1e-4, atol=1e-3)
+        np.testing.assert_allclose(ours[:, 4].numpy(), ref[:, 4].numpy(), rtol=1e-4, atol=1e-6)
+        assert torch.all(ours[:, 5] == ref[:, 5])
+
+
+def _box_iou(a, b):
+    lt = torch.maximum(a[:, None, :2], b[None, :, :2])
+    rb = torch.minimum(a[:, None, 2:4], b[None, :, 2:4])
+    wh = (rb - lt).clamp(min=0)
+    inter = wh[..., 0] * wh[..., 1]
+    aa = (a[:, 2] - a[:, 0]) * (a[:, 3] - a[:, 1])
+    ab = (b[:, 2] - b[:, 0]) * (b[:, 3] - b[:, 1])
+    return inter / (aa[:, None] + ab[None] - inter)
+
+
+@pytest.mark.parametrize("scale", ["s", "n"])
+def test_bf16_detections_close_to_oracle(scale):
+    s = setup(scale=scale, dtype="bf16")
+    for b in range(s["B"]):
+        ref = s["res"][b]
+        n = int(s["counts"][b])
+        ours = s["dets"][b, :n]
+        assert abs(n - len(ref)) <= max(2, int(0.15 * len(ref)))
+        if len(ref) == 0:
+            continue
+        iou = _box_iou(ref[:, :4], ours[:, :4])
+        best = iou.max(1).values
+        assert float((best > 0.5).float().mean()) >= 0.9
+
+
+def test_fp32_scale_n_and_padded_frame():
+    """LetterBox padding path: a 640x500 frame is centred with 6 rows of 114 top and bottom."""
+    s = setup(scale="n", dtype="fp32", frame_hw=(500, 640), K=12)
+    assert s["dm"].prog.pad_top == 6 and s["dm"].prog.in_h == 512
+    for b in range(s["B"]):
+        ref = s["res"][b]
+        n = int(s["counts"][b])
+        assert n == len(ref)
+        np.testing.assert_allclose(s["dets"][b, :n, :5].numpy(), ref[:, :5].numpy(), rtol=1e-4, atol=1e-3)

@@ -70,6 +70,14 @@ _SIGS = {
     "yk_tracker_snapshot": ([_vp, C.c_int, _vp, C.POINTER(_i32), _vp], C.c_int),
     "yk_track_op": ([_vp, C.c_int, C.c_int, C.c_int, C.c_int, _vp, C.c_int, _vp, _vp, _vp], C.c_int),
     "yk_track_create": ([_vp, C.c_int, _vp, C.c_int, _i32, _i32, _vp], C.c_int),
+    "yk_model_create": ([_vp, _vp, _vp, C.c_int64, C.POINTER(_vp)], C.c_int),
+    "yk_model_destroy": ([_vp], C.c_int),
+    "yk_detect": ([_vp, _vp, C.c_int, C.c_float, C.c_float, C.c_int, _vp, _vp, _vp], C.c_int),
+    "yk_detect_graph": ([_vp, _vp, C.c_int, C.c_float, C.c_float, C.c_int, _vp, _vp, _vp], C.c_int),
+    "yk_model_outputs": ([_vp, C.POINTER(_vp), C.POINTER(_vp)], C.c_int),
+    "yk_model_candidates": ([_vp, C.POINTER(_vp), C.POINTER(_vp)], C.c_int),
+    "yk_model_buffer": ([_vp, C.c_int, C.POINTER(_vp)], C.c_int),
+    "yk_memcpy_d2h": ([_vp, _vp, C.c_int64], C.c_int),
 }
 
 _lock = threading.Lock()

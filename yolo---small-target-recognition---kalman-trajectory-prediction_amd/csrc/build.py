@@ -30,6 +30,7 @@ ARCH = os.environ.get("YK_OFFLOAD_ARCH", "gfx950")
 SOURCES = [
     ("yk_capi.cpp", []),
     ("tracker.hip", ["-ffp-contract=off"]),
+    ("detector.hip", []),
 ]
 HEADERS = ["yk_internal.h", os.path.join("..", "..", "include", "yk.h")]
 

@@ -1,0 +1,892 @@
+// YOLOv8-small+P2 detector for gfx950 (MI355X): the predict() hot path as HIP kernels.
+//
+//   conv_input_kernel  first conv straight from uint8 BGR frames: LetterBox padding, BGR->RGB
+//                      and /255 fused into the gather (engine/predictor.py:152-204,
+//                      data/augment.py:1667-1744); f32 VALU (K = 27, 0.6% of the FLOPs)
+//   conv_igemm_kernel  every other conv (nn/modules/conv.py:39-93, block.py C2f/Bottleneck/SPPF)
+//                      as an implicit GEMM on MFMA: bf16 16x16x32 (or exact-f32 16x16x4 for the
+//                      parity build).  The weights are the A operand (rows = output channels),
+//                      activations the B operand (columns = pixels), so each lane ends with 4
+//                      consecutive output channels of one pixel -> one 8/16-byte NHWC store.
+//                      Epilogue: bias + SiLU + optional residual (Bottleneck add), written into
+//                      a channel slice of the consumer's buffer (torch.cat / chunk disappear);
+//                      up to two sources (Concat) with per-source nearest-upsample (nn.Upsample).
+//   sppf_pool_kernel   SPPF's three chained MaxPool2d(5,1,2) = windows 5/9/13, one pass.
+//   detect_kernel      Detect level: box 1x1 (MFMA) + DFL softmax-expectation + dist2bbox x stride
+//                      + cls 1x1 + sigmoid + conf threshold, compacted into per-image candidate
+//                      lists (nn/modules/head.py:116-187, utils/tal.py:367-391, utils/nms.py:77-123).
+//   nms_kernel         per image: stable (score desc, anchor asc) sort, TorchNMS.nms greedy loop
+//                      with its "no overlap -> keep all remaining" early exit (utils/nms.py:237-304),
+//                      max_det cut, scale_boxes + clip_boxes (utils/ops.py:105-184).
+#include <hip/hip_runtime.h>
+
+#include <climits>
+#include <map>
+#include <tuple>
+#include <vector>
+
+#include "yk_internal.h"
+
+namespace yk {
+namespace det {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float bf2f(unsigned short h) { return __uint_as_float((unsigned)h << 16); }
+__device__ __forceinline__ unsigned short f2bf(float f) {
+  unsigned u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (unsigned short)((u >> 16) | 0x40u);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (unsigned short)(u >> 16);
+}
+
+// Activation storage traits.  A lane's operand fragment is always 16 bytes.
+struct BF16 {
+  using T = unsigned short;
+  static constexpr int EPL = 8;  // k elements per lane per K-step (16x16x32: 4 groups x 8)
+  static constexpr bool kExact = false;
+};
+struct F32 {
+  using T = float;
+  static constexpr int EPL = 4;  // 16x16x4 issued 4x: 4 groups x 4
+  static constexpr bool kExact = true;
+};
+
+template <class Tr>
+__device__ __forceinline__ f32x4 mma(const uint4& w, const uint4& x, f32x4 acc);
+template <>
+__device__ __forceinline__ f32x4 mma<BF16>(const uint4& w, const uint4& x, f32x4 acc) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, w), __builtin_bit_cast(bf16x8, x),
+                                                 acc, 0, 0, 0);
+}
+template <>
+__device__ __forceinline__ f32x4 mma<F32>(const uint4& w, const uint4& x, f32x4 acc) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(w.x), __uint_as_float(x.x), acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(w.y), __uint_as_float(x.y), acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(w.z), __uint_as_float(x.z), acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(w.w), __uint_as_float(x.w), acc, 0, 0, 0);
+  return acc;
+}
+
+template <bool kExact>
+__device__ __forceinline__ float silu(float v) {
+  if constexpr (kExact) return v / (1.0f + expf(-v));
+  else return v / (1.0f + __expf(-v));
+}
+
+// store / load 4 consecutive channels
+__device__ __forceinline__ void store4(unsigned short* p, const float v[4]) {
+  uint2 o;
+  o.x = (unsigned)f2bf(v[0]) | ((unsigned)f2bf(v[1]) << 16);
+  o.y = (unsigned)f2bf(v[2]) | ((unsigned)f2bf(v[3]) << 16);
+  *(uint2*)p = o;
+}
+__device__ __forceinline__ void store4(float* p, const float v[4]) { *(float4*)p = make_float4(v[0], v[1], v[2], v[3]); }
+__device__ __forceinline__ void load4(const unsigned short* p, float v[4]) {
+  const uint2 i = *(const uint2*)p;
+  v[0] = bf2f(i.x & 0xffff);
+  v[1] = bf2f(i.x >> 16);
+  v[2] = bf2f(i.y & 0xffff);
+  v[3] = bf2f(i.y >> 16);
+}
+__device__ __forceinline__ void load4(const float* p, float v[4]) {
+  const float4 i = *(const float4*)p;
+  v[0] = i.x;
+  v[1] = i.y;
+  v[2] = i.z;
+  v[3] = i.w;
+}
+
+struct View {
+  const void* p;
+  int cstride, coff, h, w, up;
+};
+
+// ---------------------------------------------------------------- implicit-GEMM conv
+struct ConvArgs {
+  View src[2];
+  int ksize, stride, pad;
+  int in_h, in_w, out_h, out_w, M;
+  const uint4* wpk;  // [n_tiles][k_steps][64]
+  const float* bias; // [n_tiles * 16]
+  const int* tab;    // per 8-channel K chunk: -1 or (dx+8)<<21 | (dy+8)<<17 | src<<16 | channel
+  int k_steps, n_tiles, n_chunks;
+  void* dst;
+  int d_cstride, d_coff, cout;
+  const void* res;
+  int r_cstride, r_coff;
+  int act;
+};
+
+template <class Tr, int NNT, int NPT>
+__global__ void __launch_bounds__(256) conv_igemm_kernel(ConvArgs a) {
+  using T = typename Tr::T;
+  constexpr int EPL = Tr::EPL;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int kg = lane >> 4, col = lane & 15;
+  const int nt0 = blockIdx.y * NNT;
+  const int pbase = (blockIdx.x * 4 + wave) * (16 * NPT);
+  if (pbase >= a.M) return;
+  const int hw = a.out_h * a.out_w;
+  int pb[NPT], py[NPT], px[NPT];
+  bool pv[NPT];
+#pragma unroll
+  for (int t = 0; t < NPT; ++t) {
+    const int p = pbase + t * 16 + col;
+    pv[t] = p < a.M;
+    const int pp = pv[t] ? p : 0;
+    pb[t] = pp / hw;
+    const int r = pp - pb[t] * hw;
+    const int oy = r / a.out_w;
+    const int ox = r - oy * a.out_w;
+    py[t] = oy * a.stride;  // the K-chunk table carries the tap offset (ky - pad, kx - pad)
+    px[t] = ox * a.stride;
+  }
+  f32x4 acc[NNT][NPT];
+#pragma unroll
+  for (int i = 0; i < NNT; ++i)
+#pragma unroll
+    for (int t = 0; t < NPT; ++t) acc[i][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto load_step = [&](int ks, uint4* wf, uint4* xf) {
+#pragma unroll
+    for (int i = 0; i < NNT; ++i) {
+      const int nt = nt0 + i < a.n_tiles ? nt0 + i : a.n_tiles - 1;
+      wf[i] = a.wpk[((size_t)nt * a.k_steps + ks) * 64 + lane];
+    }
+    const int kel = ks * 4 * EPL + kg * EPL;
+    const int q = kel >> 3, sub = kel & 7;
+    const int e = q < a.n_chunks ? a.tab[q] : -1;
+#pragma unroll
+    for (int t = 0; t < NPT; ++t) {
+      uint4 v = make_uint4(0u, 0u, 0u, 0u);
+      if (e >= 0 && pv[t]) {
+        const int dx = ((e >> 21) & 15) - 8, dy = ((e >> 17) & 15) - 8;
+        const int si = (e >> 16) & 1, ch = e & 0xffff;
+        const int iy = py[t] + dy, ix = px[t] + dx;
+        if (iy >= 0 && iy < a.in_h && ix >= 0 && ix < a.in_w) {
+          const View& s = a.src[si];
+          const size_t off = (((size_t)pb[t] * s.h + (iy >> s.up)) * s.w + (ix >> s.up)) * s.cstride + s.coff + ch + sub;
+          v = *(const uint4*)((const T*)s.p + off);
+        }
+      }
+      xf[t] = v;
+    }
+  };
+
+  uint4 wf[NNT], xf[NPT], wn[NNT], xn[NPT];
+  load_step(0, wf, xf);
+  for (int ks = 0; ks < a.k_steps; ++ks) {
+    if (ks + 1 < a.k_steps) load_step(ks + 1, wn, xn);
+#pragma unroll
+    for (int i = 0; i < NNT; ++i)
+#pragma unroll
+      for (int t = 0; t < NPT; ++t) acc[i][t] = mma<Tr>(wf[i], xf[t], acc[i][t]);
+#pragma unroll
+    for (int i = 0; i < NNT; ++i) wf[i] = wn[i];
+#pragma unroll
+    for (int t = 0; t < NPT; ++t) xf[t] = xn[t];
+  }
+
+  // epilogue: lane holds channels n0..n0+3 of pixel (pbase + t*16 + col)
+#pragma unroll
+  for (int i = 0; i < NNT; ++i) {
+    const int nt = nt0 + i;
+    if (nt >= a.n_tiles) break;
+    const int n0 = nt * 16 + kg * 4;
+    if (n0 >= a.cout) continue;
+    const float4 bb = *(const float4*)(a.bias + n0);
+#pragma unroll
+    for (int t = 0; t < NPT; ++t) {
+      if (!pv[t]) continue;
+      const size_t p = (size_t)pbase + t * 16 + col;
+      float v[4] = {acc[i][t][0] + bb.x, acc[i][t][1] + bb.y, acc[i][t][2] + bb.z, acc[i][t][3] + bb.w};
+      if (a.act) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = silu<Tr::kExact>(v[j]);
+      }
+      if (a.res) {
+        float r[4];
+        load4((const T*)a.res + p * a.r_cstride + a.r_coff + n0, r);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = r[j] + v[j];
+      }
+      store4((T*)a.dst + p * a.d_cstride + a.d_coff + n0, v);
+    }
+  }
+}
+
+// ---------------------------------------------------------------- first conv from uint8 frames
+struct InputArgs {
+  const unsigned char* frames;  // [B][fh][fw][3] BGR
+  int fh, fw, pad_top, pad_left;
+  int in_h, in_w, out_h, out_w, stride, ksize, pad, M;
+  const float* w;  // [cout][3][k][k] fused weights (RGB channel order), f32
+  const float* b;  // [cout]
+  int cout;        // physical output channels (multiple of 8), weights zero-padded
+  void* dst;
+  int d_cstride, d_coff;
+};
+
+template <class Tr>
+__global__ void __launch_bounds__(256) conv_input_kernel(InputArgs a) {
+  using T = typename Tr::T;
+  extern __shared__ __attribute__((aligned(16))) float sw[];  // cout*27 weights + cout bias
+  const int nw = a.cout * 3 * a.ksize * a.ksize;
+  for (int i = threadIdx.x; i < nw; i += blockDim.x) sw[i] = a.w[i];
+  for (int i = threadIdx.x; i < a.cout; i += blockDim.x) sw[nw + i] = a.b[i];
+  __syncthreads();
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= a.M) return;
+  const int hw = a.out_h * a.out_w;
+  const int b = p / hw, r = p - b * hw, oy = r / a.out_w, ox = r - oy * a.out_w;
+  const int K = a.ksize;
+  float x[3][3][3];  // [c][ky][kx], k <= 3
+  const unsigned char* fr = a.frames + (size_t)b * a.fh * a.fw * 3;
+  for (int ky = 0; ky < K; ++ky)
+    for (int kx = 0; kx < K; ++kx) {
+      const int iy = oy * a.stride - a.pad + ky, ix = ox * a.stride - a.pad + kx;
+      float v0 = 0.f, v1 = 0.f, v2 = 0.f;
+      if (iy >= 0 && iy < a.in_h && ix >= 0 && ix < a.in_w) {
+        const int fy = iy - a.pad_top, fx = ix - a.pad_left;
+        if (fy >= 0 && fy < a.fh && fx >= 0 && fx < a.fw) {
+          const unsigned char* px = fr + ((size_t)fy * a.fw + fx) * 3;
+          v0 = (float)px[2] / 255.0f;  // R  (BGR -> RGB, then /255 as im /= 255)
+          v1 = (float)px[1] / 255.0f;  // G
+          v2 = (float)px[0] / 255.0f;  // B
+        } else {
+          v0 = v1 = v2 = 114.0f / 255.0f;  // LetterBox padding value
+        }
+      }
+      x[0][ky][kx] = v0;
+      x[1][ky][kx] = v1;
+      x[2][ky][kx] = v2;
+    }
+  T* out = (T*)a.dst + (size_t)p * a.d_cstride + a.d_coff;
+  for (int o = 0; o < a.cout; o += 4) {
+    float v[4];
+    for (int j = 0; j < 4; ++j) {
+      const float* w = sw + (o + j) * 3 * K * K;
+      float s = 0.f;
+      for (int c = 0; c < 3; ++c)
+        for (int ky = 0; ky < K; ++ky)
+          for (int kx = 0; kx < K; ++kx) s += w[(c * K + ky) * K + kx] * x[c][ky][kx];
+      v[j] = silu<Tr::kExact>(s + sw[nw + o + j]);
+    }
+    store4(out + o, v);
+  }
+}
+
+// ---------------------------------------------------------------- SPPF pooling
+// slices 1..3 of the SPPF concat buffer = max over 5x5 / 9x9 / 13x13 windows of slice 0
+// (MaxPool2d(5,1,2) applied 1/2/3 times; padding never wins a max).
+template <class Tr>
+__global__ void __launch_bounds__(256) sppf_pool_kernel(void* buf, int cstride, int coff, int C, int H, int W, int M) {
+  using T = typename Tr::T;
+  const int per = C / 4;  // 4-channel groups
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= M * per) return;
+  const int p = i / per, g = i - p * per;
+  const int hw = H * W, b = p / hw, r = p - b * hw, y = r / W, x = r - y * W;
+  T* base = (T*)buf + (size_t)b * hw * cstride + coff + g * 4;
+  float m5[4], m9[4], m13[4];
+  for (int j = 0; j < 4; ++j) m5[j] = m9[j] = m13[j] = -INFINITY;
+  for (int dy = -6; dy <= 6; ++dy) {
+    const int yy = y + dy;
+    if (yy < 0 || yy >= H) continue;
+    for (int dx = -6; dx <= 6; ++dx) {
+      const int xx = x + dx;
+      if (xx < 0 || xx >= W) continue;
+      float v[4];
+      load4(base + ((size_t)yy * W + xx) * cstride, v);
+      const int ad = max(abs(dy), abs(dx));
+      for (int j = 0; j < 4; ++j) {
+        m13[j] = fmaxf(m13[j], v[j]);
+        if (ad <= 4) m9[j] = fmaxf(m9[j], v[j]);
+        if (ad <= 2) m5[j] = fmaxf(m5[j], v[j]);
+      }
+    }
+  }
+  T* o = base + ((size_t)y * W + x) * cstride;
+  store4(o + C, m5);
+  store4(o + 2 * C, m9);
+  store4(o + 3 * C, m13);
+}
+
+// ---------------------------------------------------------------- Detect level
+struct DetArgs {
+  View src;          // second-conv output: box features at src.coff, class features at cls_off
+  int cls_off, cls_ch;
+  const uint4* wpk;  // box 1x1 packed [4][k_steps][64]
+  const float* bias; // [64]
+  int k_steps;
+  const float* wc;   // [cls_ch] then bias
+  int stride, anchor_off, M;
+  float conf;
+  float* cand;       // [B][cap][6]
+  int* cand_count;   // [B]
+  int cap;
+};
+
+template <class Tr>
+__global__ void __launch_bounds__(256) detect_kernel(DetArgs a) {
+  using T = typename Tr::T;
+  constexpr int EPL = Tr::EPL;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int kg = lane >> 4, col = lane & 15;
+  const int pbase = (blockIdx.x * 4 + wave) * 16;
+  if (pbase >= a.M) return;
+  const int p = pbase + col;
+  const bool valid = p < a.M;
+  const int pp = valid ? p : a.M - 1;
+  const T* px = (const T*)a.src.p + (size_t)pp * a.src.cstride;
+  // box logits: 4 tiles (l, t, r, b) x 16 bins
+  f32x4 acc[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) acc[s] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int ks = 0; ks < a.k_steps; ++ks) {
+    const int kel = ks * 4 * EPL + kg * EPL;
+    const uint4 x = *(const uint4*)(px + a.src.coff + kel);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) acc[s] = mma<Tr>(a.wpk[((size_t)s * a.k_steps + ks) * 64 + lane], x, acc[s]);
+  }
+  // class logit: dot product over the class features, split across the 4 lane groups
+  float cl = 0.f;
+  for (int c = kg * 4; c < a.cls_ch; c += 16) {
+    float v[4];
+    load4(px + a.cls_off + c, v);
+    cl += a.wc[c] * v[0] + a.wc[c + 1] * v[1] + a.wc[c + 2] * v[2] + a.wc[c + 3] * v[3];
+  }
+  cl += __shfl_xor(cl, 16);
+  cl += __shfl_xor(cl, 32);
+  cl += a.wc[a.cls_ch];
+  // DFL: softmax over 16 bins (4 per lane, 4 lane groups) -> expectation
+  float d[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    float v[4];
+    const float4 bb = *(const float4*)(a.bias + s * 16 + kg * 4);
+    v[0] = acc[s][0] + bb.x;
+    v[1] = acc[s][1] + bb.y;
+    v[2] = acc[s][2] + bb.z;
+    v[3] = acc[s][3] + bb.w;
+    float m = fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3]));
+    m = fmaxf(m, __shfl_xor(m, 16));
+    m = fmaxf(m, __shfl_xor(m, 32));
+    float e[4], sum = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      e[j] = expf(v[j] - m);
+      sum += e[j];
+    }
+    sum += __shfl_xor(sum, 16);
+    sum += __shfl_xor(sum, 32);
+    float ex = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) ex += (float)(kg * 4 + j) * (e[j] / sum);
+    ex += __shfl_xor(ex, 16);
+    ex += __shfl_xor(ex, 32);
+    d[s] = ex;
+  }
+  if (kg != 0 || !valid) return;
+  const float score = 1.0f / (1.0f + expf(-cl));
+  if (!(score > a.conf)) return;
+  const int hw = a.src.h * a.src.w;
+  const int b = p / hw, r = p - b * hw, gy = r / a.src.w, gx = r - gy * a.src.w;
+  const float ax = (float)gx + 0.5f, ay = (float)gy + 0.5f;
+  // dist2bbox (xywh) * stride, then xywh2xyxy
+  const float x1 = ax - d[0], y1 = ay - d[1], x2 = ax + d[2], y2 = ay + d[3];
+  const float st = (float)a.stride;
+  const float cx = ((x1 + x2) / 2.0f) * st, cy = ((y1 + y2) / 2.0f) * st;
+  const float w = (x2 - x1) * st, h = (y2 - y1) * st;
+  const float hw2 = w / 2.0f, hh2 = h / 2.0f;
+  const int slot = atomicAdd(&a.cand_count[b], 1);
+  if (slot >= a.cap) return;
+  float* c = a.cand + ((size_t)b * a.cap + slot) * 6;
+  c[0] = cx - hw2;
+  c[1] = cy - hh2;
+  c[2] = cx + hw2;
+  c[3] = cy + hh2;
+  c[4] = score;
+  c[5] = __int_as_float(a.anchor_off + r);
+}
+
+// ---------------------------------------------------------------- NMS + scale/clip
+constexpr int NMS_NT = 512;
+constexpr int NMS_LDS_N = 4096;  // candidates sorted / suppressed in LDS; more -> global scratch
+
+struct NmsArgs {
+  const float* cand;
+  int* cand_count;
+  int cap, max_nms;
+  int* slot_of;                 // [B][n_anchors] anchor -> candidate slot
+  unsigned long long* gkeys;    // [B][pow2 >= cap]
+  float* gbox;                  // [B][cap][5]
+  unsigned char* gflag;         // [B][cap]
+  int n_anchors, key_cap;
+  float iou;
+  int max_det;
+  float* dets;                  // [B][max_det][6]
+  int* counts;
+  float pad_x, pad_y, gain, clip_w, clip_h;
+};
+
+__device__ __forceinline__ void bitonic_sort(unsigned long long* k, int n2) {
+  for (int size = 2; size <= n2; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int i = threadIdx.x; i < (n2 >> 1); i += blockDim.x) {
+        const int lo = 2 * i - (i & (stride - 1));
+        const int hi = lo + stride;
+        const bool up = (lo & size) == 0;
+        const unsigned long long a = k[lo], b = k[hi];
+        if ((a > b) == up) {
+          k[lo] = b;
+          k[hi] = a;
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+__global__ void __launch_bounds__(NMS_NT) nms_kernel(NmsArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  int n = a.cand_count[b];
+  if (n > a.cap) n = a.cap;
+  const float* cand = a.cand + (size_t)b * a.cap * 6;
+  const bool in_lds = n <= NMS_LDS_N;
+  int n2 = 1;
+  while (n2 < n) n2 <<= 1;
+  unsigned long long* keys = in_lds ? (unsigned long long*)smem : a.gkeys + (size_t)b * a.key_cap;
+  float* box = in_lds ? (float*)(smem + NMS_LDS_N * 8) : a.gbox + (size_t)b * a.cap * 5;
+  unsigned char* removed = in_lds ? smem + NMS_LDS_N * 8 + NMS_LDS_N * 20 : a.gflag + (size_t)b * a.cap;
+  int* misc = (int*)(smem + NMS_LDS_N * 8 + NMS_LDS_N * 20 + NMS_LDS_N);  // [0..15] + keep list
+  int* keep = misc + 16;
+  int* slot_of = a.slot_of + (size_t)b * a.n_anchors;
+  // keys: (~score_bits, anchor) -> ascending order = score desc, anchor asc (stable order)
+  for (int i = tid; i < n2; i += NMS_NT) {
+    unsigned long long k = ~0ull;
+    if (i < n) {
+      const unsigned sb = __float_as_uint(cand[i * 6 + 4]);
+      const int anc = __float_as_int(cand[i * 6 + 5]);
+      k = ((unsigned long long)(0xffffffffu - sb) << 32) | (unsigned)anc;
+      slot_of[anc] = i;
+    }
+    keys[i] = k;
+  }
+  __syncthreads();
+  if (n > 1) bitonic_sort(keys, n2);
+  if (n > a.max_nms) n = a.max_nms;  // nms.py:138-142
+  for (int i = tid; i < n; i += NMS_NT) {
+    const int s = slot_of[(int)(keys[i] & 0xffffffffu)];
+    const float* c = cand + (size_t)s * 6;
+    const float x1 = c[0], y1 = c[1], x2 = c[2], y2 = c[3];
+    box[i * 5 + 0] = x1;
+    box[i * 5 + 1] = y1;
+    box[i * 5 + 2] = x2;
+    box[i * 5 + 3] = y2;
+    box[i * 5 + 4] = (x2 - x1) * (y2 - y1);
+    removed[i] = 0;
+  }
+  __syncthreads();
+  int k = 0;
+  const float thr = a.iou;
+  for (int i = 0; i < n && k < a.max_det; ++i) {
+    if (removed[i]) continue;
+    if (tid == 0) keep[k] = i;
+    ++k;
+    const float bx1 = box[i * 5], by1 = box[i * 5 + 1], bx2 = box[i * 5 + 2], by2 = box[i * 5 + 3],
+                ba = box[i * 5 + 4];
+    int any = 0;
+    for (int j = i + 1 + tid; j < n; j += NMS_NT) {
+      if (removed[j]) continue;
+      const float w = fmaxf(fminf(bx2, box[j * 5 + 2]) - fmaxf(bx1, box[j * 5]), 0.f);
+      const float h = fmaxf(fminf(by2, box[j * 5 + 3]) - fmaxf(by1, box[j * 5 + 1]), 0.f);
+      if (w * h != 0.f) any = 1;
+    }
+    any = __syncthreads_or(any);
+    if (!any) {
+      // inter.sum() == 0: keep every remaining box, in order, and stop (nms.py:291-296)
+      int base = k;
+      for (int j0 = i + 1; j0 < n; j0 += NMS_NT) {
+        const int j = j0 + tid;
+        const int f = (j < n && !removed[j]) ? 1 : 0;
+        const unsigned long long m = __ballot(f);
+        const int lane = tid & 63, w = tid >> 6;
+        if (lane == 0) misc[w] = __popcll(m);
+        __syncthreads();
+        int pre = 0, tot = 0;
+        for (int q = 0; q < NMS_NT / 64; ++q) {
+          pre += q < w ? misc[q] : 0;
+          tot += misc[q];
+        }
+        const int r = base + pre + __popcll(m & ((1ull << lane) - 1ull));
+        if (f && r < a.max_det) keep[r] = j;
+        __syncthreads();
+        base += tot;
+      }
+      k = base < a.max_det ? base : a.max_det;
+      break;
+    }
+    for (int j = i + 1 + tid; j < n; j += NMS_NT) {
+      if (removed[j]) continue;
+      const float w = fmaxf(fminf(bx2, box[j * 5 + 2]) - fmaxf(bx1, box[j * 5]), 0.f);
+      const float h = fmaxf(fminf(by2, box[j * 5 + 3]) - fmaxf(by1, box[j * 5 + 1]), 0.f);
+      const float inter = w * h;
+      const float iou = inter / (ba + box[j * 5 + 4] - inter);
+      if (!(iou <= thr)) removed[j] = 1;
+    }
+    __syncthreads();
+  }
+  __syncthreads();
+  // outputs: x[i] rows, then scale_boxes (x - pad) / gain and clip (ops.py:105-184)
+  for (int r = tid; r < k; r += NMS_NT) {
+    const int i = keep[r];
+    const int s = slot_of[(int)(keys[i] & 0xffffffffu)];
+    const float* c = cand + (size_t)s * 6;
+    float* o = a.dets + ((size_t)b * a.max_det + r) * 6;
+    float x1 = (c[0] - a.pad_x) / a.gain, y1 = (c[1] - a.pad_y) / a.gain;
+    float x2 = (c[2] - a.pad_x) / a.gain, y2 = (c[3] - a.pad_y) / a.gain;
+    o[0] = fminf(fmaxf(x1, 0.f), a.clip_w);
+    o[1] = fminf(fmaxf(y1, 0.f), a.clip_h);
+    o[2] = fminf(fmaxf(x2, 0.f), a.clip_w);
+    o[3] = fminf(fmaxf(y2, 0.f), a.clip_h);
+    o[4] = c[4];
+    o[5] = 0.f;
+  }
+  if (tid == 0) a.counts[b] = k;
+}
+
+size_t nms_lds_bytes() { return (size_t)NMS_LDS_N * 8 + (size_t)NMS_LDS_N * 20 + NMS_LDS_N + 64 + 4 * 4096; }
+
+}  // namespace det
+}  // namespace yk
+
+using namespace yk::det;
+
+struct yk_model {
+  yk_ctx* ctx = nullptr;
+  yk_model_desc desc{};
+  std::vector<yk_op> ops;
+  std::vector<int64_t> buf_elems;
+  std::vector<void*> bufs;
+  char* blob = nullptr;
+  float* cand = nullptr;
+  int* cand_count = nullptr;
+  int* slot_of = nullptr;
+  unsigned long long* gkeys = nullptr;
+  float* gbox = nullptr;
+  unsigned char* gflag = nullptr;
+  int key_cap = 0;
+  float* dets = nullptr;
+  int* counts = nullptr;
+  std::map<std::tuple<int, float, float, int, const void*, void*, void*>, hipGraphExec_t> graphs;
+};
+
+namespace {
+
+View make_view(yk_model* m, const yk_view& v) {
+  View o;
+  o.p = m->bufs[v.buf];
+  o.cstride = v.c_stride;
+  o.coff = v.c_off;
+  o.h = v.h;
+  o.w = v.w;
+  o.up = v.up;
+  return o;
+}
+
+template <class Tr, int NNT>
+void launch_conv_t(const ConvArgs& a, int n_tiles, hipStream_t st) {
+  constexpr int NPT = 2;
+  dim3 grid((a.M + 64 * NPT - 1) / (64 * NPT), (n_tiles + NNT - 1) / NNT);
+  hipLaunchKernelGGL((conv_igemm_kernel<Tr, NNT, NPT>), grid, dim3(256), 0, st, a);
+}
+
+template <class Tr>
+void launch_conv(const ConvArgs& a, hipStream_t st) {
+  const int nt = a.n_tiles;
+  if (nt <= 1) launch_conv_t<Tr, 1>(a, nt, st);
+  else if (nt == 2) launch_conv_t<Tr, 2>(a, nt, st);
+  else if (nt == 3 || nt == 6 || nt == 9) launch_conv_t<Tr, 3>(a, nt, st);
+  else launch_conv_t<Tr, 4>(a, nt, st);
+}
+
+template <class Tr>
+int run_ops(yk_model* m, const uint8_t* frames, int B, float conf, hipStream_t st) {
+  const yk_model_desc& D = m->desc;
+  for (const yk_op& op : m->ops) {
+    switch (op.kind) {
+      case YK_K_CONV_INPUT: {
+        InputArgs a;
+        a.frames = frames;
+        a.fh = D.frame_h;
+        a.fw = D.frame_w;
+        a.pad_top = D.pad_top;
+        a.pad_left = D.pad_left;
+        a.in_h = D.in_h;
+        a.in_w = D.in_w;
+        a.out_h = op.out_h;
+        a.out_w = op.out_w;
+        a.stride = op.stride;
+        a.ksize = op.ksize;
+        a.pad = op.ksize / 2;
+        a.M = B * op.out_h * op.out_w;
+        a.w = (const float*)(m->blob + op.w_off);
+        a.b = (const float*)(m->blob + op.b_off);
+        a.cout = op.cout;
+        a.dst = m->bufs[op.dst.buf];
+        a.d_cstride = op.dst.c_stride;
+        a.d_coff = op.dst.c_off;
+        const size_t lds = (size_t)(op.cout * 3 * op.ksize * op.ksize + op.cout) * 4;
+        hipLaunchKernelGGL(conv_input_kernel<Tr>, dim3((a.M + 255) / 256), dim3(256), lds, st, a);
+        break;
+      }
+      case YK_K_CONV: {
+        ConvArgs a;
+        for (int i = 0; i < 2; ++i) a.src[i] = make_view(m, op.src[i < op.n_src ? i : 0]);
+        a.ksize = op.ksize;
+        a.stride = op.stride;
+        a.pad = op.ksize / 2;
+        a.in_h = op.src[0].h << op.src[0].up;
+        a.in_w = op.src[0].w << op.src[0].up;
+        a.out_h = op.out_h;
+        a.out_w = op.out_w;
+        a.M = B * op.out_h * op.out_w;
+        a.wpk = (const uint4*)(m->blob + op.w_off);
+        a.bias = (const float*)(m->blob + op.b_off);
+        a.tab = (const int*)(m->blob + op.t_off);
+        a.k_steps = op.k_steps;
+        a.n_tiles = op.n_tiles;
+        a.n_chunks = op.ksize * op.ksize * (op.src_ch[0] + (op.n_src > 1 ? op.src_ch[1] : 0)) / 8;
+        a.dst = m->bufs[op.dst.buf];
+        a.d_cstride = op.dst.c_stride;
+        a.d_coff = op.dst.c_off;
+        a.cout = op.cout;
+        a.res = op.has_res ? m->bufs[op.res.buf] : nullptr;
+        a.r_cstride = op.res.c_stride;
+        a.r_coff = op.res.c_off;
+        a.act = op.act;
+        launch_conv<Tr>(a, st);
+        break;
+      }
+      case YK_K_SPPF_POOL: {
+        const int M = B * op.src[0].h * op.src[0].w;
+        const int C = op.src_ch[0];
+        const int n = M * (C / 4);
+        hipLaunchKernelGGL(sppf_pool_kernel<Tr>, dim3((n + 255) / 256), dim3(256), 0, st, m->bufs[op.src[0].buf],
+                           op.src[0].c_stride, op.src[0].c_off, C, op.src[0].h, op.src[0].w, M);
+        break;
+      }
+      case YK_K_DETECT: {
+        DetArgs a;
+        a.src = make_view(m, op.src[0]);
+        a.cls_off = op.det_cls_off;
+        a.cls_ch = op.det_cls_ch;
+        a.wpk = (const uint4*)(m->blob + op.w_off);
+        a.bias = (const float*)(m->blob + op.b_off);
+        a.k_steps = op.k_steps;
+        a.wc = (const float*)(m->blob + op.det_wc_off);
+        a.stride = op.det_stride;
+        a.anchor_off = op.det_anchor_off;
+        a.M = B * op.src[0].h * op.src[0].w;
+        a.conf = conf;
+        a.cand = m->cand;
+        a.cand_count = m->cand_count;
+        a.cap = D.n_anchors;
+        hipLaunchKernelGGL(detect_kernel<Tr>, dim3((a.M + 63) / 64), dim3(256), 0, st, a);
+        break;
+      }
+      default:
+        yk::set_error("yk_detect: unknown op kind");
+        return YK_ERR_ARG;
+    }
+  }
+  return YK_OK;
+}
+
+int detect_impl(yk_model* m, const uint8_t* frames, int B, float conf, float iou, int max_det, float* dets,
+                int32_t* counts, hipStream_t st) {
+  const yk_model_desc& D = m->desc;
+  YK_CHECK_ARG(frames, "yk_detect: frames is NULL");
+  YK_CHECK_ARG(B >= 1 && B <= D.max_batch, "yk_detect: batch out of range [1, max_batch]");
+  YK_CHECK_ARG(conf >= 0.f && conf <= 1.f, "Invalid Confidence threshold, valid values are between 0.0 and 1.0");
+  YK_CHECK_ARG(iou >= 0.f && iou <= 1.f, "Invalid IoU, valid values are between 0.0 and 1.0");
+  YK_CHECK_ARG(max_det >= 0 && max_det <= D.max_det, "yk_detect: max_det exceeds the model's capacity");
+  if (!dets) dets = m->dets;
+  if (!counts) counts = m->counts;
+  YK_HIP(hipMemsetAsync(m->cand_count, 0, sizeof(int) * B, st));
+  int rc = D.act_dtype == YK_ACT_F32 ? run_ops<F32>(m, frames, B, conf, st) : run_ops<BF16>(m, frames, B, conf, st);
+  if (rc != YK_OK) return rc;
+  NmsArgs a;
+  a.cand = m->cand;
+  a.cand_count = m->cand_count;
+  a.cap = D.n_anchors;
+  a.max_nms = 30000;
+  a.slot_of = m->slot_of;
+  a.gkeys = m->gkeys;
+  a.gbox = m->gbox;
+  a.gflag = m->gflag;
+  a.n_anchors = D.n_anchors;
+  a.key_cap = m->key_cap;
+  a.iou = iou;
+  a.max_det = max_det;
+  a.dets = dets;
+  a.counts = counts;
+  a.pad_x = (float)D.pad_left;
+  a.pad_y = (float)D.pad_top;
+  a.gain = 1.0f;
+  a.clip_w = (float)D.frame_w;
+  a.clip_h = (float)D.frame_h;
+  hipLaunchKernelGGL(nms_kernel, dim3(B), dim3(NMS_NT), nms_lds_bytes(), st, a);
+  YK_HIP(hipGetLastError());
+  return YK_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int yk_model_create(yk_ctx* ctx, const yk_model_desc* desc, const void* host_blob, int64_t blob_bytes,
+                    yk_model** out) {
+  YK_CHECK_ARG(ctx && desc && host_blob && out, "yk_model_create: NULL argument");
+  YK_CHECK_ARG(desc->n_ops > 0 && desc->ops && desc->n_bufs > 0 && desc->buf_elems, "yk_model_create: empty program");
+  YK_CHECK_ARG(desc->max_batch >= 1 && desc->n_anchors > 0 && desc->max_det >= 1, "yk_model_create: bad sizes");
+  YK_CHECK_ARG(desc->nc == 1, "yk_model_create: only single-class detection heads are supported");
+  YK_CHECK_ARG(desc->act_dtype == YK_ACT_BF16 || desc->act_dtype == YK_ACT_F32, "yk_model_create: bad act dtype");
+  for (int i = 0; i < desc->n_ops; ++i) {
+    const yk_op& op = desc->ops[i];
+    YK_CHECK_ARG(op.kind >= YK_K_CONV_INPUT && op.kind <= YK_K_DETECT, "yk_model_create: bad op kind");
+    YK_CHECK_ARG(op.dst.buf >= 0 && op.dst.buf < desc->n_bufs, "yk_model_create: dst buffer index out of range");
+    for (int s = 0; s < op.n_src; ++s)
+      YK_CHECK_ARG(op.src[s].buf >= 0 && op.src[s].buf < desc->n_bufs, "yk_model_create: src buffer out of range");
+    YK_CHECK_ARG(op.n_src >= (op.kind == YK_K_CONV_INPUT ? 0 : 1) && op.n_src <= 2, "yk_model_create: n_src");
+    YK_CHECK_ARG(op.w_off >= 0 && op.w_off < blob_bytes && op.b_off >= 0 && op.b_off < blob_bytes,
+                 "yk_model_create: weight offsets outside the blob");
+    YK_CHECK_ARG(op.kind != YK_K_CONV || (op.cout % 4 == 0 && op.k_steps > 0 && op.n_tiles > 0),
+                 "yk_model_create: conv geometry");
+    YK_CHECK_ARG(op.kind != YK_K_CONV || op.ksize == 1 || op.ksize == 3, "yk_model_create: ksize must be 1 or 3");
+    YK_CHECK_ARG(op.kind != YK_K_CONV_INPUT || op.ksize <= 3, "yk_model_create: input conv ksize <= 3");
+  }
+  yk::DeviceGuard guard(ctx->device);
+  auto* m = new yk_model();
+  m->ctx = ctx;
+  m->desc = *desc;
+  m->ops.assign(desc->ops, desc->ops + desc->n_ops);
+  m->buf_elems.assign(desc->buf_elems, desc->buf_elems + desc->n_bufs);
+  m->desc.ops = m->ops.data();
+  m->desc.buf_elems = m->buf_elems.data();
+  const size_t esz = desc->act_dtype == YK_ACT_F32 ? 4 : 2;
+  const size_t B = desc->max_batch, A = desc->n_anchors;
+  hipError_t e = hipSuccess;
+  auto alloc = [&](void** p, size_t bytes) {
+    if (e == hipSuccess) e = hipMalloc(p, bytes ? bytes : 16);
+  };
+  for (int i = 0; i < desc->n_bufs; ++i) {
+    void* p = nullptr;
+    alloc(&p, (size_t)desc->buf_elems[i] * B * esz + 64);
+    m->bufs.push_back(p);
+    if (p) (void)hipMemset(p, 0, (size_t)desc->buf_elems[i] * B * esz + 64);
+  }
+  alloc((void**)&m->blob, (size_t)blob_bytes);
+  if (e == hipSuccess) e = hipMemcpy(m->blob, host_blob, (size_t)blob_bytes, hipMemcpyHostToDevice);
+  int kc = 1;
+  while (kc < (int)A) kc <<= 1;
+  m->key_cap = kc;
+  alloc((void**)&m->cand, B * A * 6 * sizeof(float));
+  alloc((void**)&m->cand_count, B * sizeof(int));
+  alloc((void**)&m->slot_of, B * A * sizeof(int));
+  alloc((void**)&m->gkeys, B * (size_t)kc * sizeof(unsigned long long));
+  alloc((void**)&m->gbox, B * A * 5 * sizeof(float));
+  alloc((void**)&m->gflag, B * A);
+  alloc((void**)&m->dets, B * desc->max_det * 6 * sizeof(float));
+  alloc((void**)&m->counts, B * sizeof(int));
+  if (e == hipSuccess) e = hipMemset(m->counts, 0, B * sizeof(int));
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute((const void*)nms_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)nms_lds_bytes());
+  if (e != hipSuccess) {
+    yk::set_error(std::string("yk_model_create: ") + hipGetErrorString(e));
+    yk_model_destroy(m);
+    return YK_ERR_HIP;
+  }
+  *out = m;
+  return YK_OK;
+}
+
+int yk_model_destroy(yk_model* m) {
+  if (!m) return YK_OK;
+  yk::DeviceGuard guard(m->ctx->device);
+  for (auto& kv : m->graphs) (void)hipGraphExecDestroy(kv.second);
+  for (void* p : m->bufs)
+    if (p) (void)hipFree(p);
+  void* ptrs[] = {m->blob, m->cand, m->cand_count, m->slot_of, m->gkeys, m->gbox, m->gflag, m->dets, m->counts};
+  for (void* p : ptrs)
+    if (p) (void)hipFree(p);
+  delete m;
+  return YK_OK;
+}
+
+int yk_detect(yk_model* m, const uint8_t* frames, int batch, float conf, float iou, int max_det, float* dets,
+              int32_t* counts, void* stream) {
+  YK_CHECK_ARG(m, "yk_detect: NULL model");
+  yk::DeviceGuard guard(m->ctx->device);
+  return detect_impl(m, frames, batch, conf, iou, max_det, dets, counts, (hipStream_t)stream);
+}
+
+int yk_detect_graph(yk_model* m, const uint8_t* frames, int batch, float conf, float iou, int max_det, float* dets,
+                    int32_t* counts, void* stream) {
+  YK_CHECK_ARG(m, "yk_detect_graph: NULL model");
+  yk::DeviceGuard guard(m->ctx->device);
+  hipStream_t st = (hipStream_t)stream;
+  auto key = std::make_tuple(batch, conf, iou, max_det, (const void*)frames, (void*)dets, (void*)counts);
+  auto it = m->graphs.find(key);
+  if (it == m->graphs.end()) {
+    hipStream_t cap;
+    YK_HIP(hipStreamCreateWithFlags(&cap, hipStreamNonBlocking));
+    hipGraph_t g;
+    YK_HIP(hipStreamBeginCapture(cap, hipStreamCaptureModeThreadLocal));
+    int rc = detect_impl(m, frames, batch, conf, iou, max_det, dets, counts, cap);
+    hipError_t ce = hipStreamEndCapture(cap, &g);
+    (void)hipStreamDestroy(cap);
+    if (rc != YK_OK) return rc;
+    if (ce != hipSuccess) {
+      yk::set_error(std::string("yk_detect_graph: capture failed: ") + hipGetErrorString(ce));
+      return YK_ERR_HIP;
+    }
+    hipGraphExec_t ge;
+    hipError_t ie = hipGraphInstantiate(&ge, g, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(g);
+    if (ie != hipSuccess) {
+      yk::set_error(std::string("yk_detect_graph: instantiate failed: ") + hipGetErrorString(ie));
+      return YK_ERR_HIP;
+    }
+    it = m->graphs.emplace(key, ge).first;
+  }
+  YK_HIP(hipGraphLaunch(it->second, st));
+  return YK_OK;
+}
+
+int yk_model_outputs(yk_model* m, float** dets, int32_t** counts) {
+  YK_CHECK_ARG(m, "yk_model_outputs: NULL model");
+  if (dets) *dets = m->dets;
+  if (counts) *counts = m->counts;
+  return YK_OK;
+}
+
+int yk_model_candidates(yk_model* m, float** cand, int32_t** counts) {
+  YK_CHECK_ARG(m, "yk_model_candidates: NULL model");
+  if (cand) *cand = m->cand;
+  if (counts) *counts = m->cand_count;
+  return YK_OK;
+}
+
+int yk_model_buffer(yk_model* m, int buf, void** ptr) {
+  YK_CHECK_ARG(m && ptr, "yk_model_buffer: NULL argument");
+  YK_CHECK_ARG(buf >= 0 && buf < (int)m->bufs.size(), "yk_model_buffer: index out of range");
+  *ptr = m->bufs[buf];
+  return YK_OK;
+}
+
+}  // extern "C"

@@ -32,8 +32,17 @@ int64_t yk_struct_size(int which) {
     case 1: return (int64_t)sizeof(yk_tracker_stats);
     case 2: return (int64_t)sizeof(yk_track_out);
     case 3: return (int64_t)sizeof(yk_track_state);
+    case 4: return (int64_t)sizeof(yk_view);
+    case 5: return (int64_t)sizeof(yk_op);
+    case 6: return (int64_t)sizeof(yk_model_desc);
     default: return -1;
   }
+}
+
+int yk_memcpy_d2h(void* host_dst, const void* dev_src, int64_t bytes) {
+  YK_CHECK_ARG(host_dst && dev_src && bytes >= 0, "yk_memcpy_d2h: bad argument");
+  YK_HIP(hipMemcpy(host_dst, dev_src, (size_t)bytes, hipMemcpyDeviceToHost));
+  return YK_OK;
 }
 
 int yk_ctx_destroy(yk_ctx* ctx) {

@@ -107,9 +107,12 @@ class MultiStreamTracker:
 
     def __del__(self):
         h = getattr(self, "_h", None)
-        if h is not None and L._lib is not None:
-            L.lib().yk_tracker_destroy(h)
-            self._h = None
+        try:
+            if h is not None and L._lib is not None:
+                L.lib().yk_tracker_destroy(h)
+        except Exception:  # interpreter shutdown
+            pass
+        self._h = None
 
     @property
     def handle(self) -> C.c_void_p:
