@@ -1,0 +1,237 @@
+#!/usr/bin/env python3
+"""End-to-end detect-and-track benchmark (BASELINE.json metric).
+
+One step = one frame of every stream on this GPU through the whole hot path
+(kalman/aircraft_detection_tracking.py:96-109): uint8 BGR frame in HBM -> letterbox/normalise
+-> YOLOv8s+P2 forward -> Detect decode -> NMS -> EnhancedMultiTargetTracker.update per stream,
+captured as one hipGraph.  Default workload = BASELINE config 3: 8 independent 640x512 streams
+per GPU (batch 8), ~64 live tracks per stream, bf16 convs.  Multi-GPU (torchrun): streams are
+sharded one group per GPU with no data-path collective (weak scaling); RCCL only reduces the
+end-of-run counters and the max wall time.
+
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import importlib
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+PKG = "yolo---small-target-recognition---kalman-trajectory-prediction_amd"
+
+METRIC = "end-to-end frames/sec (640×512 YOLOv8s+P2, 64 tracks) at 1/2/4/8 GPUs"
+PEAK = {"bf16": 2500.0, "fp32": 157.3}  # dense MFMA TFLOP/s (MI355X_MICROARCH.md)
+HBM_PEAK = 8000.0  # GB/s
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--streams", type=int, default=8, help="streams (= frames per forward) per GPU")
+    ap.add_argument("--targets", type=int, default=48, help="synthetic targets per stream")
+    ap.add_argument("--scale", default="s", choices=["n", "s"])
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--frames", type=int, default=120, help="pre-rendered frames per stream (cycled)")
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-profile", action="store_true")
+    return ap.parse_args()
+
+
+def dist_setup():
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if ws > 1:
+        import torch.distributed as dist
+
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    return ws, rank, local
+
+
+def roofline(pipe, frames, dtype, B):
+    """Per-op device times (hipEvents on the launch stream), grouped by kernel instantiation;
+    the dominant one gives the roofline entry."""
+    prof = pipe.model.profile(frames, pipe.conf, pipe.iou, pipe.max_det, reps=5)
+    flops = pipe.prog.op_flops(B)
+    by = {}
+    for (i, kind, name, ms), fl in zip(prof, flops):
+        d = by.setdefault(name, {"ms": 0.0, "flops": 0, "launches": 0})
+        d["ms"] += ms
+        d["flops"] += fl
+        d["launches"] += 1
+    dom = max(by, key=lambda k: by[k]["ms"])
+    d = by[dom]
+    avg_ms = d["ms"] / d["launches"]
+    ach = d["flops"] / (d["ms"] * 1e-3) / 1e12 if d["ms"] > 0 else 0.0
+    total_ms = sum(v["ms"] for v in by.values())
+    return {
+        "kernel": dom, "bound": "mfma", "achieved": round(ach, 2), "peak": PEAK[dtype], "unit": "TFLOP/s",
+        "frac": round(ach / PEAK[dtype], 5), "traffic": None, "avg_launch_us": round(avg_ms * 1e3, 2),
+        "launches_per_step": d["launches"], "flops_per_launch": int(d["flops"] / d["launches"]),
+        "share_of_detect_time": round(d["ms"] / total_ms, 3),
+    }, by, prof
+
+
+def tracker_roofline(pipe, reps=20):
+    """Tracker step kernel alone (events around yk_tracker_step on the launch stream); algorithmic
+    bytes per track-step from SURVEY §8d (1,216 B: R+W of x and dense P, z, box)."""
+    torch.cuda.synchronize()
+    _, stats = pipe.stats()
+    live = int(stats["current_active_tracks"].sum())
+    st = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    # replay from a snapshot-free state: timing only (the tracker keeps evolving, which is fine)
+    e0.record(st)
+    for _ in range(reps):
+        pipe.tracker.step_device(pipe.dets, pipe.counts)
+    e1.record(st)
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) * 1e3 / reps
+    by = live * 1216
+    gbps = by / (us * 1e-6) / 1e9 if us > 0 else 0.0
+    return {"kernel": "step_kernel", "bound": "hbm", "avg_launch_us": round(us, 2), "live_tracks": live,
+            "achieved": round(gbps, 3), "peak": HBM_PEAK, "unit": "GB/s", "frac": round(gbps / HBM_PEAK, 6)}
+
+
+def cpu_baseline(P, scale, seconds, seed=0):
+    """Reference-equivalent CPU path (oracle: torch-CPU fp32 YOLOv8s+P2 + numpy tracker) on a
+    bounded sample of one stream, threads as the reference's select_device: min(8, ncpu-1)."""
+    from oracle import detector_ref as D
+    from oracle.tracker_ref import RefMultiTracker
+
+    threads = min(8, (os.cpu_count() or 2) - 1)
+    torch.set_num_threads(threads)
+    ar = P.arch.parse_arch(P.arch.load_model_dict(f"yolov8{scale}-small.yaml"))
+    sd = P.weights.synthetic_state_dict(ar, seed)
+    layers = [(Ly.i, Ly.f, Ly.kind, {**Ly.args, **({"c": int(Ly.c2 * 0.5)} if Ly.kind == "C2f" else {})})
+              for Ly in ar.layers]
+    det = D.RefDetector(layers, sd, P.arch.detect_strides(ar))
+    sc = P.synth.Scene(seed=seed, n_targets=48, n_frames=400)
+    trk = RefMultiTracker(150, 1, 0.1)
+    n, t_total = 0, 0.0
+    for t in range(400):
+        f = sc.frame(t)
+        t0 = time.perf_counter()
+        res, _ = D.predict(det, [f], 0.25, 0.7, 300)
+        boxes = res[0][:, :4].numpy()
+        scores = res[0][:, 4].numpy()
+        dets = [[b[0], b[1], b[2], b[3], s] for b, s in zip(boxes, scores) if s > 0.1]
+        trk.update(dets)
+        dt = time.perf_counter() - t0
+        if t >= 2:  # warm-up frames
+            n += 1
+            t_total += dt
+            if t_total > seconds:
+                break
+    return {"value": round(n / t_total, 3), "unit": "frames/s", "cores": threads, "kind": "port",
+            "sample": f"{n} frames of one 640x512 stream (48 targets), YOLOv8{scale}+P2 fp32 torch-CPU "
+                      f"({threads} threads) + numpy tracker, after 2 warm-up frames"}
+
+
+def main():
+    a = parse()
+    ws, rank, local = dist_setup()
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    P = importlib.import_module(PKG)
+    from importlib import import_module
+
+    pipeline = import_module(PKG + ".pipeline")
+    S, H, W = a.streams, 512, 640
+    seed0 = 1000 * rank
+    pipe = pipeline.StreamPipeline(f"yolov8{a.scale}-small.yaml", S, (H, W), a.dtype, seed=0, device=local)
+    # pre-render frames of every stream into HBM (inputs resident before the timed region)
+    F = max(2, min(a.frames, a.warmup + a.steps))
+    scenes = [P.synth.Scene(seed=seed0 + s, n_targets=a.targets, n_frames=F + 1) for s in range(S)]
+    frames = torch.empty((F, S, H, W, 3), dtype=torch.uint8, device=dev)
+    for s, sc in enumerate(scenes):
+        frames[:, s] = sc.frames_torch(0, F, dev)
+    torch.cuda.synchronize()
+    if not a.no_graph:
+        pipe.frames.copy_(frames[0])
+        pipe.capture()
+    # warm-up
+    for t in range(a.warmup):
+        pipe.run(frames[t % F])
+    torch.cuda.synchronize()
+    if ws > 1:
+        import torch.distributed as dist
+
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for t in range(a.steps):
+        pipe.run(frames[(a.warmup + t) % F])
+    torch.cuda.synchronize()
+    if ws > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    counts, stats = pipe.stats()
+    live = float(stats["current_active_tracks"].mean())
+    frames_done = S * a.steps
+    # PCIe-inclusive rate (host frames -> device each step): informational, never `value`
+    host = frames[0].cpu().pin_memory()
+    torch.cuda.synchronize()
+    tp = time.perf_counter()
+    n_pcie = min(20, a.steps)
+    for _ in range(n_pcie):
+        pipe.frames.copy_(host, non_blocking=True)
+        pipe.step()
+    torch.cuda.synchronize()
+    pcie_fps = S * n_pcie / (time.perf_counter() - tp)
+    if ws > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        c = torch.tensor([frames_done, live, float(stats["total_tracks_created"].sum())], device=dev,
+                         dtype=torch.float64)
+        dist.all_reduce(c, op=dist.ReduceOp.SUM)
+        frames_done = int(c[0].item())
+        live = float(c[1].item()) / ws
+    fps = frames_done / elapsed
+    rl = None
+    trl = None
+    if rank == 0 and not a.no_profile:
+        rl, _, _ = roofline(pipe, frames[0], a.dtype, S)
+        trl = tracker_roofline(pipe)
+    cpu = None
+    if rank == 0 and ws == 1 and not a.no_cpu_baseline:
+        cpu = cpu_baseline(P, a.scale, a.cpu_seconds)
+    if rank == 0:
+        gflop = pipe.flops_per_frame() / 1e9
+        out = {
+            "metric": METRIC, "value": round(fps, 2), "unit": "frames/s", "n_gpus": ws, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": a.dtype,
+            "data": "synthetic: seeded 640x512 IR-like scenes rendered into HBM before timing; seeded "
+                    "planted weights (no trained best.pt in the reference)",
+            "config": {"workload": f"YOLOv8{a.scale}+P2 640x512, {S} streams/GPU as batch {S}, "
+                                   f"{a.targets} targets/stream, tracker(150, 1, 0.1) (BASELINE config 3)",
+                       "streams_per_gpu": S, "global_batch": S * ws, "parallelism": f"streams sharded over {ws} GPU(s)",
+                       "graph": not a.no_graph, "live_tracks_per_stream": round(live, 1),
+                       "gflop_per_frame": round(gflop, 3)},
+            "network_mfma_frac": round(fps / ws * gflop / 1e3 / PEAK[a.dtype], 5),
+            "pcie_inclusive_fps": round(pcie_fps * ws, 2),
+            "roofline": rl, "tracker_roofline": trl, "cpu_baseline": cpu,
+        }
+        print(json.dumps(out))
+    if ws > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

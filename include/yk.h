@@ -252,6 +252,16 @@ int yk_model_outputs(yk_model* m, float** dev_dets, int32_t** dev_counts);
  * counts per image (parity harnesses compare them to the oracle's Detect output). */
 int yk_model_candidates(yk_model* m, float** dev_cand, int32_t** dev_counts);
 
+/* Per-op device time: launches every op of the program `reps` times back to back between two
+ * hipEvents on `stream` and writes the average milliseconds per launch to host_ms[op]
+ * (host_ms[n_ops] = the NMS kernel).  Outputs of the call are not meaningful. */
+int yk_model_profile(yk_model* m, const uint8_t* dev_frames, int batch, float conf, float iou, int max_det,
+                     int reps, float* host_ms, void* stream);
+
+/* Kernel instantiation launched by op `op_index` (n_ops -> the NMS kernel), as rocprofv3
+ * names it (substring of the demangled name). */
+int yk_model_op_kernel(yk_model* m, int op_index, char* buf, int len);
+
 /* Device pointer of activation buffer `buf` (debug / parity). */
 int yk_model_buffer(yk_model* m, int buf, void** dev_ptr);
 

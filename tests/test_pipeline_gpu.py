@@ -1,0 +1,95 @@
+"""End-to-end GPU parity: frames in HBM -> detector -> NMS -> tracker (device hand-off),
+against the oracle chain (torch-CPU detector -> numpy tracker) per stream, plus the
+reference driver's loop through the compat ``ultralytics`` / ``kalman`` packages."""
+import importlib
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import REPO, pkg
+from oracle import detector_ref as D
+from oracle.tracker_ref import RefMultiTracker
+
+pytestmark = pytest.mark.gpu
+
+
+def _layers(ar):
+    return [(Ly.i, Ly.f, Ly.kind, {**Ly.args, **({"c": int(Ly.c2 * 0.5)} if Ly.kind == "C2f" else {})})
+            for Ly in ar.layers]
+
+
+def _trk_dicts(P, rows, n):
+    return [P.tracker._row_to_dict(r, P.tracker.track_id_of(r["track_num"])) for r in rows[:n]]
+
+
+def test_stream_pipeline_fp32_matches_oracle_chain():
+    P = pkg()
+    pipeline = importlib.import_module(P.__name__ + ".pipeline")
+    S, F = 2, 10
+    pipe = pipeline.StreamPipeline("yolov8-small.yaml", S, (512, 640), "fp32", seed=0, max_tracks=256)
+    ar = pipe.prog.ar
+    ref = D.RefDetector(_layers(ar), pipe.prog.sd, P.arch.detect_strides(ar))
+    scenes = [P.synth.Scene(seed=20 + s, n_targets=20, n_frames=F) for s in range(S)]
+    refs = [RefMultiTracker(150, 1, 0.1, stable_ties=True) for _ in range(S)]
+    torch.set_num_threads(8)
+    for t in range(F):
+        fr = [sc.frame(t) for sc in scenes]
+        pipe.run(torch.from_numpy(np.stack(fr)).cuda())
+        rows, counts, _ = pipe.tracker.download()
+        want, _ = D.predict(ref, fr)
+        for s in range(S):
+            dets = [[b[0], b[1], b[2], b[3], b[4]] for b in want[s][:, :5].numpy()]
+            rb = refs[s].update(dets)
+            ours = _trk_dicts(P, rows[s], int(counts[s]))
+            assert [o["track_id"] for o in ours] == [r["track_id"] for r in rb], (t, s)
+            for o, r in zip(ours, rb):
+                assert (o["status"], o["age"], o["hits"], o["time_since_update"]) == \
+                    (r["status"], r["age"], r["hits"], r["time_since_update"])
+                np.testing.assert_allclose(o["bbox"], r["bbox"], rtol=1e-4, atol=1e-3)
+                np.testing.assert_allclose(o["confidence"], r["confidence"], rtol=1e-4)
+
+
+def test_reference_driver_loop_through_compat_packages():
+    """The per-frame body of kalman/aircraft_detection_tracking.py:88-131 with the compat
+    imports; video I/O and drawing (cv2) replaced by synthetic frames."""
+    sys.path.insert(0, os.path.join(REPO, pkg().__name__, "compat"))
+    try:
+        from kalman.enhanced_multi_target_tracker import EnhancedMultiTargetTracker
+        from kalman.trajectory_visualizer import TrajectoryVisualizer
+        from ultralytics import YOLO
+    finally:
+        sys.path.pop(0)
+    P = pkg()
+    model = YOLO("yolov8s-small.yaml")
+    tracker = EnhancedMultiTargetTracker(max_lost_frames=150, min_hits=1, iou_threshold=0.1)
+    vis = TrajectoryVisualizer()
+    sc = P.synth.Scene(seed=4, n_targets=12, n_frames=8)
+    detection_frames = prediction_frames = state_changes = 0
+    last = {}
+    for t in range(8):
+        frame = sc.frame(t)
+        results = model(frame, verbose=False)
+        detections = []
+        if len(results) > 0 and results[0].boxes is not None:
+            boxes = results[0].boxes.xyxy.cpu().numpy()
+            scores = results[0].boxes.conf.cpu().numpy()
+            for box, score in zip(boxes, scores):
+                if score > 0.1:
+                    detections.append([box[0], box[1], box[2], box[3], score])
+        assert all(isinstance(v, np.float32) for d in detections for v in d)
+        tracks = tracker.update(detections)
+        cur = {}
+        for tr in tracks:
+            cur[tr["track_id"]] = tr["status"]
+            if tr["track_id"] in last and last[tr["track_id"]] != tr["status"]:
+                state_changes += 1
+            detection_frames += tr["status"] == "detected"
+            prediction_frames += tr["status"] == "predicted"
+        last = cur
+        assert vis.draw_tracks(frame, tracks, detections, {}) is frame
+    assert detection_frames > 0
+    assert tracker.frame_count == 8
+    assert results[0].boxes.xyxy.is_cuda and results[0].orig_shape == (512, 640)

@@ -78,6 +78,8 @@ _SIGS = {
     "yk_model_candidates": ([_vp, C.POINTER(_vp), C.POINTER(_vp)], C.c_int),
     "yk_model_buffer": ([_vp, C.c_int, C.POINTER(_vp)], C.c_int),
     "yk_memcpy_d2h": ([_vp, _vp, C.c_int64], C.c_int),
+    "yk_model_profile": ([_vp, _vp, C.c_int, C.c_float, C.c_float, C.c_int, C.c_int, _vp, _vp], C.c_int),
+    "yk_model_op_kernel": ([_vp, C.c_int, C.c_char_p, C.c_int], C.c_int),
 }
 
 _lock = threading.Lock()

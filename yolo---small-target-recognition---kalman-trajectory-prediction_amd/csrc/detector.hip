@@ -615,9 +615,9 @@ void launch_conv(const ConvArgs& a, hipStream_t st) {
 }
 
 template <class Tr>
-int run_ops(yk_model* m, const uint8_t* frames, int B, float conf, hipStream_t st) {
+int launch_op(yk_model* m, const yk_op& op, const uint8_t* frames, int B, float conf, hipStream_t st) {
   const yk_model_desc& D = m->desc;
-  for (const yk_op& op : m->ops) {
+  {
     switch (op.kind) {
       case YK_K_CONV_INPUT: {
         InputArgs a;
@@ -707,6 +707,41 @@ int run_ops(yk_model* m, const uint8_t* frames, int B, float conf, hipStream_t s
   return YK_OK;
 }
 
+template <class Tr>
+int run_ops(yk_model* m, const uint8_t* frames, int B, float conf, hipStream_t st) {
+  for (const yk_op& op : m->ops) {
+    const int rc = launch_op<Tr>(m, op, frames, B, conf, st);
+    if (rc != YK_OK) return rc;
+  }
+  return YK_OK;
+}
+
+int launch_any(yk_model* m, const yk_op& op, const uint8_t* frames, int B, float conf, hipStream_t st) {
+  return m->desc.act_dtype == YK_ACT_F32 ? launch_op<F32>(m, op, frames, B, conf, st)
+                                         : launch_op<BF16>(m, op, frames, B, conf, st);
+}
+
+// Name of the kernel instantiation an op launches (matches rocprofv3's demangled names).
+const char* op_kernel_name(const yk_model* m, const yk_op& op) {
+  const bool f = m->desc.act_dtype == YK_ACT_F32;
+  switch (op.kind) {
+    case YK_K_CONV_INPUT: return f ? "conv_input_kernel<yk::det::F32>" : "conv_input_kernel<yk::det::BF16>";
+    case YK_K_SPPF_POOL: return f ? "sppf_pool_kernel<yk::det::F32>" : "sppf_pool_kernel<yk::det::BF16>";
+    case YK_K_DETECT: return f ? "detect_kernel<yk::det::F32>" : "detect_kernel<yk::det::BF16>";
+    default: break;
+  }
+  const int nt = op.n_tiles;
+  const int nnt = nt <= 1 ? 1 : nt == 2 ? 2 : (nt == 3 || nt == 6 || nt == 9) ? 3 : 4;
+  static const char* names[2][4] = {
+      {"conv_igemm_kernel<yk::det::BF16, 1, 2>", "conv_igemm_kernel<yk::det::BF16, 2, 2>",
+       "conv_igemm_kernel<yk::det::BF16, 3, 2>", "conv_igemm_kernel<yk::det::BF16, 4, 2>"},
+      {"conv_igemm_kernel<yk::det::F32, 1, 2>", "conv_igemm_kernel<yk::det::F32, 2, 2>",
+       "conv_igemm_kernel<yk::det::F32, 3, 2>", "conv_igemm_kernel<yk::det::F32, 4, 2>"}};
+  return names[f ? 1 : 0][nnt - 1];
+}
+
+int launch_nms(yk_model* m, int B, float iou, int max_det, float* dets, int32_t* counts, hipStream_t st);
+
 int detect_impl(yk_model* m, const uint8_t* frames, int B, float conf, float iou, int max_det, float* dets,
                 int32_t* counts, hipStream_t st) {
   const yk_model_desc& D = m->desc;
@@ -720,6 +755,11 @@ int detect_impl(yk_model* m, const uint8_t* frames, int B, float conf, float iou
   YK_HIP(hipMemsetAsync(m->cand_count, 0, sizeof(int) * B, st));
   int rc = D.act_dtype == YK_ACT_F32 ? run_ops<F32>(m, frames, B, conf, st) : run_ops<BF16>(m, frames, B, conf, st);
   if (rc != YK_OK) return rc;
+  return launch_nms(m, B, iou, max_det, dets, counts, st);
+}
+
+int launch_nms(yk_model* m, int B, float iou, int max_det, float* dets, int32_t* counts, hipStream_t st) {
+  const yk_model_desc& D = m->desc;
   NmsArgs a;
   a.cand = m->cand;
   a.cand_count = m->cand_count;
@@ -865,6 +905,52 @@ int yk_detect_graph(yk_model* m, const uint8_t* frames, int batch, float conf, f
     it = m->graphs.emplace(key, ge).first;
   }
   YK_HIP(hipGraphLaunch(it->second, st));
+  return YK_OK;
+}
+
+int yk_model_profile(yk_model* m, const uint8_t* frames, int batch, float conf, float iou, int max_det, int reps,
+                     float* host_ms, void* stream) {
+  YK_CHECK_ARG(m && frames && host_ms && reps >= 1, "yk_model_profile: bad argument");
+  YK_CHECK_ARG(batch >= 1 && batch <= m->desc.max_batch, "yk_model_profile: batch out of range");
+  YK_CHECK_ARG(max_det >= 1 && max_det <= m->desc.max_det, "yk_model_profile: max_det out of range");
+  yk::DeviceGuard guard(m->ctx->device);
+  hipStream_t st = (hipStream_t)stream;
+  hipEvent_t e0, e1;
+  YK_HIP(hipEventCreate(&e0));
+  YK_HIP(hipEventCreate(&e1));
+  const int n = (int)m->ops.size();
+  for (int i = 0; i <= n; ++i) {
+    if (i < n && m->ops[i].kind == YK_K_DETECT) YK_HIP(hipMemsetAsync(m->cand_count, 0, sizeof(int) * batch, st));
+    if (i == n) YK_HIP(hipMemsetAsync(m->cand_count, 0, sizeof(int) * batch, st));
+    if (i == n) {  // rebuild the candidate lists once so NMS sees a real input
+      for (const yk_op& op : m->ops)
+        if (op.kind == YK_K_DETECT) {
+          int rc = launch_any(m, op, frames, batch, conf, st);
+          if (rc != YK_OK) return rc;
+        }
+    }
+    YK_HIP(hipEventRecord(e0, st));
+    for (int r = 0; r < reps; ++r) {
+      int rc = i < n ? launch_any(m, m->ops[i], frames, batch, conf, st)
+                     : launch_nms(m, batch, iou, max_det, m->dets, m->counts, st);
+      if (rc != YK_OK) return rc;
+    }
+    YK_HIP(hipEventRecord(e1, st));
+    YK_HIP(hipEventSynchronize(e1));
+    float ms = 0.f;
+    YK_HIP(hipEventElapsedTime(&ms, e0, e1));
+    host_ms[i] = ms / reps;
+  }
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  return YK_OK;
+}
+
+int yk_model_op_kernel(yk_model* m, int op_index, char* buf, int len) {
+  YK_CHECK_ARG(m && buf && len > 0, "yk_model_op_kernel: bad argument");
+  YK_CHECK_ARG(op_index >= 0 && op_index <= (int)m->ops.size(), "yk_model_op_kernel: index out of range");
+  const char* nm = op_index == (int)m->ops.size() ? "nms_kernel" : op_kernel_name(m, m->ops[op_index]);
+  snprintf(buf, (size_t)len, "%s", nm);
   return YK_OK;
 }
 

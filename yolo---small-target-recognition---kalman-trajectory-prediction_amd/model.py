@@ -119,6 +119,7 @@ class Program:
         self.ops: list[Op] = []
         self.blob = bytearray()
         self.layer_out: dict[int, list[Seg]] = {}
+        self.op_meta: list[int] = []  # MACs per image of each op
         self.n_anchors = 0
         self._build()
 
@@ -217,6 +218,7 @@ class Program:
         op.b_off = self.add_blob(bias)
         op.t_off = self.add_blob(tab)
         self.ops.append(op)
+        self.op_meta.append(op.out_h * op.out_w * w.shape[0] * w.shape[1] * k * k)
         return op
 
     # -- graph lowering ------------------------------------------------------------
@@ -250,6 +252,7 @@ class Program:
                 op.b_off = self.add_blob(B0)
                 op.t_off = op.b_off
                 self.ops.append(op)
+                self.op_meta.append(oh * ow * Ly.c2 * 3 * k * k)
                 out = [Seg(buf, 0, cp, cp, Ly.c2, oh, ow)]
             elif Ly.kind == "Conv":
                 src = inp(Ly.f)
@@ -318,6 +321,7 @@ class Program:
         op.out_h, op.out_w = hh, ww
         assert Ly.args["k"] == 5
         self.ops.append(op)
+        self.op_meta.append(0)
         c2p = phys(Ly.c2)
         ob = self.new_buf(hh, ww, c2p)
         dst = Seg(ob, 0, c2p, c2p, Ly.c2, hh, ww)
@@ -369,9 +373,18 @@ class Program:
             op.det_cls_ch = c3p
             op.det_wc_off = self.add_blob(wc)
             self.ops.append(op)
+            self.op_meta.append(hh * ww * (64 * 64 + c3))
             anchor_off += hh * ww
         self.n_anchors = anchor_off
         return []
+
+    def op_flops(self, B: int) -> list:
+        """Algorithmic FLOPs of each op for a batch of B frames (2*MACs of the reference's
+        logical, unpadded conv; 0 for pooling; the Detect op counts its 1x1 box/cls convs)."""
+        out = []
+        for op, meta in zip(self.ops, self.op_meta):
+            out.append(2 * B * meta)
+        return out + [0]
 
     # -- device model ----------------------------------------------------------------
     def desc(self):
@@ -438,6 +451,22 @@ class DeviceModel:
         L.check(fn(self._h, L.ptr(frames), int(B), C.c_float(conf), C.c_float(iou), int(max_det), L.ptr(dets),
                    L.ptr(counts), st), "yk_detect")
         return dets, counts
+
+    def profile(self, frames: torch.Tensor, conf=0.25, iou=0.7, max_det=300, reps: int = 5):
+        """Per-op device milliseconds (hipEvents, `reps` back-to-back launches each) and the
+        kernel instantiation each op launches.  Returns list of (op_index, kind, kernel, ms)."""
+        n = len(self.prog.ops)
+        ms = np.zeros(n + 1, np.float32)
+        B = frames.shape[0]
+        L.check(L.lib().yk_model_profile(self._h, L.ptr(frames), int(B), C.c_float(conf), C.c_float(iou), int(max_det),
+                                         int(reps), L.ptr(ms), L.current_stream(self.device)), "yk_model_profile")
+        out = []
+        buf = C.create_string_buffer(128)
+        for i in range(n + 1):
+            L.check(L.lib().yk_model_op_kernel(self._h, i, buf, 128), "yk_model_op_kernel")
+            kind = self.prog.ops[i].kind if i < n else -1
+            out.append((i, kind, buf.value.decode(), float(ms[i])))
+        return out
 
     def candidates(self, B: int):
         """Pre-NMS candidates of the last detect() as a [B, n_anchors, 6] view + counts (copies)."""

@@ -1,0 +1,78 @@
+"""End-to-end detect-and-track step for S independent video streams on one GPU.
+
+One step = the reference driver's per-frame body (kalman/aircraft_detection_tracking.py:96-109)
+for every stream at once: ``model(frame)`` for S frames as one batch (yk_detect), then one
+``tracker.update(detections)`` per stream (yk_tracker_step, one workgroup per stream), with
+the NMS output handed to the tracker in HBM (rows [x1, y1, x2, y2, conf, cls] float32, the
+reference's np.float32 detections).  The driver's ``score > 0.1`` filter (:105) is a no-op
+at conf >= 0.1 and is checked, not executed.  The whole step is captured in one hipGraph.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import arch as A
+from . import model as M
+from . import tracker as T
+from . import weights as Wt
+
+
+class StreamPipeline:
+    def __init__(self, model_cfg: str = "yolov8s-small.yaml", n_streams: int = 8, frame_hw=(512, 640),
+                 dtype: str = "bf16", weights=None, seed: int = 0, conf: float = 0.25, iou: float = 0.7,
+                 max_det: int = 300, max_lost_frames: int = 150, min_hits: int = 1, iou_threshold: float = 0.1,
+                 max_tracks: int = 512, device: int = 0):
+        if conf < 0.1:
+            raise ValueError("conf < 0.1 would need the driver's score > 0.1 filter on the device path")
+        self.S, self.device = int(n_streams), int(device)
+        self.conf, self.iou, self.max_det = float(conf), float(iou), int(max_det)
+        ar = A.parse_arch(A.load_model_dict(model_cfg))
+        sd = weights if weights is not None else Wt.synthetic_state_dict(ar, seed)
+        self.prog = M.Program(ar, sd, frame_hw[0], frame_hw[1], 640, self.S, dtype, self.max_det)
+        self.model = M.DeviceModel(self.prog, self.device)
+        self.tracker = T.MultiStreamTracker(self.S, max_lost_frames, min_hits, iou_threshold, max_tracks,
+                                            self.max_det, self.device)
+        dev = torch.device("cuda", self.device)
+        self.frames = torch.zeros((self.S, frame_hw[0], frame_hw[1], 3), dtype=torch.uint8, device=dev)
+        self.dets = torch.zeros((self.S, self.max_det, 6), dtype=torch.float32, device=dev)
+        self.counts = torch.zeros(self.S, dtype=torch.int32, device=dev)
+        self.graph = None
+
+    def step_eager(self):
+        self.model.detect(self.frames, self.conf, self.iou, self.max_det, self.dets, self.counts)
+        self.tracker.step_device(self.dets, self.counts)
+
+    def capture(self):
+        """Capture one step (detect + NMS + tracker) into a hipGraph on a side stream."""
+        s = torch.cuda.Stream(self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(s):
+            self.step_eager()  # warm: lazy allocations / function attributes before capture
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        torch.cuda.synchronize(self.device)
+        self.tracker.reset()
+        torch.cuda.synchronize(self.device)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            self.step_eager()
+        self.graph = g
+        return g
+
+    def step(self):
+        if self.graph is not None:
+            self.graph.replay()
+        else:
+            self.step_eager()
+
+    def run(self, frames: torch.Tensor):
+        """frames [S, H, W, 3] uint8 (device) -> one step."""
+        self.frames.copy_(frames, non_blocking=True)
+        self.step()
+
+    def stats(self):
+        _, counts, stats = self.tracker.download()
+        return counts.copy(), stats.copy()
+
+    def flops_per_frame(self) -> int:
+        return int(sum(self.prog.op_flops(1)))

@@ -1,0 +1,228 @@
+"""Device-backed mirror of ``ultralytics.YOLO`` for the detection predict path.
+
+Reference surface (ultralytics/engine/model.py:82-188, 498-557; engine/results.py:240-290,
+855-980): ``YOLO(model)`` from a model YAML (scale from the file name, tasks.py:1703-1740)
+or a weights file; ``model(source, **kw)`` == ``model.predict(source, **kw)`` returning a
+list of ``Results`` whose ``boxes.xyxy / .conf / .cls / .data`` are float32 tensors on the
+model's device (so ``.cpu().numpy()`` works as in kalman/aircraft_detection_tracking.py:101-102).
+Defaults follow the predictor's effective values: conf 0.25 (model.py:544), iou 0.7,
+max_det 300, imgsz 640 (cfg/default.yaml).
+
+Everything from the uint8 frame to the NMS output runs in libyk.so (csrc/detector.hip);
+this module stages frames into HBM, keeps one compiled program per frame geometry and
+wraps the outputs.  A per-predictor lock mirrors BasePredictor's (predictor.py:149,304).
+"""
+from __future__ import annotations
+
+import os
+import threading
+import time
+
+import numpy as np
+import torch
+
+from . import _lib as L
+from . import arch as A
+from . import model as M
+from . import weights as Wt
+
+
+class Boxes:
+    """engine/results.py Boxes: data (N, 6) = x1, y1, x2, y2, conf, cls."""
+
+    def __init__(self, boxes, orig_shape):
+        if boxes.ndim == 1:
+            boxes = boxes[None, :]
+        n = boxes.shape[-1]
+        assert n in {6, 7}, f"expected 6 or 7 values but got {n}"
+        self.data = boxes
+        self.orig_shape = orig_shape
+        self.is_track = n == 7
+
+    def __len__(self):
+        return len(self.data)
+
+    def __getitem__(self, idx):
+        return Boxes(self.data[idx], self.orig_shape)
+
+    @property
+    def shape(self):
+        return self.data.shape
+
+    @property
+    def xyxy(self):
+        return self.data[:, :4]
+
+    @property
+    def conf(self):
+        return self.data[:, -2]
+
+    @property
+    def cls(self):
+        return self.data[:, -1]
+
+    @property
+    def id(self):
+        return self.data[:, -3] if self.is_track else None
+
+    @property
+    def xywh(self):
+        b = self.xyxy
+        return torch.cat(((b[:, :2] + b[:, 2:]) / 2, b[:, 2:] - b[:, :2]), 1)
+
+    @property
+    def xyxyn(self):
+        b = self.xyxy.clone()
+        b[:, [0, 2]] /= self.orig_shape[1]
+        b[:, [1, 3]] /= self.orig_shape[0]
+        return b
+
+    def cpu(self):
+        return Boxes(self.data.cpu(), self.orig_shape)
+
+    def numpy(self):
+        return Boxes(self.data.cpu().numpy(), self.orig_shape)
+
+    def cuda(self):
+        return Boxes(self.data.cuda(), self.orig_shape)
+
+    def to(self, *a, **k):
+        return Boxes(self.data.to(*a, **k), self.orig_shape)
+
+
+class Results:
+    """engine/results.py Results for detection: orig_img, orig_shape, boxes, names, path, speed."""
+
+    def __init__(self, orig_img, path, names, boxes=None, speed=None):
+        self.orig_img = orig_img
+        self.orig_shape = orig_img.shape[:2]
+        self.boxes = Boxes(boxes, self.orig_shape) if boxes is not None else None
+        self.masks = self.probs = self.keypoints = self.obb = None
+        self.speed = speed if speed is not None else {"preprocess": None, "inference": None, "postprocess": None}
+        self.names = names
+        self.path = path
+        self.save_dir = None
+
+    def __len__(self):
+        return 0 if self.boxes is None else len(self.boxes)
+
+    def cpu(self):
+        return Results(self.orig_img, self.path, self.names, None if self.boxes is None else self.boxes.data.cpu(),
+                       self.speed)
+
+
+class YOLO:
+    """YOLO(model='yolov8s-small.yaml') -> detector executed by libyk.so.
+
+    ``weights``: None (seeded synthetic weights in the reference's shapes), a
+    state dict in the reference's naming, or a path to one saved with torch.save (loaded
+    with weights_only=True).  ``dtype``: 'bf16' (production) or 'fp32' (exact-f32 MFMA,
+    parity).  Pickled ultralytics checkpoints (best.pt) need the ultralytics classes and
+    are not loaded."""
+
+    def __init__(self, model: str = "yolov8s-small.yaml", task=None, verbose: bool = False, *, weights=None,
+                 dtype: str = "bf16", device: int = 0, seed: int = 0, max_batch: int = 8):
+        if task not in (None, "detect"):
+            raise NotImplementedError(f"task {task!r}: only detection is on this path")
+        if str(model).endswith(".pt"):
+            if weights is not None:
+                raise ValueError("give either a .pt model or weights=, not both")
+            weights, model = model, os.environ.get("YK_MODEL_CFG", "yolov8s-small.yaml")
+        self.cfg = str(model)
+        self.arch = A.parse_arch(A.load_model_dict(self.cfg))
+        if weights is None:
+            sd = Wt.synthetic_state_dict(self.arch, seed)
+        elif isinstance(weights, dict):
+            sd = weights
+        else:
+            sd = torch.load(weights, map_location="cpu", weights_only=True)
+            if not isinstance(sd, dict) or not any(k.startswith("model.") for k in sd):
+                raise ValueError(f"{weights}: expected a state dict with 'model.*' keys")
+        self.state_dict = sd
+        self.dtype, self.device, self.max_batch = dtype, int(device), int(max_batch)
+        self.names = {i: f"class{i}" for i in range(self.arch.nc)}
+        if self.arch.nc == 1:
+            self.names = {0: "aircraft"}
+        self.task = "detect"
+        self.overrides = {"conf": 0.25, "iou": 0.7, "max_det": 300, "imgsz": 640}
+        self._engines = {}
+        self._lock = threading.Lock()
+        self._staging = None
+
+    # -- engines ------------------------------------------------------------------
+    def engine(self, frame_h: int, frame_w: int, imgsz=640, max_det: int = 300) -> M.DeviceModel:
+        key = (frame_h, frame_w, imgsz if isinstance(imgsz, int) else tuple(imgsz), max_det)
+        e = self._engines.get(key)
+        if e is None:
+            prog = M.Program(self.arch, self.state_dict, frame_h, frame_w, imgsz, self.max_batch, self.dtype, max_det)
+            e = M.DeviceModel(prog, self.device)
+            self._engines[key] = e
+        return e
+
+    # -- predict --------------------------------------------------------------------
+    def __call__(self, source=None, stream: bool = False, **kwargs):
+        return self.predict(source, stream, **kwargs)
+
+    def predict(self, source=None, stream: bool = False, conf=None, iou=None, imgsz=None, max_det=None,
+                classes=None, agnostic_nms=False, half=False, device=None, verbose=False, batch=1, **kwargs):
+        conf = self.overrides["conf"] if conf is None else conf
+        iou = self.overrides["iou"] if iou is None else iou
+        imgsz = self.overrides["imgsz"] if imgsz is None else imgsz
+        max_det = self.overrides["max_det"] if max_det is None else max_det
+        assert 0 <= conf <= 1, f"Invalid Confidence threshold {conf}, valid values are between 0.0 and 1.0"
+        assert 0 <= iou <= 1, f"Invalid IoU {iou}, valid values are between 0.0 and 1.0"
+        frames = self._frames(source)
+        with self._lock:
+            out = []
+            for i in range(0, len(frames), self.max_batch):
+                out.extend(self._predict_batch(frames[i:i + self.max_batch], conf, iou, imgsz, max_det, classes))
+        return iter(out) if stream else out
+
+    @staticmethod
+    def _frames(source):
+        if isinstance(source, np.ndarray):
+            return [source]
+        if isinstance(source, (list, tuple)) and all(isinstance(s, np.ndarray) for s in source):
+            return list(source)
+        raise NotImplementedError("source must be an HxWx3 uint8 BGR ndarray or a list of them "
+                                  "(file/video/stream loaders are outside the hot path)")
+
+    def _predict_batch(self, frames, conf, iou, imgsz, max_det, classes):
+        shapes = {f.shape for f in frames}
+        if len(shapes) != 1:
+            out = []
+            for f in frames:
+                out.extend(self._predict_batch([f], conf, iou, imgsz, max_det, classes))
+            return out
+        h, w, c = frames[0].shape
+        if c != 3 or frames[0].dtype != np.uint8:
+            raise ValueError("frames must be uint8 HxWx3 (BGR)")
+        t0 = time.perf_counter()
+        eng = self.engine(h, w, imgsz, max(max_det, 1))
+        B = len(frames)
+        host = torch.from_numpy(np.ascontiguousarray(np.stack(frames)))
+        dev = host.to(f"cuda:{self.device}", non_blocking=False)
+        t1 = time.perf_counter()
+        dets, counts = eng.detect(dev, conf, iou, max(max_det, 1))
+        cnt = counts.cpu().tolist()
+        t2 = time.perf_counter()
+        res = []
+        for b in range(B):
+            n = min(int(cnt[b]), max_det)
+            d = dets[b, :n]
+            if classes is not None:
+                keep = torch.isin(d[:, 5], torch.tensor(classes, dtype=d.dtype, device=d.device))
+                d = d[keep]
+            res.append(Results(frames[b], f"image{b}.jpg", self.names, boxes=d))
+        t3 = time.perf_counter()
+        sp = {"preprocess": (t1 - t0) * 1e3 / B, "inference": (t2 - t1) * 1e3 / B, "postprocess": (t3 - t2) * 1e3 / B}
+        for r in res:
+            r.speed = sp
+        return res
+
+    def fuse(self, verbose=True):
+        return self  # Conv+BN is always fused at program build (weights.fuse_conv_bn)
+
+    def info(self, verbose=True):
+        n = sum(v.numel() for k, v in self.state_dict.items() if not k.endswith("num_batches_tracked"))
+        return {"layers": len(self.arch.layers), "parameters": n, "scale": self.arch.scale}

@@ -20,8 +20,8 @@ from . import arch as A
 BN_EPS = 1e-3  # initialize_weights (ultralytics/utils/torch_utils.py:488-498)
 
 
-def synthetic_state_dict(ar: A.Arch, seed: int = 0, planted: bool = True, box_bins: float = 6.0,
-                         p2_gain: float = 1.0, p2_threshold: float = 3.0, dog: float = 2.0) -> dict:
+def synthetic_state_dict(ar: A.Arch, seed: int = 0, planted: bool = True, box_bins: float = 12.0,
+                         p2_gain: float = 1.0, p2_threshold: float = 5.0, dog: float = 1.0) -> dict:
     g = torch.Generator().manual_seed(seed)
 
     def rn(*shape, std=1.0):
