@@ -46,6 +46,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-profile", action="store_true")
+    ap.add_argument("--dump-ops", default="", help="write per-op device times (json) to this path")
     return ap.parse_args()
 
 
@@ -206,8 +207,13 @@ def main():
     rl = None
     trl = None
     if rank == 0 and not a.no_profile:
-        rl, _, _ = roofline(pipe, frames[0], a.dtype, S)
+        rl, by_kernel, prof = roofline(pipe, frames[0], a.dtype, S)
         trl = tracker_roofline(pipe)
+        if a.dump_ops:
+            flops = pipe.prog.op_flops(S)
+            with open(a.dump_ops, "w") as f:
+                json.dump({"ops": [{"op": i, "kind": k, "kernel": n, "us": round(ms * 1e3, 2), "gflop": fl / 1e9}
+                                   for (i, k, n, ms), fl in zip(prof, flops)], "by_kernel": by_kernel}, f, indent=1)
     cpu = None
     if rank == 0 and ws == 1 and not a.no_cpu_baseline:
         cpu = cpu_baseline(P, a.scale, a.cpu_seconds)

@@ -21,6 +21,7 @@
 #include <hip/hip_runtime.h>
 
 #include <climits>
+#include <cstdlib>
 #include <map>
 #include <tuple>
 #include <vector>
@@ -217,6 +218,163 @@ __global__ void __launch_bounds__(256) conv_igemm_kernel(ConvArgs a) {
   }
 }
 
+// ---------------------------------------------------------------- LDS-tiled implicit-GEMM conv
+// One workgroup = a 16-column x TH-row output tile of one image for NNT x 16 output channels.
+// The input tile with its halo (all K-space channels of both sources, upsample applied) is
+// staged once into LDS with an odd number of 16-byte slots per pixel (conflict-free
+// ds_read_b128 for 16 consecutive pixels); weights stream through LDS in chunks of KCH K-steps
+// shared by the four waves.  Wave w computes output rows [w*NPT, (w+1)*NPT) of the tile.
+constexpr int KCH = 4;
+
+struct TileArgs {
+  View src[2];
+  int c0, cin;               // K-space channels of src[0]; total (multiple of 8)
+  int ksize, stride, pad;
+  int in_h, in_w, out_h, out_w;
+  int tiles_x, tiles_y, tih, tiw, ps;  // tile grid per image; input tile dims; LDS pixel stride (elements)
+  const uint4* wpk;
+  const float* bias;
+  const int* tab;
+  int k_steps, n_tiles, n_chunks;
+  void* dst;
+  int d_cstride, d_coff, cout;
+  const void* res;
+  int r_cstride, r_coff;
+  int act;
+};
+
+template <class Tr, int NNT, int NPT>
+__global__ void __launch_bounds__(256) conv_tile_kernel(TileArgs a) {
+  using T = typename Tr::T;
+  constexpr int EPL = Tr::EPL;
+  constexpr int EU = 16 / (int)sizeof(T);   // elements per 16-byte unit
+  constexpr int WU = NNT * KCH * 64;        // 16-byte weight units per chunk
+  constexpr int WPT = (WU + 255) / 256;     // per thread
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  uint4* wl = (uint4*)smem;                                  // [2][NNT][KCH][64] double-buffered chunks
+  T* xt = (T*)(smem + (size_t)2 * WU * 16);                  // [tih][tiw][ps]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int kg = lane >> 4, col = lane & 15;
+  const int tpi = a.tiles_x * a.tiles_y;
+  int t = blockIdx.x;
+  const int b = t / tpi;
+  t -= b * tpi;
+  const int ty0 = (t / a.tiles_x) * (4 * NPT), tx0 = (t % a.tiles_x) * 16;
+  const int iy0 = ty0 * a.stride - a.pad, ix0 = tx0 * a.stride - a.pad;
+  const int nt0 = blockIdx.y * NNT;
+  uint4 wreg[WPT];
+  auto fetch = [&](int k0) {  // global -> registers (stays in flight over the compute)
+#pragma unroll
+    for (int r = 0; r < WPT; ++r) {
+      const int i = tid + r * 256;
+      if (i < WU) {
+        const int j = i >> 6, l = i & 63;
+        const int ni = j / KCH, kk = j - ni * KCH;
+        const int nt = nt0 + ni < a.n_tiles ? nt0 + ni : a.n_tiles - 1;
+        const int ks = k0 + kk;
+        wreg[r] = ks < a.k_steps ? a.wpk[((size_t)nt * a.k_steps + ks) * 64 + l] : make_uint4(0u, 0u, 0u, 0u);
+      }
+    }
+  };
+  auto commit = [&](int buf) {
+#pragma unroll
+    for (int r = 0; r < WPT; ++r) {
+      const int i = tid + r * 256;
+      if (i < WU) wl[buf * WU + i] = wreg[r];
+    }
+  };
+  fetch(0);
+  // ---- stage the input tile (zero outside the image = conv zero padding)
+  {
+    const int U = a.cin / EU;
+    const int total = a.tih * a.tiw * U;
+    for (int i = tid; i < total; i += 256) {
+      const int pix = i / U, u = i - pix * U;
+      const int ry = pix / a.tiw, rx = pix - ry * a.tiw;
+      const int iy = iy0 + ry, ix = ix0 + rx;
+      const int c = u * EU;
+      uint4 v = make_uint4(0u, 0u, 0u, 0u);
+      if (iy >= 0 && iy < a.in_h && ix >= 0 && ix < a.in_w) {
+        const int si = c < a.c0 ? 0 : 1;
+        const View& sv = a.src[si];
+        const int cc = si ? c - a.c0 : c;
+        v = *(const uint4*)((const T*)sv.p +
+                            (((size_t)b * sv.h + (iy >> sv.up)) * sv.w + (ix >> sv.up)) * sv.cstride + sv.coff + cc);
+      }
+      *(uint4*)(xt + (size_t)pix * a.ps + c) = v;
+    }
+  }
+  commit(0);
+  __syncthreads();
+  f32x4 acc[NNT][NPT];
+#pragma unroll
+  for (int i = 0; i < NNT; ++i)
+#pragma unroll
+    for (int q = 0; q < NPT; ++q) acc[i][q] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int s = a.stride;
+  int buf = 0;
+  for (int k0 = 0; k0 < a.k_steps; k0 += KCH) {
+    const bool more = k0 + KCH < a.k_steps;
+    if (more) fetch(k0 + KCH);
+    const uint4* wc = wl + buf * WU;
+    const int kn = a.k_steps - k0 < KCH ? a.k_steps - k0 : KCH;
+    for (int kk = 0; kk < kn; ++kk) {
+      const int kel = (k0 + kk) * 4 * EPL + kg * EPL;
+      const int q = kel >> 3, sub = kel & 7;
+      const int e = q < a.n_chunks ? a.tab[q] : -1;
+      uint4 xf[NPT];
+      if (e >= 0) {
+        const int kx = ((e >> 21) & 15) - 8 + a.pad, ky = ((e >> 17) & 15) - 8 + a.pad;
+        const int cK = (e & 0xffff) + (((e >> 16) & 1) ? a.c0 : 0) + sub;
+#pragma unroll
+        for (int pt = 0; pt < NPT; ++pt) {
+          const int ty = wave * NPT + pt;
+          xf[pt] = *(const uint4*)(xt + (size_t)((ty * s + ky) * a.tiw + col * s + kx) * a.ps + cK);
+        }
+      } else {
+#pragma unroll
+        for (int pt = 0; pt < NPT; ++pt) xf[pt] = make_uint4(0u, 0u, 0u, 0u);
+      }
+#pragma unroll
+      for (int ni = 0; ni < NNT; ++ni) {
+        const uint4 w = wc[(ni * KCH + kk) * 64 + lane];
+#pragma unroll
+        for (int pt = 0; pt < NPT; ++pt) acc[ni][pt] = mma<Tr>(w, xf[pt], acc[ni][pt]);
+      }
+    }
+    if (more) commit(buf ^ 1);
+    __syncthreads();
+    buf ^= 1;
+  }
+  // ---- epilogue: bias + SiLU + residual, 4 consecutive channels of one pixel per lane
+#pragma unroll
+  for (int ni = 0; ni < NNT; ++ni) {
+    const int nt = nt0 + ni;
+    if (nt >= a.n_tiles) break;
+    const int n0 = nt * 16 + kg * 4;
+    if (n0 >= a.cout) continue;
+    const float4 bb = *(const float4*)(a.bias + n0);
+#pragma unroll
+    for (int pt = 0; pt < NPT; ++pt) {
+      const int oy = ty0 + wave * NPT + pt, ox = tx0 + col;
+      if (oy >= a.out_h || ox >= a.out_w) continue;
+      const size_t p = ((size_t)b * a.out_h + oy) * a.out_w + ox;
+      float v[4] = {acc[ni][pt][0] + bb.x, acc[ni][pt][1] + bb.y, acc[ni][pt][2] + bb.z, acc[ni][pt][3] + bb.w};
+      if (a.act) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = silu<Tr::kExact>(v[j]);
+      }
+      if (a.res) {
+        float r[4];
+        load4((const T*)a.res + p * a.r_cstride + a.r_coff + n0, r);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = r[j] + v[j];
+      }
+      store4((T*)a.dst + p * a.d_cstride + a.d_coff + n0, v);
+    }
+  }
+}
+
 // ---------------------------------------------------------------- first conv from uint8 frames
 struct InputArgs {
   const unsigned char* frames;  // [B][fh][fw][3] BGR
@@ -231,48 +389,65 @@ struct InputArgs {
 
 template <class Tr>
 __global__ void __launch_bounds__(256) conv_input_kernel(InputArgs a) {
+  // One workgroup = a 16x16 output tile.  The frame patch it reads (3x3 taps, stride <= 2) is
+  // staged once into LDS as RGB floats already divided by 255 (BGR->RGB, im /= 255, LetterBox
+  // value 114 outside the frame, conv zero padding outside the network input); each thread then
+  // computes one output pixel.  Weights/bias are read with wave-uniform indices (scalar cache).
   using T = typename Tr::T;
-  extern __shared__ __attribute__((aligned(16))) float sw[];  // cout*27 weights + cout bias
-  const int nw = a.cout * 3 * a.ksize * a.ksize;
-  for (int i = threadIdx.x; i < nw; i += blockDim.x) sw[i] = a.w[i];
-  for (int i = threadIdx.x; i < a.cout; i += blockDim.x) sw[nw + i] = a.b[i];
-  __syncthreads();
-  const int p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= a.M) return;
-  const int hw = a.out_h * a.out_w;
-  const int b = p / hw, r = p - b * hw, oy = r / a.out_w, ox = r - oy * a.out_w;
-  const int K = a.ksize;
-  float x[3][3][3];  // [c][ky][kx], k <= 3
+  constexpr int TI = 15 * 2 + 3;  // patch edge for stride 2 (also covers stride 1)
+  __shared__ float xs[3][TI][TI + 1];
+  const int tiles_x = (a.out_w + 15) / 16, tiles_y = (a.out_h + 15) / 16;
+  int t = blockIdx.x;
+  const int b = t / (tiles_x * tiles_y);
+  t -= b * tiles_x * tiles_y;
+  const int ty0 = (t / tiles_x) * 16, tx0 = (t % tiles_x) * 16;
+  const int s = a.stride;
+  const int ti = 15 * s + 3;
+  const int iy0 = ty0 * s - a.pad, ix0 = tx0 * s - a.pad;
   const unsigned char* fr = a.frames + (size_t)b * a.fh * a.fw * 3;
-  for (int ky = 0; ky < K; ++ky)
-    for (int kx = 0; kx < K; ++kx) {
-      const int iy = oy * a.stride - a.pad + ky, ix = ox * a.stride - a.pad + kx;
-      float v0 = 0.f, v1 = 0.f, v2 = 0.f;
-      if (iy >= 0 && iy < a.in_h && ix >= 0 && ix < a.in_w) {
-        const int fy = iy - a.pad_top, fx = ix - a.pad_left;
-        if (fy >= 0 && fy < a.fh && fx >= 0 && fx < a.fw) {
-          const unsigned char* px = fr + ((size_t)fy * a.fw + fx) * 3;
-          v0 = (float)px[2] / 255.0f;  // R  (BGR -> RGB, then /255 as im /= 255)
-          v1 = (float)px[1] / 255.0f;  // G
-          v2 = (float)px[0] / 255.0f;  // B
-        } else {
-          v0 = v1 = v2 = 114.0f / 255.0f;  // LetterBox padding value
-        }
+  for (int i = threadIdx.x; i < ti * ti; i += 256) {
+    const int ry = i / ti, rx = i - ry * ti;
+    const int iy = iy0 + ry, ix = ix0 + rx;
+    float v0 = 0.f, v1 = 0.f, v2 = 0.f;
+    if (iy >= 0 && iy < a.in_h && ix >= 0 && ix < a.in_w) {
+      const int fy = iy - a.pad_top, fx = ix - a.pad_left;
+      if (fy >= 0 && fy < a.fh && fx >= 0 && fx < a.fw) {
+        const unsigned char* px = fr + ((size_t)fy * a.fw + fx) * 3;
+        v0 = (float)px[2] / 255.0f;
+        v1 = (float)px[1] / 255.0f;
+        v2 = (float)px[0] / 255.0f;
+      } else {
+        v0 = v1 = v2 = 114.0f / 255.0f;
       }
-      x[0][ky][kx] = v0;
-      x[1][ky][kx] = v1;
-      x[2][ky][kx] = v2;
     }
-  T* out = (T*)a.dst + (size_t)p * a.d_cstride + a.d_coff;
+    xs[0][ry][rx] = v0;
+    xs[1][ry][rx] = v1;
+    xs[2][ry][rx] = v2;
+  }
+  __syncthreads();
+  const int ty = threadIdx.x >> 4, tx = threadIdx.x & 15;
+  const int oy = ty0 + ty, ox = tx0 + tx;
+  if (oy >= a.out_h || ox >= a.out_w) return;
+  float x[27];
+#pragma unroll
+  for (int c = 0; c < 3; ++c)
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) x[c * 9 + ky * 3 + kx] = xs[c][ty * s + ky][tx * s + kx];
+  const size_t p = ((size_t)b * a.out_h + oy) * a.out_w + ox;
+  T* out = (T*)a.dst + p * a.d_cstride + a.d_coff;
+  const float* __restrict__ W = a.w;
+  const float* __restrict__ Bb = a.b;
   for (int o = 0; o < a.cout; o += 4) {
     float v[4];
+#pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const float* w = sw + (o + j) * 3 * K * K;
-      float s = 0.f;
-      for (int c = 0; c < 3; ++c)
-        for (int ky = 0; ky < K; ++ky)
-          for (int kx = 0; kx < K; ++kx) s += w[(c * K + ky) * K + kx] * x[c][ky][kx];
-      v[j] = silu<Tr::kExact>(s + sw[nw + o + j]);
+      const float* w = W + (o + j) * 27;
+      float acc = 0.f;
+#pragma unroll
+      for (int q = 0; q < 27; ++q) acc += w[q] * x[q];
+      v[j] = silu<Tr::kExact>(acc + Bb[o + j]);
     }
     store4(out + o, v);
   }
@@ -414,7 +589,15 @@ __global__ void __launch_bounds__(256) detect_kernel(DetArgs a) {
 
 // ---------------------------------------------------------------- NMS + scale/clip
 constexpr int NMS_NT = 512;
-constexpr int NMS_LDS_N = 4096;  // candidates sorted / suppressed in LDS; more -> global scratch
+constexpr int NMS_LDS_N = 2048;   // candidates sorted in LDS; more -> global scratch
+constexpr int NMS_MASK_N = 512;   // bitmask suppression in LDS up to this many candidates
+constexpr size_t NMS_OFF_BOX = (size_t)NMS_LDS_N * 8;
+constexpr size_t NMS_OFF_REM = NMS_OFF_BOX + (size_t)NMS_LDS_N * 20;
+constexpr size_t NMS_OFF_MISC = NMS_OFF_REM + NMS_LDS_N;
+constexpr size_t NMS_OFF_KEEP = NMS_OFF_MISC + 64;
+constexpr size_t NMS_OFF_MASK = NMS_OFF_KEEP + (size_t)NMS_LDS_N * 4;
+constexpr int NMS_W = NMS_MASK_N / 64;
+constexpr size_t NMS_LDS = NMS_OFF_MASK + (size_t)NMS_MASK_N * NMS_W * 8 * 2;
 
 struct NmsArgs {
   const float* cand;
@@ -450,6 +633,91 @@ __device__ __forceinline__ void bitonic_sort(unsigned long long* k, int n2) {
   }
 }
 
+// bits of word `w` (candidates w*64 .. w*64+63) that lie strictly after candidate i
+__device__ __forceinline__ unsigned long long after_mask(int w, int i) {
+  const int base = w * 64;
+  if (i < base) return ~0ull;
+  if (i >= base + 63) return 0ull;
+  return ~0ull << (i - base + 1);
+}
+
+// TorchNMS.nms on one image's sorted candidates as bitmasks (utils/nms.py:237-304):
+// sup[i] = later boxes with !(iou <= thr), ovl[i] = later boxes with inter != 0.  One wave then
+// walks the kept boxes: next kept = first candidate not yet removed; if it overlaps no remaining
+// box, every remaining box is kept (the :291-296 early exit) and the walk ends.
+__device__ int nms_bitmask(const float* box, int n, float thr, int max_det, unsigned long long* sup,
+                           unsigned long long* ovl, int* keep, int* k_out) {
+  const int W = (n + 63) / 64;
+  for (int job = threadIdx.x; job < n * W; job += blockDim.x) {
+    const int i = job / W, w = job - i * W;
+    unsigned long long sm = 0, om = 0;
+    if (w * 64 + 63 > i) {
+      const float bx1 = box[i * 5], by1 = box[i * 5 + 1], bx2 = box[i * 5 + 2], by2 = box[i * 5 + 3],
+                  ba = box[i * 5 + 4];
+      const int j0 = w * 64;
+      for (int jj = 0; jj < 64; ++jj) {
+        const int j = j0 + jj;
+        if (j <= i || j >= n) continue;
+        const float ww = fmaxf(fminf(bx2, box[j * 5 + 2]) - fmaxf(bx1, box[j * 5]), 0.f);
+        const float hh = fmaxf(fminf(by2, box[j * 5 + 3]) - fmaxf(by1, box[j * 5 + 1]), 0.f);
+        const float inter = ww * hh;
+        const float iou = inter / (ba + box[j * 5 + 4] - inter);
+        if (inter != 0.f) om |= 1ull << jj;
+        if (!(iou <= thr)) sm |= 1ull << jj;
+      }
+    }
+    sup[i * NMS_W + w] = sm;
+    ovl[i * NMS_W + w] = om;
+  }
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    unsigned long long R = ~0ull;  // removed (or beyond n)
+    if (lane < W) {
+      const int rem = n - lane * 64;
+      R = rem >= 64 ? 0ull : ~0ull << rem;
+    }
+    int k = 0, i = -1;
+    while (k < max_det) {
+      const unsigned long long cand = lane < W ? (~R & after_mask(lane, i)) : 0ull;
+      const unsigned long long bal = __ballot(cand != 0ull);
+      if (bal == 0ull) break;
+      const int fl = __ffsll((long long)bal) - 1;
+      const unsigned long long word = __shfl(cand, fl);
+      i = fl * 64 + __ffsll((long long)word) - 1;
+      if (lane == 0) keep[k] = i;
+      ++k;
+      if (k >= max_det) break;
+      const unsigned long long o = lane < W ? (ovl[i * NMS_W + lane] & ~R) : 0ull;
+      if (__ballot(o != 0ull) == 0ull) {
+        // keep every remaining candidate after i, in order
+        const unsigned long long rem = lane < W ? (~R & after_mask(lane, i)) : 0ull;
+        const int c = __popcll(rem);
+        int incl = c;
+        for (int d = 1; d < 64; d <<= 1) {
+          const int v = __shfl_up(incl, d);
+          if (lane >= d) incl += v;
+        }
+        int r = k + incl - c;
+        unsigned long long bits = rem;
+        while (bits) {
+          const int bpos = __ffsll((long long)bits) - 1;
+          bits &= bits - 1;
+          if (r < max_det) keep[r] = lane * 64 + bpos;
+          ++r;
+        }
+        const int total = __shfl(incl, 63);
+        k = k + total < max_det ? k + total : max_det;
+        break;
+      }
+      if (lane < W) R |= sup[i * NMS_W + lane];
+    }
+    if (lane == 0) *k_out = k;
+  }
+  __syncthreads();
+  return *k_out;
+}
+
 __global__ void __launch_bounds__(NMS_NT) nms_kernel(NmsArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int b = blockIdx.x, tid = threadIdx.x;
@@ -460,10 +728,10 @@ __global__ void __launch_bounds__(NMS_NT) nms_kernel(NmsArgs a) {
   int n2 = 1;
   while (n2 < n) n2 <<= 1;
   unsigned long long* keys = in_lds ? (unsigned long long*)smem : a.gkeys + (size_t)b * a.key_cap;
-  float* box = in_lds ? (float*)(smem + NMS_LDS_N * 8) : a.gbox + (size_t)b * a.cap * 5;
-  unsigned char* removed = in_lds ? smem + NMS_LDS_N * 8 + NMS_LDS_N * 20 : a.gflag + (size_t)b * a.cap;
-  int* misc = (int*)(smem + NMS_LDS_N * 8 + NMS_LDS_N * 20 + NMS_LDS_N);  // [0..15] + keep list
-  int* keep = misc + 16;
+  float* box = in_lds ? (float*)(smem + NMS_OFF_BOX) : a.gbox + (size_t)b * a.cap * 5;
+  unsigned char* removed = in_lds ? smem + NMS_OFF_REM : a.gflag + (size_t)b * a.cap;
+  int* misc = (int*)(smem + NMS_OFF_MISC);
+  int* keep = (int*)(smem + NMS_OFF_KEEP);
   int* slot_of = a.slot_of + (size_t)b * a.n_anchors;
   // keys: (~score_bits, anchor) -> ascending order = score desc, anchor asc (stable order)
   for (int i = tid; i < n2; i += NMS_NT) {
@@ -493,52 +761,57 @@ __global__ void __launch_bounds__(NMS_NT) nms_kernel(NmsArgs a) {
   __syncthreads();
   int k = 0;
   const float thr = a.iou;
-  for (int i = 0; i < n && k < a.max_det; ++i) {
-    if (removed[i]) continue;
-    if (tid == 0) keep[k] = i;
-    ++k;
-    const float bx1 = box[i * 5], by1 = box[i * 5 + 1], bx2 = box[i * 5 + 2], by2 = box[i * 5 + 3],
-                ba = box[i * 5 + 4];
-    int any = 0;
-    for (int j = i + 1 + tid; j < n; j += NMS_NT) {
-      if (removed[j]) continue;
-      const float w = fmaxf(fminf(bx2, box[j * 5 + 2]) - fmaxf(bx1, box[j * 5]), 0.f);
-      const float h = fmaxf(fminf(by2, box[j * 5 + 3]) - fmaxf(by1, box[j * 5 + 1]), 0.f);
-      if (w * h != 0.f) any = 1;
-    }
-    any = __syncthreads_or(any);
-    if (!any) {
-      // inter.sum() == 0: keep every remaining box, in order, and stop (nms.py:291-296)
-      int base = k;
-      for (int j0 = i + 1; j0 < n; j0 += NMS_NT) {
-        const int j = j0 + tid;
-        const int f = (j < n && !removed[j]) ? 1 : 0;
-        const unsigned long long m = __ballot(f);
-        const int lane = tid & 63, w = tid >> 6;
-        if (lane == 0) misc[w] = __popcll(m);
-        __syncthreads();
-        int pre = 0, tot = 0;
-        for (int q = 0; q < NMS_NT / 64; ++q) {
-          pre += q < w ? misc[q] : 0;
-          tot += misc[q];
-        }
-        const int r = base + pre + __popcll(m & ((1ull << lane) - 1ull));
-        if (f && r < a.max_det) keep[r] = j;
-        __syncthreads();
-        base += tot;
+  if (n <= NMS_MASK_N) {
+    unsigned long long* sup = (unsigned long long*)(smem + NMS_OFF_MASK);
+    k = nms_bitmask(box, n, thr, a.max_det, sup, sup + NMS_MASK_N * NMS_W, keep, misc + 15);
+  } else {
+    for (int i = 0; i < n && k < a.max_det; ++i) {
+      if (removed[i]) continue;
+      if (tid == 0) keep[k] = i;
+      ++k;
+      const float bx1 = box[i * 5], by1 = box[i * 5 + 1], bx2 = box[i * 5 + 2], by2 = box[i * 5 + 3],
+                  ba = box[i * 5 + 4];
+      int any = 0;
+      for (int j = i + 1 + tid; j < n; j += NMS_NT) {
+        if (removed[j]) continue;
+        const float w = fmaxf(fminf(bx2, box[j * 5 + 2]) - fmaxf(bx1, box[j * 5]), 0.f);
+        const float h = fmaxf(fminf(by2, box[j * 5 + 3]) - fmaxf(by1, box[j * 5 + 1]), 0.f);
+        if (w * h != 0.f) any = 1;
       }
-      k = base < a.max_det ? base : a.max_det;
-      break;
+      any = __syncthreads_or(any);
+      if (!any) {
+        // inter.sum() == 0: keep every remaining box, in order, and stop (nms.py:291-296)
+        int base = k;
+        for (int j0 = i + 1; j0 < n; j0 += NMS_NT) {
+          const int j = j0 + tid;
+          const int f = (j < n && !removed[j]) ? 1 : 0;
+          const unsigned long long m = __ballot(f);
+          const int lane = tid & 63, w = tid >> 6;
+          if (lane == 0) misc[w] = __popcll(m);
+          __syncthreads();
+          int pre = 0, tot = 0;
+          for (int q = 0; q < NMS_NT / 64; ++q) {
+            pre += q < w ? misc[q] : 0;
+            tot += misc[q];
+          }
+          const int r = base + pre + __popcll(m & ((1ull << lane) - 1ull));
+          if (f && r < a.max_det) keep[r] = j;
+          __syncthreads();
+          base += tot;
+        }
+        k = base < a.max_det ? base : a.max_det;
+        break;
+      }
+      for (int j = i + 1 + tid; j < n; j += NMS_NT) {
+        if (removed[j]) continue;
+        const float w = fmaxf(fminf(bx2, box[j * 5 + 2]) - fmaxf(bx1, box[j * 5]), 0.f);
+        const float h = fmaxf(fminf(by2, box[j * 5 + 3]) - fmaxf(by1, box[j * 5 + 1]), 0.f);
+        const float inter = w * h;
+        const float iou = inter / (ba + box[j * 5 + 4] - inter);
+        if (!(iou <= thr)) removed[j] = 1;
+      }
+      __syncthreads();
     }
-    for (int j = i + 1 + tid; j < n; j += NMS_NT) {
-      if (removed[j]) continue;
-      const float w = fmaxf(fminf(bx2, box[j * 5 + 2]) - fmaxf(bx1, box[j * 5]), 0.f);
-      const float h = fmaxf(fminf(by2, box[j * 5 + 3]) - fmaxf(by1, box[j * 5 + 1]), 0.f);
-      const float inter = w * h;
-      const float iou = inter / (ba + box[j * 5 + 4] - inter);
-      if (!(iou <= thr)) removed[j] = 1;
-    }
-    __syncthreads();
   }
   __syncthreads();
   // outputs: x[i] rows, then scale_boxes (x - pad) / gain and clip (ops.py:105-184)
@@ -559,7 +832,7 @@ __global__ void __launch_bounds__(NMS_NT) nms_kernel(NmsArgs a) {
   if (tid == 0) a.counts[b] = k;
 }
 
-size_t nms_lds_bytes() { return (size_t)NMS_LDS_N * 8 + (size_t)NMS_LDS_N * 20 + NMS_LDS_N + 64 + 4 * 4096; }
+size_t nms_lds_bytes() { return NMS_LDS; }
 
 }  // namespace det
 }  // namespace yk
@@ -583,6 +856,8 @@ struct yk_model {
   float* dets = nullptr;
   int* counts = nullptr;
   std::map<std::tuple<int, float, float, int, const void*, void*, void*>, hipGraphExec_t> graphs;
+  int plan_batch = 1;  // batch the kernel names of yk_model_op_kernel are reported for
+  bool tiled = true;  // LDS-tiled conv kernel where its tile fits (YK_CONV_DIRECT=1 forces the direct kernel)
 };
 
 namespace {
@@ -614,6 +889,103 @@ void launch_conv(const ConvArgs& a, hipStream_t st) {
   else launch_conv_t<Tr, 4>(a, nt, st);
 }
 
+// Tile geometry of the LDS-tiled conv for one op (ok = false -> the direct-load kernel).
+struct TilePlan {
+  bool ok = false;
+  int nnt = 4, npt = 1, tih = 0, tiw = 0, ps = 0, tiles_x = 0, tiles_y = 0;
+  size_t lds = 0;
+};
+constexpr size_t kTileLdsMax = 144 * 1024;
+
+TilePlan tile_plan(const yk_op& op, int esz, int B) {
+  TilePlan t;
+  const int nt = op.n_tiles;
+  const int cin = op.src_ch[0] + (op.n_src > 1 ? op.src_ch[1] : 0);
+  int U = cin * esz / 16;
+  if ((U & 1) == 0) U += 1;  // odd number of 16-byte slots per pixel: conflict-free b128 reads
+  t.ps = U * 16 / esz;
+  const int s = op.stride, k = op.ksize;
+  const int oh4 = (op.out_h + 3) / 4 * 4;
+  const int tiles_x = (op.out_w + 15) / 16;
+  // Prefer the largest tiles (weights reused over more pixels) that still give >= 2 workgroups
+  // per CU; small-M layers fall back to 4-row tiles and fewer N tiles per workgroup, and if
+  // nothing reaches 512 workgroups take the most parallel geometry that fits.
+  const int nnt0 = nt <= 4 ? nt : (nt == 5 || nt == 6 || nt == 9) ? 3 : 4;
+  const int cand_nnt[3] = {nnt0, nnt0 > 2 ? 2 : 0, nnt0 > 1 ? 1 : 0};
+  long best_wgs = -1;
+  for (int ci = 0; ci < 3; ++ci) {
+    const int nnt = cand_nnt[ci];
+    if (nnt <= 0) continue;
+    for (int npt = 4; npt >= 1; npt >>= 1) {
+      const int th = 4 * npt;
+      if (npt > 1 && th > oh4) continue;
+      const int tih = (th - 1) * s + k, tiw = 15 * s + k;
+      const size_t lds = (size_t)2 * nnt * KCH * 1024 + (size_t)tih * tiw * t.ps * esz;
+      if (lds > kTileLdsMax) continue;
+      const int tiles_y = (op.out_h + th - 1) / th;
+      const long wgs = (long)B * tiles_x * tiles_y * ((nt + nnt - 1) / nnt);
+      if (wgs >= 512 || wgs > best_wgs) {
+        best_wgs = wgs;
+        t.ok = true;
+        t.nnt = nnt;
+        t.npt = npt;
+        t.tih = tih;
+        t.tiw = tiw;
+        t.lds = lds;
+        t.tiles_y = tiles_y;
+        t.tiles_x = tiles_x;
+        if (wgs >= 512) return t;
+      }
+    }
+  }
+  return t;
+}
+
+template <class Tr, int NNT, int NPT>
+void launch_tile_t(const TileArgs& a, const TilePlan& tp, int B, hipStream_t st) {
+  dim3 grid(B * tp.tiles_x * tp.tiles_y, (a.n_tiles + NNT - 1) / NNT);
+  hipLaunchKernelGGL((conv_tile_kernel<Tr, NNT, NPT>), grid, dim3(256), tp.lds, st, a);
+}
+
+template <class Tr, int NNT>
+void launch_tile_n(const TileArgs& a, const TilePlan& tp, int B, hipStream_t st) {
+  if (tp.npt == 4) launch_tile_t<Tr, NNT, 4>(a, tp, B, st);
+  else if (tp.npt == 2) launch_tile_t<Tr, NNT, 2>(a, tp, B, st);
+  else launch_tile_t<Tr, NNT, 1>(a, tp, B, st);
+}
+
+template <class Tr>
+void launch_tile(const TileArgs& a, const TilePlan& tp, int B, hipStream_t st) {
+  switch (tp.nnt) {
+    case 1: launch_tile_n<Tr, 1>(a, tp, B, st); break;
+    case 2: launch_tile_n<Tr, 2>(a, tp, B, st); break;
+    case 3: launch_tile_n<Tr, 3>(a, tp, B, st); break;
+    default: launch_tile_n<Tr, 4>(a, tp, B, st); break;
+  }
+}
+
+template <class Tr, int NNT, int NPT>
+void set_tile_attr() {
+  (void)hipFuncSetAttribute((const void*)conv_tile_kernel<Tr, NNT, NPT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)kTileLdsMax);
+}
+template <class Tr, int NNT>
+void set_tile_attr_n() {
+  set_tile_attr<Tr, NNT, 1>();
+  set_tile_attr<Tr, NNT, 2>();
+  set_tile_attr<Tr, NNT, 4>();
+}
+void set_tile_attrs() {
+  set_tile_attr_n<BF16, 1>();
+  set_tile_attr_n<BF16, 2>();
+  set_tile_attr_n<BF16, 3>();
+  set_tile_attr_n<BF16, 4>();
+  set_tile_attr_n<F32, 1>();
+  set_tile_attr_n<F32, 2>();
+  set_tile_attr_n<F32, 3>();
+  set_tile_attr_n<F32, 4>();
+}
+
 template <class Tr>
 int launch_op(yk_model* m, const yk_op& op, const uint8_t* frames, int B, float conf, hipStream_t st) {
   const yk_model_desc& D = m->desc;
@@ -640,8 +1012,8 @@ int launch_op(yk_model* m, const yk_op& op, const uint8_t* frames, int B, float 
         a.dst = m->bufs[op.dst.buf];
         a.d_cstride = op.dst.c_stride;
         a.d_coff = op.dst.c_off;
-        const size_t lds = (size_t)(op.cout * 3 * op.ksize * op.ksize + op.cout) * 4;
-        hipLaunchKernelGGL(conv_input_kernel<Tr>, dim3((a.M + 255) / 256), dim3(256), lds, st, a);
+        const int tiles = B * ((op.out_h + 15) / 16) * ((op.out_w + 15) / 16);
+        hipLaunchKernelGGL(conv_input_kernel<Tr>, dim3(tiles), dim3(256), 0, st, a);
         break;
       }
       case YK_K_CONV: {
@@ -669,7 +1041,43 @@ int launch_op(yk_model* m, const yk_op& op, const uint8_t* frames, int B, float 
         a.r_cstride = op.res.c_stride;
         a.r_coff = op.res.c_off;
         a.act = op.act;
-        launch_conv<Tr>(a, st);
+        const TilePlan tp = m->tiled ? tile_plan(op, (int)sizeof(typename Tr::T), B) : TilePlan{};
+        if (tp.ok) {
+          TileArgs t;
+          t.src[0] = a.src[0];
+          t.src[1] = a.src[1];
+          t.c0 = op.src_ch[0];
+          t.cin = op.src_ch[0] + (op.n_src > 1 ? op.src_ch[1] : 0);
+          t.ksize = a.ksize;
+          t.stride = a.stride;
+          t.pad = a.pad;
+          t.in_h = a.in_h;
+          t.in_w = a.in_w;
+          t.out_h = a.out_h;
+          t.out_w = a.out_w;
+          t.tiles_x = tp.tiles_x;
+          t.tiles_y = tp.tiles_y;
+          t.tih = tp.tih;
+          t.tiw = tp.tiw;
+          t.ps = tp.ps;
+          t.wpk = a.wpk;
+          t.bias = a.bias;
+          t.tab = a.tab;
+          t.k_steps = a.k_steps;
+          t.n_tiles = a.n_tiles;
+          t.n_chunks = a.n_chunks;
+          t.dst = a.dst;
+          t.d_cstride = a.d_cstride;
+          t.d_coff = a.d_coff;
+          t.cout = a.cout;
+          t.res = a.res;
+          t.r_cstride = a.r_cstride;
+          t.r_coff = a.r_coff;
+          t.act = a.act;
+          launch_tile<Tr>(t, tp, B, st);
+        } else {
+          launch_conv<Tr>(a, st);
+        }
         break;
       }
       case YK_K_SPPF_POOL: {
@@ -730,6 +1138,14 @@ const char* op_kernel_name(const yk_model* m, const yk_op& op) {
     case YK_K_DETECT: return f ? "detect_kernel<yk::det::F32>" : "detect_kernel<yk::det::BF16>";
     default: break;
   }
+  if (m->tiled) {
+    const TilePlan tp = tile_plan(op, f ? 4 : 2, m->plan_batch);
+    if (tp.ok) {
+      static thread_local char buf[96];
+      snprintf(buf, sizeof buf, "conv_tile_kernel<yk::det::%s, %d, %d>", f ? "F32" : "BF16", tp.nnt, tp.npt);
+      return buf;
+    }
+  }
   const int nt = op.n_tiles;
   const int nnt = nt <= 1 ? 1 : nt == 2 ? 2 : (nt == 3 || nt == 6 || nt == 9) ? 3 : 4;
   static const char* names[2][4] = {
@@ -750,6 +1166,7 @@ int detect_impl(yk_model* m, const uint8_t* frames, int B, float conf, float iou
   YK_CHECK_ARG(conf >= 0.f && conf <= 1.f, "Invalid Confidence threshold, valid values are between 0.0 and 1.0");
   YK_CHECK_ARG(iou >= 0.f && iou <= 1.f, "Invalid IoU, valid values are between 0.0 and 1.0");
   YK_CHECK_ARG(max_det >= 0 && max_det <= D.max_det, "yk_detect: max_det exceeds the model's capacity");
+  m->plan_batch = B;
   if (!dets) dets = m->dets;
   if (!counts) counts = m->counts;
   YK_HIP(hipMemsetAsync(m->cand_count, 0, sizeof(int) * B, st));
@@ -795,6 +1212,7 @@ int yk_model_create(yk_ctx* ctx, const yk_model_desc* desc, const void* host_blo
   YK_CHECK_ARG(desc->n_ops > 0 && desc->ops && desc->n_bufs > 0 && desc->buf_elems, "yk_model_create: empty program");
   YK_CHECK_ARG(desc->max_batch >= 1 && desc->n_anchors > 0 && desc->max_det >= 1, "yk_model_create: bad sizes");
   YK_CHECK_ARG(desc->nc == 1, "yk_model_create: only single-class detection heads are supported");
+  YK_CHECK_ARG(desc->max_det <= 2048, "yk_model_create: max_det must be <= 2048");
   YK_CHECK_ARG(desc->act_dtype == YK_ACT_BF16 || desc->act_dtype == YK_ACT_F32, "yk_model_create: bad act dtype");
   for (int i = 0; i < desc->n_ops; ++i) {
     const yk_op& op = desc->ops[i];
@@ -808,7 +1226,8 @@ int yk_model_create(yk_ctx* ctx, const yk_model_desc* desc, const void* host_blo
     YK_CHECK_ARG(op.kind != YK_K_CONV || (op.cout % 4 == 0 && op.k_steps > 0 && op.n_tiles > 0),
                  "yk_model_create: conv geometry");
     YK_CHECK_ARG(op.kind != YK_K_CONV || op.ksize == 1 || op.ksize == 3, "yk_model_create: ksize must be 1 or 3");
-    YK_CHECK_ARG(op.kind != YK_K_CONV_INPUT || op.ksize <= 3, "yk_model_create: input conv ksize <= 3");
+    YK_CHECK_ARG(op.kind != YK_K_CONV_INPUT || (op.ksize == 3 && op.stride <= 2),
+                 "yk_model_create: the input conv must be 3x3 with stride <= 2");
   }
   yk::DeviceGuard guard(ctx->device);
   auto* m = new yk_model();
@@ -846,6 +1265,8 @@ int yk_model_create(yk_ctx* ctx, const yk_model_desc* desc, const void* host_blo
   if (e == hipSuccess) e = hipMemset(m->counts, 0, B * sizeof(int));
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)nms_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)nms_lds_bytes());
+  set_tile_attrs();
+  if (const char* env = getenv("YK_CONV_DIRECT")) m->tiled = env[0] != '1';
   if (e != hipSuccess) {
     yk::set_error(std::string("yk_model_create: ") + hipGetErrorString(e));
     yk_model_destroy(m);
@@ -915,6 +1336,7 @@ int yk_model_profile(yk_model* m, const uint8_t* frames, int batch, float conf, 
   YK_CHECK_ARG(max_det >= 1 && max_det <= m->desc.max_det, "yk_model_profile: max_det out of range");
   yk::DeviceGuard guard(m->ctx->device);
   hipStream_t st = (hipStream_t)stream;
+  m->plan_batch = batch;
   hipEvent_t e0, e1;
   YK_HIP(hipEventCreate(&e0));
   YK_HIP(hipEventCreate(&e1));

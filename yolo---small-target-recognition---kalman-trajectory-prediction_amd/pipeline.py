@@ -5,7 +5,8 @@ for every stream at once: ``model(frame)`` for S frames as one batch (yk_detect)
 ``tracker.update(detections)`` per stream (yk_tracker_step, one workgroup per stream), with
 the NMS output handed to the tracker in HBM (rows [x1, y1, x2, y2, conf, cls] float32, the
 reference's np.float32 detections).  The driver's ``score > 0.1`` filter (:105) is a no-op
-at conf >= 0.1 and is checked, not executed.  The whole step is captured in one hipGraph.
+at conf >= 0.1 and is checked, not executed.  The detector (~90 launches) replays as one
+native hipGraph (yk_detect_graph); the tracker is one more launch on the same stream.
 """
 from __future__ import annotations
 
@@ -39,31 +40,17 @@ class StreamPipeline:
         self.counts = torch.zeros(self.S, dtype=torch.int32, device=dev)
         self.graph = None
 
-    def step_eager(self):
-        self.model.detect(self.frames, self.conf, self.iou, self.max_det, self.dets, self.counts)
-        self.tracker.step_device(self.dets, self.counts)
-
     def capture(self):
-        """Capture one step (detect + NMS + tracker) into a hipGraph on a side stream."""
-        s = torch.cuda.Stream(self.device)
-        s.wait_stream(torch.cuda.current_stream(self.device))
-        with torch.cuda.stream(s):
-            self.step_eager()  # warm: lazy allocations / function attributes before capture
-        torch.cuda.current_stream(self.device).wait_stream(s)
+        """Build (and warm) the detector's native hipGraph; later steps replay it."""
+        self.graph = True
+        self.model.detect(self.frames, self.conf, self.iou, self.max_det, self.dets, self.counts, graph=True)
         torch.cuda.synchronize(self.device)
-        self.tracker.reset()
-        torch.cuda.synchronize(self.device)
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, stream=s):
-            self.step_eager()
-        self.graph = g
-        return g
+        return self.graph
 
     def step(self):
-        if self.graph is not None:
-            self.graph.replay()
-        else:
-            self.step_eager()
+        self.model.detect(self.frames, self.conf, self.iou, self.max_det, self.dets, self.counts,
+                          graph=bool(self.graph))
+        self.tracker.step_device(self.dets, self.counts)
 
     def run(self, frames: torch.Tensor):
         """frames [S, H, W, 3] uint8 (device) -> one step."""
