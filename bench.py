@@ -38,11 +38,14 @@ def parse():
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--streams", type=int, default=8, help="streams (= frames per forward) per GPU")
-    ap.add_argument("--targets", type=int, default=48, help="synthetic targets per stream")
+    ap.add_argument("--targets", type=int, default=20,
+                    help="synthetic targets per stream (20 -> ~64 live tracks/stream with lost-track retention)")
     ap.add_argument("--scale", default="s", choices=["n", "s"])
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--frames", type=int, default=120, help="pre-rendered frames per stream (cycled)")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-tune", action="store_true", help="skip the per-op conv kernel autotune")
+    ap.add_argument("--lanes", type=int, default=3, help="streams the detector's op DAG is scheduled onto")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-profile", action="store_true")
@@ -108,7 +111,7 @@ def tracker_roofline(pipe, reps=20):
             "achieved": round(gbps, 3), "peak": HBM_PEAK, "unit": "GB/s", "frac": round(gbps / HBM_PEAK, 6)}
 
 
-def cpu_baseline(P, scale, seconds, seed=0):
+def cpu_baseline(P, scale, seconds, targets, seed=0):
     """Reference-equivalent CPU path (oracle: torch-CPU fp32 YOLOv8s+P2 + numpy tracker) on a
     bounded sample of one stream, threads as the reference's select_device: min(8, ncpu-1)."""
     from oracle import detector_ref as D
@@ -121,7 +124,7 @@ def cpu_baseline(P, scale, seconds, seed=0):
     layers = [(Ly.i, Ly.f, Ly.kind, {**Ly.args, **({"c": int(Ly.c2 * 0.5)} if Ly.kind == "C2f" else {})})
               for Ly in ar.layers]
     det = D.RefDetector(layers, sd, P.arch.detect_strides(ar))
-    sc = P.synth.Scene(seed=seed, n_targets=48, n_frames=400)
+    sc = P.synth.Scene(seed=seed, n_targets=targets, n_frames=400)
     trk = RefMultiTracker(150, 1, 0.1)
     n, t_total = 0, 0.0
     for t in range(400):
@@ -139,7 +142,7 @@ def cpu_baseline(P, scale, seconds, seed=0):
             if t_total > seconds:
                 break
     return {"value": round(n / t_total, 3), "unit": "frames/s", "cores": threads, "kind": "port",
-            "sample": f"{n} frames of one 640x512 stream (48 targets), YOLOv8{scale}+P2 fp32 torch-CPU "
+            "sample": f"{n} frames of one 640x512 stream ({targets} targets), YOLOv8{scale}+P2 fp32 torch-CPU "
                       f"({threads} threads) + numpy tracker, after 2 warm-up frames"}
 
 
@@ -162,9 +165,12 @@ def main():
     for s, sc in enumerate(scenes):
         frames[:, s] = sc.frames_torch(0, F, dev)
     torch.cuda.synchronize()
+    pipe.model.set_lanes(a.lanes)
+    pipe.frames.copy_(frames[0])
     if not a.no_graph:
-        pipe.frames.copy_(frames[0])
-        pipe.capture()
+        pipe.capture(tune=not a.no_tune)
+    elif not a.no_tune:
+        pipe.model.autotune(pipe.frames, pipe.conf)
     # warm-up
     for t in range(a.warmup):
         pipe.run(frames[t % F])
@@ -216,7 +222,7 @@ def main():
                                    for (i, k, n, ms), fl in zip(prof, flops)], "by_kernel": by_kernel}, f, indent=1)
     cpu = None
     if rank == 0 and ws == 1 and not a.no_cpu_baseline:
-        cpu = cpu_baseline(P, a.scale, a.cpu_seconds)
+        cpu = cpu_baseline(P, a.scale, a.cpu_seconds, a.targets)
     if rank == 0:
         gflop = pipe.flops_per_frame() / 1e9
         out = {
@@ -228,7 +234,8 @@ def main():
             "config": {"workload": f"YOLOv8{a.scale}+P2 640x512, {S} streams/GPU as batch {S}, "
                                    f"{a.targets} targets/stream, tracker(150, 1, 0.1) (BASELINE config 3)",
                        "streams_per_gpu": S, "global_batch": S * ws, "parallelism": f"streams sharded over {ws} GPU(s)",
-                       "graph": not a.no_graph, "live_tracks_per_stream": round(live, 1),
+                       "graph": not a.no_graph, "autotuned": not a.no_tune, "dag_lanes": a.lanes,
+                       "live_tracks_per_stream": round(live, 1),
                        "gflop_per_frame": round(gflop, 3)},
             "network_mfma_frac": round(fps / ws * gflop / 1e3 / PEAK[a.dtype], 5),
             "pcie_inclusive_fps": round(pcie_fps * ws, 2),

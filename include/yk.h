@@ -262,6 +262,25 @@ int yk_model_profile(yk_model* m, const uint8_t* dev_frames, int batch, float co
  * names it (substring of the demangled name). */
 int yk_model_op_kernel(yk_model* m, int op_index, char* buf, int len);
 
+/* Concurrency of the op program: ops are list-scheduled onto `lanes` HIP streams (1..8,
+ * default 3; lane 0 is the caller's stream) with an event edge for every cross-lane buffer
+ * hazard (RAW/WAR/WAW), so independent branches of the graph -- e.g. the P2 head/Detect branch
+ * and the P3-P5 path after nn/tasks.py layer 15 -- overlap; yk_detect_graph captures that as
+ * parallel graph branches.  Invalidates cached graphs.  No reference counterpart (the
+ * reference runs nn.Module layers sequentially, nn/tasks.py:159-188). */
+int yk_model_set_lanes(yk_model* m, int lanes);
+/* Time every applicable conv kernel variant (direct, LDS-tiled, split-K x fragment tiles) for
+ * each conv op at this batch on `dev_frames` (`reps` launches each) and keep the fastest; later
+ * calls at the same batch use the choice.  Each variant computes the same conv (fp32: the same
+ * to summation order).  Invalidates cached graphs.  No reference counterpart. */
+int yk_model_autotune(yk_model* m, const uint8_t* dev_frames, int batch, float conf, int reps, void* stream);
+/* Force the conv kernel of one op (op_index >= 0) or of every conv op (-1) at `batch`:
+ * kind -1 = heuristic, 0 = direct, 1 = LDS-tiled (falls back to direct where the tile does not
+ * fit), 2 = split-K with an nnt x npt fragment tile (nnt, npt in {1, 2, 4}). */
+int yk_model_set_plan(yk_model* m, int op_index, int batch, int kind, int nnt, int npt);
+/* The schedule: per op, its lane and the number of cross-lane waits (arrays of n_ops). */
+int yk_model_get_schedule(yk_model* m, int32_t* lane_of, int32_t* n_waits);
+
 /* Device pointer of activation buffer `buf` (debug / parity). */
 int yk_model_buffer(yk_model* m, int buf, void** dev_ptr);
 

@@ -22,6 +22,7 @@
 
 #include <climits>
 #include <cstdlib>
+#include <array>
 #include <map>
 #include <tuple>
 #include <vector>
@@ -105,6 +106,15 @@ struct View {
 };
 
 // ---------------------------------------------------------------- implicit-GEMM conv
+// The K-chunk table is staged into LDS once per workgroup: read from global inside the K loop,
+// each lookup (and the gather that depends on it) would make the wave wait on its vmcnt --
+// i.e. on every weight/input prefetch issued before it -- and serialise the pipeline.
+constexpr int kTabMax = 1024;
+__device__ __forceinline__ void stage_table(int* stab, const int* tab, int n) {
+  for (int i = threadIdx.x; i < n; i += blockDim.x) stab[i] = tab[i];
+  __syncthreads();
+}
+
 struct ConvArgs {
   View src[2];
   int ksize, stride, pad;
@@ -128,6 +138,8 @@ __global__ void __launch_bounds__(256) conv_igemm_kernel(ConvArgs a) {
   const int kg = lane >> 4, col = lane & 15;
   const int nt0 = blockIdx.y * NNT;
   const int pbase = (blockIdx.x * 4 + wave) * (16 * NPT);
+  __shared__ int stab[kTabMax];
+  stage_table(stab, a.tab, a.n_chunks);
   if (pbase >= a.M) return;
   const int hw = a.out_h * a.out_w;
   int pb[NPT], py[NPT], px[NPT];
@@ -158,7 +170,7 @@ __global__ void __launch_bounds__(256) conv_igemm_kernel(ConvArgs a) {
     }
     const int kel = ks * 4 * EPL + kg * EPL;
     const int q = kel >> 3, sub = kel & 7;
-    const int e = q < a.n_chunks ? a.tab[q] : -1;
+    const int e = q < a.n_chunks ? stab[q] : -1;
 #pragma unroll
     for (int t = 0; t < NPT; ++t) {
       uint4 v = make_uint4(0u, 0u, 0u, 0u);
@@ -218,14 +230,139 @@ __global__ void __launch_bounds__(256) conv_igemm_kernel(ConvArgs a) {
   }
 }
 
+// ---------------------------------------------------------------- split-K direct conv (low resolution)
+// For the P4/P5 layers (<= 1,280 pixels per image) whole-tile workgroups are too few and their
+// K loops too long: the kernel is a chain of dependent global round trips.  Here a workgroup
+// owns only 16*NPT flattened output pixels x NNT*16 channels and its four waves split the K
+// steps into contiguous quarters; each wave streams its weight fragments (coalesced 1 KB per
+// step and n-tile, L2-resident) and gathers its input fragments straight from global memory
+// with SKD steps in flight, and the four partial tiles meet in LDS before the epilogue.
+constexpr int SKD = 4;  // K steps in flight per wave
+
+template <class Tr, int NNT, int NPT>
+__global__ void __launch_bounds__(256) conv_splitk_kernel(ConvArgs a) {
+  using T = typename Tr::T;
+  constexpr int EPL = Tr::EPL;
+  __shared__ f32x4 red[4 * NNT * NPT * 64];
+  __shared__ int stab[kTabMax];
+  stage_table(stab, a.tab, a.n_chunks);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int kg = lane >> 4, col = lane & 15;
+  const int nt0 = blockIdx.y * NNT;
+  const int pbase = blockIdx.x * (16 * NPT);
+  const int hw = a.out_h * a.out_w;
+  int pb[NPT], py[NPT], px[NPT];
+  bool pv[NPT];
+#pragma unroll
+  for (int t = 0; t < NPT; ++t) {
+    const int p = pbase + t * 16 + col;
+    pv[t] = p < a.M;
+    const int pp = pv[t] ? p : 0;
+    pb[t] = pp / hw;
+    const int r = pp - pb[t] * hw;
+    const int oy = r / a.out_w;
+    const int ox = r - oy * a.out_w;
+    py[t] = oy * a.stride;
+    px[t] = ox * a.stride;
+  }
+  f32x4 acc[NNT][NPT];
+#pragma unroll
+  for (int i = 0; i < NNT; ++i)
+#pragma unroll
+    for (int t = 0; t < NPT; ++t) acc[i][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto load_step = [&](int ks, uint4* wf, uint4* xf) {
+#pragma unroll
+    for (int i = 0; i < NNT; ++i) {
+      const int nt = nt0 + i < a.n_tiles ? nt0 + i : a.n_tiles - 1;
+      wf[i] = a.wpk[((size_t)nt * a.k_steps + ks) * 64 + lane];
+    }
+    const int kel = ks * 4 * EPL + kg * EPL;
+    const int q = kel >> 3, sub = kel & 7;
+    const int e = q < a.n_chunks ? stab[q] : -1;
+#pragma unroll
+    for (int t = 0; t < NPT; ++t) {
+      uint4 v = make_uint4(0u, 0u, 0u, 0u);
+      if (e >= 0 && pv[t]) {
+        const int dx = ((e >> 21) & 15) - 8, dy = ((e >> 17) & 15) - 8;
+        const int si = (e >> 16) & 1, ch = e & 0xffff;
+        const int iy = py[t] + dy, ix = px[t] + dx;
+        if (iy >= 0 && iy < a.in_h && ix >= 0 && ix < a.in_w) {
+          const View& s = a.src[si];
+          const size_t off = (((size_t)pb[t] * s.h + (iy >> s.up)) * s.w + (ix >> s.up)) * s.cstride + s.coff + ch + sub;
+          v = *(const uint4*)((const T*)s.p + off);
+        }
+      }
+      xf[t] = v;
+    }
+  };
+
+  const int kq = (a.k_steps + 3) >> 2;
+  const int k0 = wave * kq, k1 = k0 + kq < a.k_steps ? k0 + kq : a.k_steps;
+  uint4 wb[SKD][NNT], xb[SKD][NPT];
+#pragma unroll
+  for (int d = 0; d < SKD; ++d)
+    if (k0 + d < k1) load_step(k0 + d, wb[d], xb[d]);
+  for (int ks = k0; ks < k1; ks += SKD) {
+#pragma unroll
+    for (int d = 0; d < SKD; ++d) {
+      if (ks + d < k1) {
+#pragma unroll
+        for (int i = 0; i < NNT; ++i)
+#pragma unroll
+          for (int t = 0; t < NPT; ++t) acc[i][t] = mma<Tr>(wb[d][i], xb[d][t], acc[i][t]);
+        if (ks + d + SKD < k1) load_step(ks + d + SKD, wb[d], xb[d]);
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < NNT; ++i)
+#pragma unroll
+    for (int t = 0; t < NPT; ++t) red[((wave * NNT + i) * NPT + t) * 64 + lane] = acc[i][t];
+  __syncthreads();
+  // epilogue: wave w finishes the (i, t) fragments with (i * NPT + t) % 4 == w
+#pragma unroll
+  for (int i = 0; i < NNT; ++i) {
+    const int nt = nt0 + i;
+    if (nt >= a.n_tiles) break;
+    const int n0 = nt * 16 + kg * 4;
+    if (n0 >= a.cout) continue;
+#pragma unroll
+    for (int t = 0; t < NPT; ++t) {
+      if (((i * NPT + t) & 3) != wave || !pv[t]) continue;
+      f32x4 v4 = red[((0 * NNT + i) * NPT + t) * 64 + lane];
+#pragma unroll
+      for (int w = 1; w < 4; ++w) {
+        const f32x4 u = red[((w * NNT + i) * NPT + t) * 64 + lane];
+        v4[0] += u[0];
+        v4[1] += u[1];
+        v4[2] += u[2];
+        v4[3] += u[3];
+      }
+      const float4 bb = *(const float4*)(a.bias + n0);
+      const size_t p = (size_t)pbase + t * 16 + col;
+      float v[4] = {v4[0] + bb.x, v4[1] + bb.y, v4[2] + bb.z, v4[3] + bb.w};
+      if (a.act) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = silu<Tr::kExact>(v[j]);
+      }
+      if (a.res) {
+        float r[4];
+        load4((const T*)a.res + p * a.r_cstride + a.r_coff + n0, r);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = r[j] + v[j];
+      }
+      store4((T*)a.dst + p * a.d_cstride + a.d_coff + n0, v);
+    }
+  }
+}
+
 // ---------------------------------------------------------------- LDS-tiled implicit-GEMM conv
 // One workgroup = a 16-column x TH-row output tile of one image for NNT x 16 output channels.
 // The input tile with its halo (all K-space channels of both sources, upsample applied) is
 // staged once into LDS with an odd number of 16-byte slots per pixel (conflict-free
 // ds_read_b128 for 16 consecutive pixels); weights stream through LDS in chunks of KCH K-steps
 // shared by the four waves.  Wave w computes output rows [w*NPT, (w+1)*NPT) of the tile.
-constexpr int KCH = 4;
-
 struct TileArgs {
   View src[2];
   int c0, cin;               // K-space channels of src[0]; total (multiple of 8)
@@ -243,25 +380,33 @@ struct TileArgs {
   int act;
 };
 
-template <class Tr, int NNT, int NPT>
+template <class Tr, int NNT, int NPT, bool KSPLIT>
 __global__ void __launch_bounds__(256) conv_tile_kernel(TileArgs a) {
+  // KSPLIT: the four waves share one 16 x NPT output tile and split every weight chunk's K
+  // steps between them (wave w takes steps w, w+4, ...); partial sums meet in LDS.  Used for
+  // the low-resolution layers, where whole-tile workgroups are too few and their K loops long.
   using T = typename Tr::T;
   constexpr int EPL = Tr::EPL;
+  constexpr int KCH = KSPLIT ? 8 : 4;
+  constexpr int ROWS = KSPLIT ? NPT : 4 * NPT;  // output rows per tile
   constexpr int EU = 16 / (int)sizeof(T);   // elements per 16-byte unit
   constexpr int WU = NNT * KCH * 64;        // 16-byte weight units per chunk
   constexpr int WPT = (WU + 255) / 256;     // per thread
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   uint4* wl = (uint4*)smem;                                  // [2][NNT][KCH][64] double-buffered chunks
   T* xt = (T*)(smem + (size_t)2 * WU * 16);                  // [tih][tiw][ps]
+  __shared__ int stab[kTabMax];
+  stage_table(stab, a.tab, a.n_chunks);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int kg = lane >> 4, col = lane & 15;
   const int tpi = a.tiles_x * a.tiles_y;
   int t = blockIdx.x;
   const int b = t / tpi;
   t -= b * tpi;
-  const int ty0 = (t / a.tiles_x) * (4 * NPT), tx0 = (t % a.tiles_x) * 16;
+  const int ty0 = (t / a.tiles_x) * ROWS, tx0 = (t % a.tiles_x) * 16;
   const int iy0 = ty0 * a.stride - a.pad, ix0 = tx0 * a.stride - a.pad;
   const int nt0 = blockIdx.y * NNT;
+  const int wrow = KSPLIT ? 0 : wave * NPT;  // first tile row of this wave
   uint4 wreg[WPT];
   auto fetch = [&](int k0) {  // global -> registers (stays in flight over the compute)
 #pragma unroll
@@ -318,17 +463,17 @@ __global__ void __launch_bounds__(256) conv_tile_kernel(TileArgs a) {
     if (more) fetch(k0 + KCH);
     const uint4* wc = wl + buf * WU;
     const int kn = a.k_steps - k0 < KCH ? a.k_steps - k0 : KCH;
-    for (int kk = 0; kk < kn; ++kk) {
+    for (int kk = KSPLIT ? wave : 0; kk < kn; kk += KSPLIT ? 4 : 1) {
       const int kel = (k0 + kk) * 4 * EPL + kg * EPL;
       const int q = kel >> 3, sub = kel & 7;
-      const int e = q < a.n_chunks ? a.tab[q] : -1;
+      const int e = q < a.n_chunks ? stab[q] : -1;
       uint4 xf[NPT];
       if (e >= 0) {
         const int kx = ((e >> 21) & 15) - 8 + a.pad, ky = ((e >> 17) & 15) - 8 + a.pad;
         const int cK = (e & 0xffff) + (((e >> 16) & 1) ? a.c0 : 0) + sub;
 #pragma unroll
         for (int pt = 0; pt < NPT; ++pt) {
-          const int ty = wave * NPT + pt;
+          const int ty = wrow + pt;
           xf[pt] = *(const uint4*)(xt + (size_t)((ty * s + ky) * a.tiw + col * s + kx) * a.ps + cK);
         }
       } else {
@@ -346,7 +491,32 @@ __global__ void __launch_bounds__(256) conv_tile_kernel(TileArgs a) {
     __syncthreads();
     buf ^= 1;
   }
+  // ---- split-K: sum the four waves' partial tiles through LDS (the weight buffers are free now)
+  if constexpr (KSPLIT) {
+    f32x4* red = (f32x4*)smem;  // [4 waves][NNT][NPT][64]
+#pragma unroll
+    for (int ni = 0; ni < NNT; ++ni)
+#pragma unroll
+      for (int pt = 0; pt < NPT; ++pt) red[((wave * NNT + ni) * NPT + pt) * 64 + lane] = acc[ni][pt];
+    __syncthreads();
+#pragma unroll
+    for (int ni = 0; ni < NNT; ++ni)
+#pragma unroll
+      for (int pt = 0; pt < NPT; ++pt) {
+        f32x4 v = red[((0 * NNT + ni) * NPT + pt) * 64 + lane];
+#pragma unroll
+        for (int w = 1; w < 4; ++w) {
+          const f32x4 u = red[((w * NNT + ni) * NPT + pt) * 64 + lane];
+          v[0] += u[0];
+          v[1] += u[1];
+          v[2] += u[2];
+          v[3] += u[3];
+        }
+        acc[ni][pt] = v;
+      }
+  }
   // ---- epilogue: bias + SiLU + residual, 4 consecutive channels of one pixel per lane
+  // (split-K: wave w stores the (ni, pt) pairs with (ni * NPT + pt) % 4 == w)
 #pragma unroll
   for (int ni = 0; ni < NNT; ++ni) {
     const int nt = nt0 + ni;
@@ -356,7 +526,8 @@ __global__ void __launch_bounds__(256) conv_tile_kernel(TileArgs a) {
     const float4 bb = *(const float4*)(a.bias + n0);
 #pragma unroll
     for (int pt = 0; pt < NPT; ++pt) {
-      const int oy = ty0 + wave * NPT + pt, ox = tx0 + col;
+      if (KSPLIT && ((ni * NPT + pt) & 3) != wave) continue;
+      const int oy = ty0 + wrow + pt, ox = tx0 + col;
       if (oy >= a.out_h || ox >= a.out_w) continue;
       const size_t p = ((size_t)b * a.out_h + oy) * a.out_w + ox;
       float v[4] = {acc[ni][pt][0] + bb.x, acc[ni][pt][1] + bb.y, acc[ni][pt][2] + bb.z, acc[ni][pt][3] + bb.w};
@@ -376,6 +547,8 @@ __global__ void __launch_bounds__(256) conv_tile_kernel(TileArgs a) {
 }
 
 // ---------------------------------------------------------------- first conv from uint8 frames
+constexpr int kInputCoutMax = 64;
+
 struct InputArgs {
   const unsigned char* frames;  // [B][fh][fw][3] BGR
   int fh, fw, pad_top, pad_left;
@@ -392,10 +565,14 @@ __global__ void __launch_bounds__(256) conv_input_kernel(InputArgs a) {
   // One workgroup = a 16x16 output tile.  The frame patch it reads (3x3 taps, stride <= 2) is
   // staged once into LDS as RGB floats already divided by 255 (BGR->RGB, im /= 255, LetterBox
   // value 114 outside the frame, conv zero padding outside the network input); each thread then
-  // computes one output pixel.  Weights/bias are read with wave-uniform indices (scalar cache).
+  // computes one output pixel.  Weights, bias and the exact v/255 table live in LDS too:
+  // loaded per output channel from global they would be a chain of dependent VMEM round trips.
   using T = typename Tr::T;
   constexpr int TI = 15 * 2 + 3;  // patch edge for stride 2 (also covers stride 1)
   __shared__ float xs[3][TI][TI + 1];
+  __shared__ float ws[kInputCoutMax * 27];
+  __shared__ float bs[kInputCoutMax];
+  __shared__ float lut[256];
   const int tiles_x = (a.out_w + 15) / 16, tiles_y = (a.out_h + 15) / 16;
   int t = blockIdx.x;
   const int b = t / (tiles_x * tiles_y);
@@ -405,6 +582,10 @@ __global__ void __launch_bounds__(256) conv_input_kernel(InputArgs a) {
   const int ti = 15 * s + 3;
   const int iy0 = ty0 * s - a.pad, ix0 = tx0 * s - a.pad;
   const unsigned char* fr = a.frames + (size_t)b * a.fh * a.fw * 3;
+  lut[threadIdx.x] = (float)threadIdx.x / 255.0f;  // im /= 255 (exact division, as torch)
+  for (int i = threadIdx.x; i < a.cout * 27; i += 256) ws[i] = a.w[i];
+  if (threadIdx.x < a.cout) bs[threadIdx.x] = a.b[threadIdx.x];
+  __syncthreads();
   for (int i = threadIdx.x; i < ti * ti; i += 256) {
     const int ry = i / ti, rx = i - ry * ti;
     const int iy = iy0 + ry, ix = ix0 + rx;
@@ -413,11 +594,11 @@ __global__ void __launch_bounds__(256) conv_input_kernel(InputArgs a) {
       const int fy = iy - a.pad_top, fx = ix - a.pad_left;
       if (fy >= 0 && fy < a.fh && fx >= 0 && fx < a.fw) {
         const unsigned char* px = fr + ((size_t)fy * a.fw + fx) * 3;
-        v0 = (float)px[2] / 255.0f;
-        v1 = (float)px[1] / 255.0f;
-        v2 = (float)px[0] / 255.0f;
+        v0 = lut[px[2]];
+        v1 = lut[px[1]];
+        v2 = lut[px[0]];
       } else {
-        v0 = v1 = v2 = 114.0f / 255.0f;
+        v0 = v1 = v2 = lut[114];
       }
     }
     xs[0][ry][rx] = v0;
@@ -437,8 +618,8 @@ __global__ void __launch_bounds__(256) conv_input_kernel(InputArgs a) {
       for (int kx = 0; kx < 3; ++kx) x[c * 9 + ky * 3 + kx] = xs[c][ty * s + ky][tx * s + kx];
   const size_t p = ((size_t)b * a.out_h + oy) * a.out_w + ox;
   T* out = (T*)a.dst + p * a.d_cstride + a.d_coff;
-  const float* __restrict__ W = a.w;
-  const float* __restrict__ Bb = a.b;
+  const float* W = ws;
+  const float* Bb = bs;
   for (int o = 0; o < a.cout; o += 4) {
     float v[4];
 #pragma unroll
@@ -487,6 +668,65 @@ __global__ void __launch_bounds__(256) sppf_pool_kernel(void* buf, int cstride, 
   store4(o + C, m5);
   store4(o + 2 * C, m9);
   store4(o + 3 * C, m13);
+}
+
+// One workgroup = one image x 8 channels: the plane is staged in LDS as f32, the 5/9/13-wide
+// row maxima are formed, then the column maxima (square windows are separable), so each input
+// element is read from HBM once instead of 169 times.  max is exact in any precision.
+constexpr int kSppfLdsMaxHW = 1024;
+template <class Tr>
+__global__ void __launch_bounds__(256) sppf_lds_kernel(void* buf, int cstride, int coff, int C, int H, int W) {
+  using T = typename Tr::T;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int HW = H * W, cg = C / 8;
+  const int b = blockIdx.x / cg, c0 = (blockIdx.x - b * cg) * 8;
+  float* x = (float*)smem;  // [HW][8]
+  float* r5 = x + HW * 8;
+  float* r9 = r5 + HW * 8;
+  float* r13 = r9 + HW * 8;
+  T* base = (T*)buf + (size_t)b * HW * cstride + coff + c0;
+  for (int i = threadIdx.x; i < HW * 2; i += blockDim.x) {  // 4 channels per item
+    const int p = i >> 1, h = (i & 1) * 4;
+    float v[4];
+    load4(base + (size_t)p * cstride + h, v);
+    *(float4*)(x + p * 8 + h) = make_float4(v[0], v[1], v[2], v[3]);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < HW * 8; i += blockDim.x) {
+    const int p = i >> 3, c = i & 7, yy = p / W, xx = p - yy * W;
+    float m5 = -INFINITY, m9 = -INFINITY, m13 = -INFINITY;
+    for (int dx = -6; dx <= 6; ++dx) {
+      const int u = xx + dx;
+      if (u < 0 || u >= W) continue;
+      const float v = x[(yy * W + u) * 8 + c];
+      m13 = fmaxf(m13, v);
+      if (dx >= -4 && dx <= 4) m9 = fmaxf(m9, v);
+      if (dx >= -2 && dx <= 2) m5 = fmaxf(m5, v);
+    }
+    r5[i] = m5;
+    r9[i] = m9;
+    r13[i] = m13;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < HW * 2; i += blockDim.x) {
+    const int p = i >> 1, h = (i & 1) * 4, yy = p / W, xx = p - yy * W;
+    float m5[4], m9[4], m13[4];
+    for (int j = 0; j < 4; ++j) m5[j] = m9[j] = m13[j] = -INFINITY;
+    for (int dy = -6; dy <= 6; ++dy) {
+      const int v = yy + dy;
+      if (v < 0 || v >= H) continue;
+      const int q = (v * W + xx) * 8 + h;
+      for (int j = 0; j < 4; ++j) {
+        m13[j] = fmaxf(m13[j], r13[q + j]);
+        if (dy >= -4 && dy <= 4) m9[j] = fmaxf(m9[j], r9[q + j]);
+        if (dy >= -2 && dy <= 2) m5[j] = fmaxf(m5[j], r5[q + j]);
+      }
+    }
+    T* o = base + (size_t)p * cstride + h;
+    store4(o + C, m5);
+    store4(o + 2 * C, m9);
+    store4(o + 3 * C, m13);
+  }
 }
 
 // ---------------------------------------------------------------- Detect level
@@ -858,6 +1098,17 @@ struct yk_model {
   std::map<std::tuple<int, float, float, int, const void*, void*, void*>, hipGraphExec_t> graphs;
   int plan_batch = 1;  // batch the kernel names of yk_model_op_kernel are reported for
   bool tiled = true;  // LDS-tiled conv kernel where its tile fits (YK_CONV_DIRECT=1 forces the direct kernel)
+  // DAG schedule: ops run on `lanes` streams (lane 0 = the caller's stream) with event edges
+  // for every cross-lane hazard; under capture this becomes a graph with parallel branches.
+  int lanes = 3;
+  std::vector<int> lane_of;                 // per op
+  std::vector<std::vector<int>> wait_on;    // per op: producer ops on other lanes (latest per lane)
+  std::vector<char> needs_event;            // per op: some later op on another lane waits on it
+  std::vector<hipStream_t> aux;             // lanes 1..lanes-1
+  std::vector<hipEvent_t> ev;               // per op + fork + joins
+  // per-op conv plan chosen by yk_model_autotune (kind < 0: not tuned, use the heuristic)
+  std::vector<std::array<int, 3>> tuned;    // {kind, nnt, npt}
+  int tuned_batch = 0;
 };
 
 namespace {
@@ -891,7 +1142,7 @@ void launch_conv(const ConvArgs& a, hipStream_t st) {
 
 // Tile geometry of the LDS-tiled conv for one op (ok = false -> the direct-load kernel).
 struct TilePlan {
-  bool ok = false;
+  bool ok = false, split = false;
   int nnt = 4, npt = 1, tih = 0, tiw = 0, ps = 0, tiles_x = 0, tiles_y = 0;
   size_t lds = 0;
 };
@@ -907,12 +1158,11 @@ TilePlan tile_plan(const yk_op& op, int esz, int B) {
   const int s = op.stride, k = op.ksize;
   const int oh4 = (op.out_h + 3) / 4 * 4;
   const int tiles_x = (op.out_w + 15) / 16;
-  // Prefer the largest tiles (weights reused over more pixels) that still give >= 2 workgroups
-  // per CU; small-M layers fall back to 4-row tiles and fewer N tiles per workgroup, and if
-  // nothing reaches 512 workgroups take the most parallel geometry that fits.
+  // Prefer the largest whole-tile geometry (weights reused over more pixels) that gives >= 2
+  // workgroups per CU.  Otherwise (low-resolution layers) use split-K tiles (the four waves
+  // split K over one 16 x NPT tile), choosing the geometry with the most workgroups.
   const int nnt0 = nt <= 4 ? nt : (nt == 5 || nt == 6 || nt == 9) ? 3 : 4;
   const int cand_nnt[3] = {nnt0, nnt0 > 2 ? 2 : 0, nnt0 > 1 ? 1 : 0};
-  long best_wgs = -1;
   for (int ci = 0; ci < 3; ++ci) {
     const int nnt = cand_nnt[ci];
     if (nnt <= 0) continue;
@@ -920,12 +1170,11 @@ TilePlan tile_plan(const yk_op& op, int esz, int B) {
       const int th = 4 * npt;
       if (npt > 1 && th > oh4) continue;
       const int tih = (th - 1) * s + k, tiw = 15 * s + k;
-      const size_t lds = (size_t)2 * nnt * KCH * 1024 + (size_t)tih * tiw * t.ps * esz;
+      const size_t lds = (size_t)2 * nnt * 4 * 1024 + (size_t)tih * tiw * t.ps * esz;
       if (lds > kTileLdsMax) continue;
       const int tiles_y = (op.out_h + th - 1) / th;
       const long wgs = (long)B * tiles_x * tiles_y * ((nt + nnt - 1) / nnt);
-      if (wgs >= 512 || wgs > best_wgs) {
-        best_wgs = wgs;
+      if (wgs >= 512) {
         t.ok = true;
         t.nnt = nnt;
         t.npt = npt;
@@ -934,56 +1183,174 @@ TilePlan tile_plan(const yk_op& op, int esz, int B) {
         t.lds = lds;
         t.tiles_y = tiles_y;
         t.tiles_x = tiles_x;
-        if (wgs >= 512) return t;
+        return t;
+      }
+    }
+  }
+  long best = -1;
+  for (int nnt = (nnt0 < 2 ? nnt0 : 2); nnt >= 1; --nnt) {
+    for (int npt = 4; npt >= 1; npt >>= 1) {
+      const int th = npt;
+      const int tih = (th - 1) * s + k, tiw = 15 * s + k;
+      const size_t red = (size_t)4 * nnt * npt * 64 * 16;
+      const size_t wbytes = (size_t)2 * nnt * 8 * 1024;
+      const size_t lds = (wbytes > red ? wbytes : red) + (size_t)tih * tiw * t.ps * esz;
+      if (lds > kTileLdsMax) continue;
+      const int tiles_y = (op.out_h + th - 1) / th;
+      const long wgs = (long)B * tiles_x * tiles_y * ((nt + nnt - 1) / nnt);
+      // most workgroups, then the larger tile (fewer redundant halo loads)
+      if (wgs > best + best / 8) {
+        best = wgs;
+        t.ok = true;
+        t.split = true;
+        t.nnt = nnt;
+        t.npt = npt;
+        t.tih = tih;
+        t.tiw = tiw;
+        t.lds = lds;
+        t.tiles_y = tiles_y;
+        t.tiles_x = tiles_x;
       }
     }
   }
   return t;
 }
 
-template <class Tr, int NNT, int NPT>
+template <class Tr, int NNT, int NPT, bool SPLIT>
 void launch_tile_t(const TileArgs& a, const TilePlan& tp, int B, hipStream_t st) {
   dim3 grid(B * tp.tiles_x * tp.tiles_y, (a.n_tiles + NNT - 1) / NNT);
-  hipLaunchKernelGGL((conv_tile_kernel<Tr, NNT, NPT>), grid, dim3(256), tp.lds, st, a);
+  hipLaunchKernelGGL((conv_tile_kernel<Tr, NNT, NPT, SPLIT>), grid, dim3(256), tp.lds, st, a);
 }
 
-template <class Tr, int NNT>
+template <class Tr, int NNT, bool SPLIT>
 void launch_tile_n(const TileArgs& a, const TilePlan& tp, int B, hipStream_t st) {
-  if (tp.npt == 4) launch_tile_t<Tr, NNT, 4>(a, tp, B, st);
-  else if (tp.npt == 2) launch_tile_t<Tr, NNT, 2>(a, tp, B, st);
-  else launch_tile_t<Tr, NNT, 1>(a, tp, B, st);
+  if (tp.npt == 4) launch_tile_t<Tr, NNT, 4, SPLIT>(a, tp, B, st);
+  else if (tp.npt == 2) launch_tile_t<Tr, NNT, 2, SPLIT>(a, tp, B, st);
+  else launch_tile_t<Tr, NNT, 1, SPLIT>(a, tp, B, st);
 }
 
 template <class Tr>
 void launch_tile(const TileArgs& a, const TilePlan& tp, int B, hipStream_t st) {
+  if (tp.split) {
+    if (tp.nnt == 2) launch_tile_n<Tr, 2, true>(a, tp, B, st);
+    else launch_tile_n<Tr, 1, true>(a, tp, B, st);
+    return;
+  }
   switch (tp.nnt) {
-    case 1: launch_tile_n<Tr, 1>(a, tp, B, st); break;
-    case 2: launch_tile_n<Tr, 2>(a, tp, B, st); break;
-    case 3: launch_tile_n<Tr, 3>(a, tp, B, st); break;
-    default: launch_tile_n<Tr, 4>(a, tp, B, st); break;
+    case 1: launch_tile_n<Tr, 1, false>(a, tp, B, st); break;
+    case 2: launch_tile_n<Tr, 2, false>(a, tp, B, st); break;
+    case 3: launch_tile_n<Tr, 3, false>(a, tp, B, st); break;
+    default: launch_tile_n<Tr, 4, false>(a, tp, B, st); break;
   }
 }
 
-template <class Tr, int NNT, int NPT>
+template <class Tr, int NNT, int NPT, bool SPLIT>
 void set_tile_attr() {
-  (void)hipFuncSetAttribute((const void*)conv_tile_kernel<Tr, NNT, NPT>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)kTileLdsMax);
+  (void)hipFuncSetAttribute((const void*)conv_tile_kernel<Tr, NNT, NPT, SPLIT>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)kTileLdsMax);
 }
-template <class Tr, int NNT>
+template <class Tr, int NNT, bool SPLIT>
 void set_tile_attr_n() {
-  set_tile_attr<Tr, NNT, 1>();
-  set_tile_attr<Tr, NNT, 2>();
-  set_tile_attr<Tr, NNT, 4>();
+  set_tile_attr<Tr, NNT, 1, SPLIT>();
+  set_tile_attr<Tr, NNT, 2, SPLIT>();
+  set_tile_attr<Tr, NNT, 4, SPLIT>();
+}
+template <class Tr>
+void set_tile_attrs_t() {
+  set_tile_attr_n<Tr, 1, false>();
+  set_tile_attr_n<Tr, 2, false>();
+  set_tile_attr_n<Tr, 3, false>();
+  set_tile_attr_n<Tr, 4, false>();
+  set_tile_attr_n<Tr, 1, true>();
+  set_tile_attr_n<Tr, 2, true>();
 }
 void set_tile_attrs() {
-  set_tile_attr_n<BF16, 1>();
-  set_tile_attr_n<BF16, 2>();
-  set_tile_attr_n<BF16, 3>();
-  set_tile_attr_n<BF16, 4>();
-  set_tile_attr_n<F32, 1>();
-  set_tile_attr_n<F32, 2>();
-  set_tile_attr_n<F32, 3>();
-  set_tile_attr_n<F32, 4>();
+  set_tile_attrs_t<BF16>();
+  set_tile_attrs_t<F32>();
+  (void)hipFuncSetAttribute((const void*)sppf_lds_kernel<BF16>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            kSppfLdsMaxHW * 128);
+  (void)hipFuncSetAttribute((const void*)sppf_lds_kernel<F32>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            kSppfLdsMaxHW * 128);
+}
+
+// Conv kernel choice for one op at batch B.
+enum { CK_DIRECT = 0, CK_TILE = 1, CK_SPLITK = 2 };
+struct ConvPlan {
+  int kind = CK_DIRECT, nnt = 0, npt = 0;
+  TilePlan tp;
+};
+
+// split-K geometry: the largest fragment tile (NNT x NPT) that still gives >= 1024 workgroups
+// and wastes < 25% of the n-tiles, else the one with the most workgroups.
+ConvPlan splitk_plan(const yk_op& op, int B, int nnt_force = 0, int npt_force = 0) {
+  static const int cand[9][2] = {{4, 4}, {4, 2}, {2, 4}, {2, 2}, {4, 1}, {1, 4}, {2, 1}, {1, 2}, {1, 1}};
+  const long M = (long)B * op.out_h * op.out_w;
+  const int nt = op.n_tiles;
+  ConvPlan p;
+  p.kind = CK_SPLITK;
+  if (nnt_force) {
+    p.nnt = nnt_force;
+    p.npt = npt_force;
+    return p;
+  }
+  long best = -1;
+  for (auto& c : cand) {
+    const int nnt = c[0], npt = c[1];
+    const int groups = (nt + nnt - 1) / nnt;
+    if (nnt > 1 && 4 * nt < 3 * groups * nnt) continue;
+    const long wgs = (M + 16 * npt - 1) / (16 * npt) * groups;
+    if (wgs >= 1024) {
+      p.nnt = nnt;
+      p.npt = npt;
+      return p;
+    }
+    if (wgs > best) {
+      best = wgs;
+      p.nnt = nnt;
+      p.npt = npt;
+    }
+  }
+  return p;
+}
+
+ConvPlan conv_plan(const yk_model* m, const yk_op& op, int B) {
+  const int esz = m->desc.act_dtype == YK_ACT_F32 ? 4 : 2;
+  const size_t idx = (size_t)(&op - m->ops.data());
+  if (idx < m->tuned.size() && m->tuned[idx][0] >= 0 && m->tuned_batch == B) {
+    const auto& t = m->tuned[idx];
+    if (t[0] == CK_SPLITK) return splitk_plan(op, B, t[1], t[2]);
+    if (t[0] == CK_TILE) {
+      ConvPlan p;
+      p.kind = CK_TILE;
+      p.tp = tile_plan(op, esz, B);
+      if (p.tp.ok) return p;
+    }
+    return ConvPlan{};
+  }
+  if (!m->tiled) return ConvPlan{};
+  if (op.out_h * op.out_w <= 1280) return splitk_plan(op, B);
+  ConvPlan p;
+  p.tp = tile_plan(op, esz, B);
+  p.kind = p.tp.ok ? CK_TILE : CK_DIRECT;
+  return p;
+}
+
+template <class Tr, int NNT, int NPT>
+void launch_splitk_t(const ConvArgs& a, hipStream_t st) {
+  dim3 grid((a.M + 16 * NPT - 1) / (16 * NPT), (a.n_tiles + NNT - 1) / NNT);
+  hipLaunchKernelGGL((conv_splitk_kernel<Tr, NNT, NPT>), grid, dim3(256), 0, st, a);
+}
+template <class Tr, int NNT>
+void launch_splitk_n(const ConvArgs& a, int npt, hipStream_t st) {
+  if (npt == 4) launch_splitk_t<Tr, NNT, 4>(a, st);
+  else if (npt == 2) launch_splitk_t<Tr, NNT, 2>(a, st);
+  else launch_splitk_t<Tr, NNT, 1>(a, st);
+}
+template <class Tr>
+void launch_splitk(const ConvArgs& a, const ConvPlan& p, hipStream_t st) {
+  if (p.nnt == 4) launch_splitk_n<Tr, 4>(a, p.npt, st);
+  else if (p.nnt == 2) launch_splitk_n<Tr, 2>(a, p.npt, st);
+  else launch_splitk_n<Tr, 1>(a, p.npt, st);
 }
 
 template <class Tr>
@@ -1041,8 +1408,11 @@ int launch_op(yk_model* m, const yk_op& op, const uint8_t* frames, int B, float 
         a.r_cstride = op.res.c_stride;
         a.r_coff = op.res.c_off;
         a.act = op.act;
-        const TilePlan tp = m->tiled ? tile_plan(op, (int)sizeof(typename Tr::T), B) : TilePlan{};
-        if (tp.ok) {
+        const ConvPlan cp = conv_plan(m, op, B);
+        const TilePlan& tp = cp.tp;
+        if (cp.kind == CK_SPLITK) {
+          launch_splitk<Tr>(a, cp, st);
+        } else if (cp.kind == CK_TILE) {
           TileArgs t;
           t.src[0] = a.src[0];
           t.src[1] = a.src[1];
@@ -1083,6 +1453,13 @@ int launch_op(yk_model* m, const yk_op& op, const uint8_t* frames, int B, float 
       case YK_K_SPPF_POOL: {
         const int M = B * op.src[0].h * op.src[0].w;
         const int C = op.src_ch[0];
+        const int HW = op.src[0].h * op.src[0].w;
+        if (HW <= kSppfLdsMaxHW && C % 8 == 0) {
+          hipLaunchKernelGGL(sppf_lds_kernel<Tr>, dim3(B * (C / 8)), dim3(256), (size_t)HW * 8 * 4 * 4, st,
+                             m->bufs[op.src[0].buf], op.src[0].c_stride, op.src[0].c_off, C, op.src[0].h,
+                             op.src[0].w);
+          break;
+        }
         const int n = M * (C / 4);
         hipLaunchKernelGGL(sppf_pool_kernel<Tr>, dim3((n + 255) / 256), dim3(256), 0, st, m->bufs[op.src[0].buf],
                            op.src[0].c_stride, op.src[0].c_off, C, op.src[0].h, op.src[0].w, M);
@@ -1134,17 +1511,24 @@ const char* op_kernel_name(const yk_model* m, const yk_op& op) {
   const bool f = m->desc.act_dtype == YK_ACT_F32;
   switch (op.kind) {
     case YK_K_CONV_INPUT: return f ? "conv_input_kernel<yk::det::F32>" : "conv_input_kernel<yk::det::BF16>";
-    case YK_K_SPPF_POOL: return f ? "sppf_pool_kernel<yk::det::F32>" : "sppf_pool_kernel<yk::det::BF16>";
+    case YK_K_SPPF_POOL:
+      if (op.src[0].h * op.src[0].w <= kSppfLdsMaxHW && op.src_ch[0] % 8 == 0)
+        return f ? "sppf_lds_kernel<yk::det::F32>" : "sppf_lds_kernel<yk::det::BF16>";
+      return f ? "sppf_pool_kernel<yk::det::F32>" : "sppf_pool_kernel<yk::det::BF16>";
     case YK_K_DETECT: return f ? "detect_kernel<yk::det::F32>" : "detect_kernel<yk::det::BF16>";
     default: break;
   }
-  if (m->tiled) {
-    const TilePlan tp = tile_plan(op, f ? 4 : 2, m->plan_batch);
-    if (tp.ok) {
-      static thread_local char buf[96];
-      snprintf(buf, sizeof buf, "conv_tile_kernel<yk::det::%s, %d, %d>", f ? "F32" : "BF16", tp.nnt, tp.npt);
-      return buf;
-    }
+  const ConvPlan cp = conv_plan(m, op, m->plan_batch);
+  static thread_local char buf[96];
+  if (cp.kind == CK_SPLITK) {
+    snprintf(buf, sizeof buf, "conv_splitk_kernel<yk::det::%s, %d, %d>", f ? "F32" : "BF16", cp.nnt, cp.npt);
+    return buf;
+  }
+  if (cp.kind == CK_TILE) {
+    const TilePlan& tp = cp.tp;
+    snprintf(buf, sizeof buf, "conv_tile_kernel<yk::det::%s, %d, %d, %s>", f ? "F32" : "BF16", tp.nnt, tp.npt,
+             tp.split ? "true" : "false");
+    return buf;
   }
   const int nt = op.n_tiles;
   const int nnt = nt <= 1 ? 1 : nt == 2 ? 2 : (nt == 3 || nt == 6 || nt == 9) ? 3 : 4;
@@ -1158,6 +1542,100 @@ const char* op_kernel_name(const yk_model* m, const yk_op& op) {
 
 int launch_nms(yk_model* m, int B, float iou, int max_det, float* dets, int32_t* counts, hipStream_t st);
 
+// Buffers an op reads and writes.  The candidate list (virtual buffer n_bufs) is appended to
+// with atomics by every Detect op, so Detect ops do not order against each other.
+void op_access(const yk_model* m, const yk_op& op, std::vector<int>& rd, std::vector<int>& wr) {
+  rd.clear();
+  wr.clear();
+  switch (op.kind) {
+    case YK_K_CONV_INPUT: wr.push_back(op.dst.buf); break;
+    case YK_K_SPPF_POOL:
+      rd.push_back(op.src[0].buf);
+      wr.push_back(op.src[0].buf);
+      break;
+    case YK_K_DETECT:
+      for (int i = 0; i < op.n_src; ++i) rd.push_back(op.src[i].buf);
+      wr.push_back(m->desc.n_bufs);
+      break;
+    default:
+      for (int i = 0; i < op.n_src; ++i) rd.push_back(op.src[i].buf);
+      if (op.has_res) rd.push_back(op.res.buf);
+      wr.push_back(op.dst.buf);
+      break;
+  }
+}
+
+// List-schedule the op program onto `lanes` streams: an op continues the lane whose tail is
+// its latest producer (keeps chains on one stream), else takes the lane that went idle first.
+void plan_dag(yk_model* m) {
+  const int n = (int)m->ops.size(), nb = m->desc.n_bufs + 1, L = m->lanes;
+  std::vector<int> last_w(nb, -1);
+  std::vector<std::vector<int>> readers(nb);
+  std::vector<int> tail(L, -1);
+  m->lane_of.assign(n, 0);
+  m->wait_on.assign(n, {});
+  m->needs_event.assign(n, 0);
+  std::vector<int> rd, wr;
+  for (int j = 0; j < n; ++j) {
+    op_access(m, m->ops[j], rd, wr);
+    std::vector<int> deps;
+    for (int b : rd)
+      if (last_w[b] >= 0) deps.push_back(last_w[b]);
+    for (int b : wr) {
+      const bool accum = b == m->desc.n_bufs;
+      if (last_w[b] >= 0 && !accum) deps.push_back(last_w[b]);
+      for (int r : readers[b]) deps.push_back(r);
+    }
+    int lane = -1, best = -1;
+    for (int l = 0; l < L; ++l)
+      for (int d : deps)
+        if (tail[l] == d && d > best) best = d, lane = l;
+    if (lane < 0) {
+      lane = 0;
+      for (int l = 1; l < L; ++l)
+        if (tail[l] < tail[lane]) lane = l;
+    }
+    std::vector<int> latest(L, -1);  // per other lane, the latest producer to wait for
+    for (int d : deps)
+      if (m->lane_of[d] != lane && d > latest[m->lane_of[d]]) latest[m->lane_of[d]] = d;
+    for (int l = 0; l < L; ++l)
+      if (latest[l] >= 0) {
+        m->wait_on[j].push_back(latest[l]);
+        m->needs_event[latest[l]] = 1;
+      }
+    m->lane_of[j] = lane;
+    tail[lane] = j;
+    for (int b : rd) readers[b].push_back(j);
+    for (int b : wr) {
+      if (b == m->desc.n_bufs) continue;
+      last_w[b] = j;
+      readers[b].clear();
+    }
+  }
+}
+
+template <class Tr>
+int run_dag(yk_model* m, const uint8_t* frames, int B, float conf, hipStream_t st) {
+  const int n = (int)m->ops.size(), L = m->lanes;
+  if (L <= 1) return run_ops<Tr>(m, frames, B, conf, st);
+  auto lane_stream = [&](int l) { return l == 0 ? st : m->aux[l - 1]; };
+  hipEvent_t fork = m->ev[n];
+  YK_HIP(hipEventRecord(fork, st));
+  for (int l = 1; l < L; ++l) YK_HIP(hipStreamWaitEvent(m->aux[l - 1], fork, 0));
+  for (int j = 0; j < n; ++j) {
+    hipStream_t s = lane_stream(m->lane_of[j]);
+    for (int d : m->wait_on[j]) YK_HIP(hipStreamWaitEvent(s, m->ev[d], 0));
+    const int rc = launch_op<Tr>(m, m->ops[j], frames, B, conf, s);
+    if (rc != YK_OK) return rc;
+    if (m->needs_event[j]) YK_HIP(hipEventRecord(m->ev[j], s));
+  }
+  for (int l = 1; l < L; ++l) {
+    YK_HIP(hipEventRecord(m->ev[n + l], m->aux[l - 1]));
+    YK_HIP(hipStreamWaitEvent(st, m->ev[n + l], 0));
+  }
+  return YK_OK;
+}
+
 int detect_impl(yk_model* m, const uint8_t* frames, int B, float conf, float iou, int max_det, float* dets,
                 int32_t* counts, hipStream_t st) {
   const yk_model_desc& D = m->desc;
@@ -1170,7 +1648,7 @@ int detect_impl(yk_model* m, const uint8_t* frames, int B, float conf, float iou
   if (!dets) dets = m->dets;
   if (!counts) counts = m->counts;
   YK_HIP(hipMemsetAsync(m->cand_count, 0, sizeof(int) * B, st));
-  int rc = D.act_dtype == YK_ACT_F32 ? run_ops<F32>(m, frames, B, conf, st) : run_ops<BF16>(m, frames, B, conf, st);
+  int rc = D.act_dtype == YK_ACT_F32 ? run_dag<F32>(m, frames, B, conf, st) : run_dag<BF16>(m, frames, B, conf, st);
   if (rc != YK_OK) return rc;
   return launch_nms(m, B, iou, max_det, dets, counts, st);
 }
@@ -1202,6 +1680,29 @@ int launch_nms(yk_model* m, int B, float iou, int max_det, float* dets, int32_t*
   return YK_OK;
 }
 
+hipError_t set_lanes(yk_model* m, int lanes) {
+  for (auto& kv : m->graphs) (void)hipGraphExecDestroy(kv.second);
+  m->graphs.clear();
+  for (hipStream_t s : m->aux) (void)hipStreamDestroy(s);
+  for (hipEvent_t v : m->ev) (void)hipEventDestroy(v);
+  m->aux.clear();
+  m->ev.clear();
+  m->lanes = lanes;
+  hipError_t e = hipSuccess;
+  for (int l = 1; l < lanes && e == hipSuccess; ++l) {
+    hipStream_t s;
+    e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+    if (e == hipSuccess) m->aux.push_back(s);
+  }
+  for (size_t i = 0; i < m->ops.size() + 1 + lanes && e == hipSuccess; ++i) {
+    hipEvent_t v;
+    e = hipEventCreateWithFlags(&v, hipEventDisableTiming);
+    if (e == hipSuccess) m->ev.push_back(v);
+  }
+  plan_dag(m);
+  return e;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1226,8 +1727,13 @@ int yk_model_create(yk_ctx* ctx, const yk_model_desc* desc, const void* host_blo
     YK_CHECK_ARG(op.kind != YK_K_CONV || (op.cout % 4 == 0 && op.k_steps > 0 && op.n_tiles > 0),
                  "yk_model_create: conv geometry");
     YK_CHECK_ARG(op.kind != YK_K_CONV || op.ksize == 1 || op.ksize == 3, "yk_model_create: ksize must be 1 or 3");
+    YK_CHECK_ARG(op.kind != YK_K_CONV ||
+                     op.ksize * op.ksize * (op.src_ch[0] + (op.n_src > 1 ? op.src_ch[1] : 0)) / 8 <= kTabMax,
+                 "yk_model_create: conv input too wide (K-chunk table > 1024 entries)");
     YK_CHECK_ARG(op.kind != YK_K_CONV_INPUT || (op.ksize == 3 && op.stride <= 2),
                  "yk_model_create: the input conv must be 3x3 with stride <= 2");
+    YK_CHECK_ARG(op.kind != YK_K_CONV_INPUT || op.cout <= kInputCoutMax,
+                 "yk_model_create: the input conv must have <= 64 (padded) output channels");
   }
   yk::DeviceGuard guard(ctx->device);
   auto* m = new yk_model();
@@ -1267,6 +1773,7 @@ int yk_model_create(yk_ctx* ctx, const yk_model_desc* desc, const void* host_blo
     e = hipFuncSetAttribute((const void*)nms_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)nms_lds_bytes());
   set_tile_attrs();
   if (const char* env = getenv("YK_CONV_DIRECT")) m->tiled = env[0] != '1';
+  if (e == hipSuccess) e = set_lanes(m, 3);
   if (e != hipSuccess) {
     yk::set_error(std::string("yk_model_create: ") + hipGetErrorString(e));
     yk_model_destroy(m);
@@ -1276,10 +1783,29 @@ int yk_model_create(yk_ctx* ctx, const yk_model_desc* desc, const void* host_blo
   return YK_OK;
 }
 
+int yk_model_set_lanes(yk_model* m, int lanes) {
+  YK_CHECK_ARG(m && lanes >= 1 && lanes <= 8, "yk_model_set_lanes: lanes must be in [1, 8]");
+  yk::DeviceGuard guard(m->ctx->device);
+  YK_HIP(hipDeviceSynchronize());
+  YK_HIP(set_lanes(m, lanes));
+  return YK_OK;
+}
+
+int yk_model_get_schedule(yk_model* m, int32_t* lane_of, int32_t* n_waits) {
+  YK_CHECK_ARG(m && lane_of && n_waits, "yk_model_get_schedule: NULL argument");
+  for (size_t i = 0; i < m->ops.size(); ++i) {
+    lane_of[i] = m->lane_of[i];
+    n_waits[i] = (int32_t)m->wait_on[i].size();
+  }
+  return YK_OK;
+}
+
 int yk_model_destroy(yk_model* m) {
   if (!m) return YK_OK;
   yk::DeviceGuard guard(m->ctx->device);
   for (auto& kv : m->graphs) (void)hipGraphExecDestroy(kv.second);
+  for (hipStream_t s : m->aux) (void)hipStreamDestroy(s);
+  for (hipEvent_t v : m->ev) (void)hipEventDestroy(v);
   for (void* p : m->bufs)
     if (p) (void)hipFree(p);
   void* ptrs[] = {m->blob, m->cand, m->cand_count, m->slot_of, m->gkeys, m->gbox, m->gflag, m->dets, m->counts};
@@ -1362,6 +1888,72 @@ int yk_model_profile(yk_model* m, const uint8_t* frames, int batch, float conf, 
     float ms = 0.f;
     YK_HIP(hipEventElapsedTime(&ms, e0, e1));
     host_ms[i] = ms / reps;
+  }
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  return YK_OK;
+}
+
+int yk_model_set_plan(yk_model* m, int op_index, int batch, int kind, int nnt, int npt) {
+  YK_CHECK_ARG(m && op_index >= -1 && op_index < (int)m->ops.size(), "yk_model_set_plan: bad op index");
+  YK_CHECK_ARG(kind >= -1 && kind <= CK_SPLITK, "yk_model_set_plan: kind must be -1 (heuristic), 0, 1 or 2");
+  YK_CHECK_ARG(kind != CK_SPLITK || ((nnt == 1 || nnt == 2 || nnt == 4) && (npt == 1 || npt == 2 || npt == 4)),
+               "yk_model_set_plan: split-K fragment tile must be nnt, npt in {1, 2, 4}");
+  YK_CHECK_ARG(batch >= 1 && batch <= m->desc.max_batch, "yk_model_set_plan: batch out of range");
+  if (m->tuned.size() != m->ops.size() || m->tuned_batch != batch) m->tuned.assign(m->ops.size(), {-1, 0, 0});
+  m->tuned_batch = batch;
+  for (int i = 0; i < (int)m->ops.size(); ++i)
+    if ((op_index < 0 || i == op_index) && m->ops[i].kind == YK_K_CONV) m->tuned[i] = {kind, nnt, npt};
+  for (auto& kv : m->graphs) (void)hipGraphExecDestroy(kv.second);
+  m->graphs.clear();
+  return YK_OK;
+}
+
+int yk_model_autotune(yk_model* m, const uint8_t* frames, int batch, float conf, int reps, void* stream) {
+  YK_CHECK_ARG(m && frames && reps >= 1, "yk_model_autotune: bad argument");
+  YK_CHECK_ARG(batch >= 1 && batch <= m->desc.max_batch, "yk_model_autotune: batch out of range");
+  yk::DeviceGuard guard(m->ctx->device);
+  hipStream_t st = (hipStream_t)stream;
+  const int n = (int)m->ops.size();
+  m->tuned.assign(n, {-1, 0, 0});
+  m->tuned_batch = batch;
+  for (auto& kv : m->graphs) (void)hipGraphExecDestroy(kv.second);
+  m->graphs.clear();
+  int rc = detect_impl(m, frames, batch, conf, 0.7f, 1, nullptr, nullptr, st);  // valid activations
+  if (rc != YK_OK) return rc;
+  hipEvent_t e0, e1;
+  YK_HIP(hipEventCreate(&e0));
+  YK_HIP(hipEventCreate(&e1));
+  const int esz = m->desc.act_dtype == YK_ACT_F32 ? 4 : 2;
+  for (int i = 0; i < n; ++i) {
+    const yk_op& op = m->ops[i];
+    if (op.kind != YK_K_CONV) continue;
+    if (op.has_res && op.res.buf == op.dst.buf && op.res.c_off == op.dst.c_off) continue;  // in place
+    std::vector<std::array<int, 3>> cands = {{CK_DIRECT, 0, 0}};
+    if (tile_plan(op, esz, batch).ok) cands.push_back({CK_TILE, 0, 0});
+    for (int nnt : {1, 2, 4})
+      for (int npt : {1, 2, 4}) {
+        if (nnt > 1 && 4 * op.n_tiles < 3 * ((op.n_tiles + nnt - 1) / nnt) * nnt) continue;
+        cands.push_back({CK_SPLITK, nnt, npt});
+      }
+    float best = 1e30f;
+    std::array<int, 3> pick = {-1, 0, 0};
+    for (const auto& c : cands) {
+      m->tuned[i] = c;
+      rc = launch_any(m, op, frames, batch, conf, st);  // warm
+      if (rc != YK_OK) return rc;
+      YK_HIP(hipEventRecord(e0, st));
+      for (int r = 0; r < reps; ++r) {
+        rc = launch_any(m, op, frames, batch, conf, st);
+        if (rc != YK_OK) return rc;
+      }
+      YK_HIP(hipEventRecord(e1, st));
+      YK_HIP(hipEventSynchronize(e1));
+      float ms = 0.f;
+      YK_HIP(hipEventElapsedTime(&ms, e0, e1));
+      if (ms < best) best = ms, pick = c;
+    }
+    m->tuned[i] = pick;
   }
   (void)hipEventDestroy(e0);
   (void)hipEventDestroy(e1);

@@ -452,6 +452,28 @@ class DeviceModel:
                    L.ptr(counts), st), "yk_detect")
         return dets, counts
 
+    def set_lanes(self, lanes: int):
+        """Streams the op DAG is scheduled onto (1 = strictly sequential, the reference's order)."""
+        L.check(L.lib().yk_model_set_lanes(self._h, int(lanes)), "yk_model_set_lanes")
+
+    def autotune(self, frames: torch.Tensor, conf=0.25, reps: int = 10):
+        """Pick the fastest conv kernel variant per op for this batch size (yk_model_autotune)."""
+        L.check(L.lib().yk_model_autotune(self._h, L.ptr(frames), int(frames.shape[0]), C.c_float(conf), int(reps),
+                                          L.current_stream(self.device)), "yk_model_autotune")
+        torch.cuda.synchronize(self.device)
+
+    def set_plan(self, batch: int, kind: int, nnt: int = 0, npt: int = 0, op: int = -1):
+        """Force the conv kernel (-1 heuristic, 0 direct, 1 LDS-tiled, 2 split-K nnt x npt)."""
+        L.check(L.lib().yk_model_set_plan(self._h, int(op), int(batch), int(kind), int(nnt), int(npt)),
+                "yk_model_set_plan")
+
+    def schedule(self):
+        """(lane per op, cross-lane waits per op) of the current DAG schedule."""
+        n = len(self.prog.ops)
+        lane, waits = np.zeros(n, np.int32), np.zeros(n, np.int32)
+        L.check(L.lib().yk_model_get_schedule(self._h, L.ptr(lane), L.ptr(waits)), "yk_model_get_schedule")
+        return lane, waits
+
     def profile(self, frames: torch.Tensor, conf=0.25, iou=0.7, max_det=300, reps: int = 5):
         """Per-op device milliseconds (hipEvents, `reps` back-to-back launches each) and the
         kernel instantiation each op launches.  Returns list of (op_index, kind, kernel, ms)."""

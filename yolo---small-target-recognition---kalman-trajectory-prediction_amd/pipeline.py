@@ -40,8 +40,11 @@ class StreamPipeline:
         self.counts = torch.zeros(self.S, dtype=torch.int32, device=dev)
         self.graph = None
 
-    def capture(self):
-        """Build (and warm) the detector's native hipGraph; later steps replay it."""
+    def capture(self, tune: bool = True):
+        """Autotune the conv kernels for this batch (on the current frames), then build and warm
+        the detector's native hipGraph; later steps replay it."""
+        if tune:
+            self.model.autotune(self.frames, self.conf)
         self.graph = True
         self.model.detect(self.frames, self.conf, self.iou, self.max_det, self.dets, self.counts, graph=True)
         torch.cuda.synchronize(self.device)
