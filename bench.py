@@ -45,7 +45,8 @@ def parse():
     ap.add_argument("--frames", type=int, default=120, help="pre-rendered frames per stream (cycled)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-tune", action="store_true", help="skip the per-op conv kernel autotune")
-    ap.add_argument("--lanes", type=int, default=3, help="streams the detector's op DAG is scheduled onto")
+    ap.add_argument("--lanes", type=int, default=3, help="streams per batch group the detector's op DAG runs on")
+    ap.add_argument("--groups", type=int, default=2, help="independent sub-batches run concurrently")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-profile", action="store_true")
@@ -165,7 +166,7 @@ def main():
     for s, sc in enumerate(scenes):
         frames[:, s] = sc.frames_torch(0, F, dev)
     torch.cuda.synchronize()
-    pipe.model.set_lanes(a.lanes)
+    pipe.model.set_schedule(a.groups, a.lanes)
     pipe.frames.copy_(frames[0])
     if not a.no_graph:
         pipe.capture(tune=not a.no_tune)
@@ -213,10 +214,11 @@ def main():
     rl = None
     trl = None
     if rank == 0 and not a.no_profile:
-        rl, by_kernel, prof = roofline(pipe, frames[0], a.dtype, S)
+        bg = (S + a.groups - 1) // a.groups  # the batch each group's kernels run at
+        rl, by_kernel, prof = roofline(pipe, frames[0][:bg], a.dtype, bg)
         trl = tracker_roofline(pipe)
         if a.dump_ops:
-            flops = pipe.prog.op_flops(S)
+            flops = pipe.prog.op_flops(bg)
             with open(a.dump_ops, "w") as f:
                 json.dump({"ops": [{"op": i, "kind": k, "kernel": n, "us": round(ms * 1e3, 2), "gflop": fl / 1e9}
                                    for (i, k, n, ms), fl in zip(prof, flops)], "by_kernel": by_kernel}, f, indent=1)
@@ -235,6 +237,7 @@ def main():
                                    f"{a.targets} targets/stream, tracker(150, 1, 0.1) (BASELINE config 3)",
                        "streams_per_gpu": S, "global_batch": S * ws, "parallelism": f"streams sharded over {ws} GPU(s)",
                        "graph": not a.no_graph, "autotuned": not a.no_tune, "dag_lanes": a.lanes,
+                       "batch_groups": a.groups,
                        "live_tracks_per_stream": round(live, 1),
                        "gflop_per_frame": round(gflop, 3)},
             "network_mfma_frac": round(fps / ws * gflop / 1e3 / PEAK[a.dtype], 5),

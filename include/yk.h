@@ -135,6 +135,11 @@ int yk_tracker_outputs(yk_tracker* trk, yk_track_out** dev_rows, int32_t** dev_c
 int yk_tracker_download(yk_tracker* trk, yk_track_out* host_rows, int32_t* host_counts,
                         yk_tracker_stats* host_stats, void* stream);
 
+/* Profiling: wall_clock64 (100 MHz) timestamps of stream s's last step at its phase
+ * boundaries: [0] start, [1] predict, [2] IoU candidates, [3] greedy rounds, [4] update /
+ * mark_lost, [5] new tracks, [6] delete, [7] outputs; [10] = association rounds used. */
+int yk_tracker_phase_ticks(yk_tracker* trk, int stream_index, int64_t* host_ticks16, void* stream);
+
 /* Snapshot the live tracks of one stream in list order (EnhancedMultiTargetTracker.trackers).
  * host_states must hold max_tracks entries; *n_out receives the number written. */
 int yk_tracker_snapshot(yk_tracker* trk, int stream_index, yk_track_state* host_states,
@@ -269,16 +274,21 @@ int yk_model_op_kernel(yk_model* m, int op_index, char* buf, int len);
  * parallel graph branches.  Invalidates cached graphs.  No reference counterpart (the
  * reference runs nn.Module layers sequentially, nn/tasks.py:159-188). */
 int yk_model_set_lanes(yk_model* m, int lanes);
+/* Batch groups x lanes: the batch is cut into `groups` sub-batches (sizes differ by at most
+ * one), each an independent copy of the op DAG on its own `lanes` streams, so the groups'
+ * latency-bound kernel chains overlap.  groups * lanes <= 16.  Invalidates cached graphs. */
+int yk_model_set_schedule(yk_model* m, int groups, int lanes);
 /* Time every applicable conv kernel variant (direct, LDS-tiled, split-K x fragment tiles) for
- * each conv op at this batch on `dev_frames` (`reps` launches each) and keep the fastest; later
- * calls at the same batch use the choice.  Each variant computes the same conv (fp32: the same
+ * each conv op on `dev_frames` (`reps` launches each, best of 3) at the batch one schedule group
+ * runs (ceil(batch / groups)) and keep the fastest; later calls at that batch use the choice.  Each variant computes the same conv (fp32: the same
  * to summation order).  Invalidates cached graphs.  No reference counterpart. */
 int yk_model_autotune(yk_model* m, const uint8_t* dev_frames, int batch, float conf, int reps, void* stream);
 /* Force the conv kernel of one op (op_index >= 0) or of every conv op (-1) at `batch`:
  * kind -1 = heuristic, 0 = direct, 1 = LDS-tiled (falls back to direct where the tile does not
  * fit), 2 = split-K with an nnt x npt fragment tile (nnt, npt in {1, 2, 4}). */
 int yk_model_set_plan(yk_model* m, int op_index, int batch, int kind, int nnt, int npt);
-/* The schedule: per op, its lane and the number of cross-lane waits (arrays of n_ops). */
+/* The schedule: per task (op-major: task = op * groups + group), its lane and the number of
+ * cross-lane waits (arrays of n_ops * groups). */
 int yk_model_get_schedule(yk_model* m, int32_t* lane_of, int32_t* n_waits);
 
 /* Device pointer of activation buffer `buf` (debug / parity). */

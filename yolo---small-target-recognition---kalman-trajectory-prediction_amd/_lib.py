@@ -80,7 +80,9 @@ _SIGS = {
     "yk_memcpy_d2h": ([_vp, _vp, C.c_int64], C.c_int),
     "yk_model_profile": ([_vp, _vp, C.c_int, C.c_float, C.c_float, C.c_int, C.c_int, _vp, _vp], C.c_int),
     "yk_model_op_kernel": ([_vp, C.c_int, C.c_char_p, C.c_int], C.c_int),
+    "yk_tracker_phase_ticks": ([_vp, C.c_int, _vp, _vp], C.c_int),
     "yk_model_set_lanes": ([_vp, C.c_int], C.c_int),
+    "yk_model_set_schedule": ([_vp, C.c_int, C.c_int], C.c_int),
     "yk_model_set_plan": ([_vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int], C.c_int),
     "yk_model_autotune": ([_vp, _vp, C.c_int, C.c_float, C.c_int, _vp], C.c_int),
     "yk_model_get_schedule": ([_vp, _vp, _vp], C.c_int),

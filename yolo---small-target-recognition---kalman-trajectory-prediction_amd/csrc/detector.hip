@@ -21,6 +21,7 @@
 #include <hip/hip_runtime.h>
 
 #include <climits>
+#include <cstdio>
 #include <cstdlib>
 #include <array>
 #include <map>
@@ -105,14 +106,54 @@ struct View {
   int cstride, coff, h, w, up;
 };
 
+// Indexing the kernel-argument array with a per-lane value (a.src[si]) -- or selecting between
+// two of its members, which LLVM folds into a selected kernarg address -- makes the compiler
+// fetch the View with vector loads and drain vmcnt before the gather, serialising every
+// prefetch in flight.  uniform_view() pins each integer field in an SGPR once (readfirstlane
+// breaks the link to the kernarg address) and pick_view() selects member-wise per lane.  The
+// data pointer stays derived from the kernel's first source pointer (base + a uniform element
+// delta), so address-space inference keeps the gathers global loads: flat loads would force
+// vmcnt(0) + lgkmcnt(0) waits.
+__device__ __forceinline__ int rfl(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ long long rfl64(long long v) {
+  const unsigned lo = (unsigned)rfl((int)(unsigned long long)v);
+  const unsigned hi = (unsigned)rfl((int)((unsigned long long)v >> 32));
+  return (long long)(((unsigned long long)hi << 32) | lo);
+}
+__device__ __forceinline__ View uniform_view(const View& v) {
+  View r;
+  r.p = v.p;
+  r.cstride = rfl(v.cstride);
+  r.coff = rfl(v.coff);
+  r.h = rfl(v.h);
+  r.w = rfl(v.w);
+  r.up = rfl(v.up);
+  return r;
+}
+__device__ __forceinline__ View pick_view(const View& v0, const View& v1, bool second) {
+  View r;
+  r.p = nullptr;  // data pointer: gbase + (second ? gdelta : 0), see above
+  r.cstride = second ? v1.cstride : v0.cstride;
+  r.coff = second ? v1.coff : v0.coff;
+  r.h = second ? v1.h : v0.h;
+  r.w = second ? v1.w : v0.w;
+  r.up = second ? v1.up : v0.up;
+  return r;
+}
+
 // ---------------------------------------------------------------- implicit-GEMM conv
-// The K-chunk table is staged into LDS once per workgroup: read from global inside the K loop,
-// each lookup (and the gather that depends on it) would make the wave wait on its vmcnt --
-// i.e. on every weight/input prefetch issued before it -- and serialise the pipeline.
 constexpr int kTabMax = 1024;
-__device__ __forceinline__ void stage_table(int* stab, const int* tab, int n) {
-  for (int i = threadIdx.x; i < n; i += blockDim.x) stab[i] = tab[i];
-  __syncthreads();
+
+// Table entry of K chunk q computed arithmetically (model.py Program.pack: tap, ch =
+// divmod(8q, cin); src = ch >= c0): no table load, so no memory round trip in the K loop.
+__device__ __forceinline__ int chunk_entry(int q, int n_chunks, int cin, int c0, int k) {
+  if (q >= n_chunks) return -1;
+  const int cq = cin >> 3;
+  const int tap = q / cq, c = (q - tap * cq) << 3;
+  const int ky = tap / k, kx = tap - ky * k, pad = k >> 1;
+  const int src = c >= c0 ? 1 : 0;
+  const int ch = src ? c - c0 : c;
+  return ((kx - pad + 8) << 21) | ((ky - pad + 8) << 17) | (src << 16) | ch;
 }
 
 struct ConvArgs {
@@ -123,6 +164,8 @@ struct ConvArgs {
   const float* bias; // [n_tiles * 16]
   const int* tab;    // per 8-channel K chunk: -1 or (dx+8)<<21 | (dy+8)<<17 | src<<16 | channel
   int k_steps, n_tiles, n_chunks;
+  int c0, cin;       // K-space channels of src[0]; of both (the table is q -> (tap, channel) =
+                     // divmod(8q, cin), so the K-loop kernels derive it arithmetically)
   void* dst;
   int d_cstride, d_coff, cout;
   const void* res;
@@ -138,8 +181,9 @@ __global__ void __launch_bounds__(256) conv_igemm_kernel(ConvArgs a) {
   const int kg = lane >> 4, col = lane & 15;
   const int nt0 = blockIdx.y * NNT;
   const int pbase = (blockIdx.x * 4 + wave) * (16 * NPT);
-  __shared__ int stab[kTabMax];
-  stage_table(stab, a.tab, a.n_chunks);
+  const View sv0 = uniform_view(a.src[0]), sv1 = uniform_view(a.src[1]);
+  const typename Tr::T* gbase = (const typename Tr::T*)a.src[0].p;
+  const long long gdelta = rfl64((const typename Tr::T*)a.src[1].p - gbase);
   if (pbase >= a.M) return;
   const int hw = a.out_h * a.out_w;
   int pb[NPT], py[NPT], px[NPT];
@@ -170,7 +214,7 @@ __global__ void __launch_bounds__(256) conv_igemm_kernel(ConvArgs a) {
     }
     const int kel = ks * 4 * EPL + kg * EPL;
     const int q = kel >> 3, sub = kel & 7;
-    const int e = q < a.n_chunks ? stab[q] : -1;
+    const int e = chunk_entry(q, a.n_chunks, a.cin, a.c0, a.ksize);
 #pragma unroll
     for (int t = 0; t < NPT; ++t) {
       uint4 v = make_uint4(0u, 0u, 0u, 0u);
@@ -179,9 +223,9 @@ __global__ void __launch_bounds__(256) conv_igemm_kernel(ConvArgs a) {
         const int si = (e >> 16) & 1, ch = e & 0xffff;
         const int iy = py[t] + dy, ix = px[t] + dx;
         if (iy >= 0 && iy < a.in_h && ix >= 0 && ix < a.in_w) {
-          const View& s = a.src[si];
+          const View s = pick_view(sv0, sv1, si != 0);
           const size_t off = (((size_t)pb[t] * s.h + (iy >> s.up)) * s.w + (ix >> s.up)) * s.cstride + s.coff + ch + sub;
-          v = *(const uint4*)((const T*)s.p + off);
+          v = *(const uint4*)(gbase + (si ? gdelta : 0ll) + off);
         }
       }
       xf[t] = v;
@@ -244,8 +288,9 @@ __global__ void __launch_bounds__(256) conv_splitk_kernel(ConvArgs a) {
   using T = typename Tr::T;
   constexpr int EPL = Tr::EPL;
   __shared__ f32x4 red[4 * NNT * NPT * 64];
-  __shared__ int stab[kTabMax];
-  stage_table(stab, a.tab, a.n_chunks);
+  const View sv0 = uniform_view(a.src[0]), sv1 = uniform_view(a.src[1]);
+  const typename Tr::T* gbase = (const typename Tr::T*)a.src[0].p;
+  const long long gdelta = rfl64((const typename Tr::T*)a.src[1].p - gbase);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int kg = lane >> 4, col = lane & 15;
   const int nt0 = blockIdx.y * NNT;
@@ -279,7 +324,7 @@ __global__ void __launch_bounds__(256) conv_splitk_kernel(ConvArgs a) {
     }
     const int kel = ks * 4 * EPL + kg * EPL;
     const int q = kel >> 3, sub = kel & 7;
-    const int e = q < a.n_chunks ? stab[q] : -1;
+    const int e = chunk_entry(q, a.n_chunks, a.cin, a.c0, a.ksize);
 #pragma unroll
     for (int t = 0; t < NPT; ++t) {
       uint4 v = make_uint4(0u, 0u, 0u, 0u);
@@ -288,15 +333,21 @@ __global__ void __launch_bounds__(256) conv_splitk_kernel(ConvArgs a) {
         const int si = (e >> 16) & 1, ch = e & 0xffff;
         const int iy = py[t] + dy, ix = px[t] + dx;
         if (iy >= 0 && iy < a.in_h && ix >= 0 && ix < a.in_w) {
-          const View& s = a.src[si];
+          const View s = pick_view(sv0, sv1, si != 0);
           const size_t off = (((size_t)pb[t] * s.h + (iy >> s.up)) * s.w + (ix >> s.up)) * s.cstride + s.coff + ch + sub;
-          v = *(const uint4*)((const T*)s.p + off);
+          v = *(const uint4*)(gbase + (si ? gdelta : 0ll) + off);
         }
       }
       xf[t] = v;
     }
   };
 
+  float4 bb[NNT];  // epilogue bias, loaded up front (off the critical path)
+#pragma unroll
+  for (int i = 0; i < NNT; ++i) {
+    const int n0 = (nt0 + i) * 16 + kg * 4;
+    bb[i] = (nt0 + i < a.n_tiles && n0 < a.cout) ? *(const float4*)(a.bias + n0) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
   const int kq = (a.k_steps + 3) >> 2;
   const int k0 = wave * kq, k1 = k0 + kq < a.k_steps ? k0 + kq : a.k_steps;
   uint4 wb[SKD][NNT], xb[SKD][NPT];
@@ -339,9 +390,8 @@ __global__ void __launch_bounds__(256) conv_splitk_kernel(ConvArgs a) {
         v4[2] += u[2];
         v4[3] += u[3];
       }
-      const float4 bb = *(const float4*)(a.bias + n0);
       const size_t p = (size_t)pbase + t * 16 + col;
-      float v[4] = {v4[0] + bb.x, v4[1] + bb.y, v4[2] + bb.z, v4[3] + bb.w};
+      float v[4] = {v4[0] + bb[i].x, v4[1] + bb[i].y, v4[2] + bb[i].z, v4[3] + bb[i].w};
       if (a.act) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) v[j] = silu<Tr::kExact>(v[j]);
@@ -378,6 +428,7 @@ struct TileArgs {
   const void* res;
   int r_cstride, r_coff;
   int act;
+  int single;  // whole weight slab LDS-resident
 };
 
 template <class Tr, int NNT, int NPT, bool KSPLIT>
@@ -385,6 +436,12 @@ __global__ void __launch_bounds__(256) conv_tile_kernel(TileArgs a) {
   // KSPLIT: the four waves share one 16 x NPT output tile and split every weight chunk's K
   // steps between them (wave w takes steps w, w+4, ...); partial sums meet in LDS.  Used for
   // the low-resolution layers, where whole-tile workgroups are too few and their K loops long.
+  // a.single: the whole weight slab (NNT x k_steps) is LDS-resident -- one prologue, one
+  // barrier, then a K loop with no global traffic.  Otherwise weights stream in double-buffered
+  // chunks of KCH steps.  The prologue issues every global load (input tile, weights, bias)
+  // before the first LDS store, so a workgroup pays one memory round trip
+  // instead of one per staging-loop iteration.  K-chunk table entries are computed
+  // arithmetically (chunk_entry).
   using T = typename Tr::T;
   constexpr int EPL = Tr::EPL;
   constexpr int KCH = KSPLIT ? 8 : 4;
@@ -392,13 +449,16 @@ __global__ void __launch_bounds__(256) conv_tile_kernel(TileArgs a) {
   constexpr int EU = 16 / (int)sizeof(T);   // elements per 16-byte unit
   constexpr int WU = NNT * KCH * 64;        // 16-byte weight units per chunk
   constexpr int WPT = (WU + 255) / 256;     // per thread
+  constexpr int SU = 8;                     // staging loads in flight per thread
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  uint4* wl = (uint4*)smem;                                  // [2][NNT][KCH][64] double-buffered chunks
-  T* xt = (T*)(smem + (size_t)2 * WU * 16);                  // [tih][tiw][ps]
-  __shared__ int stab[kTabMax];
-  stage_table(stab, a.tab, a.n_chunks);
+  uint4* wl = (uint4*)smem;  // single: [NNT][k_steps][64]; else [2][NNT][KCH][64]
+  const int wslab = a.single ? NNT * a.k_steps * 64 : 2 * WU;
+  T* xt = (T*)(smem + (size_t)wslab * 16);  // [tih][tiw][ps]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int kg = lane >> 4, col = lane & 15;
+  const View sv0 = uniform_view(a.src[0]), sv1 = uniform_view(a.src[1]);
+  const typename Tr::T* gbase = (const typename Tr::T*)a.src[0].p;
+  const long long gdelta = rfl64((const typename Tr::T*)a.src[1].p - gbase);
   const int tpi = a.tiles_x * a.tiles_y;
   int t = blockIdx.x;
   const int b = t / tpi;
@@ -428,28 +488,73 @@ __global__ void __launch_bounds__(256) conv_tile_kernel(TileArgs a) {
       if (i < WU) wl[buf * WU + i] = wreg[r];
     }
   };
-  fetch(0);
-  // ---- stage the input tile (zero outside the image = conv zero padding)
+  if (!a.single) fetch(0);
+  // bias of this workgroup's channels (epilogue), loaded with the prologue
+  float4 bb[NNT];
+#pragma unroll
+  for (int ni = 0; ni < NNT; ++ni) {
+    const int n0 = (nt0 + ni) * 16 + kg * 4;
+    bb[ni] = (nt0 + ni < a.n_tiles && n0 < a.cout) ? *(const float4*)(a.bias + n0) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  // ---- stage the input tile (zero outside the image = conv zero padding), SU loads in flight
   {
     const int U = a.cin / EU;
     const int total = a.tih * a.tiw * U;
-    for (int i = tid; i < total; i += 256) {
-      const int pix = i / U, u = i - pix * U;
-      const int ry = pix / a.tiw, rx = pix - ry * a.tiw;
-      const int iy = iy0 + ry, ix = ix0 + rx;
-      const int c = u * EU;
-      uint4 v = make_uint4(0u, 0u, 0u, 0u);
-      if (iy >= 0 && iy < a.in_h && ix >= 0 && ix < a.in_w) {
-        const int si = c < a.c0 ? 0 : 1;
-        const View& sv = a.src[si];
-        const int cc = si ? c - a.c0 : c;
-        v = *(const uint4*)((const T*)sv.p +
-                            (((size_t)b * sv.h + (iy >> sv.up)) * sv.w + (ix >> sv.up)) * sv.cstride + sv.coff + cc);
+    for (int base = tid; base < total; base += 256 * SU) {
+      uint4 v[SU];
+#pragma unroll
+      for (int u = 0; u < SU; ++u) {
+        const int i = base + u * 256;
+        v[u] = make_uint4(0u, 0u, 0u, 0u);
+        if (i < total) {
+          const int pix = i / U, uu = i - pix * U;
+          const int ry = pix / a.tiw, rx = pix - ry * a.tiw;
+          const int iy = iy0 + ry, ix = ix0 + rx;
+          const int c = uu * EU;
+          if (iy >= 0 && iy < a.in_h && ix >= 0 && ix < a.in_w) {
+            const int si = c < a.c0 ? 0 : 1;
+            const View sv = pick_view(sv0, sv1, si != 0);
+            const int cc = si ? c - a.c0 : c;
+            v[u] = *(const uint4*)(gbase + (si ? gdelta : 0ll) +
+                                   (((size_t)b * sv.h + (iy >> sv.up)) * sv.w + (ix >> sv.up)) * sv.cstride + sv.coff +
+                                   cc);
+          }
+        }
       }
-      *(uint4*)(xt + (size_t)pix * a.ps + c) = v;
+#pragma unroll
+      for (int u = 0; u < SU; ++u) {
+        const int i = base + u * 256;
+        if (i < total) {
+          const int pix = i / U, uu = i - pix * U;
+          *(uint4*)(xt + (size_t)pix * a.ps + uu * EU) = v[u];
+        }
+      }
     }
   }
-  commit(0);
+  // ---- whole weight slab (single mode), SU loads in flight
+  if (a.single) {
+    const int ks = a.k_steps, total = NNT * ks * 64;
+    for (int base = tid; base < total; base += 256 * SU) {
+      uint4 v[SU];
+#pragma unroll
+      for (int u = 0; u < SU; ++u) {
+        const int i = base + u * 256;
+        v[u] = make_uint4(0u, 0u, 0u, 0u);
+        if (i < total) {
+          const int ni = i / (ks * 64), r = i - ni * ks * 64;
+          const int nt = nt0 + ni < a.n_tiles ? nt0 + ni : a.n_tiles - 1;
+          v[u] = a.wpk[(size_t)nt * ks * 64 + r];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < SU; ++u) {
+        const int i = base + u * 256;
+        if (i < total) wl[i] = v[u];
+      }
+    }
+  } else {
+    commit(0);
+  }
   __syncthreads();
   f32x4 acc[NNT][NPT];
 #pragma unroll
@@ -458,15 +563,16 @@ __global__ void __launch_bounds__(256) conv_tile_kernel(TileArgs a) {
     for (int q = 0; q < NPT; ++q) acc[i][q] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int s = a.stride;
   int buf = 0;
-  for (int k0 = 0; k0 < a.k_steps; k0 += KCH) {
-    const bool more = k0 + KCH < a.k_steps;
+  const int kch = a.single ? a.k_steps : KCH;  // steps per chunk (= the slab row stride)
+  for (int k0 = 0; k0 < a.k_steps; k0 += kch) {
+    const bool more = k0 + kch < a.k_steps;
     if (more) fetch(k0 + KCH);
     const uint4* wc = wl + buf * WU;
-    const int kn = a.k_steps - k0 < KCH ? a.k_steps - k0 : KCH;
+    const int kn = a.k_steps - k0 < kch ? a.k_steps - k0 : kch;
     for (int kk = KSPLIT ? wave : 0; kk < kn; kk += KSPLIT ? 4 : 1) {
       const int kel = (k0 + kk) * 4 * EPL + kg * EPL;
       const int q = kel >> 3, sub = kel & 7;
-      const int e = q < a.n_chunks ? stab[q] : -1;
+      const int e = chunk_entry(q, a.n_chunks, a.cin, a.c0, a.ksize);
       uint4 xf[NPT];
       if (e >= 0) {
         const int kx = ((e >> 21) & 15) - 8 + a.pad, ky = ((e >> 17) & 15) - 8 + a.pad;
@@ -482,7 +588,7 @@ __global__ void __launch_bounds__(256) conv_tile_kernel(TileArgs a) {
       }
 #pragma unroll
       for (int ni = 0; ni < NNT; ++ni) {
-        const uint4 w = wc[(ni * KCH + kk) * 64 + lane];
+        const uint4 w = wc[(ni * kch + kk) * 64 + lane];
 #pragma unroll
         for (int pt = 0; pt < NPT; ++pt) acc[ni][pt] = mma<Tr>(w, xf[pt], acc[ni][pt]);
       }
@@ -523,14 +629,14 @@ __global__ void __launch_bounds__(256) conv_tile_kernel(TileArgs a) {
     if (nt >= a.n_tiles) break;
     const int n0 = nt * 16 + kg * 4;
     if (n0 >= a.cout) continue;
-    const float4 bb = *(const float4*)(a.bias + n0);
 #pragma unroll
     for (int pt = 0; pt < NPT; ++pt) {
       if (KSPLIT && ((ni * NPT + pt) & 3) != wave) continue;
       const int oy = ty0 + wrow + pt, ox = tx0 + col;
       if (oy >= a.out_h || ox >= a.out_w) continue;
       const size_t p = ((size_t)b * a.out_h + oy) * a.out_w + ox;
-      float v[4] = {acc[ni][pt][0] + bb.x, acc[ni][pt][1] + bb.y, acc[ni][pt][2] + bb.z, acc[ni][pt][3] + bb.w};
+      float v[4] = {acc[ni][pt][0] + bb[ni].x, acc[ni][pt][1] + bb[ni].y, acc[ni][pt][2] + bb[ni].z,
+                    acc[ni][pt][3] + bb[ni].w};
       if (a.act) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) v[j] = silu<Tr::kExact>(v[j]);
@@ -1100,12 +1206,19 @@ struct yk_model {
   bool tiled = true;  // LDS-tiled conv kernel where its tile fits (YK_CONV_DIRECT=1 forces the direct kernel)
   // DAG schedule: ops run on `lanes` streams (lane 0 = the caller's stream) with event edges
   // for every cross-lane hazard; under capture this becomes a graph with parallel branches.
-  int lanes = 3;
-  std::vector<int> lane_of;                 // per op
-  std::vector<std::vector<int>> wait_on;    // per op: producer ops on other lanes (latest per lane)
-  std::vector<char> needs_event;            // per op: some later op on another lane waits on it
-  std::vector<hipStream_t> aux;             // lanes 1..lanes-1
-  std::vector<hipEvent_t> ev;               // per op + fork + joins
+  // With `groups` > 1 the batch is cut into that many sub-batches, each an independent copy of
+  // the DAG on its own `lanes` streams: the detector's kernels are latency-bound, so
+  // independent chains overlap on the chip.
+  int lanes = 3, groups = 1;
+  struct Task {
+    int op, grp, lane;
+    std::vector<int> waits;  // producer tasks on other lanes (latest per lane)
+    bool ev;                 // some later task on another lane waits on this one
+  };
+  std::vector<Task> tasks;
+  std::vector<char> lane_used;              // lanes that run at least one task
+  std::vector<hipStream_t> aux;             // lanes 1..groups*lanes-1
+  std::vector<hipEvent_t> ev;               // per task + fork + joins
   // per-op conv plan chosen by yk_model_autotune (kind < 0: not tuned, use the heuristic)
   std::vector<std::array<int, 3>> tuned;    // {kind, nnt, npt}
   int tuned_batch = 0;
@@ -1113,9 +1226,16 @@ struct yk_model {
 
 namespace {
 
-View make_view(yk_model* m, const yk_view& v) {
+size_t act_bytes(const yk_model* m) { return m->desc.act_dtype == YK_ACT_F32 ? 4 : 2; }
+
+// Base of image b0 of a buffer whose per-image extent is h x w x c_stride elements.
+void* img_ptr(const yk_model* m, int buf, int h, int w, int cstride, int b0) {
+  return (char*)m->bufs[buf] + (size_t)b0 * h * w * cstride * act_bytes(m);
+}
+
+View make_view(yk_model* m, const yk_view& v, int b0 = 0) {
   View o;
-  o.p = m->bufs[v.buf];
+  o.p = img_ptr(m, v.buf, v.h, v.w, v.c_stride, b0);
   o.cstride = v.c_stride;
   o.coff = v.c_off;
   o.h = v.h;
@@ -1142,13 +1262,32 @@ void launch_conv(const ConvArgs& a, hipStream_t st) {
 
 // Tile geometry of the LDS-tiled conv for one op (ok = false -> the direct-load kernel).
 struct TilePlan {
-  bool ok = false, split = false;
+  bool ok = false, split = false, single = false;
   int nnt = 4, npt = 1, tih = 0, tiw = 0, ps = 0, tiles_x = 0, tiles_y = 0;
   size_t lds = 0;
 };
 constexpr size_t kTileLdsMax = 144 * 1024;
 
+TilePlan tile_plan_geom(const yk_op& op, int esz, int B);
+
+// Geometry, then whether the whole weight slab fits LDS next to the input tile (one prologue,
+// no chunk barriers) without costing occupancy beyond ~96 KB per workgroup.
 TilePlan tile_plan(const yk_op& op, int esz, int B) {
+  TilePlan t = tile_plan_geom(op, esz, B);
+  if (!t.ok) return t;
+  const size_t tile = (size_t)t.tih * t.tiw * t.ps * esz;
+  const size_t slab = (size_t)t.nnt * op.k_steps * 1024;
+  const size_t red = t.split ? (size_t)4 * t.nnt * t.npt * 64 * 16 : 0;
+  const size_t lds1 = (slab > red ? slab : red) + tile;
+  const size_t cap = t.lds > 96 * 1024 ? t.lds : 96 * 1024;
+  if (lds1 <= cap && lds1 <= kTileLdsMax) {
+    t.single = true;
+    t.lds = lds1;
+  }
+  return t;
+}
+
+TilePlan tile_plan_geom(const yk_op& op, int esz, int B) {
   TilePlan t;
   const int nt = op.n_tiles;
   const int cin = op.src_ch[0] + (op.n_src > 1 ? op.src_ch[1] : 0);
@@ -1354,13 +1493,14 @@ void launch_splitk(const ConvArgs& a, const ConvPlan& p, hipStream_t st) {
 }
 
 template <class Tr>
-int launch_op(yk_model* m, const yk_op& op, const uint8_t* frames, int B, float conf, hipStream_t st) {
+int launch_op(yk_model* m, const yk_op& op, const uint8_t* frames, int B, float conf, hipStream_t st, int b0 = 0) {
+  // images [b0, b0 + B) of the batch
   const yk_model_desc& D = m->desc;
   {
     switch (op.kind) {
       case YK_K_CONV_INPUT: {
         InputArgs a;
-        a.frames = frames;
+        a.frames = frames + (size_t)b0 * D.frame_h * D.frame_w * 3;
         a.fh = D.frame_h;
         a.fw = D.frame_w;
         a.pad_top = D.pad_top;
@@ -1376,7 +1516,7 @@ int launch_op(yk_model* m, const yk_op& op, const uint8_t* frames, int B, float 
         a.w = (const float*)(m->blob + op.w_off);
         a.b = (const float*)(m->blob + op.b_off);
         a.cout = op.cout;
-        a.dst = m->bufs[op.dst.buf];
+        a.dst = img_ptr(m, op.dst.buf, op.out_h, op.out_w, op.dst.c_stride, b0);
         a.d_cstride = op.dst.c_stride;
         a.d_coff = op.dst.c_off;
         const int tiles = B * ((op.out_h + 15) / 16) * ((op.out_w + 15) / 16);
@@ -1385,7 +1525,7 @@ int launch_op(yk_model* m, const yk_op& op, const uint8_t* frames, int B, float 
       }
       case YK_K_CONV: {
         ConvArgs a;
-        for (int i = 0; i < 2; ++i) a.src[i] = make_view(m, op.src[i < op.n_src ? i : 0]);
+        for (int i = 0; i < 2; ++i) a.src[i] = make_view(m, op.src[i < op.n_src ? i : 0], b0);
         a.ksize = op.ksize;
         a.stride = op.stride;
         a.pad = op.ksize / 2;
@@ -1400,11 +1540,13 @@ int launch_op(yk_model* m, const yk_op& op, const uint8_t* frames, int B, float 
         a.k_steps = op.k_steps;
         a.n_tiles = op.n_tiles;
         a.n_chunks = op.ksize * op.ksize * (op.src_ch[0] + (op.n_src > 1 ? op.src_ch[1] : 0)) / 8;
-        a.dst = m->bufs[op.dst.buf];
+        a.c0 = op.src_ch[0];
+        a.cin = op.src_ch[0] + (op.n_src > 1 ? op.src_ch[1] : 0);
+        a.dst = img_ptr(m, op.dst.buf, op.out_h, op.out_w, op.dst.c_stride, b0);
         a.d_cstride = op.dst.c_stride;
         a.d_coff = op.dst.c_off;
         a.cout = op.cout;
-        a.res = op.has_res ? m->bufs[op.res.buf] : nullptr;
+        a.res = op.has_res ? img_ptr(m, op.res.buf, op.out_h, op.out_w, op.res.c_stride, b0) : nullptr;
         a.r_cstride = op.res.c_stride;
         a.r_coff = op.res.c_off;
         a.act = op.act;
@@ -1444,6 +1586,7 @@ int launch_op(yk_model* m, const yk_op& op, const uint8_t* frames, int B, float 
           t.r_cstride = a.r_cstride;
           t.r_coff = a.r_coff;
           t.act = a.act;
+          t.single = tp.single ? 1 : 0;
           launch_tile<Tr>(t, tp, B, st);
         } else {
           launch_conv<Tr>(a, st);
@@ -1456,18 +1599,20 @@ int launch_op(yk_model* m, const yk_op& op, const uint8_t* frames, int B, float 
         const int HW = op.src[0].h * op.src[0].w;
         if (HW <= kSppfLdsMaxHW && C % 8 == 0) {
           hipLaunchKernelGGL(sppf_lds_kernel<Tr>, dim3(B * (C / 8)), dim3(256), (size_t)HW * 8 * 4 * 4, st,
-                             m->bufs[op.src[0].buf], op.src[0].c_stride, op.src[0].c_off, C, op.src[0].h,
+                             img_ptr(m, op.src[0].buf, op.src[0].h, op.src[0].w, op.src[0].c_stride, b0),
+                             op.src[0].c_stride, op.src[0].c_off, C, op.src[0].h,
                              op.src[0].w);
           break;
         }
         const int n = M * (C / 4);
-        hipLaunchKernelGGL(sppf_pool_kernel<Tr>, dim3((n + 255) / 256), dim3(256), 0, st, m->bufs[op.src[0].buf],
+        hipLaunchKernelGGL(sppf_pool_kernel<Tr>, dim3((n + 255) / 256), dim3(256), 0, st,
+                           img_ptr(m, op.src[0].buf, op.src[0].h, op.src[0].w, op.src[0].c_stride, b0),
                            op.src[0].c_stride, op.src[0].c_off, C, op.src[0].h, op.src[0].w, M);
         break;
       }
       case YK_K_DETECT: {
         DetArgs a;
-        a.src = make_view(m, op.src[0]);
+        a.src = make_view(m, op.src[0], b0);
         a.cls_off = op.det_cls_off;
         a.cls_ch = op.det_cls_ch;
         a.wpk = (const uint4*)(m->blob + op.w_off);
@@ -1478,8 +1623,8 @@ int launch_op(yk_model* m, const yk_op& op, const uint8_t* frames, int B, float 
         a.anchor_off = op.det_anchor_off;
         a.M = B * op.src[0].h * op.src[0].w;
         a.conf = conf;
-        a.cand = m->cand;
-        a.cand_count = m->cand_count;
+        a.cand = m->cand + (size_t)b0 * D.n_anchors * 6;
+        a.cand_count = m->cand_count + b0;
         a.cap = D.n_anchors;
         hipLaunchKernelGGL(detect_kernel<Tr>, dim3((a.M + 63) / 64), dim3(256), 0, st, a);
         break;
@@ -1565,73 +1710,93 @@ void op_access(const yk_model* m, const yk_op& op, std::vector<int>& rd, std::ve
   }
 }
 
-// List-schedule the op program onto `lanes` streams: an op continues the lane whose tail is
-// its latest producer (keeps chains on one stream), else takes the lane that went idle first.
+// List-schedule the op program onto `lanes` streams per batch group: an op continues the lane
+// whose tail is its latest producer (keeps chains on one stream), else takes the lane that went
+// idle first.  Groups touch disjoint images of every buffer, so they never order against each
+// other; tasks are visited op-major so every group's chain advances together.
 void plan_dag(yk_model* m) {
-  const int n = (int)m->ops.size(), nb = m->desc.n_bufs + 1, L = m->lanes;
-  std::vector<int> last_w(nb, -1);
-  std::vector<std::vector<int>> readers(nb);
-  std::vector<int> tail(L, -1);
-  m->lane_of.assign(n, 0);
-  m->wait_on.assign(n, {});
-  m->needs_event.assign(n, 0);
+  const int n = (int)m->ops.size(), nb = m->desc.n_bufs + 1, L = m->lanes, G = m->groups;
+  m->tasks.clear();
+  m->lane_used.assign(G * L, 0);
+  m->lane_used[0] = 1;
   std::vector<int> rd, wr;
+  std::vector<std::vector<int>> last_w(G, std::vector<int>(nb, -1));
+  std::vector<std::vector<std::vector<int>>> readers(G, std::vector<std::vector<int>>(nb));
+  std::vector<int> tail(G * L, -1);
   for (int j = 0; j < n; ++j) {
     op_access(m, m->ops[j], rd, wr);
-    std::vector<int> deps;
-    for (int b : rd)
-      if (last_w[b] >= 0) deps.push_back(last_w[b]);
-    for (int b : wr) {
-      const bool accum = b == m->desc.n_bufs;
-      if (last_w[b] >= 0 && !accum) deps.push_back(last_w[b]);
-      for (int r : readers[b]) deps.push_back(r);
-    }
-    int lane = -1, best = -1;
-    for (int l = 0; l < L; ++l)
-      for (int d : deps)
-        if (tail[l] == d && d > best) best = d, lane = l;
-    if (lane < 0) {
-      lane = 0;
-      for (int l = 1; l < L; ++l)
-        if (tail[l] < tail[lane]) lane = l;
-    }
-    std::vector<int> latest(L, -1);  // per other lane, the latest producer to wait for
-    for (int d : deps)
-      if (m->lane_of[d] != lane && d > latest[m->lane_of[d]]) latest[m->lane_of[d]] = d;
-    for (int l = 0; l < L; ++l)
-      if (latest[l] >= 0) {
-        m->wait_on[j].push_back(latest[l]);
-        m->needs_event[latest[l]] = 1;
+    for (int g = 0; g < G; ++g) {
+      const int t = (int)m->tasks.size();
+      std::vector<int> deps;
+      for (int b : rd)
+        if (last_w[g][b] >= 0) deps.push_back(last_w[g][b]);
+      for (int b : wr) {
+        const bool accum = b == m->desc.n_bufs;
+        if (last_w[g][b] >= 0 && !accum) deps.push_back(last_w[g][b]);
+        for (int r : readers[g][b]) deps.push_back(r);
       }
-    m->lane_of[j] = lane;
-    tail[lane] = j;
-    for (int b : rd) readers[b].push_back(j);
-    for (int b : wr) {
-      if (b == m->desc.n_bufs) continue;
-      last_w[b] = j;
-      readers[b].clear();
+      int lane = -1, best = -1;
+      for (int l = g * L; l < (g + 1) * L; ++l)
+        for (int d : deps)
+          if (tail[l] == d && d > best) best = d, lane = l;
+      if (lane < 0) {
+        lane = g * L;
+        for (int l = g * L + 1; l < (g + 1) * L; ++l)
+          if (tail[l] < tail[lane]) lane = l;
+      }
+      yk_model::Task task{j, g, lane, {}, false};
+      std::vector<int> latest(G * L, -1);
+      for (int d : deps) {
+        const int dl = m->tasks[d].lane;
+        if (dl != lane && d > latest[dl]) latest[dl] = d;
+      }
+      for (int l = 0; l < G * L; ++l)
+        if (latest[l] >= 0) {
+          task.waits.push_back(latest[l]);
+          m->tasks[latest[l]].ev = true;
+        }
+      m->tasks.push_back(task);
+      m->lane_used[lane] = 1;
+      tail[lane] = t;
+      for (int b : rd) readers[g][b].push_back(t);
+      for (int b : wr) {
+        if (b == m->desc.n_bufs) continue;
+        last_w[g][b] = t;
+        readers[g][b].clear();
+      }
     }
   }
 }
 
 template <class Tr>
 int run_dag(yk_model* m, const uint8_t* frames, int B, float conf, hipStream_t st) {
-  const int n = (int)m->ops.size(), L = m->lanes;
+  const int G = m->groups, L = G * m->lanes, nt = (int)m->tasks.size();
   if (L <= 1) return run_ops<Tr>(m, frames, B, conf, st);
+  int gb0[9], gbn[9];  // images of each group
+  for (int g = 0, b0 = 0; g < G; ++g) {
+    gbn[g] = B / G + (g < B % G ? 1 : 0);
+    gb0[g] = b0;
+    b0 += gbn[g];
+  }
   auto lane_stream = [&](int l) { return l == 0 ? st : m->aux[l - 1]; };
-  hipEvent_t fork = m->ev[n];
+  hipEvent_t fork = m->ev[nt];
   YK_HIP(hipEventRecord(fork, st));
-  for (int l = 1; l < L; ++l) YK_HIP(hipStreamWaitEvent(m->aux[l - 1], fork, 0));
-  for (int j = 0; j < n; ++j) {
-    hipStream_t s = lane_stream(m->lane_of[j]);
-    for (int d : m->wait_on[j]) YK_HIP(hipStreamWaitEvent(s, m->ev[d], 0));
-    const int rc = launch_op<Tr>(m, m->ops[j], frames, B, conf, s);
-    if (rc != YK_OK) return rc;
-    if (m->needs_event[j]) YK_HIP(hipEventRecord(m->ev[j], s));
+  for (int l = 1; l < L; ++l)
+    if (m->lane_used[l]) YK_HIP(hipStreamWaitEvent(m->aux[l - 1], fork, 0));
+  for (int t = 0; t < nt; ++t) {
+    const yk_model::Task& task = m->tasks[t];
+    hipStream_t s = lane_stream(task.lane);
+    for (int d : task.waits) YK_HIP(hipStreamWaitEvent(s, m->ev[d], 0));
+    if (gbn[task.grp] > 0) {
+      const int rc = launch_op<Tr>(m, m->ops[task.op], frames, gbn[task.grp], conf, s, gb0[task.grp]);
+      if (rc != YK_OK) return rc;
+    }
+    if (task.ev) YK_HIP(hipEventRecord(m->ev[t], s));
   }
   for (int l = 1; l < L; ++l) {
-    YK_HIP(hipEventRecord(m->ev[n + l], m->aux[l - 1]));
-    YK_HIP(hipStreamWaitEvent(st, m->ev[n + l], 0));
+    if (!m->lane_used[l]) continue;
+    YK_HIP(hipEventRecord(m->ev[nt + l], m->aux[l - 1]));
+    YK_HIP(hipStreamWaitEvent(st, m->ev[nt + l], 0));
   }
   return YK_OK;
 }
@@ -1644,7 +1809,7 @@ int detect_impl(yk_model* m, const uint8_t* frames, int B, float conf, float iou
   YK_CHECK_ARG(conf >= 0.f && conf <= 1.f, "Invalid Confidence threshold, valid values are between 0.0 and 1.0");
   YK_CHECK_ARG(iou >= 0.f && iou <= 1.f, "Invalid IoU, valid values are between 0.0 and 1.0");
   YK_CHECK_ARG(max_det >= 0 && max_det <= D.max_det, "yk_detect: max_det exceeds the model's capacity");
-  m->plan_batch = B;
+  m->plan_batch = (B + m->groups - 1) / m->groups;
   if (!dets) dets = m->dets;
   if (!counts) counts = m->counts;
   YK_HIP(hipMemsetAsync(m->cand_count, 0, sizeof(int) * B, st));
@@ -1680,7 +1845,7 @@ int launch_nms(yk_model* m, int B, float iou, int max_det, float* dets, int32_t*
   return YK_OK;
 }
 
-hipError_t set_lanes(yk_model* m, int lanes) {
+hipError_t set_schedule(yk_model* m, int groups, int lanes) {
   for (auto& kv : m->graphs) (void)hipGraphExecDestroy(kv.second);
   m->graphs.clear();
   for (hipStream_t s : m->aux) (void)hipStreamDestroy(s);
@@ -1688,18 +1853,19 @@ hipError_t set_lanes(yk_model* m, int lanes) {
   m->aux.clear();
   m->ev.clear();
   m->lanes = lanes;
+  m->groups = groups;
+  plan_dag(m);
   hipError_t e = hipSuccess;
-  for (int l = 1; l < lanes && e == hipSuccess; ++l) {
+  for (int l = 1; l < groups * lanes && e == hipSuccess; ++l) {
     hipStream_t s;
     e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
     if (e == hipSuccess) m->aux.push_back(s);
   }
-  for (size_t i = 0; i < m->ops.size() + 1 + lanes && e == hipSuccess; ++i) {
+  for (size_t i = 0; i < m->tasks.size() + 1 + (size_t)groups * lanes && e == hipSuccess; ++i) {
     hipEvent_t v;
     e = hipEventCreateWithFlags(&v, hipEventDisableTiming);
     if (e == hipSuccess) m->ev.push_back(v);
   }
-  plan_dag(m);
   return e;
 }
 
@@ -1773,7 +1939,7 @@ int yk_model_create(yk_ctx* ctx, const yk_model_desc* desc, const void* host_blo
     e = hipFuncSetAttribute((const void*)nms_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)nms_lds_bytes());
   set_tile_attrs();
   if (const char* env = getenv("YK_CONV_DIRECT")) m->tiled = env[0] != '1';
-  if (e == hipSuccess) e = set_lanes(m, 3);
+  if (e == hipSuccess) e = set_schedule(m, 1, 3);
   if (e != hipSuccess) {
     yk::set_error(std::string("yk_model_create: ") + hipGetErrorString(e));
     yk_model_destroy(m);
@@ -1785,17 +1951,23 @@ int yk_model_create(yk_ctx* ctx, const yk_model_desc* desc, const void* host_blo
 
 int yk_model_set_lanes(yk_model* m, int lanes) {
   YK_CHECK_ARG(m && lanes >= 1 && lanes <= 8, "yk_model_set_lanes: lanes must be in [1, 8]");
+  return yk_model_set_schedule(m, m->groups, lanes);
+}
+
+int yk_model_set_schedule(yk_model* m, int groups, int lanes) {
+  YK_CHECK_ARG(m && lanes >= 1 && lanes <= 8 && groups >= 1 && groups <= 8 && groups * lanes <= 16,
+               "yk_model_set_schedule: need 1 <= groups, lanes <= 8 and groups * lanes <= 16");
   yk::DeviceGuard guard(m->ctx->device);
   YK_HIP(hipDeviceSynchronize());
-  YK_HIP(set_lanes(m, lanes));
+  YK_HIP(set_schedule(m, groups, lanes));
   return YK_OK;
 }
 
 int yk_model_get_schedule(yk_model* m, int32_t* lane_of, int32_t* n_waits) {
   YK_CHECK_ARG(m && lane_of && n_waits, "yk_model_get_schedule: NULL argument");
-  for (size_t i = 0; i < m->ops.size(); ++i) {
-    lane_of[i] = m->lane_of[i];
-    n_waits[i] = (int32_t)m->wait_on[i].size();
+  for (size_t i = 0; i < m->tasks.size(); ++i) {
+    lane_of[i] = m->tasks[i].lane;
+    n_waits[i] = (int32_t)m->tasks[i].waits.size();
   }
   return YK_OK;
 }
@@ -1833,9 +2005,13 @@ int yk_detect_graph(yk_model* m, const uint8_t* frames, int batch, float conf, f
     hipStream_t cap;
     YK_HIP(hipStreamCreateWithFlags(&cap, hipStreamNonBlocking));
     hipGraph_t g;
+    const bool dbg = getenv("YK_DEBUG_GRAPH") != nullptr;
     YK_HIP(hipStreamBeginCapture(cap, hipStreamCaptureModeThreadLocal));
+    if (dbg) fprintf(stderr, "[yk] capture begun\n");
     int rc = detect_impl(m, frames, batch, conf, iou, max_det, dets, counts, cap);
+    if (dbg) fprintf(stderr, "[yk] ops recorded rc=%d\n", rc);
     hipError_t ce = hipStreamEndCapture(cap, &g);
+    if (dbg) fprintf(stderr, "[yk] capture ended: %s\n", hipGetErrorString(ce));
     (void)hipStreamDestroy(cap);
     if (rc != YK_OK) return rc;
     if (ce != hipSuccess) {
@@ -1843,7 +2019,13 @@ int yk_detect_graph(yk_model* m, const uint8_t* frames, int batch, float conf, f
       return YK_ERR_HIP;
     }
     hipGraphExec_t ge;
+    if (dbg) {
+      size_t nn = 0;
+      (void)hipGraphGetNodes(g, nullptr, &nn);
+      fprintf(stderr, "[yk] graph nodes %zu, instantiating\n", nn);
+    }
     hipError_t ie = hipGraphInstantiate(&ge, g, nullptr, nullptr, 0);
+    if (dbg) fprintf(stderr, "[yk] instantiated: %s\n", hipGetErrorString(ie));
     (void)hipGraphDestroy(g);
     if (ie != hipSuccess) {
       yk::set_error(std::string("yk_detect_graph: instantiate failed: ") + hipGetErrorString(ie));
@@ -1915,8 +2097,9 @@ int yk_model_autotune(yk_model* m, const uint8_t* frames, int batch, float conf,
   yk::DeviceGuard guard(m->ctx->device);
   hipStream_t st = (hipStream_t)stream;
   const int n = (int)m->ops.size();
+  const int bt = (batch + m->groups - 1) / m->groups;  // the batch each group's kernels run at
   m->tuned.assign(n, {-1, 0, 0});
-  m->tuned_batch = batch;
+  m->tuned_batch = bt;
   for (auto& kv : m->graphs) (void)hipGraphExecDestroy(kv.second);
   m->graphs.clear();
   int rc = detect_impl(m, frames, batch, conf, 0.7f, 1, nullptr, nullptr, st);  // valid activations
@@ -1930,7 +2113,7 @@ int yk_model_autotune(yk_model* m, const uint8_t* frames, int batch, float conf,
     if (op.kind != YK_K_CONV) continue;
     if (op.has_res && op.res.buf == op.dst.buf && op.res.c_off == op.dst.c_off) continue;  // in place
     std::vector<std::array<int, 3>> cands = {{CK_DIRECT, 0, 0}};
-    if (tile_plan(op, esz, batch).ok) cands.push_back({CK_TILE, 0, 0});
+    if (tile_plan(op, esz, bt).ok) cands.push_back({CK_TILE, 0, 0});
     for (int nnt : {1, 2, 4})
       for (int npt : {1, 2, 4}) {
         if (nnt > 1 && 4 * op.n_tiles < 3 * ((op.n_tiles + nnt - 1) / nnt) * nnt) continue;
@@ -1940,18 +2123,20 @@ int yk_model_autotune(yk_model* m, const uint8_t* frames, int batch, float conf,
     std::array<int, 3> pick = {-1, 0, 0};
     for (const auto& c : cands) {
       m->tuned[i] = c;
-      rc = launch_any(m, op, frames, batch, conf, st);  // warm
+      rc = launch_any(m, op, frames, bt, conf, st);  // warm
       if (rc != YK_OK) return rc;
-      YK_HIP(hipEventRecord(e0, st));
-      for (int r = 0; r < reps; ++r) {
-        rc = launch_any(m, op, frames, batch, conf, st);
-        if (rc != YK_OK) return rc;
+      for (int trial = 0; trial < 3; ++trial) {  // min over trials: robust to clock / queue noise
+        YK_HIP(hipEventRecord(e0, st));
+        for (int r = 0; r < reps; ++r) {
+          rc = launch_any(m, op, frames, bt, conf, st);
+          if (rc != YK_OK) return rc;
+        }
+        YK_HIP(hipEventRecord(e1, st));
+        YK_HIP(hipEventSynchronize(e1));
+        float ms = 0.f;
+        YK_HIP(hipEventElapsedTime(&ms, e0, e1));
+        if (ms < best) best = ms, pick = c;
       }
-      YK_HIP(hipEventRecord(e1, st));
-      YK_HIP(hipEventSynchronize(e1));
-      float ms = 0.f;
-      YK_HIP(hipEventElapsedTime(&ms, e0, e1));
-      if (ms < best) best = ms, pick = c;
     }
     m->tuned[i] = pick;
   }

@@ -63,6 +63,7 @@ struct Dev {
   yk_track_out* rows;   // [S][T]
   int* counts;          // [S]
   yk_tracker_stats* stats;  // [S]
+  long long* phase;         // [S][16] wall_clock64 at the step's phase boundaries (profiling)
   int T, D, C;
   int max_lost, min_hits;
   double thr;
@@ -473,6 +474,7 @@ __global__ void __launch_bounds__(NT) step_kernel(Dev g, const DT* __restrict__ 
   int* fstack = g.free_stack + (size_t)s * T;
   int* wsum = L.misc + M_WSUM;
 
+  if (tid == 0) g.phase[s * 16 + 0] = wall_clock64();
   int Draw = counts[s];
   if (Draw < 0) Draw = 0;
   const int D = Draw < g.D ? Draw : g.D;
@@ -492,6 +494,7 @@ __global__ void __launch_bounds__(NT) step_kernel(Dev g, const DT* __restrict__ 
     state_to_bbox(sl.x, &L.pb[4 * i]);
   }
   __syncthreads();
+  if (tid == 0) g.phase[s * 16 + 1] = wall_clock64();
 
   // Step 2: association (multi:61-68, 134-178)
   if (D > 0 && n > 0) {
@@ -513,6 +516,7 @@ __global__ void __launch_bounds__(NT) step_kernel(Dev g, const DT* __restrict__ 
       }
     }
     __syncthreads();
+    if (tid == 0) g.phase[s * 16 + 2] = wall_clock64();
     int nc = L.misc[M_NCAND];
     if (nc > g.C) {
       if (tid == 0) L.misc[M_OVERFLOW] += nc - g.C;
@@ -541,7 +545,10 @@ __global__ void __launch_bounds__(NT) step_kernel(Dev g, const DT* __restrict__ 
       }
       if (local_active) atomicAdd(&L.misc[M_ACTIVE], local_active);
       __syncthreads();
-      if (L.misc[M_ACTIVE] == 0) break;
+      if (L.misc[M_ACTIVE] == 0) {
+        if (tid == 0) g.phase[s * 16 + 10] = round;
+        break;
+      }
       for (int c = tid; c < nc; c += NT) {
         const int f = cflat[c], d = f / n, t = f - d * n;
         if (L.det_match[d] < 0 && L.trk_match[t] < 0) {
@@ -562,6 +569,7 @@ __global__ void __launch_bounds__(NT) step_kernel(Dev g, const DT* __restrict__ 
     }
   }
 
+  if (tid == 0) g.phase[s * 16 + 3] = wall_clock64();
   // Steps 3-4: update matched tracks, mark the others lost (multi:71-89)
   int recov = 0;
   for (int i = tid; i < n; i += NT) {
@@ -578,6 +586,8 @@ __global__ void __launch_bounds__(NT) step_kernel(Dev g, const DT* __restrict__ 
     }
   }
   if (recov) atomicAdd(&L.misc[M_RECOVER], recov);
+  __syncthreads();
+  if (tid == 0) g.phase[s * 16 + 4] = wall_clock64();
 
   // Step 5: new tracks for unmatched detections, ascending detection order (multi:92-101)
   int n_new_total = 0;
@@ -610,6 +620,7 @@ __global__ void __launch_bounds__(NT) step_kernel(Dev g, const DT* __restrict__ 
   if (n_new > nfree0) n_new = nfree0;
   __syncthreads();
 
+  if (tid == 0) g.phase[s * 16 + 5] = wall_clock64();
   // Step 6: delete (multi:104-113) with a stable compaction of the list
   const int n_all = n + n_new;
   int kept = 0, n_del = 0;
@@ -650,6 +661,7 @@ __global__ void __launch_bounds__(NT) step_kernel(Dev g, const DT* __restrict__ 
   for (int i = tid; i < kept; i += NT) order[i] = L.order_tmp[i];
   __syncthreads();
 
+  if (tid == 0) g.phase[s * 16 + 6] = wall_clock64();
   // Step 7: outputs in list order (multi:116-126), get_track_info may predict (quirk A)
   const int fc = (int)H.st.frame_count + 1;
   int nout = 0, lt = 0;
@@ -672,6 +684,7 @@ __global__ void __launch_bounds__(NT) step_kernel(Dev g, const DT* __restrict__ 
   }
   if (lt) atomicAdd(&L.misc[M_LONGTERM], lt);
   __syncthreads();
+  if (tid == 0) g.phase[s * 16 + 7] = wall_clock64();
   if (tid == 0) {
     H.n_tracks = kept;
     H.n_free = nfree0 - n_new + n_del;
@@ -864,6 +877,8 @@ int yk_tracker_create(yk_ctx* ctx, int n_streams, const yk_tracker_cfg* cfg, yk_
   A((void**)&g.rows, S * T * sizeof(yk_track_out));
   A((void**)&g.counts, S * sizeof(int));
   A((void**)&g.stats, S * sizeof(yk_tracker_stats));
+  A((void**)&g.phase, S * 16 * sizeof(long long));
+  if (e == hipSuccess) e = hipMemset(g.phase, 0, S * 16 * sizeof(long long));
   A((void**)&t->d_snap, T * sizeof(yk_track_state));
   A((void**)&t->d_row1, sizeof(yk_track_out));
   A((void**)&t->d_box, 16 * sizeof(double));
@@ -894,7 +909,7 @@ int yk_tracker_destroy(yk_tracker* t) {
   yk::DeviceGuard guard(t->ctx->device);
   Dev& g = t->dev;
   void* ptrs[] = {g.slots, g.hdr, g.order, g.free_stack, g.cand_key, g.cand_flat, g.rows,
-                  g.counts, g.stats, t->d_snap, t->d_row1, t->d_box, t->d_status};
+                  g.counts, g.stats, g.phase, t->d_snap, t->d_row1, t->d_box, t->d_status};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   delete t;
@@ -1025,6 +1040,17 @@ int yk_track_create(yk_tracker* t, int s, const double* box, int dtype, int32_t 
     yk::set_error("yk_track_create: stream is at max_tracks capacity");
     return YK_ERR_CAPACITY;
   }
+  return YK_OK;
+}
+
+int yk_tracker_phase_ticks(yk_tracker* t, int s, int64_t* host_ticks16, void* stream) {
+  YK_CHECK_ARG(t && host_ticks16, "yk_tracker_phase_ticks: NULL argument");
+  YK_CHECK_ARG(s >= 0 && s < t->S, "yk_tracker_phase_ticks: stream index out of range");
+  yk::DeviceGuard guard(t->ctx->device);
+  hipStream_t st = (hipStream_t)stream;
+  YK_HIP(hipMemcpyAsync(host_ticks16, t->dev.phase + (size_t)s * 16, 16 * sizeof(long long), hipMemcpyDeviceToHost,
+                        st));
+  YK_HIP(hipStreamSynchronize(st));
   return YK_OK;
 }
 

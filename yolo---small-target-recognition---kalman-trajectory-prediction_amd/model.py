@@ -467,9 +467,14 @@ class DeviceModel:
         L.check(L.lib().yk_model_set_plan(self._h, int(op), int(batch), int(kind), int(nnt), int(npt)),
                 "yk_model_set_plan")
 
+    def set_schedule(self, groups: int, lanes: int):
+        """Cut the batch into `groups` independent sub-batches, each on `lanes` streams."""
+        L.check(L.lib().yk_model_set_schedule(self._h, int(groups), int(lanes)), "yk_model_set_schedule")
+        self.groups = int(groups)
+
     def schedule(self):
-        """(lane per op, cross-lane waits per op) of the current DAG schedule."""
-        n = len(self.prog.ops)
+        """(lane per task, cross-lane waits per task) of the current DAG schedule (op-major)."""
+        n = len(self.prog.ops) * getattr(self, "groups", 1)
         lane, waits = np.zeros(n, np.int32), np.zeros(n, np.int32)
         L.check(L.lib().yk_model_get_schedule(self._h, L.ptr(lane), L.ptr(waits)), "yk_model_get_schedule")
         return lane, waits

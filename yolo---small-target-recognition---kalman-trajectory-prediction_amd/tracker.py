@@ -166,6 +166,15 @@ class MultiStreamTracker:
                 "yk_tracker_outputs")
         return rows.value, counts.value, stats.value
 
+    def phase_us(self, stream_index: int = 0):
+        """Per-phase device time (µs) of the last step on one stream: predict, candidates,
+        rounds, update, create, delete, outputs; plus the association rounds used."""
+        t = np.zeros(16, np.int64)
+        L.check(L.lib().yk_tracker_phase_ticks(self._h, int(stream_index), L.ptr(t), L.current_stream(self.device)),
+                "yk_tracker_phase_ticks")
+        names = ["predict", "candidates", "rounds", "update", "create", "delete", "outputs"]
+        return {n: float(t[k + 1] - t[k]) / 100.0 for k, n in enumerate(names)} | {"n_rounds": int(t[10])}
+
     def snapshot(self, stream_index: int = 0) -> np.ndarray:
         out = np.zeros(self.max_tracks, dtype=L.TRACK_STATE_DTYPE)
         n = C.c_int32()
