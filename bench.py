@@ -46,10 +46,12 @@ def parse():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-tune", action="store_true", help="skip the per-op conv kernel autotune")
     ap.add_argument("--lanes", type=int, default=3, help="streams per batch group the detector's op DAG runs on")
-    ap.add_argument("--groups", type=int, default=2, help="independent sub-batches run concurrently")
+    ap.add_argument("--groups", type=int, default=1, help="independent sub-batches run concurrently")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-profile", action="store_true")
+    ap.add_argument("--plan-out", default="", help="write the autotuned conv plan (json) here")
+    ap.add_argument("--plan-in", default="", help="load a conv plan (json) instead of autotuning")
     ap.add_argument("--dump-ops", default="", help="write per-op device times (json) to this path")
     return ap.parse_args()
 
@@ -85,10 +87,24 @@ def roofline(pipe, frames, dtype, B):
     total_ms = sum(v["ms"] for v in by.values())
     return {
         "kernel": dom, "bound": "mfma", "achieved": round(ach, 2), "peak": PEAK[dtype], "unit": "TFLOP/s",
-        "frac": round(ach / PEAK[dtype], 5), "traffic": None, "avg_launch_us": round(avg_ms * 1e3, 2),
+        "frac": round(ach / PEAK[dtype], 5), "traffic": pmc_traffic(dom), "traffic_unit": "bytes/launch", "avg_launch_us": round(avg_ms * 1e3, 2),
         "launches_per_step": d["launches"], "flops_per_launch": int(d["flops"] / d["launches"]),
         "share_of_detect_time": round(d["ms"] / total_ms, 3),
     }, by, prof
+
+
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
+    (tools/pmc_summary.py: FETCH_SIZE x2 + WRITE_SIZE, separate passes), or None."""
+    path = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            k = json.load(f)["kernels"]
+    except (OSError, ValueError, KeyError):
+        return None
+    short = kernel.replace("yk::det::", "").replace("yk::trk::", "")
+    v = k.get(short)
+    return None if v is None else round(v["hbm_bytes_per_launch"])
 
 
 def tracker_roofline(pipe, reps=20):
@@ -147,6 +163,10 @@ def cpu_baseline(P, scale, seconds, targets, seed=0):
                       f"({threads} threads) + numpy tracker, after 2 warm-up frames"}
 
 
+def log(msg):
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def main():
     a = parse()
     ws, rank, local = dist_setup()
@@ -166,12 +186,24 @@ def main():
     for s, sc in enumerate(scenes):
         frames[:, s] = sc.frames_torch(0, F, dev)
     torch.cuda.synchronize()
+    log("frames resident; setting schedule")
     pipe.model.set_schedule(a.groups, a.lanes)
     pipe.frames.copy_(frames[0])
+    tune = not a.no_tune
+    if a.plan_in:
+        with open(a.plan_in) as f:
+            pl = json.load(f)
+        pipe.model.load_plan(pl["batch"], pl["plan"])
+        tune = False
     if not a.no_graph:
-        pipe.capture(tune=not a.no_tune)
-    elif not a.no_tune:
+        pipe.capture(tune=tune)
+    elif tune:
         pipe.model.autotune(pipe.frames, pipe.conf)
+    if a.plan_out and rank == 0:
+        b, pl = pipe.model.get_plan()
+        with open(a.plan_out, "w") as f:
+            json.dump({"batch": b, "plan": pl}, f)
+    log("graph captured; warm-up")
     # warm-up
     for t in range(a.warmup):
         pipe.run(frames[t % F])
@@ -188,6 +220,7 @@ def main():
     if ws > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    log(f"timed {a.steps} steps in {elapsed:.3f}s")
     counts, stats = pipe.stats()
     live = float(stats["current_active_tracks"].mean())
     frames_done = S * a.steps
@@ -222,6 +255,7 @@ def main():
             with open(a.dump_ops, "w") as f:
                 json.dump({"ops": [{"op": i, "kind": k, "kernel": n, "us": round(ms * 1e3, 2), "gflop": fl / 1e9}
                                    for (i, k, n, ms), fl in zip(prof, flops)], "by_kernel": by_kernel}, f, indent=1)
+    log("profile done")
     cpu = None
     if rank == 0 and ws == 1 and not a.no_cpu_baseline:
         cpu = cpu_baseline(P, a.scale, a.cpu_seconds, a.targets)

@@ -287,6 +287,10 @@ int yk_model_autotune(yk_model* m, const uint8_t* dev_frames, int batch, float c
  * kind -1 = heuristic, 0 = direct, 1 = LDS-tiled (falls back to direct where the tile does not
  * fit), 2 = split-K with an nnt x npt fragment tile (nnt, npt in {1, 2, 4}). */
 int yk_model_set_plan(yk_model* m, int op_index, int batch, int kind, int nnt, int npt);
+/* The current per-op conv plan (n_ops x {kind, nnt, npt}; kind -1 = heuristic) and the batch
+ * it was tuned for (0 if none): with yk_model_set_plan, replays an autotune without re-running
+ * it (e.g. under a profiler). */
+int yk_model_get_plan(yk_model* m, int32_t* plan, int32_t* batch);
 /* The schedule: per task (op-major: task = op * groups + group), its lane and the number of
  * cross-lane waits (arrays of n_ops * groups). */
 int yk_model_get_schedule(yk_model* m, int32_t* lane_of, int32_t* n_waits);

@@ -86,6 +86,7 @@ _SIGS = {
     "yk_model_set_plan": ([_vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int], C.c_int),
     "yk_model_autotune": ([_vp, _vp, C.c_int, C.c_float, C.c_int, _vp], C.c_int),
     "yk_model_get_schedule": ([_vp, _vp, _vp], C.c_int),
+    "yk_model_get_plan": ([_vp, _vp, _vp], C.c_int),
 }
 
 _lock = threading.Lock()

@@ -1957,6 +1957,9 @@ int yk_model_set_lanes(yk_model* m, int lanes) {
 int yk_model_set_schedule(yk_model* m, int groups, int lanes) {
   YK_CHECK_ARG(m && lanes >= 1 && lanes <= 8 && groups >= 1 && groups <= 8 && groups * lanes <= 16,
                "yk_model_set_schedule: need 1 <= groups, lanes <= 8 and groups * lanes <= 16");
+  // Several groups each fanned out over several lanes crash hipStreamEndCapture (ROCm 7.2) when
+  // the schedule is captured into a graph; each combination on its own captures fine.
+  YK_CHECK_ARG(groups == 1 || lanes == 1, "yk_model_set_schedule: groups > 1 needs lanes == 1");
   yk::DeviceGuard guard(m->ctx->device);
   YK_HIP(hipDeviceSynchronize());
   YK_HIP(set_schedule(m, groups, lanes));
@@ -2088,6 +2091,15 @@ int yk_model_set_plan(yk_model* m, int op_index, int batch, int kind, int nnt, i
     if ((op_index < 0 || i == op_index) && m->ops[i].kind == YK_K_CONV) m->tuned[i] = {kind, nnt, npt};
   for (auto& kv : m->graphs) (void)hipGraphExecDestroy(kv.second);
   m->graphs.clear();
+  return YK_OK;
+}
+
+int yk_model_get_plan(yk_model* m, int32_t* plan, int32_t* batch) {
+  YK_CHECK_ARG(m && plan && batch, "yk_model_get_plan: NULL argument");
+  const bool have = m->tuned.size() == m->ops.size();
+  *batch = have ? m->tuned_batch : 0;
+  for (size_t i = 0; i < m->ops.size(); ++i)
+    for (int j = 0; j < 3; ++j) plan[i * 3 + j] = have ? m->tuned[i][j] : (j == 0 ? -1 : 0);
   return YK_OK;
 }
 

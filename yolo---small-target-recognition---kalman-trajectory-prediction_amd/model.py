@@ -467,6 +467,19 @@ class DeviceModel:
         L.check(L.lib().yk_model_set_plan(self._h, int(op), int(batch), int(kind), int(nnt), int(npt)),
                 "yk_model_set_plan")
 
+    def get_plan(self):
+        """(batch, [[kind, nnt, npt] per op]) of the current conv plan (autotune result)."""
+        n = len(self.prog.ops)
+        plan, b = np.zeros(3 * n, np.int32), np.zeros(1, np.int32)
+        L.check(L.lib().yk_model_get_plan(self._h, L.ptr(plan), L.ptr(b)), "yk_model_get_plan")
+        return int(b[0]), plan.reshape(n, 3).tolist()
+
+    def load_plan(self, batch: int, plan):
+        """Re-apply a plan from get_plan() (per conv op; kind -1 keeps the heuristic)."""
+        for i, (kind, nnt, npt) in enumerate(plan):
+            if self.prog.ops[i].kind == YK_K_CONV:
+                self.set_plan(batch, kind, nnt, npt, op=i)
+
     def set_schedule(self, groups: int, lanes: int):
         """Cut the batch into `groups` independent sub-batches, each on `lanes` streams."""
         L.check(L.lib().yk_model_set_schedule(self._h, int(groups), int(lanes)), "yk_model_set_schedule")
