@@ -44,6 +44,8 @@ def parse():
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--frames", type=int, default=120, help="pre-rendered frames per stream (cycled)")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-pipeline", action="store_true",
+                    help="run tracker(t) on the detector's stream instead of overlapping it with detector(t+1)")
     ap.add_argument("--no-tune", action="store_true", help="skip the per-op conv kernel autotune")
     ap.add_argument("--lanes", type=int, default=3, help="streams per batch group the detector's op DAG runs on")
     ap.add_argument("--groups", type=int, default=1, help="independent sub-batches run concurrently")
@@ -178,7 +180,8 @@ def main():
     pipeline = import_module(PKG + ".pipeline")
     S, H, W = a.streams, 512, 640
     seed0 = 1000 * rank
-    pipe = pipeline.StreamPipeline(f"yolov8{a.scale}-small.yaml", S, (H, W), a.dtype, seed=0, device=local)
+    pipe = pipeline.StreamPipeline(f"yolov8{a.scale}-small.yaml", S, (H, W), a.dtype, seed=0, device=local,
+                                   pipelined=not a.no_pipeline)
     # pre-render frames of every stream into HBM (inputs resident before the timed region)
     F = max(2, min(a.frames, a.warmup + a.steps))
     scenes = [P.synth.Scene(seed=seed0 + s, n_targets=a.targets, n_frames=F + 1) for s in range(S)]
@@ -270,7 +273,7 @@ def main():
             "config": {"workload": f"YOLOv8{a.scale}+P2 640x512, {S} streams/GPU as batch {S}, "
                                    f"{a.targets} targets/stream, tracker(150, 1, 0.1) (BASELINE config 3)",
                        "streams_per_gpu": S, "global_batch": S * ws, "parallelism": f"streams sharded over {ws} GPU(s)",
-                       "graph": not a.no_graph, "autotuned": not a.no_tune, "dag_lanes": a.lanes,
+                       "graph": not a.no_graph, "tracker_overlapped": not a.no_pipeline, "autotuned": not a.no_tune, "dag_lanes": a.lanes,
                        "batch_groups": a.groups,
                        "live_tracks_per_stream": round(live, 1),
                        "gflop_per_frame": round(gflop, 3)},

@@ -93,3 +93,29 @@ def test_reference_driver_loop_through_compat_packages():
     assert detection_frames > 0
     assert tracker.frame_count == 8
     assert results[0].boxes.xyxy.is_cuda and results[0].orig_shape == (512, 640)
+
+
+def test_pipelined_tracker_stream_matches_serial():
+    """pipelined=True (tracker(t) on its own stream, overlapping detector(t+1), double-buffered
+    detections) gives exactly the serial pipeline's tracker state."""
+    P = pkg()
+    pipeline = importlib.import_module(P.__name__ + ".pipeline")
+    S, F = 4, 24
+    runs = []
+    for pipelined in (False, True):
+        pipe = pipeline.StreamPipeline("yolov8s-small.yaml", S, (512, 640), "bf16", seed=0, max_tracks=256,
+                                       pipelined=pipelined)
+        scenes = [P.synth.Scene(seed=40 + s, n_targets=16, n_frames=F) for s in range(S)]
+        frames = torch.stack([sc.frames_torch(0, F, "cuda") for sc in scenes], 1)
+        pipe.frames.copy_(frames[0])
+        pipe.capture(tune=False)
+        for t in range(F):
+            pipe.run(frames[t])
+        pipe.sync()
+        rows, counts, stats = pipe.tracker.download()
+        runs.append((rows.copy(), counts.copy(), stats.copy()))
+    (r0, c0, s0), (r1, c1, s1) = runs
+    np.testing.assert_array_equal(c0, c1)
+    np.testing.assert_array_equal(s0, s1)
+    for s in range(S):
+        assert r0[s][: c0[s]].tobytes() == r1[s][: c1[s]].tobytes()

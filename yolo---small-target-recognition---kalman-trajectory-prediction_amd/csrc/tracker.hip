@@ -172,27 +172,32 @@ __device__ double np_pairwise_sum(const double* a, int n) {
   return res;
 }
 
-__device__ void analyze_motion(Slot& s) {
+// The velocity history in chronological order (oldest first), as three arrays vx, vy, ang of
+// n = s.vh_len entries: the step kernel keeps them in LDS, so the serial reductions below --
+// numpy's evaluation order, bit for bit -- run on unit-stride LDS reads.  dch (m = n - 1
+// entries) may alias vx: vx is dead once the mean and std are done.
+__device__ void analyze_motion(Slot& s, const double* vx, const double* vy, const double* ang, double* dch) {
   // kf.py:137-182
   const int n = s.vh_len;
   if (n < 5) return;
   double mean[2], sq[2];
+  const double* v[2] = {vx, vy};
+#pragma unroll
   for (int j = 0; j < 2; ++j) {  // np.mean(axis=0): sequential over rows
-    int idx = s.vh_head;
-    double acc = s.vh[idx][j];
-    for (int k = 1; k < n; ++k) {
-      idx = (idx + 1 == VH) ? 0 : idx + 1;
-      acc += s.vh[idx][j];
-    }
+    const double* a = v[j];
+    double acc = a[0];
+#pragma unroll 8
+    for (int k = 1; k < n; ++k) acc += a[k];
     mean[j] = acc / (double)n;
   }
+#pragma unroll
   for (int j = 0; j < 2; ++j) {  // np.std(axis=0), ddof=0
-    int idx = s.vh_head;
-    double d = s.vh[idx][j] - mean[j];
+    const double* a = v[j];
+    double d = a[0] - mean[j];
     double acc = d * d;
+#pragma unroll 8
     for (int k = 1; k < n; ++k) {
-      idx = (idx + 1 == VH) ? 0 : idx + 1;
-      d = s.vh[idx][j] - mean[j];
+      d = a[k] - mean[j];
       acc += d * d;
     }
     sq[j] = sqrt(acc / (double)n);
@@ -205,21 +210,15 @@ __device__ void analyze_motion(Slot& s) {
   s.direction = atan2(mean[1], mean[0]);
   const double speed_stab = 1.0 / (1.0 + ((0.0 + sq[0]) + sq[1]) / 2.0);
   // _calculate_direction_consistency (kf.py:165-182); n >= 5 here, so the n<3 exit is dead
-  double dch[VH];
   const int m = n - 1;
-  {
-    int idx = s.vh_head;
-    double prev = s.vang[idx];
-    for (int k = 0; k < m; ++k) {
-      idx = (idx + 1 == VH) ? 0 : idx + 1;
-      const double cur = s.vang[idx];
-      double c = cur - prev;
-      if (!(fabs(c) < kPi)) c = c - 2.0 * kPi * (c > 0.0 ? 1.0 : (c < 0.0 ? -1.0 : c));
-      dch[k] = c;
-      prev = cur;
-    }
+#pragma unroll 8
+  for (int k = 0; k < m; ++k) {
+    double c = ang[k + 1] - ang[k];
+    if (!(fabs(c) < kPi)) c = c - 2.0 * kPi * (c > 0.0 ? 1.0 : (c < 0.0 ? -1.0 : c));
+    dch[k] = c;
   }
   const double dmean = np_pairwise_sum(dch, m) / (double)m;
+#pragma unroll 8
   for (int k = 0; k < m; ++k) {
     const double d = dch[k] - dmean;
     dch[k] = d * d;
@@ -231,8 +230,22 @@ __device__ void analyze_motion(Slot& s) {
   s.pconf = s.stability * (1.0 < frac ? 1.0 : frac);
 }
 
+constexpr int VS = VH + 1;  // staged entries per array (one spare for the push onto a full ring)
+
+// Chronological copy of the velocity history (before an update) into st[3][VS].
+__device__ void stage_chrono(const Slot& s, double* st) {
+  int idx = s.vh_head;
+  for (int k = 0; k < s.vh_len; ++k) {
+    st[k] = s.vh[idx][0];
+    st[VS + k] = s.vh[idx][1];
+    st[2 * VS + k] = s.vang[idx];
+    idx = (idx + 1 == VH) ? 0 : idx + 1;
+  }
+}
+
+// st: stage_chrono() of the slot before this update ([3][VS], LDS in the step kernel).
 template <typename DT>
-__device__ void kf_update(Slot& s, const DT* box) {
+__device__ void kf_update(Slot& s, const DT* box, double* st) {
   // kf.py:249-297 (recovery print omitted; the count is kept by the caller)
   s.tsu = 0;
   s.hits += 1;
@@ -258,10 +271,18 @@ __device__ void kf_update(Slot& s, const DT* box) {
     s.P[4 * c + 3] = nkv * a + v;
   }
   int pos;
+  const int len0 = s.vh_len;
   ring_push(s.vh, VH, s.vh_len, s.vh_head, s.x[4], s.x[5], &pos);
-  s.vang[pos] = atan2(s.x[5], s.x[4]);
+  const double ang = atan2(s.x[5], s.x[4]);
+  s.vang[pos] = ang;
+  // the staged chronological copy: append; a full ring drops its oldest entry (base 1)
+  const int at = len0 < VH ? len0 : VH;
+  st[at] = s.x[4];
+  st[VS + at] = s.x[5];
+  st[2 * VS + at] = ang;
+  const int base = len0 < VH ? 0 : 1;
   ring_push(s.th, TH, s.th_len, s.th_head, s.x[0], s.x[1]);
-  analyze_motion(s);
+  analyze_motion(s, st + base, st + VS + base, st + 2 * VS + base, st + base);
 }
 
 __device__ __forceinline__ void mark_lost(Slot& s) {
@@ -326,7 +347,7 @@ __device__ void lost_prediction(Slot& s, double* box, double& conf) {
 
 // get_track_info (kf.py:335-383) including quirk A (a second predict() on the first
 // lost frame, via get_lost_prediction -> enhanced_long_term_predict(1)).
-__device__ void track_info(Slot& s, yk_track_out& o) {
+__device__ void track_info(Slot& s, yk_track_out& o, bool copy_traj = true) {
   double box[4];
   double conf;
   int status;
@@ -360,6 +381,7 @@ __device__ void track_info(Slot& s, yk_track_out& o) {
   o.direction = s.direction;
   const int nt = s.th_len < TOUT ? s.th_len : TOUT;
   o.traj_len = nt;
+  if (!copy_traj) return;  // the step kernel copies trajectories cooperatively
   int idx = s.th_head + (s.th_len - nt);
   if (idx >= TH) idx -= TH;
   for (int k = 0; k < nt; ++k) {
@@ -427,11 +449,24 @@ struct Lds {
   int* col_arg;               // [T]
   int* order_tmp;             // [T]
   int* misc;                  // [16]
+  double* stage;              // [ch][3][VS] chronological velocity history of the tracks being updated
 };
 
+constexpr int STAGE_D = 3 * (VH + 1);   // doubles per staged track
+constexpr int CH_MAX = 64;              // tracks staged per update chunk (at most)
+
+__host__ __device__ inline size_t lds_base_bytes(int T, int D) {
+  const size_t b = (size_t)T * 32 + (size_t)D * 32 + (size_t)D * 4 + (size_t)T * 4 + (size_t)D * 8 +
+                   (size_t)T * 8 + (size_t)D * 4 + (size_t)T * 4 + (size_t)T * 4 + 16 * 4;
+  return (b + 15) / 16 * 16;
+}
+// staging chunk: as many tracks as fit the 160 KiB LDS budget, up to CH_MAX
+__host__ __device__ inline int stage_chunk(int T, int D) {
+  const long room = (160L * 1024 - (long)lds_base_bytes(T, D)) / (STAGE_D * 8);
+  return room < 1 ? 0 : room > CH_MAX ? CH_MAX : (int)room;
+}
 __host__ __device__ inline size_t lds_bytes(int T, int D) {
-  return (size_t)T * 32 + (size_t)D * 32 + (size_t)D * 4 + (size_t)T * 4 + (size_t)D * 8 +
-         (size_t)T * 8 + (size_t)D * 4 + (size_t)T * 4 + (size_t)T * 4 + 16 * 4;
+  return lds_base_bytes(T, D) + (size_t)stage_chunk(T, D) * STAGE_D * 8;
 }
 
 __device__ Lds carve(char* base, int T, int D) {
@@ -455,6 +490,8 @@ __device__ Lds carve(char* base, int T, int D) {
   L.order_tmp = (int*)base;
   base += (size_t)T * 4;
   L.misc = (int*)base;
+  base += 16 * 4;
+  L.stage = (double*)(((size_t)base + 15) / 16 * 16);
   return L;
 }
 
@@ -570,20 +607,50 @@ __global__ void __launch_bounds__(NT) step_kernel(Dev g, const DT* __restrict__ 
   }
 
   if (tid == 0) g.phase[s * 16 + 3] = wall_clock64();
-  // Steps 3-4: update matched tracks, mark the others lost (multi:71-89)
+  // Steps 3-4: update matched tracks, mark the others lost (multi:71-89).  The matched
+  // tracks' velocity rings (1.2 KB each) are staged into LDS CH tracks at a time by the whole
+  // workgroup (coalesced 16-B loads, all in flight at once); each track's thread then runs
+  // the KF update and analyze_motion_pattern's serial reductions out of LDS.
   int recov = 0;
-  for (int i = tid; i < n; i += NT) {
-    Slot& sl = slots[order[i]];
-    const int d = L.trk_match[i];
-    if (d >= 0) {
+  int n_upd = 0;
+  for (int base = 0; base < n; base += NT) {
+    const int i = base + tid;
+    const int flag = (i < n && L.trk_match[i] >= 0) ? 1 : 0;
+    int tot;
+    const int r = n_upd + block_scan(flag, wsum, tot);
+    if (flag) L.order_tmp[r] = i;
+    else if (i < n) mark_lost(slots[order[i]]);
+    n_upd += tot;
+  }
+  __syncthreads();
+  const int CH = stage_chunk(T, g.D);
+  for (int c0 = 0; c0 < n_upd; c0 += CH) {
+    const int m = n_upd - c0 < CH ? n_upd - c0 : CH;
+    for (int u = tid; u < m * VH; u += NT) {  // chronological copy of each ring
+      const int j = u / VH, k = u - j * VH;
+      const Slot& sl = slots[order[L.order_tmp[c0 + j]]];
+      if (k < sl.vh_len) {
+        int idx = sl.vh_head + k;
+        if (idx >= VH) idx -= VH;
+        const double2 v = *(const double2*)&sl.vh[idx][0];
+        double* st = L.stage + (size_t)j * STAGE_D;
+        st[k] = v.x;
+        st[VS + k] = v.y;
+        st[2 * VS + k] = sl.vang[idx];
+      }
+    }
+    __syncthreads();
+    if (tid < m) {
+      const int i = L.order_tmp[c0 + tid];
+      Slot& sl = slots[order[i]];
+      const int d = L.trk_match[i];
       DT db[4];
 #pragma unroll
       for (int k = 0; k < 4; ++k) db[k] = (DT)L.det[4 * d + k];
       recov += sl.is_lost ? 1 : 0;
-      kf_update<DT>(sl, db);
-    } else {
-      mark_lost(sl);
+      kf_update<DT>(sl, db, L.stage + (size_t)tid * STAGE_D);
     }
+    __syncthreads();
   }
   if (recov) atomicAdd(&L.misc[M_RECOVER], recov);
   __syncthreads();
@@ -662,7 +729,9 @@ __global__ void __launch_bounds__(NT) step_kernel(Dev g, const DT* __restrict__ 
   __syncthreads();
 
   if (tid == 0) g.phase[s * 16 + 6] = wall_clock64();
-  // Step 7: outputs in list order (multi:116-126), get_track_info may predict (quirk A)
+  // Step 7: outputs in list order (multi:116-126), get_track_info may predict (quirk A).
+  // Rows are filled one thread per track; the 30-point trajectories are then copied by the
+  // whole workgroup, one 16-B point per thread (the ring reads are independent loads).
   const int fc = (int)H.st.frame_count + 1;
   int nout = 0, lt = 0;
   for (int base = 0; base < kept; base += NT) {
@@ -677,12 +746,26 @@ __global__ void __launch_bounds__(NT) step_kernel(Dev g, const DT* __restrict__ 
     const int r = nout + block_scan(q, wsum, tot);
     if (q) {
       yk_track_out& o = g.rows[(size_t)s * T + r];
-      track_info(*sl, o);
+      track_info(*sl, o, false);
       if (o.status == 1 && o.time_since_update > 30) ++lt;
+      L.order_tmp[r] = order[i];
     }
     nout += tot;
   }
   if (lt) atomicAdd(&L.misc[M_LONGTERM], lt);
+  __syncthreads();
+  for (int u = tid; u < nout * TOUT; u += NT) {
+    const int r = u / TOUT, k = u - r * TOUT;
+    const Slot& sl = slots[L.order_tmp[r]];
+    const int nt = sl.th_len < TOUT ? sl.th_len : TOUT;
+    double2 v = make_double2(0.0, 0.0);
+    if (k < nt) {
+      int idx = sl.th_head + (sl.th_len - nt) + k;
+      if (idx >= TH) idx -= TH;
+      v = make_double2(sl.th[idx][0], sl.th[idx][1]);
+    }
+    *(double2*)&g.rows[(size_t)s * T + r].traj[k][0] = v;
+  }
   __syncthreads();
   if (tid == 0) g.phase[s * 16 + 7] = wall_clock64();
   if (tid == 0) {
@@ -783,7 +866,9 @@ __global__ void track_op_kernel(Dev g, int s, int pos, int op, int arg, const do
     case YK_OP_UPDATE: {
       DT b[4];
       for (int k = 0; k < 4; ++k) b[k] = (DT)in_box[k];
-      kf_update<DT>(sl, b);
+      double st[3 * VS];
+      stage_chrono(sl, st);
+      kf_update<DT>(sl, b, st);
       break;
     }
     case YK_OP_MARK_LOST:
@@ -849,7 +934,8 @@ int yk_tracker_create(yk_ctx* ctx, int n_streams, const yk_tracker_cfg* cfg, yk_
   YK_CHECK_ARG(cfg->max_dets >= 1 && cfg->max_dets <= 1024, "yk_tracker_create: max_dets must be in [1, 1024]");
   YK_CHECK_ARG(cfg->max_lost_frames >= 0, "yk_tracker_create: max_lost_frames must be >= 0");
   const size_t lds = yk::trk::lds_bytes(cfg->max_tracks, cfg->max_dets);
-  YK_CHECK_ARG(lds <= 160 * 1024, "yk_tracker_create: max_tracks x max_dets exceed the 160 KiB LDS budget");
+  YK_CHECK_ARG(yk::trk::stage_chunk(cfg->max_tracks, cfg->max_dets) >= 1 && lds <= 160 * 1024,
+               "yk_tracker_create: max_tracks x max_dets exceed the 160 KiB LDS budget");
   yk::DeviceGuard guard(ctx->device);
   auto* t = new yk_tracker{};
   t->ctx = ctx;
