@@ -652,6 +652,204 @@ __global__ void __launch_bounds__(256) conv_tile_kernel(TileArgs a) {
   }
 }
 
+// ---------------------------------------------------------------- table-driven implicit-GEMM conv
+// The gather kernels above derive every K chunk's (tap, source, channel) and every pixel's
+// address inside the K loop: ~120 VALU per K step against 4-16 MFMAs (issue-bound, measured
+// SQ_ACTIVE_INST_ANY / SQ_WAVE_CYCLES ~ 0.5).  Here the host precomputes, per op, one entry
+// per (K step, lane group kg): {element delta from the window origin, tap | src << 4 | valid
+// << 5} (model create, yk_model::ktab); the workgroup copies the op's table into LDS once.
+// Each lane computes its pixels' window-origin offsets in both sources and a 9-bit tap
+// validity mask once, so a K step costs one ds_read_b64, a mask test and an add per pixel
+// fragment.  WS: the four waves share one 16*NPT-pixel tile and split the K steps (partial
+// tiles summed in LDS); otherwise each wave owns its own 16*NPT pixels and the full K.
+// SKD K steps of loads stay in flight per wave.
+struct FastArgs {
+  const void* arena;             // every activation buffer lives in one allocation (< 2 GiB)
+  unsigned arena_bytes;
+  unsigned soff0, soff1;         // byte offsets of the two source views (image b0, channel coff)
+  int h0, w0, cs0, up0, h1, w1, cs1, up1;
+  int stride, pad, in_h, in_w, out_h, out_w, M;
+  const void* wblob;             // packed weights: byte offset woff, [n_tiles][k_steps][64][16 B]
+  unsigned wbytes, woff;
+  const float* bias;
+  const int2* ktab;              // [k_steps][4] {byte delta, tap | src << 4 | valid << 5}
+  int k_steps, n_tiles;
+  void* dst;
+  int d_cstride, d_coff, cout;
+  const void* res;
+  int r_cstride, r_coff;
+  int act;
+};
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+constexpr unsigned kOOB = 0x80000000u;  // buffer offset past every num_records: the load returns 0
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_srd(const void* base, unsigned bytes) {
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)(size_t)base);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)((size_t)base >> 32));
+  void* b = (void*)(((size_t)hi << 32) | lo);
+  return __builtin_amdgcn_make_buffer_rsrc(b, (short)0, (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+__device__ __forceinline__ uint4 bload(__amdgpu_buffer_rsrc_t r, unsigned voff, int soff) {
+  const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, soff, 0);
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+template <class Tr, int NNT, int NPT, bool WS, int SKD>
+__global__ void __launch_bounds__(256) conv_fast_kernel(FastArgs a) {
+  using T = typename Tr::T;
+  constexpr int ESZ = (int)sizeof(T);
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  int2* tab = (int2*)smem;  // [k_steps * 4]; WS: then the f32x4 reduction buffer
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int kg = lane >> 4, col = lane & 15;
+  const int nt0 = blockIdx.y * NNT;
+  const int pbase = WS ? blockIdx.x * (16 * NPT) : (blockIdx.x * 4 + wave) * (16 * NPT);
+  const int nk = a.k_steps;
+  for (int i = tid; i < nk * 4; i += 256) tab[i] = a.ktab[i];
+  const __amdgpu_buffer_rsrc_t xr = make_srd(a.arena, a.arena_bytes);
+  const __amdgpu_buffer_rsrc_t wr = make_srd(a.wblob, a.wbytes);
+  const int hw = a.out_h * a.out_w;
+  unsigned vo0[NPT], vo1[NPT], vm[NPT];
+#pragma unroll
+  for (int t = 0; t < NPT; ++t) {
+    const int p = pbase + t * 16 + col;
+    const bool pv = p < a.M;
+    const int pp = pv ? p : 0;
+    const int b = pp / hw;
+    const int r = pp - b * hw;
+    const int oy = r / a.out_w;
+    const int ox = r - oy * a.out_w;
+    const int iy0 = oy * a.stride - a.pad, ix0 = ox * a.stride - a.pad;
+    vo0[t] = a.soff0 + (unsigned)(((b * a.h0 + (iy0 >> a.up0)) * a.w0 + (ix0 >> a.up0)) * a.cs0 * ESZ);
+    vo1[t] = a.soff1 + (unsigned)(((b * a.h1 + (iy0 >> a.up1)) * a.w1 + (ix0 >> a.up1)) * a.cs1 * ESZ);
+    unsigned m = 0;
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) {
+        const int iy = iy0 + ky, ix = ix0 + kx;
+        if (iy >= 0 && iy < a.in_h && ix >= 0 && ix < a.in_w) m |= 1u << (ky * 3 + kx);
+      }
+    vm[t] = pv ? m : 0u;  // 1x1 convs use tap 0 = the pixel itself
+  }
+  f32x4 acc[NNT][NPT];
+#pragma unroll
+  for (int i = 0; i < NNT; ++i)
+#pragma unroll
+    for (int t = 0; t < NPT; ++t) acc[i][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float4 bb[NNT];
+  unsigned wo[NNT];
+#pragma unroll
+  for (int i = 0; i < NNT; ++i) {
+    const int n0 = (nt0 + i) * 16 + kg * 4;
+    bb[i] = (nt0 + i < a.n_tiles && n0 < a.cout) ? *(const float4*)(a.bias + n0) : make_float4(0.f, 0.f, 0.f, 0.f);
+    const int nt = nt0 + i < a.n_tiles ? nt0 + i : a.n_tiles - 1;
+    wo[i] = a.woff + (unsigned)(((size_t)nt * nk * 64 + lane) * 16);
+  }
+  __syncthreads();
+  auto load_step = [&](int ks, uint4* wf, uint4* xf) {
+#pragma unroll
+    for (int i = 0; i < NNT; ++i) wf[i] = bload(wr, wo[i], ks * 1024);
+    const int2 e = tab[ks * 4 + kg];
+    const unsigned tap = (unsigned)e.y & 15u;
+    const bool s1 = (e.y & 16) != 0, ev = (e.y & 32) != 0;
+#pragma unroll
+    for (int t = 0; t < NPT; ++t) {
+      const bool ok = ev && ((vm[t] >> tap) & 1u);
+      const unsigned off = (s1 ? vo1[t] : vo0[t]) + (unsigned)e.x;
+      xf[t] = bload(xr, ok ? off : kOOB, 0);
+    }
+  };
+  int k0 = 0, k1 = nk;
+  if (WS) {
+    const int kq = (nk + 3) >> 2;
+    k0 = wave * kq;
+    k1 = k0 + kq < nk ? k0 + kq : nk;
+  }
+  uint4 wb[SKD][NNT], xb[SKD][NPT];
+#pragma unroll
+  for (int d = 0; d < SKD; ++d)
+    if (k0 + d < k1) load_step(k0 + d, wb[d], xb[d]);
+  int ks = k0;
+  // steady state: no conditionals, so the waitcnt pass keeps SKD steps of loads in flight
+  for (; ks + 2 * SKD <= k1; ks += SKD) {
+#pragma unroll
+    for (int d = 0; d < SKD; ++d) {
+#pragma unroll
+      for (int i = 0; i < NNT; ++i)
+#pragma unroll
+        for (int t = 0; t < NPT; ++t) acc[i][t] = mma<Tr>(wb[d][i], xb[d][t], acc[i][t]);
+      load_step(ks + d + SKD, wb[d], xb[d]);
+    }
+  }
+  for (; ks < k1; ks += SKD) {
+#pragma unroll
+    for (int d = 0; d < SKD; ++d) {
+      if (ks + d < k1) {
+#pragma unroll
+        for (int i = 0; i < NNT; ++i)
+#pragma unroll
+          for (int t = 0; t < NPT; ++t) acc[i][t] = mma<Tr>(wb[d][i], xb[d][t], acc[i][t]);
+        if (ks + d + SKD < k1) load_step(ks + d + SKD, wb[d], xb[d]);
+      }
+    }
+  }
+  if constexpr (WS) {
+    f32x4* red = (f32x4*)(smem + (((size_t)nk * 4 * 8 + 15) & ~(size_t)15));
+#pragma unroll
+    for (int i = 0; i < NNT; ++i)
+#pragma unroll
+      for (int t = 0; t < NPT; ++t) red[((wave * NNT + i) * NPT + t) * 64 + lane] = acc[i][t];
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < NNT; ++i) {
+    const int nt = nt0 + i;
+    if (nt >= a.n_tiles) break;
+    const int n0 = nt * 16 + kg * 4;
+    if (n0 >= a.cout) continue;
+#pragma unroll
+    for (int t = 0; t < NPT; ++t) {
+      if (WS && ((i * NPT + t) & 3) != wave) continue;
+      const int p = pbase + t * 16 + col;
+      if (p >= a.M) continue;
+      f32x4 v4 = acc[i][t];
+      if constexpr (WS) {
+        const f32x4* red = (const f32x4*)(smem + (((size_t)nk * 4 * 8 + 15) & ~(size_t)15));
+        v4 = red[((0 * NNT + i) * NPT + t) * 64 + lane];
+#pragma unroll
+        for (int w = 1; w < 4; ++w) {
+          const f32x4 u = red[((w * NNT + i) * NPT + t) * 64 + lane];
+          v4[0] += u[0];
+          v4[1] += u[1];
+          v4[2] += u[2];
+          v4[3] += u[3];
+        }
+      }
+      float v[4] = {v4[0] + bb[i].x, v4[1] + bb[i].y, v4[2] + bb[i].z, v4[3] + bb[i].w};
+      if (a.act) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = silu<Tr::kExact>(v[j]);
+      }
+      if (a.res) {
+        float r[4];
+        load4((const T*)a.res + (size_t)p * a.r_cstride + a.r_coff + n0, r);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = r[j] + v[j];
+      }
+      store4((T*)a.dst + (size_t)p * a.d_cstride + a.d_coff + n0, v);
+    }
+  }
+}
+
+// LDS bytes of conv_fast_kernel for an op: the K-step table (+ the split-K reduction buffer).
+inline size_t fast_lds(int k_steps, int nnt, int npt, bool ws) {
+  const size_t t = ((size_t)k_steps * 4 * 8 + 15) & ~(size_t)15;
+  return t + (ws ? (size_t)4 * nnt * npt * 64 * 16 : 0);
+}
+
 // ---------------------------------------------------------------- first conv from uint8 frames
 constexpr int kInputCoutMax = 64;
 
@@ -1222,6 +1420,12 @@ struct yk_model {
   // per-op conv plan chosen by yk_model_autotune (kind < 0: not tuned, use the heuristic)
   std::vector<std::array<int, 3>> tuned;    // {kind, nnt, npt}
   int tuned_batch = 0;
+  // conv_fast_kernel K-step tables: one device array, per-op offsets (entries of int2)
+  int2* ktab = nullptr;
+  std::vector<int64_t> ktab_off;
+  char* arena = nullptr;      // every activation buffer (bufs[i] point into it)
+  size_t arena_bytes = 0;
+  size_t blob_bytes = 0;
 };
 
 namespace {
@@ -1403,9 +1607,32 @@ void set_tile_attrs_t() {
   set_tile_attr_n<Tr, 1, true>();
   set_tile_attr_n<Tr, 2, true>();
 }
+template <class Tr, int NNT, int NPT, bool WS>
+void set_fast_attr() {
+  constexpr int SKD = NNT * NPT >= 8 ? 2 : 4;
+  (void)hipFuncSetAttribute((const void*)conv_fast_kernel<Tr, NNT, NPT, WS, SKD>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
+}
+template <class Tr, int NNT, bool WS>
+void set_fast_attr_n() {
+  set_fast_attr<Tr, NNT, 1, WS>();
+  set_fast_attr<Tr, NNT, 2, WS>();
+  set_fast_attr<Tr, NNT, 4, WS>();
+}
+template <class Tr, bool WS>
+void set_fast_attr_w() {
+  set_fast_attr_n<Tr, 1, WS>();
+  set_fast_attr_n<Tr, 2, WS>();
+  set_fast_attr_n<Tr, 3, WS>();
+  set_fast_attr_n<Tr, 4, WS>();
+}
 void set_tile_attrs() {
   set_tile_attrs_t<BF16>();
   set_tile_attrs_t<F32>();
+  set_fast_attr_w<BF16, false>();
+  set_fast_attr_w<BF16, true>();
+  set_fast_attr_w<F32, false>();
+  set_fast_attr_w<F32, true>();
   (void)hipFuncSetAttribute((const void*)sppf_lds_kernel<BF16>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             kSppfLdsMaxHW * 128);
   (void)hipFuncSetAttribute((const void*)sppf_lds_kernel<F32>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1413,7 +1640,8 @@ void set_tile_attrs() {
 }
 
 // Conv kernel choice for one op at batch B.
-enum { CK_DIRECT = 0, CK_TILE = 1, CK_SPLITK = 2 };
+enum { CK_DIRECT = 0, CK_TILE = 1, CK_SPLITK = 2, CK_FAST = 3 };
+// CK_FAST plan: nnt in {1, 2, 3, 4}, npt = NPT | (WS << 4) with NPT in {1, 2, 4}
 struct ConvPlan {
   int kind = CK_DIRECT, nnt = 0, npt = 0;
   TilePlan tp;
@@ -1452,12 +1680,51 @@ ConvPlan splitk_plan(const yk_op& op, int B, int nnt_force = 0, int npt_force = 
   return p;
 }
 
+// conv_fast_kernel geometry: the largest fragment tile (NNT x NPT) that still gives >= 1024
+// workgroups (>= 4 waves per CU) and wastes < 25% of the n-tiles; the four waves split K (WS)
+// when the per-wave-pixel layout would give too few workgroups.
+ConvPlan fast_plan(const yk_op& op, int B) {
+  static const int cand[9][2] = {{4, 4}, {4, 2}, {2, 4}, {2, 2}, {4, 1}, {1, 4}, {2, 1}, {1, 2}, {1, 1}};
+  const long M = (long)B * op.out_h * op.out_w;
+  const int nt = op.n_tiles;
+  ConvPlan p;
+  p.kind = CK_FAST;
+  long best = -1;
+  for (int ws = 0; ws < 2; ++ws)
+    for (auto& c : cand) {
+      int nnt = c[0];
+      const int npt = c[1];
+      if (nnt == 4 && (nt == 3 || nt == 6 || nt == 9)) nnt = 3;
+      const int groups = (nt + nnt - 1) / nnt;
+      if (nnt > 1 && 4 * nt < 3 * groups * nnt) continue;
+      const long wgs = (M + (ws ? 16 : 64) * npt - 1) / ((ws ? 16 : 64) * npt) * groups;
+      if (wgs >= 1024) {
+        p.nnt = nnt;
+        p.npt = npt | (ws << 4);
+        return p;
+      }
+      if (wgs > best) {
+        best = wgs;
+        p.nnt = nnt;
+        p.npt = npt | (ws << 4);
+      }
+    }
+  return p;
+}
+
 ConvPlan conv_plan(const yk_model* m, const yk_op& op, int B) {
   const int esz = m->desc.act_dtype == YK_ACT_F32 ? 4 : 2;
   const size_t idx = (size_t)(&op - m->ops.data());
   if (idx < m->tuned.size() && m->tuned[idx][0] >= 0 && m->tuned_batch == B) {
     const auto& t = m->tuned[idx];
     if (t[0] == CK_SPLITK) return splitk_plan(op, B, t[1], t[2]);
+    if (t[0] == CK_FAST && m->ktab && m->ktab_off[idx] >= 0) {
+      ConvPlan p;
+      p.kind = CK_FAST;
+      p.nnt = t[1];
+      p.npt = t[2];
+      return p;
+    }
     if (t[0] == CK_TILE) {
       ConvPlan p;
       p.kind = CK_TILE;
@@ -1467,6 +1734,8 @@ ConvPlan conv_plan(const yk_model* m, const yk_op& op, int B) {
     return ConvPlan{};
   }
   if (!m->tiled) return ConvPlan{};
+  const size_t oi = (size_t)(&op - m->ops.data());
+  if (m->ktab && oi < m->ktab_off.size() && m->ktab_off[oi] >= 0) return fast_plan(op, B);
   if (op.out_h * op.out_w <= 1280) return splitk_plan(op, B);
   ConvPlan p;
   p.tp = tile_plan(op, esz, B);
@@ -1490,6 +1759,35 @@ void launch_splitk(const ConvArgs& a, const ConvPlan& p, hipStream_t st) {
   if (p.nnt == 4) launch_splitk_n<Tr, 4>(a, p.npt, st);
   else if (p.nnt == 2) launch_splitk_n<Tr, 2>(a, p.npt, st);
   else launch_splitk_n<Tr, 1>(a, p.npt, st);
+}
+
+template <class Tr, int NNT, int NPT, bool WS>
+void launch_fast_t(const FastArgs& a, hipStream_t st) {
+  constexpr int SKD = NNT * NPT >= 8 ? 2 : 4;
+  const int px = WS ? 16 * NPT : 64 * NPT;
+  dim3 grid((a.M + px - 1) / px, (a.n_tiles + NNT - 1) / NNT);
+  hipLaunchKernelGGL((conv_fast_kernel<Tr, NNT, NPT, WS, SKD>), grid, dim3(256), fast_lds(a.k_steps, NNT, NPT, WS), st,
+                     a);
+}
+template <class Tr, int NNT, bool WS>
+void launch_fast_n(const FastArgs& a, int npt, hipStream_t st) {
+  if (npt == 4) launch_fast_t<Tr, NNT, 4, WS>(a, st);
+  else if (npt == 2) launch_fast_t<Tr, NNT, 2, WS>(a, st);
+  else launch_fast_t<Tr, NNT, 1, WS>(a, st);
+}
+template <class Tr, bool WS>
+void launch_fast_w(const FastArgs& a, int nnt, int npt, hipStream_t st) {
+  switch (nnt) {
+    case 1: launch_fast_n<Tr, 1, WS>(a, npt, st); break;
+    case 2: launch_fast_n<Tr, 2, WS>(a, npt, st); break;
+    case 3: launch_fast_n<Tr, 3, WS>(a, npt, st); break;
+    default: launch_fast_n<Tr, 4, WS>(a, npt, st); break;
+  }
+}
+template <class Tr>
+void launch_fast(const FastArgs& a, const ConvPlan& p, hipStream_t st) {
+  if (p.npt >> 4) launch_fast_w<Tr, true>(a, p.nnt, p.npt & 15, st);
+  else launch_fast_w<Tr, false>(a, p.nnt, p.npt & 15, st);
 }
 
 template <class Tr>
@@ -1552,7 +1850,45 @@ int launch_op(yk_model* m, const yk_op& op, const uint8_t* frames, int B, float 
         a.act = op.act;
         const ConvPlan cp = conv_plan(m, op, B);
         const TilePlan& tp = cp.tp;
-        if (cp.kind == CK_SPLITK) {
+        if (cp.kind == CK_FAST) {
+          FastArgs f;
+          const size_t esz = sizeof(typename Tr::T);
+          f.arena = m->arena;
+          f.arena_bytes = (unsigned)m->arena_bytes;
+          f.soff0 = (unsigned)(((const char*)a.src[0].p - (const char*)m->arena) + (size_t)a.src[0].coff * esz);
+          f.soff1 = (unsigned)(((const char*)a.src[1].p - (const char*)m->arena) + (size_t)a.src[1].coff * esz);
+          f.h0 = a.src[0].h;
+          f.w0 = a.src[0].w;
+          f.cs0 = a.src[0].cstride;
+          f.up0 = a.src[0].up;
+          f.h1 = a.src[1].h;
+          f.w1 = a.src[1].w;
+          f.cs1 = a.src[1].cstride;
+          f.up1 = a.src[1].up;
+          f.wblob = m->blob;
+          f.wbytes = (unsigned)m->blob_bytes;
+          f.woff = (unsigned)op.w_off;
+          f.stride = a.stride;
+          f.pad = a.pad;
+          f.in_h = a.in_h;
+          f.in_w = a.in_w;
+          f.out_h = a.out_h;
+          f.out_w = a.out_w;
+          f.M = a.M;
+          f.bias = a.bias;
+          f.ktab = m->ktab + m->ktab_off[(size_t)(&op - m->ops.data())];
+          f.k_steps = a.k_steps;
+          f.n_tiles = a.n_tiles;
+          f.dst = a.dst;
+          f.d_cstride = a.d_cstride;
+          f.d_coff = a.d_coff;
+          f.cout = a.cout;
+          f.res = a.res;
+          f.r_cstride = a.r_cstride;
+          f.r_coff = a.r_coff;
+          f.act = a.act;
+          launch_fast<Tr>(f, cp, st);
+        } else if (cp.kind == CK_SPLITK) {
           launch_splitk<Tr>(a, cp, st);
         } else if (cp.kind == CK_TILE) {
           TileArgs t;
@@ -1665,6 +2001,13 @@ const char* op_kernel_name(const yk_model* m, const yk_op& op) {
   }
   const ConvPlan cp = conv_plan(m, op, m->plan_batch);
   static thread_local char buf[96];
+  if (cp.kind == CK_FAST) {
+    const int npt = cp.npt & 15, ws = cp.npt >> 4;
+    const int skd = cp.nnt * npt >= 8 ? 2 : 4;
+    snprintf(buf, sizeof buf, "conv_fast_kernel<yk::det::%s, %d, %d, %s, %d>", f ? "F32" : "BF16", cp.nnt, npt,
+             ws ? "true" : "false", skd);
+    return buf;
+  }
   if (cp.kind == CK_SPLITK) {
     snprintf(buf, sizeof buf, "conv_splitk_kernel<yk::det::%s, %d, %d>", f ? "F32" : "BF16", cp.nnt, cp.npt);
     return buf;
@@ -1845,6 +2188,45 @@ int launch_nms(yk_model* m, int B, float iou, int max_det, float* dets, int32_t*
   return YK_OK;
 }
 
+// conv_fast_kernel tables (see FastArgs): per conv op, per (K step, lane group kg), the element
+// offset of the K chunk's (tap, channel) from the pixel's window origin in its source view
+// and tap | src << 4 | valid << 5.  K order = model.py Program.pack: (tap, K-space channel).
+hipError_t build_ktabs(yk_model* m) {
+  const int epl = m->desc.act_dtype == YK_ACT_F32 ? 4 : 2 * 4;
+  const int esz = m->desc.act_dtype == YK_ACT_F32 ? 4 : 2;
+  if (m->arena_bytes >= 0x7fff0000ull || m->blob_bytes >= 0x7fff0000ull) return hipSuccess;  // 32-bit offsets
+  std::vector<int2> all;
+  m->ktab_off.assign(m->ops.size(), -1);
+  for (size_t i = 0; i < m->ops.size(); ++i) {
+    const yk_op& op = m->ops[i];
+    if (op.kind != YK_K_CONV) continue;
+    const int k = op.ksize, c0 = op.src_ch[0], cin = op.src_ch[0] + (op.n_src > 1 ? op.src_ch[1] : 0);
+    bool ok = (cin % 8) == 0;
+    for (int sidx = 0; sidx < op.n_src; ++sidx) ok = ok && (k == 1 || op.src[sidx].up == 0);
+    if (!ok) continue;
+    const int cq = cin / 8, n_chunks = k * k * cq;
+    m->ktab_off[i] = (int64_t)all.size();
+    for (int ks = 0; ks < op.k_steps; ++ks)
+      for (int kg = 0; kg < 4; ++kg) {
+        const int kel = ks * 4 * epl + kg * epl, q = kel >> 3, sub = kel & 7;
+        if (q >= n_chunks) {
+          all.push_back(make_int2(0, 0));
+          continue;
+        }
+        const int tap = q / cq, c = (q - tap * cq) * 8, ky = tap / k, kx = tap - ky * k;
+        const int src = c >= c0 ? 1 : 0, ch = src ? c - c0 : c;
+        const yk_view& v = op.src[src < op.n_src ? src : 0];
+        const int delta = ((ky * v.w + kx) * v.c_stride + ch + sub) * esz;
+        const int bit = k == 3 ? ky * 3 + kx : 0;
+        all.push_back(make_int2(delta, bit | (src << 4) | 32));
+      }
+  }
+  if (all.empty()) return hipSuccess;
+  hipError_t e = hipMalloc((void**)&m->ktab, all.size() * sizeof(int2));
+  if (e == hipSuccess) e = hipMemcpy(m->ktab, all.data(), all.size() * sizeof(int2), hipMemcpyHostToDevice);
+  return e;
+}
+
 hipError_t set_schedule(yk_model* m, int groups, int lanes) {
   for (auto& kv : m->graphs) (void)hipGraphExecDestroy(kv.second);
   m->graphs.clear();
@@ -1915,13 +2297,20 @@ int yk_model_create(yk_ctx* ctx, const yk_model_desc* desc, const void* host_blo
   auto alloc = [&](void** p, size_t bytes) {
     if (e == hipSuccess) e = hipMalloc(p, bytes ? bytes : 16);
   };
-  for (int i = 0; i < desc->n_bufs; ++i) {
-    void* p = nullptr;
-    alloc(&p, (size_t)desc->buf_elems[i] * B * esz + 64);
-    m->bufs.push_back(p);
-    if (p) (void)hipMemset(p, 0, (size_t)desc->buf_elems[i] * B * esz + 64);
+  {
+    std::vector<size_t> offs;
+    size_t total = 0;
+    for (int i = 0; i < desc->n_bufs; ++i) {
+      offs.push_back(total);
+      total += ((size_t)desc->buf_elems[i] * B * esz + 64 + 255) / 256 * 256;
+    }
+    alloc((void**)&m->arena, total);
+    m->arena_bytes = total;
+    if (m->arena) (void)hipMemset(m->arena, 0, total);
+    for (int i = 0; i < desc->n_bufs; ++i) m->bufs.push_back(m->arena ? m->arena + offs[i] : nullptr);
   }
   alloc((void**)&m->blob, (size_t)blob_bytes);
+  m->blob_bytes = (size_t)blob_bytes;
   if (e == hipSuccess) e = hipMemcpy(m->blob, host_blob, (size_t)blob_bytes, hipMemcpyHostToDevice);
   int kc = 1;
   while (kc < (int)A) kc <<= 1;
@@ -1939,6 +2328,7 @@ int yk_model_create(yk_ctx* ctx, const yk_model_desc* desc, const void* host_blo
     e = hipFuncSetAttribute((const void*)nms_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)nms_lds_bytes());
   set_tile_attrs();
   if (const char* env = getenv("YK_CONV_DIRECT")) m->tiled = env[0] != '1';
+  if (e == hipSuccess && !(getenv("YK_CONV_FAST") && getenv("YK_CONV_FAST")[0] == '0')) e = build_ktabs(m);
   if (e == hipSuccess) e = set_schedule(m, 1, 3);
   if (e != hipSuccess) {
     yk::set_error(std::string("yk_model_create: ") + hipGetErrorString(e));
@@ -1981,9 +2371,8 @@ int yk_model_destroy(yk_model* m) {
   for (auto& kv : m->graphs) (void)hipGraphExecDestroy(kv.second);
   for (hipStream_t s : m->aux) (void)hipStreamDestroy(s);
   for (hipEvent_t v : m->ev) (void)hipEventDestroy(v);
-  for (void* p : m->bufs)
-    if (p) (void)hipFree(p);
-  void* ptrs[] = {m->blob, m->cand, m->cand_count, m->slot_of, m->gkeys, m->gbox, m->gflag, m->dets, m->counts};
+  if (m->arena) (void)hipFree(m->arena);
+  void* ptrs[] = {m->blob, m->cand, m->cand_count, m->slot_of, m->gkeys, m->gbox, m->gflag, m->dets, m->counts, m->ktab};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   delete m;
@@ -2081,7 +2470,10 @@ int yk_model_profile(yk_model* m, const uint8_t* frames, int batch, float conf, 
 
 int yk_model_set_plan(yk_model* m, int op_index, int batch, int kind, int nnt, int npt) {
   YK_CHECK_ARG(m && op_index >= -1 && op_index < (int)m->ops.size(), "yk_model_set_plan: bad op index");
-  YK_CHECK_ARG(kind >= -1 && kind <= CK_SPLITK, "yk_model_set_plan: kind must be -1 (heuristic), 0, 1 or 2");
+  YK_CHECK_ARG(kind >= -1 && kind <= CK_FAST, "yk_model_set_plan: kind must be -1 (heuristic), 0, 1, 2 or 3");
+  YK_CHECK_ARG(kind != CK_FAST || (nnt >= 1 && nnt <= 4 && ((npt & 15) == 1 || (npt & 15) == 2 || (npt & 15) == 4) &&
+                                   (npt >> 4) <= 1),
+               "yk_model_set_plan: table conv needs nnt in [1, 4], npt in {1, 2, 4} (+16: waves split K)");
   YK_CHECK_ARG(kind != CK_SPLITK || ((nnt == 1 || nnt == 2 || nnt == 4) && (npt == 1 || npt == 2 || npt == 4)),
                "yk_model_set_plan: split-K fragment tile must be nnt, npt in {1, 2, 4}");
   YK_CHECK_ARG(batch >= 1 && batch <= m->desc.max_batch, "yk_model_set_plan: batch out of range");
@@ -2131,6 +2523,16 @@ int yk_model_autotune(yk_model* m, const uint8_t* frames, int batch, float conf,
         if (nnt > 1 && 4 * op.n_tiles < 3 * ((op.n_tiles + nnt - 1) / nnt) * nnt) continue;
         cands.push_back({CK_SPLITK, nnt, npt});
       }
+    if (m->ktab && m->ktab_off[i] >= 0)
+      for (int ws = 0; ws < 2; ++ws)
+        for (int nnt : {1, 2, 3, 4})
+          for (int npt : {1, 2, 4}) {
+            if (nnt > 1 && 4 * op.n_tiles < 3 * ((op.n_tiles + nnt - 1) / nnt) * nnt) continue;
+            const long px = ws ? 16 * npt : 64 * npt;
+            const long wgs = ((long)bt * op.out_h * op.out_w + px - 1) / px * ((op.n_tiles + nnt - 1) / nnt);
+            if (wgs < 64) continue;
+            cands.push_back({CK_FAST, nnt, npt | (ws << 4)});
+          }
     float best = 1e30f;
     std::array<int, 3> pick = {-1, 0, 0};
     for (const auto& c : cands) {
