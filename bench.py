@@ -38,8 +38,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--streams", type=int, default=8, help="streams (= frames per forward) per GPU")
-    ap.add_argument("--targets", type=int, default=20,
-                    help="synthetic targets per stream (20 -> ~64 live tracks/stream with lost-track retention)")
+    ap.add_argument("--targets", type=int, default=22,
+                    help="synthetic targets per stream (22 -> ~64 live tracks/stream: the planted detector plus lost-track retention)")
     ap.add_argument("--scale", default="s", choices=["n", "s"])
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--frames", type=int, default=120, help="pre-rendered frames per stream (cycled)")
@@ -179,12 +179,13 @@ def main():
 
     pipeline = import_module(PKG + ".pipeline")
     S, H, W = a.streams, 512, 640
-    seed0 = 1000 * rank
+    shard = P.shard
+    my_streams = shard.stream_ids(rank, ws, S)  # this GPU's block of independent streams
     pipe = pipeline.StreamPipeline(f"yolov8{a.scale}-small.yaml", S, (H, W), a.dtype, seed=0, device=local,
                                    pipelined=not a.no_pipeline)
     # pre-render frames of every stream into HBM (inputs resident before the timed region)
     F = max(2, min(a.frames, a.warmup + a.steps))
-    scenes = [P.synth.Scene(seed=seed0 + s, n_targets=a.targets, n_frames=F + 1) for s in range(S)]
+    scenes = [P.synth.Scene(seed=shard.stream_seed(g, S), n_targets=a.targets, n_frames=F + 1) for g in my_streams]
     frames = torch.empty((F, S, H, W, 3), dtype=torch.uint8, device=dev)
     for s, sc in enumerate(scenes):
         frames[:, s] = sc.frames_torch(0, F, dev)
@@ -237,15 +238,10 @@ def main():
         pipe.step()
     torch.cuda.synchronize()
     pcie_fps = S * n_pcie / (time.perf_counter() - tp)
-    if ws > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        c = torch.tensor([frames_done, live, float(stats["total_tracks_created"].sum())], device=dev,
-                         dtype=torch.float64)
-        dist.all_reduce(c, op=dist.ReduceOp.SUM)
-        frames_done = int(c[0].item())
-        live = float(c[1].item()) / ws
+    # end-of-run exchange (RCCL): SUM of counters, MAX of wall time -- the only collective
+    run, elapsed = shard.reduce_run(shard.local_counters(frames_done, stats), elapsed, dev)
+    frames_done = int(run["frames"])
+    live = run["current_active_tracks"] / (S * ws)
     fps = frames_done / elapsed
     rl = None
     trl = None
@@ -276,6 +272,7 @@ def main():
                        "graph": not a.no_graph, "tracker_overlapped": not a.no_pipeline, "autotuned": not a.no_tune, "dag_lanes": a.lanes,
                        "batch_groups": a.groups,
                        "live_tracks_per_stream": round(live, 1),
+                       "tracks_created": int(run["total_tracks_created"]),
                        "gflop_per_frame": round(gflop, 3)},
             "network_mfma_frac": round(fps / ws * gflop / 1e3 / PEAK[a.dtype], 5),
             "pcie_inclusive_fps": round(pcie_fps * ws, 2),
