@@ -44,6 +44,8 @@ def parse():
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--frames", type=int, default=120, help="pre-rendered frames per stream (cycled)")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--frame-copy", default="copy", choices=["copy", "none"],
+                    help="how each step's frames reach the detector's input buffer (none: diagnostic only)")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="run tracker(t) on the detector's stream instead of overlapping it with detector(t+1)")
     ap.add_argument("--no-tune", action="store_true", help="skip the per-op conv kernel autotune")
@@ -219,7 +221,10 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for t in range(a.steps):
-        pipe.run(frames[(a.warmup + t) % F])
+        if a.frame_copy == "none":
+            pipe.step()
+        else:
+            pipe.run(frames[(a.warmup + t) % F])
     torch.cuda.synchronize()
     if ws > 1:
         dist.barrier()

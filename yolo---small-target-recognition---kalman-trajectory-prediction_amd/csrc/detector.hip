@@ -75,14 +75,20 @@ __device__ __forceinline__ f32x4 mma<F32>(const uint4& w, const uint4& x, f32x4 
 template <bool kExact>
 __device__ __forceinline__ float silu(float v) {
   if constexpr (kExact) return v / (1.0f + expf(-v));
-  else return v / (1.0f + __expf(-v));
+  else return v * __builtin_amdgcn_rcpf(1.0f + __expf(-v));  // v_exp + v_rcp: bf16 outputs
 }
 
 // store / load 4 consecutive channels
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+// f32 -> bf16 round-to-nearest-even with the hardware v_cvt_pk_bf16_f32 (NaN stays NaN)
+__device__ __forceinline__ unsigned pack_bf16x2(float a, float b) {
+  const bf16x2 h = {(__bf16)a, (__bf16)b};
+  return __builtin_bit_cast(unsigned, h);
+}
 __device__ __forceinline__ void store4(unsigned short* p, const float v[4]) {
   uint2 o;
-  o.x = (unsigned)f2bf(v[0]) | ((unsigned)f2bf(v[1]) << 16);
-  o.y = (unsigned)f2bf(v[2]) | ((unsigned)f2bf(v[3]) << 16);
+  o.x = pack_bf16x2(v[0], v[1]);
+  o.y = pack_bf16x2(v[2], v[3]);
   *(uint2*)p = o;
 }
 __device__ __forceinline__ void store4(float* p, const float v[4]) { *(float4*)p = make_float4(v[0], v[1], v[2], v[3]); }
@@ -454,7 +460,11 @@ __global__ void __launch_bounds__(256) conv_tile_kernel(TileArgs a) {
   uint4* wl = (uint4*)smem;  // single: [NNT][k_steps][64]; else [2][NNT][KCH][64]
   const int wslab = a.single ? NNT * a.k_steps * 64 : 2 * WU;
   T* xt = (T*)(smem + (size_t)wslab * 16);  // [tih][tiw][ps]
+  // K-step table [k_steps][4]: LDS element offset of each lane group's K chunk from the
+  // pixel's window origin in the tile (-1: padding chunk), built by the host (build_ktabs)
+  int* ltab = (int*)(smem + (size_t)wslab * 16 + (((size_t)a.tih * a.tiw * a.ps * sizeof(T) + 15) & ~(size_t)15));
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (int i = tid; i < a.k_steps * 4; i += 256) ltab[i] = a.tab[i];
   const int kg = lane >> 4, col = lane & 15;
   const View sv0 = uniform_view(a.src[0]), sv1 = uniform_view(a.src[1]);
   const typename Tr::T* gbase = (const typename Tr::T*)a.src[0].p;
@@ -562,6 +572,9 @@ __global__ void __launch_bounds__(256) conv_tile_kernel(TileArgs a) {
 #pragma unroll
     for (int q = 0; q < NPT; ++q) acc[i][q] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int s = a.stride;
+  int prow[NPT];  // LDS element offset of each pixel fragment's window origin
+#pragma unroll
+  for (int pt = 0; pt < NPT; ++pt) prow[pt] = ((wrow + pt) * s * a.tiw + col * s) * a.ps;
   int buf = 0;
   const int kch = a.single ? a.k_steps : KCH;  // steps per chunk (= the slab row stride)
   for (int k0 = 0; k0 < a.k_steps; k0 += kch) {
@@ -570,18 +583,11 @@ __global__ void __launch_bounds__(256) conv_tile_kernel(TileArgs a) {
     const uint4* wc = wl + buf * WU;
     const int kn = a.k_steps - k0 < kch ? a.k_steps - k0 : kch;
     for (int kk = KSPLIT ? wave : 0; kk < kn; kk += KSPLIT ? 4 : 1) {
-      const int kel = (k0 + kk) * 4 * EPL + kg * EPL;
-      const int q = kel >> 3, sub = kel & 7;
-      const int e = chunk_entry(q, a.n_chunks, a.cin, a.c0, a.ksize);
+      const int e = ltab[(k0 + kk) * 4 + kg];
       uint4 xf[NPT];
       if (e >= 0) {
-        const int kx = ((e >> 21) & 15) - 8 + a.pad, ky = ((e >> 17) & 15) - 8 + a.pad;
-        const int cK = (e & 0xffff) + (((e >> 16) & 1) ? a.c0 : 0) + sub;
 #pragma unroll
-        for (int pt = 0; pt < NPT; ++pt) {
-          const int ty = wrow + pt;
-          xf[pt] = *(const uint4*)(xt + (size_t)((ty * s + ky) * a.tiw + col * s + kx) * a.ps + cK);
-        }
+        for (int pt = 0; pt < NPT; ++pt) xf[pt] = *(const uint4*)(xt + prow[pt] + e);
       } else {
 #pragma unroll
         for (int pt = 0; pt < NPT; ++pt) xf[pt] = make_uint4(0u, 0u, 0u, 0u);
@@ -669,6 +675,7 @@ struct FastArgs {
   unsigned soff0, soff1;         // byte offsets of the two source views (image b0, channel coff)
   int h0, w0, cs0, up0, h1, w1, cs1, up1;
   int stride, pad, in_h, in_w, out_h, out_w, M;
+  float inv_hw, inv_w;           // 1 / (out_h * out_w), 1 / out_w (fdiv)
   const void* wblob;             // packed weights: byte offset woff, [n_tiles][k_steps][64][16 B]
   unsigned wbytes, woff;
   const float* bias;
@@ -695,6 +702,15 @@ __device__ __forceinline__ uint4 bload(__amdgpu_buffer_rsrc_t r, unsigned voff, 
   return make_uint4(v.x, v.y, v.z, v.w);
 }
 
+// floor(n / d) for 0 <= n < 2^22, d >= 1, with inv = 1/d rounded up to f32 by the host:
+// the f32 product is within one of the quotient, fixed by one compare.
+__device__ __forceinline__ int fdiv(int n, int d, float inv) {
+  int q = (int)((float)n * inv);
+  q -= (q * d > n) ? 1 : 0;
+  q += ((q + 1) * d <= n) ? 1 : 0;
+  return q;
+}
+
 template <class Tr, int NNT, int NPT, bool WS, int SKD>
 __global__ void __launch_bounds__(256) conv_fast_kernel(FastArgs a) {
   using T = typename Tr::T;
@@ -717,21 +733,19 @@ __global__ void __launch_bounds__(256) conv_fast_kernel(FastArgs a) {
     const int p = pbase + t * 16 + col;
     const bool pv = p < a.M;
     const int pp = pv ? p : 0;
-    const int b = pp / hw;
+    // exact small-integer division through f32 (operands < 2^22): q = floor(n / d)
+    const int b = fdiv(pp, hw, a.inv_hw);
     const int r = pp - b * hw;
-    const int oy = r / a.out_w;
+    const int oy = fdiv(r, a.out_w, a.inv_w);
     const int ox = r - oy * a.out_w;
     const int iy0 = oy * a.stride - a.pad, ix0 = ox * a.stride - a.pad;
     vo0[t] = a.soff0 + (unsigned)(((b * a.h0 + (iy0 >> a.up0)) * a.w0 + (ix0 >> a.up0)) * a.cs0 * ESZ);
     vo1[t] = a.soff1 + (unsigned)(((b * a.h1 + (iy0 >> a.up1)) * a.w1 + (ix0 >> a.up1)) * a.cs1 * ESZ);
-    unsigned m = 0;
-#pragma unroll
-    for (int ky = 0; ky < 3; ++ky)
-#pragma unroll
-      for (int kx = 0; kx < 3; ++kx) {
-        const int iy = iy0 + ky, ix = ix0 + kx;
-        if (iy >= 0 && iy < a.in_h && ix >= 0 && ix < a.in_w) m |= 1u << (ky * 3 + kx);
-      }
+    // 9-bit tap mask = valid rows x valid columns of the 3x3 window
+    const unsigned cm = ((unsigned)(ix0 >= 0 && ix0 < a.in_w)) | ((unsigned)(ix0 + 1 >= 0 && ix0 + 1 < a.in_w) << 1) |
+                        ((unsigned)(ix0 + 2 >= 0 && ix0 + 2 < a.in_w) << 2);
+    const unsigned m = ((iy0 >= 0 && iy0 < a.in_h) ? cm : 0u) | ((iy0 + 1 >= 0 && iy0 + 1 < a.in_h) ? cm << 3 : 0u) |
+                       ((iy0 + 2 >= 0 && iy0 + 2 < a.in_h) ? cm << 6 : 0u);
     vm[t] = pv ? m : 0u;  // 1x1 convs use tap 0 = the pixel itself
   }
   f32x4 acc[NNT][NPT];
@@ -749,10 +763,9 @@ __global__ void __launch_bounds__(256) conv_fast_kernel(FastArgs a) {
     wo[i] = a.woff + (unsigned)(((size_t)nt * nk * 64 + lane) * 16);
   }
   __syncthreads();
-  auto load_step = [&](int ks, uint4* wf, uint4* xf) {
+  auto issue = [&](int ks, int2 e, uint4* wf, uint4* xf) {
 #pragma unroll
     for (int i = 0; i < NNT; ++i) wf[i] = bload(wr, wo[i], ks * 1024);
-    const int2 e = tab[ks * 4 + kg];
     const unsigned tap = (unsigned)e.y & 15u;
     const bool s1 = (e.y & 16) != 0, ev = (e.y & 32) != 0;
 #pragma unroll
@@ -762,6 +775,7 @@ __global__ void __launch_bounds__(256) conv_fast_kernel(FastArgs a) {
       xf[t] = bload(xr, ok ? off : kOOB, 0);
     }
   };
+  auto load_step = [&](int ks, uint4* wf, uint4* xf) { issue(ks, tab[ks * 4 + kg], wf, xf); };
   int k0 = 0, k1 = nk;
   if (WS) {
     const int kq = (nk + 3) >> 2;
@@ -769,32 +783,45 @@ __global__ void __launch_bounds__(256) conv_fast_kernel(FastArgs a) {
     k1 = k0 + kq < nk ? k0 + kq : nk;
   }
   uint4 wb[SKD][NNT], xb[SKD][NPT];
-#pragma unroll
-  for (int d = 0; d < SKD; ++d)
-    if (k0 + d < k1) load_step(k0 + d, wb[d], xb[d]);
   int ks = k0;
-  // steady state: no conditionals, so the waitcnt pass keeps SKD steps of loads in flight
-  for (; ks + 2 * SKD <= k1; ks += SKD) {
+  if (k1 - k0 >= 2 * SKD) {
+    // prologue and steady state issue the loads in the same pinned order (MFMAs of step d,
+    // then step d + SKD's loads), so the waitcnt pass sees one consistent FIFO of SKD steps
+#pragma unroll
+    for (int d = 0; d < SKD; ++d) {
+      __builtin_amdgcn_sched_barrier(0);
+      load_step(k0 + d, wb[d], xb[d]);
+    }
+    for (; ks + 2 * SKD <= k1; ks += SKD) {
+#pragma unroll
+      for (int d = 0; d < SKD; ++d) {
+        __builtin_amdgcn_sched_barrier(0);
+        const int2 e = tab[(ks + d + SKD) * 4 + kg];  // LDS read in flight over the MFMAs
+#pragma unroll
+        for (int i = 0; i < NNT; ++i)
+#pragma unroll
+          for (int t = 0; t < NPT; ++t) acc[i][t] = mma<Tr>(wb[d][i], xb[d][t], acc[i][t]);
+        __builtin_amdgcn_sched_barrier(0);
+        issue(ks + d + SKD, e, wb[d], xb[d]);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int d = 0; d < SKD; ++d) {
 #pragma unroll
       for (int i = 0; i < NNT; ++i)
 #pragma unroll
         for (int t = 0; t < NPT; ++t) acc[i][t] = mma<Tr>(wb[d][i], xb[d][t], acc[i][t]);
-      load_step(ks + d + SKD, wb[d], xb[d]);
     }
+    ks += SKD;
   }
-  for (; ks < k1; ks += SKD) {
+  // short K ranges and the tail: one step at a time
+  for (; ks < k1; ++ks) {
+    load_step(ks, wb[0], xb[0]);
 #pragma unroll
-    for (int d = 0; d < SKD; ++d) {
-      if (ks + d < k1) {
+    for (int i = 0; i < NNT; ++i)
 #pragma unroll
-        for (int i = 0; i < NNT; ++i)
-#pragma unroll
-          for (int t = 0; t < NPT; ++t) acc[i][t] = mma<Tr>(wb[d][i], xb[d][t], acc[i][t]);
-        if (ks + d + SKD < k1) load_step(ks + d + SKD, wb[d], xb[d]);
-      }
-    }
+      for (int t = 0; t < NPT; ++t) acc[i][t] = mma<Tr>(wb[0][i], xb[0][t], acc[i][t]);
   }
   if constexpr (WS) {
     f32x4* red = (f32x4*)(smem + (((size_t)nk * 4 * 8 + 15) & ~(size_t)15));
@@ -1423,6 +1450,8 @@ struct yk_model {
   // conv_fast_kernel K-step tables: one device array, per-op offsets (entries of int2)
   int2* ktab = nullptr;
   std::vector<int64_t> ktab_off;
+  int* ltab = nullptr;                // conv_tile_kernel K-step tables (LDS element offsets)
+  std::vector<int64_t> ltab_off;
   char* arena = nullptr;      // every activation buffer (bufs[i] point into it)
   size_t arena_bytes = 0;
   size_t blob_bytes = 0;
@@ -1479,10 +1508,11 @@ TilePlan tile_plan_geom(const yk_op& op, int esz, int B);
 TilePlan tile_plan(const yk_op& op, int esz, int B) {
   TilePlan t = tile_plan_geom(op, esz, B);
   if (!t.ok) return t;
+  t.lds = (t.lds + 15) / 16 * 16 + (size_t)op.k_steps * 16;  // + the K-step table
   const size_t tile = (size_t)t.tih * t.tiw * t.ps * esz;
   const size_t slab = (size_t)t.nnt * op.k_steps * 1024;
   const size_t red = t.split ? (size_t)4 * t.nnt * t.npt * 64 * 16 : 0;
-  const size_t lds1 = (slab > red ? slab : red) + tile;
+  const size_t lds1 = (slab > red ? slab : red) + (tile + 15) / 16 * 16 + (size_t)op.k_steps * 16;
   const size_t cap = t.lds > 96 * 1024 ? t.lds : 96 * 1024;
   if (lds1 <= cap && lds1 <= kTileLdsMax) {
     t.single = true;
@@ -1718,14 +1748,14 @@ ConvPlan conv_plan(const yk_model* m, const yk_op& op, int B) {
   if (idx < m->tuned.size() && m->tuned[idx][0] >= 0 && m->tuned_batch == B) {
     const auto& t = m->tuned[idx];
     if (t[0] == CK_SPLITK) return splitk_plan(op, B, t[1], t[2]);
-    if (t[0] == CK_FAST && m->ktab && m->ktab_off[idx] >= 0) {
+    if (t[0] == CK_FAST && m->ktab && m->ktab_off[idx] >= 0 && (long)B * op.out_h * op.out_w < (1L << 22)) {
       ConvPlan p;
       p.kind = CK_FAST;
       p.nnt = t[1];
       p.npt = t[2];
       return p;
     }
-    if (t[0] == CK_TILE) {
+    if (t[0] == CK_TILE && m->ltab && m->ltab_off[idx] >= 0) {
       ConvPlan p;
       p.kind = CK_TILE;
       p.tp = tile_plan(op, esz, B);
@@ -1735,11 +1765,12 @@ ConvPlan conv_plan(const yk_model* m, const yk_op& op, int B) {
   }
   if (!m->tiled) return ConvPlan{};
   const size_t oi = (size_t)(&op - m->ops.data());
-  if (m->ktab && oi < m->ktab_off.size() && m->ktab_off[oi] >= 0) return fast_plan(op, B);
+  if (m->ktab && oi < m->ktab_off.size() && m->ktab_off[oi] >= 0 && (long)B * op.out_h * op.out_w < (1L << 22))
+    return fast_plan(op, B);  // (fdiv: pixel indices < 2^22)
   if (op.out_h * op.out_w <= 1280) return splitk_plan(op, B);
   ConvPlan p;
   p.tp = tile_plan(op, esz, B);
-  p.kind = p.tp.ok ? CK_TILE : CK_DIRECT;
+  p.kind = p.tp.ok && m->ltab && m->ltab_off[oi] >= 0 ? CK_TILE : CK_DIRECT;
   return p;
 }
 
@@ -1875,6 +1906,8 @@ int launch_op(yk_model* m, const yk_op& op, const uint8_t* frames, int B, float 
           f.out_h = a.out_h;
           f.out_w = a.out_w;
           f.M = a.M;
+          f.inv_hw = 1.0f / (float)(a.out_h * a.out_w);
+          f.inv_w = 1.0f / (float)a.out_w;
           f.bias = a.bias;
           f.ktab = m->ktab + m->ktab_off[(size_t)(&op - m->ops.data())];
           f.k_steps = a.k_steps;
@@ -1910,7 +1943,7 @@ int launch_op(yk_model* m, const yk_op& op, const uint8_t* frames, int B, float 
           t.ps = tp.ps;
           t.wpk = a.wpk;
           t.bias = a.bias;
-          t.tab = a.tab;
+          t.tab = m->ltab + m->ltab_off[(size_t)(&op - m->ops.data())];
           t.k_steps = a.k_steps;
           t.n_tiles = a.n_tiles;
           t.n_chunks = a.n_chunks;
@@ -2191,13 +2224,13 @@ int launch_nms(yk_model* m, int B, float iou, int max_det, float* dets, int32_t*
 // conv_fast_kernel tables (see FastArgs): per conv op, per (K step, lane group kg), the element
 // offset of the K chunk's (tap, channel) from the pixel's window origin in its source view
 // and tap | src << 4 | valid << 5.  K order = model.py Program.pack: (tap, K-space channel).
-hipError_t build_ktabs(yk_model* m) {
+hipError_t build_ktabs(yk_model* m, bool fast) {
   const int epl = m->desc.act_dtype == YK_ACT_F32 ? 4 : 2 * 4;
   const int esz = m->desc.act_dtype == YK_ACT_F32 ? 4 : 2;
-  if (m->arena_bytes >= 0x7fff0000ull || m->blob_bytes >= 0x7fff0000ull) return hipSuccess;  // 32-bit offsets
+  if (m->arena_bytes >= 0x7fff0000ull || m->blob_bytes >= 0x7fff0000ull) fast = false;  // 32-bit offsets
   std::vector<int2> all;
   m->ktab_off.assign(m->ops.size(), -1);
-  for (size_t i = 0; i < m->ops.size(); ++i) {
+  for (size_t i = 0; i < m->ops.size() && fast; ++i) {
     const yk_op& op = m->ops[i];
     if (op.kind != YK_K_CONV) continue;
     const int k = op.ksize, c0 = op.src_ch[0], cin = op.src_ch[0] + (op.n_src > 1 ? op.src_ch[1] : 0);
@@ -2221,8 +2254,38 @@ hipError_t build_ktabs(yk_model* m) {
         all.push_back(make_int2(delta, bit | (src << 4) | 32));
       }
   }
-  if (all.empty()) return hipSuccess;
-  hipError_t e = hipMalloc((void**)&m->ktab, all.size() * sizeof(int2));
+  // conv_tile_kernel: offsets inside the LDS input tile (row width 15 * stride + k pixels,
+  // pixel stride ps = odd number of 16-B units >= cin, as tile_plan_geom)
+  std::vector<int> lt;
+  m->ltab_off.assign(m->ops.size(), -1);
+  for (size_t i = 0; i < m->ops.size(); ++i) {
+    const yk_op& op = m->ops[i];
+    if (op.kind != YK_K_CONV) continue;
+    const int k = op.ksize, cin = op.src_ch[0] + (op.n_src > 1 ? op.src_ch[1] : 0);
+    if (cin % 8) continue;
+    int U = cin * esz / 16;
+    if ((U & 1) == 0) U += 1;
+    const int ps = U * 16 / esz, tiw = 15 * op.stride + k;
+    const int cq = cin / 8, n_chunks = k * k * cq;
+    m->ltab_off[i] = (int64_t)lt.size();
+    for (int ks = 0; ks < op.k_steps; ++ks)
+      for (int kg = 0; kg < 4; ++kg) {
+        const int kel = ks * 4 * epl + kg * epl, q = kel >> 3, sub = kel & 7;
+        if (q >= n_chunks) {
+          lt.push_back(-1);
+          continue;
+        }
+        const int tap = q / cq, c = (q - tap * cq) * 8, ky = tap / k, kx = tap - ky * k;
+        lt.push_back((ky * tiw + kx) * ps + c + sub);
+      }
+  }
+  hipError_t e = hipSuccess;
+  if (!lt.empty()) {
+    e = hipMalloc((void**)&m->ltab, lt.size() * sizeof(int));
+    if (e == hipSuccess) e = hipMemcpy(m->ltab, lt.data(), lt.size() * sizeof(int), hipMemcpyHostToDevice);
+  }
+  if (all.empty() || e != hipSuccess) return e;
+  e = hipMalloc((void**)&m->ktab, all.size() * sizeof(int2));
   if (e == hipSuccess) e = hipMemcpy(m->ktab, all.data(), all.size() * sizeof(int2), hipMemcpyHostToDevice);
   return e;
 }
@@ -2328,7 +2391,7 @@ int yk_model_create(yk_ctx* ctx, const yk_model_desc* desc, const void* host_blo
     e = hipFuncSetAttribute((const void*)nms_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)nms_lds_bytes());
   set_tile_attrs();
   if (const char* env = getenv("YK_CONV_DIRECT")) m->tiled = env[0] != '1';
-  if (e == hipSuccess && !(getenv("YK_CONV_FAST") && getenv("YK_CONV_FAST")[0] == '0')) e = build_ktabs(m);
+  if (e == hipSuccess) e = build_ktabs(m, !(getenv("YK_CONV_FAST") && getenv("YK_CONV_FAST")[0] == '0'));
   if (e == hipSuccess) e = set_schedule(m, 1, 3);
   if (e != hipSuccess) {
     yk::set_error(std::string("yk_model_create: ") + hipGetErrorString(e));
@@ -2372,7 +2435,8 @@ int yk_model_destroy(yk_model* m) {
   for (hipStream_t s : m->aux) (void)hipStreamDestroy(s);
   for (hipEvent_t v : m->ev) (void)hipEventDestroy(v);
   if (m->arena) (void)hipFree(m->arena);
-  void* ptrs[] = {m->blob, m->cand, m->cand_count, m->slot_of, m->gkeys, m->gbox, m->gflag, m->dets, m->counts, m->ktab};
+  void* ptrs[] = {m->blob, m->cand, m->cand_count, m->slot_of, m->gkeys, m->gbox, m->gflag, m->dets, m->counts, m->ktab,
+                  m->ltab};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   delete m;
@@ -2517,13 +2581,13 @@ int yk_model_autotune(yk_model* m, const uint8_t* frames, int batch, float conf,
     if (op.kind != YK_K_CONV) continue;
     if (op.has_res && op.res.buf == op.dst.buf && op.res.c_off == op.dst.c_off) continue;  // in place
     std::vector<std::array<int, 3>> cands = {{CK_DIRECT, 0, 0}};
-    if (tile_plan(op, esz, bt).ok) cands.push_back({CK_TILE, 0, 0});
+    if (tile_plan(op, esz, bt).ok && m->ltab && m->ltab_off[i] >= 0) cands.push_back({CK_TILE, 0, 0});
     for (int nnt : {1, 2, 4})
       for (int npt : {1, 2, 4}) {
         if (nnt > 1 && 4 * op.n_tiles < 3 * ((op.n_tiles + nnt - 1) / nnt) * nnt) continue;
         cands.push_back({CK_SPLITK, nnt, npt});
       }
-    if (m->ktab && m->ktab_off[i] >= 0)
+    if (m->ktab && m->ktab_off[i] >= 0 && (long)bt * op.out_h * op.out_w < (1L << 22))
       for (int ws = 0; ws < 2; ++ws)
         for (int nnt : {1, 2, 3, 4})
           for (int npt : {1, 2, 4}) {
