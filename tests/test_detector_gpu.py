@@ -220,3 +220,16 @@ def test_fp32_conv_variants_match_oracle(plan):
         n = int(counts[b])
         assert n == len(ref)
         np.testing.assert_allclose(dets[b, :n, :4].cpu().numpy(), ref[:, :4].numpy(), rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("frame_hw", [(512, 640), (500, 640)])
+def test_bf16_first_conv_mfma_close_to_oracle(frame_hw):
+    """conv_input_mfma_kernel (bf16 build): layer 0 (LetterBox fill 114 + BGR->RGB + /255
+    folded into bf16 weights, 16x16x32 MFMA) within bf16 rounding of the oracle's fp32 layer 0;
+    the padded frame exercises the LetterBox border."""
+    s = setup(dtype="bf16", frame_hw=frame_hw)
+    got = s["dm"].layer_nchw(0, s["B"])
+    want = s["ref"].outputs[0]
+    assert got.shape == want.shape
+    assert rel_err(got, want) < 2e-2
+    assert float((got.double() - want.double()).abs().mean()) < 5e-3 * float(want.abs().mean())

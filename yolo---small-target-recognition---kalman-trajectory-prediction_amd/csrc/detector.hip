@@ -965,6 +965,90 @@ __global__ void __launch_bounds__(256) conv_input_kernel(InputArgs a) {
   }
 }
 
+// bf16 production variant of the first conv on MFMA.  K = 3 channels x 9 taps = 27 (padded to
+// one 16x16x32 K step), N = cout (<= 32: two 16-row tiles).  The uint8 pixel values are exact
+// in bf16, so the staged patch holds raw values (LetterBox fill 114, conv zero padding 0) and
+// the 1/255 of `im /= 255` is folded into the weights (the only rounding is the bf16 weight,
+// as for every other layer).  A workgroup = a 16x16 output tile; wave w computes rows
+// 4w..4w+3: per row one B fragment (8 LDS reads per lane) and two MFMAs.
+__global__ void __launch_bounds__(256) conv_input_mfma_kernel(InputArgs a) {
+  constexpr int TI = 15 * 2 + 3;
+  constexpr int TP = TI + 1;
+  __shared__ float xs[3][TI][TP];
+  __shared__ float ws[32 * 27];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int kg = lane >> 4, col = lane & 15;
+  const int tiles_x = (a.out_w + 15) / 16, tiles_y = (a.out_h + 15) / 16;
+  int t = blockIdx.x;
+  const int b = t / (tiles_x * tiles_y);
+  t -= b * tiles_x * tiles_y;
+  const int ty0 = (t / tiles_x) * 16, tx0 = (t % tiles_x) * 16;
+  const int s = a.stride;
+  const int ti = 15 * s + 3;
+  const int iy0 = ty0 * s - a.pad, ix0 = tx0 * s - a.pad;
+  const unsigned char* fr = a.frames + (size_t)b * a.fh * a.fw * 3;
+  for (int i = tid; i < 32 * 27; i += 256) ws[i] = i < a.cout * 27 ? a.w[i] * (1.0f / 255.0f) : 0.f;
+  for (int i = tid; i < ti * ti; i += 256) {
+    const int ry = i / ti, rx = i - ry * ti;
+    const int iy = iy0 + ry, ix = ix0 + rx;
+    float v0 = 0.f, v1 = 0.f, v2 = 0.f;
+    if (iy >= 0 && iy < a.in_h && ix >= 0 && ix < a.in_w) {
+      const int fy = iy - a.pad_top, fx = ix - a.pad_left;
+      if (fy >= 0 && fy < a.fh && fx >= 0 && fx < a.fw) {
+        const unsigned char* px = fr + ((size_t)fy * a.fw + fx) * 3;
+        v0 = (float)px[2];  // BGR -> RGB
+        v1 = (float)px[1];
+        v2 = (float)px[0];
+      } else {
+        v0 = v1 = v2 = 114.f;
+      }
+    }
+    xs[0][ry][rx] = v0;
+    xs[1][ry][rx] = v1;
+    xs[2][ry][rx] = v2;
+  }
+  __syncthreads();
+  // A fragments: rows = output channels nt*16 + col, K = kg*8 + e (k = c*9 + ky*3 + kx)
+  bf16x8 wa[2];
+  int xoff[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int k = kg * 8 + e;
+    wa[0][e] = (__bf16)(k < 27 ? ws[col * 27 + k] : 0.f);
+    wa[1][e] = (__bf16)(k < 27 ? ws[(16 + col) * 27 + k] : 0.f);
+    const int c = k / 9, tap = k - c * 9, ky = tap / 3, kx = tap - ky * 3;
+    xoff[e] = k < 27 ? (c * TI + ky) * TP + col * s + kx : -1;
+  }
+  const float* xsf = &xs[0][0][0];
+  f32x4 acc[2][4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int roff = (wave * 4 + r) * s * TP;
+    bf16x8 xb;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) xb[e] = (__bf16)(xoff[e] >= 0 ? xsf[xoff[e] + roff] : 0.f);
+    acc[0][r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[0], xb, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+    acc[1][r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[1], xb, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+  }
+  const int ox = tx0 + col;
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt) {
+    const int n0 = nt * 16 + kg * 4;
+    if (n0 >= a.cout) continue;
+    const float4 bb = *(const float4*)(a.b + n0);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int oy = ty0 + wave * 4 + r;
+      if (oy >= a.out_h || ox >= a.out_w) continue;
+      float v[4] = {acc[nt][r][0] + bb.x, acc[nt][r][1] + bb.y, acc[nt][r][2] + bb.z, acc[nt][r][3] + bb.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = silu<false>(v[j]);
+      const size_t p = ((size_t)b * a.out_h + oy) * a.out_w + ox;
+      store4((unsigned short*)a.dst + p * a.d_cstride + a.d_coff + n0, v);
+    }
+  }
+}
+
 // ---------------------------------------------------------------- SPPF pooling
 // slices 1..3 of the SPPF concat buffer = max over 5x5 / 9x9 / 13x13 windows of slice 0
 // (MaxPool2d(5,1,2) applied 1/2/3 times; padding never wins a max).
@@ -1451,6 +1535,7 @@ struct yk_model {
   int2* ktab = nullptr;
   std::vector<int64_t> ktab_off;
   int* ltab = nullptr;                // conv_tile_kernel K-step tables (LDS element offsets)
+  bool input_valu = false;            // YK_INPUT_VALU=1: f32-VALU first conv in the bf16 build too
   std::vector<int64_t> ltab_off;
   char* arena = nullptr;      // every activation buffer (bufs[i] point into it)
   size_t arena_bytes = 0;
@@ -1849,7 +1934,10 @@ int launch_op(yk_model* m, const yk_op& op, const uint8_t* frames, int B, float 
         a.d_cstride = op.dst.c_stride;
         a.d_coff = op.dst.c_off;
         const int tiles = B * ((op.out_h + 15) / 16) * ((op.out_w + 15) / 16);
-        hipLaunchKernelGGL(conv_input_kernel<Tr>, dim3(tiles), dim3(256), 0, st, a);
+        if (!Tr::kExact && op.cout <= 32 && !m->input_valu)
+          hipLaunchKernelGGL(conv_input_mfma_kernel, dim3(tiles), dim3(256), 0, st, a);
+        else
+          hipLaunchKernelGGL(conv_input_kernel<Tr>, dim3(tiles), dim3(256), 0, st, a);
         break;
       }
       case YK_K_CONV: {
@@ -2024,7 +2112,9 @@ int launch_any(yk_model* m, const yk_op& op, const uint8_t* frames, int B, float
 const char* op_kernel_name(const yk_model* m, const yk_op& op) {
   const bool f = m->desc.act_dtype == YK_ACT_F32;
   switch (op.kind) {
-    case YK_K_CONV_INPUT: return f ? "conv_input_kernel<yk::det::F32>" : "conv_input_kernel<yk::det::BF16>";
+    case YK_K_CONV_INPUT:
+      return f ? "conv_input_kernel<yk::det::F32>"
+               : (op.cout <= 32 && !m->input_valu ? "conv_input_mfma_kernel" : "conv_input_kernel<yk::det::BF16>");
     case YK_K_SPPF_POOL:
       if (op.src[0].h * op.src[0].w <= kSppfLdsMaxHW && op.src_ch[0] % 8 == 0)
         return f ? "sppf_lds_kernel<yk::det::F32>" : "sppf_lds_kernel<yk::det::BF16>";
@@ -2391,6 +2481,7 @@ int yk_model_create(yk_ctx* ctx, const yk_model_desc* desc, const void* host_blo
     e = hipFuncSetAttribute((const void*)nms_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)nms_lds_bytes());
   set_tile_attrs();
   if (const char* env = getenv("YK_CONV_DIRECT")) m->tiled = env[0] != '1';
+  if (const char* env = getenv("YK_INPUT_VALU")) m->input_valu = env[0] == '1';
   if (e == hipSuccess) e = build_ktabs(m, !(getenv("YK_CONV_FAST") && getenv("YK_CONV_FAST")[0] == '0'));
   if (e == hipSuccess) e = set_schedule(m, 1, 3);
   if (e != hipSuccess) {
