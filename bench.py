@@ -37,8 +37,11 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--config", type=int, default=3, choices=[3, 5],
+                    help="BASELINE config: 3 = 640x512, ~64 live tracks/stream (the metric's workload); "
+                         "5 = 1280x1024 at imgsz 1280, ~256 live tracks/stream, 150-frame occlusion bursts")
     ap.add_argument("--streams", type=int, default=8, help="streams (= frames per forward) per GPU")
-    ap.add_argument("--targets", type=int, default=22,
+    ap.add_argument("--targets", type=int, default=None,
                     help="synthetic targets per stream (22 -> ~64 live tracks/stream: the planted detector plus lost-track retention)")
     ap.add_argument("--scale", default="s", choices=["n", "s"])
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
@@ -132,7 +135,7 @@ def tracker_roofline(pipe, reps=20):
             "achieved": round(gbps, 3), "peak": HBM_PEAK, "unit": "GB/s", "frac": round(gbps / HBM_PEAK, 6)}
 
 
-def cpu_baseline(P, scale, seconds, targets, seed=0):
+def cpu_baseline(P, scale, seconds, targets, seed=0, hw=(512, 640), imgsz=640):
     """Reference-equivalent CPU path (oracle: torch-CPU fp32 YOLOv8s+P2 + numpy tracker) on a
     bounded sample of one stream, threads as the reference's select_device: min(8, ncpu-1)."""
     from oracle import detector_ref as D
@@ -145,13 +148,13 @@ def cpu_baseline(P, scale, seconds, targets, seed=0):
     layers = [(Ly.i, Ly.f, Ly.kind, {**Ly.args, **({"c": int(Ly.c2 * 0.5)} if Ly.kind == "C2f" else {})})
               for Ly in ar.layers]
     det = D.RefDetector(layers, sd, P.arch.detect_strides(ar))
-    sc = P.synth.Scene(seed=seed, n_targets=targets, n_frames=400)
+    sc = P.synth.Scene(seed=seed, n_targets=targets, n_frames=400, height=hw[0], width=hw[1])
     trk = RefMultiTracker(150, 1, 0.1)
     n, t_total = 0, 0.0
     for t in range(400):
         f = sc.frame(t)
         t0 = time.perf_counter()
-        res, _ = D.predict(det, [f], 0.25, 0.7, 300)
+        res, _ = D.predict(det, [f], 0.25, 0.7, 300, imgsz)
         boxes = res[0][:, :4].numpy()
         scores = res[0][:, 4].numpy()
         dets = [[b[0], b[1], b[2], b[3], s] for b, s in zip(boxes, scores) if s > 0.1]
@@ -163,7 +166,7 @@ def cpu_baseline(P, scale, seconds, targets, seed=0):
             if t_total > seconds:
                 break
     return {"value": round(n / t_total, 3), "unit": "frames/s", "cores": threads, "kind": "port",
-            "sample": f"{n} frames of one 640x512 stream ({targets} targets), YOLOv8{scale}+P2 fp32 torch-CPU "
+            "sample": f"{n} frames of one {hw[1]}x{hw[0]} stream ({targets} targets), YOLOv8{scale}+P2 fp32 torch-CPU "
                       f"({threads} threads) + numpy tracker, after 2 warm-up frames"}
 
 
@@ -180,14 +183,18 @@ def main():
     from importlib import import_module
 
     pipeline = import_module(PKG + ".pipeline")
-    S, H, W = a.streams, 512, 640
+    S = a.streams
+    H, W, imgsz, max_tracks = (512, 640, 640, 512) if a.config == 3 else (1024, 1280, 1280, 2048)
+    if a.targets is None:
+        a.targets = 22 if a.config == 3 else 66
     shard = P.shard
     my_streams = shard.stream_ids(rank, ws, S)  # this GPU's block of independent streams
     pipe = pipeline.StreamPipeline(f"yolov8{a.scale}-small.yaml", S, (H, W), a.dtype, seed=0, device=local,
-                                   pipelined=not a.no_pipeline)
+                                   pipelined=not a.no_pipeline, imgsz=imgsz, max_tracks=max_tracks)
     # pre-render frames of every stream into HBM (inputs resident before the timed region)
     F = max(2, min(a.frames, a.warmup + a.steps))
-    scenes = [P.synth.Scene(seed=shard.stream_seed(g, S), n_targets=a.targets, n_frames=F + 1) for g in my_streams]
+    scenes = [P.synth.Scene(seed=shard.stream_seed(g, S), n_targets=a.targets, n_frames=F + 1, width=W, height=H)
+              for g in my_streams]
     frames = torch.empty((F, S, H, W, 3), dtype=torch.uint8, device=dev)
     for s, sc in enumerate(scenes):
         frames[:, s] = sc.frames_torch(0, F, dev)
@@ -262,17 +269,17 @@ def main():
     log("profile done")
     cpu = None
     if rank == 0 and ws == 1 and not a.no_cpu_baseline:
-        cpu = cpu_baseline(P, a.scale, a.cpu_seconds, a.targets)
+        cpu = cpu_baseline(P, a.scale, a.cpu_seconds, a.targets, hw=(H, W), imgsz=imgsz)
     if rank == 0:
         gflop = pipe.flops_per_frame() / 1e9
         out = {
             "metric": METRIC, "value": round(fps, 2), "unit": "frames/s", "n_gpus": ws, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": a.dtype,
-            "data": "synthetic: seeded 640x512 IR-like scenes rendered into HBM before timing; seeded "
+            "data": f"synthetic: seeded {W}x{H} IR-like scenes rendered into HBM before timing; seeded "
                     "planted weights (no trained best.pt in the reference)",
-            "config": {"workload": f"YOLOv8{a.scale}+P2 640x512, {S} streams/GPU as batch {S}, "
-                                   f"{a.targets} targets/stream, tracker(150, 1, 0.1) (BASELINE config 3)",
+            "config": {"workload": f"YOLOv8{a.scale}+P2 {W}x{H} (imgsz {imgsz}), {S} streams/GPU as batch {S}, "
+                                   f"{a.targets} targets/stream, tracker(150, 1, 0.1) (BASELINE config {a.config})",
                        "streams_per_gpu": S, "global_batch": S * ws, "parallelism": f"streams sharded over {ws} GPU(s)",
                        "graph": not a.no_graph, "tracker_overlapped": not a.no_pipeline, "autotuned": not a.no_tune, "dag_lanes": a.lanes,
                        "batch_groups": a.groups,

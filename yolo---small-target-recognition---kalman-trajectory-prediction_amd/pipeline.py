@@ -28,14 +28,14 @@ class StreamPipeline:
     def __init__(self, model_cfg: str = "yolov8s-small.yaml", n_streams: int = 8, frame_hw=(512, 640),
                  dtype: str = "bf16", weights=None, seed: int = 0, conf: float = 0.25, iou: float = 0.7,
                  max_det: int = 300, max_lost_frames: int = 150, min_hits: int = 1, iou_threshold: float = 0.1,
-                 max_tracks: int = 512, device: int = 0, pipelined: bool = False):
+                 max_tracks: int = 512, device: int = 0, pipelined: bool = False, imgsz=640):
         if conf < 0.1:
             raise ValueError("conf < 0.1 would need the driver's score > 0.1 filter on the device path")
         self.S, self.device = int(n_streams), int(device)
         self.conf, self.iou, self.max_det = float(conf), float(iou), int(max_det)
         ar = A.parse_arch(A.load_model_dict(model_cfg))
         sd = weights if weights is not None else Wt.synthetic_state_dict(ar, seed)
-        self.prog = M.Program(ar, sd, frame_hw[0], frame_hw[1], 640, self.S, dtype, self.max_det)
+        self.prog = M.Program(ar, sd, frame_hw[0], frame_hw[1], imgsz, self.S, dtype, self.max_det)
         self.model = M.DeviceModel(self.prog, self.device)
         self.tracker = T.MultiStreamTracker(self.S, max_lost_frames, min_hits, iou_threshold, max_tracks,
                                             self.max_det, self.device)
