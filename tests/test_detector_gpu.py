@@ -196,7 +196,7 @@ def test_dag_schedule_matches_sequential(dtype):
                 np.testing.assert_allclose(a, b, rtol=1e-4, atol=1e-3)
 
 
-@pytest.mark.parametrize("plan", [(0, 0, 0), (1, 0, 0), (2, 1, 1), (2, 2, 4), (2, 4, 2), (3, 1, 1), (3, 2, 4), (3, 3, 2),
+@pytest.mark.parametrize("plan", [(0, 0, 0), (1, 0, 0), (1, 1, 0), (4, 2, 0), (4, 4, 0), (4, 2, 8), (2, 1, 1), (2, 2, 4), (2, 4, 2), (3, 1, 1), (3, 2, 4), (3, 3, 2),
                                   (3, 4, 4), (3, 1, 4 | 16), (3, 2, 2 | 16), (3, 4, 4 | 16), "tuned"])
 def test_fp32_conv_variants_match_oracle(plan):
     """Every conv kernel variant (direct, LDS-tiled, split-K fragment tiles, autotuned mix)

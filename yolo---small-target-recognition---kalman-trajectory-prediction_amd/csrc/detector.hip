@@ -461,7 +461,7 @@ __global__ void __launch_bounds__(256) conv_tile_kernel(TileArgs a) {
   const int wslab = a.single ? NNT * a.k_steps * 64 : 2 * WU;
   T* xt = (T*)(smem + (size_t)wslab * 16);  // [tih][tiw][ps]
   // K-step table [k_steps][4]: LDS element offset of each lane group's K chunk from the
-  // pixel's window origin in the tile (-1: padding chunk), built by the host (build_ktabs)
+  // pixel's window origin in the tile (K padding: 0, zero weights), built by the host (build_ktabs)
   int* ltab = (int*)(smem + (size_t)wslab * 16 + (((size_t)a.tih * a.tiw * a.ps * sizeof(T) + 15) & ~(size_t)15));
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   for (int i = tid; i < a.k_steps * 4; i += 256) ltab[i] = a.tab[i];
@@ -583,15 +583,10 @@ __global__ void __launch_bounds__(256) conv_tile_kernel(TileArgs a) {
     const uint4* wc = wl + buf * WU;
     const int kn = a.k_steps - k0 < kch ? a.k_steps - k0 : kch;
     for (int kk = KSPLIT ? wave : 0; kk < kn; kk += KSPLIT ? 4 : 1) {
-      const int e = ltab[(k0 + kk) * 4 + kg];
+      const int e = ltab[(k0 + kk) * 4 + kg];  // K padding chunks: zero weights, finite data
       uint4 xf[NPT];
-      if (e >= 0) {
 #pragma unroll
-        for (int pt = 0; pt < NPT; ++pt) xf[pt] = *(const uint4*)(xt + prow[pt] + e);
-      } else {
-#pragma unroll
-        for (int pt = 0; pt < NPT; ++pt) xf[pt] = make_uint4(0u, 0u, 0u, 0u);
-      }
+      for (int pt = 0; pt < NPT; ++pt) xf[pt] = *(const uint4*)(xt + prow[pt] + e);
 #pragma unroll
       for (int ni = 0; ni < NNT; ++ni) {
         const uint4 w = wc[(ni * kch + kk) * 64 + lane];
@@ -723,7 +718,16 @@ __global__ void __launch_bounds__(256) conv_fast_kernel(FastArgs a) {
   const int nt0 = blockIdx.y * NNT;
   const int pbase = WS ? blockIdx.x * (16 * NPT) : (blockIdx.x * 4 + wave) * (16 * NPT);
   const int nk = a.k_steps;
-  for (int i = tid; i < nk * 4; i += 256) tab[i] = a.ktab[i];
+  {
+    int2 tv[2];  // <= 512 entries (nk <= 128) in one round trip
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+      if (tid + u * 256 < nk * 4) tv[u] = a.ktab[tid + u * 256];
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+      if (tid + u * 256 < nk * 4) tab[tid + u * 256] = tv[u];
+    for (int i = tid + 512; i < nk * 4; i += 256) tab[i] = a.ktab[i];
+  }
   const __amdgpu_buffer_rsrc_t xr = make_srd(a.arena, a.arena_bytes);
   const __amdgpu_buffer_rsrc_t wr = make_srd(a.wblob, a.wbytes);
   const int hw = a.out_h * a.out_w;
@@ -868,6 +872,216 @@ __global__ void __launch_bounds__(256) conv_fast_kernel(FastArgs a) {
       }
       store4((T*)a.dst + (size_t)p * a.d_cstride + a.d_coff + n0, v);
     }
+  }
+}
+
+// ---------------------------------------------------------------- persistent LDS-tiled conv (wide layers)
+// For the high-resolution layers (P2/P3: 20,480 / 5,120 pixels per image) the gather kernel
+// re-fetches every input pixel once per tap and every weight fragment once per wave through
+// the 32 KiB L1 (L1/L2-bandwidth-bound).  Here a workgroup keeps its NNT x 16 output
+// channels' whole weight slab resident in LDS, loops over 16 x 16-pixel output tiles (grid =
+// resident capacity, blockIdx.y = output-channel group) and double-buffers the input tiles
+// (+ halo, all K-space channels of both sources) in LDS: tile i+1's global loads are in flight
+// while tile i computes.  Staging addresses are precomputed per thread (the unit pattern is
+// the same for every tile); invalid pixels are buffer offsets past the arena (hardware zeros).
+// Wave w computes rows 4w..4w+3 of a tile; a K step is one LDS table read, 4 + NNT
+// ds_read_b128 and 4 x NNT MFMAs.
+struct WideArgs {
+  const void* arena;
+  unsigned arena_bytes;
+  unsigned soff0, soff1;
+  int h0, w0, cs0, up0, h1, w1, cs1, up1;
+  int c0, cin;
+  int stride, pad, in_h, in_w, out_h, out_w, B;
+  int tiles_x, tiles_y, tih, tiw, ps;
+  const uint4* wpk;
+  const float* bias;
+  const int* ltab;               // [k_steps][4] LDS element offsets (K padding: 0, zero weights)
+  int k_steps, n_tiles;
+  void* dst;
+  int d_cstride, d_coff, cout;
+  const void* res;
+  int r_cstride, r_coff;
+  int act;
+  int dbg;  // diagnostics (YK_WIDE_DBG): 1 = no K loop, 2 = no epilogue stores, 4 = no staging
+};
+
+__host__ __device__ inline size_t wide_tile_bytes(int tih, int tiw, int ps, int esz) {
+  return (((size_t)tih * tiw * ps * esz) + 15) & ~(size_t)15;
+}
+inline size_t wide_lds(int nnt, int k_steps, int tih, int tiw, int ps, int esz) {
+  return (size_t)nnt * k_steps * 1024 + (size_t)((k_steps + 3) & ~3) * 16 + 2 * wide_tile_bytes(tih, tiw, ps, esz);
+}
+
+template <class Tr, int NNT, int UPT, int NW>
+__global__ void __launch_bounds__(64 * NW) conv_wide_kernel(WideArgs a) {
+  // NW waves per workgroup (4 or 8: one or two per SIMD, the second hides the LDS latency of
+  // the first); wave w computes rows NPT*w .. NPT*w + NPT - 1 of the 16-row tile
+  using T = typename Tr::T;
+  constexpr int ESZ = (int)sizeof(T);
+  constexpr int EU = 16 / ESZ;
+  constexpr int NTH = 64 * NW;
+  constexpr int NPT = 16 / NW;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int nk = a.k_steps;
+  uint4* wl = (uint4*)smem;                                   // [NNT][nk][64]
+  int* ltab = (int*)(smem + (size_t)NNT * nk * 1024);         // [nk][4]
+  T* xt0 = (T*)(smem + (size_t)NNT * nk * 1024 + (size_t)((nk + 3) & ~3) * 16);
+  const size_t tbytes = wide_tile_bytes(a.tih, a.tiw, a.ps, ESZ);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int kg = lane >> 4, col = lane & 15;
+  const int nt0 = blockIdx.y * NNT;
+  const int nsp = a.B * a.tiles_y * a.tiles_x;
+  int t = blockIdx.x;
+  if (t >= nsp) return;
+  const __amdgpu_buffer_rsrc_t xr = make_srd(a.arena, a.arena_bytes);
+  // resident weights + table
+  for (int i = tid; i < NNT * nk * 64; i += NTH) {
+    const int ni = i / (nk * 64), r = i - ni * nk * 64;
+    const int nt = nt0 + ni < a.n_tiles ? nt0 + ni : a.n_tiles - 1;
+    wl[i] = a.wpk[(size_t)nt * nk * 64 + r];
+  }
+  // table transposed to [kg][nk4] (nk4 = nk rounded up to 4; padding entries 0): a lane's four
+  // consecutive K steps are one ds_read_b128
+  const int nk4 = (nk + 3) & ~3;
+  for (int i = tid; i < nk4 * 4; i += NTH) {
+    const int g = i / nk4, ks = i - g * nk4;
+    ltab[i] = ks < nk ? a.ltab[ks * 4 + g] : 0;
+  }
+  // per-thread staging units: packed (ry << 24 | rx << 16 | src << 15 | channel), LDS offset
+  const int U = a.cin / EU;
+  const int total = a.tih * a.tiw * U;
+  int ud[UPT], ul[UPT];
+#pragma unroll
+  for (int j = 0; j < UPT; ++j) {
+    const int i = tid + j * NTH;
+    ud[j] = -1;
+    ul[j] = 0;
+    if (i < total) {
+      const int pix = i / U, uu = i - pix * U;
+      const int ry = pix / a.tiw, rx = pix - ry * a.tiw;
+      const int c = uu * EU;
+      const int src = c >= a.c0 ? 1 : 0;
+      ud[j] = (ry << 24) | (rx << 16) | (src << 15) | (src ? c - a.c0 : c);
+      ul[j] = pix * a.ps + uu * EU;
+    }
+  }
+  int prow[NPT];
+#pragma unroll
+  for (int pt = 0; pt < NPT; ++pt) prow[pt] = ((wave * NPT + pt) * a.stride * a.tiw + col * a.stride) * a.ps;
+  float4 bb[NNT];
+#pragma unroll
+  for (int ni = 0; ni < NNT; ++ni) {
+    const int n0 = (nt0 + ni) * 16 + kg * 4;
+    bb[ni] = (nt0 + ni < a.n_tiles && n0 < a.cout) ? *(const float4*)(a.bias + n0) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  const int tpi = a.tiles_y * a.tiles_x;
+  uint4 st[UPT];
+  auto fetch = [&](int tt) {
+    const int b = tt / tpi, r = tt - b * tpi;
+    const int ty = r / a.tiles_x, tx = r - ty * a.tiles_x;
+    const int iy0 = ty * 16 * a.stride - a.pad, ix0 = tx * 16 * a.stride - a.pad;
+#pragma unroll
+    for (int j = 0; j < UPT; ++j) {
+      const int d = ud[j];
+      const int iy = iy0 + (d >> 24), ix = ix0 + ((d >> 16) & 255);
+      const bool s1 = (d >> 15) & 1;
+      const int h = s1 ? a.h1 : a.h0, w = s1 ? a.w1 : a.w0, cs = s1 ? a.cs1 : a.cs0, up = s1 ? a.up1 : a.up0;
+      const unsigned so = s1 ? a.soff1 : a.soff0;
+      const bool ok = d >= 0 && iy >= 0 && iy < a.in_h && ix >= 0 && ix < a.in_w;
+      const unsigned off = so + (unsigned)((((b * h + (iy >> up)) * w + (ix >> up)) * cs + (d & 0x7fff)) * ESZ);
+      st[j] = bload(xr, ok ? off : kOOB, 0);
+    }
+  };
+  auto commit = [&](T* xt) {
+#pragma unroll
+    for (int j = 0; j < UPT; ++j)
+      if (ud[j] >= 0) *(uint4*)(xt + ul[j]) = st[j];
+  };
+  fetch(t);
+  commit(xt0);
+  __syncthreads();
+  for (int it = 0;; ++it) {
+    const int tn = t + gridDim.x;
+    if (tn < nsp && !(a.dbg & 4)) fetch(tn);  // in flight over this tile's K loop
+    const T* xt = (const T*)((const unsigned char*)xt0 + (it & 1) * tbytes);
+    f32x4 acc[NNT][NPT];
+#pragma unroll
+    for (int ni = 0; ni < NNT; ++ni)
+#pragma unroll
+      for (int pt = 0; pt < NPT; ++pt) acc[ni][pt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int nkl = (a.dbg & 1) ? 0 : nk;
+    // four K steps per iteration: every LDS read of the group is issued before its MFMAs
+    // (sched_barrier: the scheduler would otherwise sink each read to its first use)
+    const int4* lt4 = (const int4*)(ltab + kg * nk4);
+    int k4 = 0;
+    for (; k4 + 4 <= nkl; k4 += 4) {
+      const int4 e4 = lt4[k4 >> 2];
+      const int ev[4] = {e4.x, e4.y, e4.z, e4.w};
+      uint4 xf[4][NPT], wf[4][NNT];
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+#pragma unroll
+        for (int ni = 0; ni < NNT; ++ni) wf[d][ni] = wl[(ni * nk + k4 + d) * 64 + lane];
+#pragma unroll
+        for (int pt = 0; pt < NPT; ++pt) xf[d][pt] = *(const uint4*)(xt + prow[pt] + ev[d]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int d = 0; d < 4; ++d)
+#pragma unroll
+        for (int ni = 0; ni < NNT; ++ni)
+#pragma unroll
+          for (int pt = 0; pt < NPT; ++pt) acc[ni][pt] = mma<Tr>(wf[d][ni], xf[d][pt], acc[ni][pt]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    for (; k4 < nkl; ++k4) {
+      const int e = ltab[kg * nk4 + k4];
+      uint4 xf[NPT];
+#pragma unroll
+      for (int pt = 0; pt < NPT; ++pt) xf[pt] = *(const uint4*)(xt + prow[pt] + e);
+#pragma unroll
+      for (int ni = 0; ni < NNT; ++ni) {
+        const uint4 w = wl[(ni * nk + k4) * 64 + lane];
+#pragma unroll
+        for (int pt = 0; pt < NPT; ++pt) acc[ni][pt] = mma<Tr>(w, xf[pt], acc[ni][pt]);
+      }
+    }
+    // epilogue of tile t
+    {
+      const int b = t / tpi, r = t - b * tpi;
+      const int ty = r / a.tiles_x, tx = r - ty * a.tiles_x;
+      const int ox = tx * 16 + col;
+#pragma unroll
+      for (int ni = 0; ni < NNT; ++ni) {
+        const int n0 = (nt0 + ni) * 16 + kg * 4;
+        if (nt0 + ni >= a.n_tiles || n0 >= a.cout) continue;
+#pragma unroll
+        for (int pt = 0; pt < NPT; ++pt) {
+          const int oy = ty * 16 + wave * NPT + pt;
+          if (oy >= a.out_h || ox >= a.out_w) continue;
+          const size_t p = ((size_t)b * a.out_h + oy) * a.out_w + ox;
+          float v[4] = {acc[ni][pt][0] + bb[ni].x, acc[ni][pt][1] + bb[ni].y, acc[ni][pt][2] + bb[ni].z,
+                        acc[ni][pt][3] + bb[ni].w};
+          if (a.act) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[j] = silu<Tr::kExact>(v[j]);
+          }
+          if (a.res) {
+            float rr[4];
+            load4((const T*)a.res + p * a.r_cstride + a.r_coff + n0, rr);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[j] = rr[j] + v[j];
+          }
+          if (!(a.dbg & 2) || v[0] == 12345.f) store4((T*)a.dst + p * a.d_cstride + a.d_coff + n0, v);
+        }
+      }
+    }
+    if (tn >= nsp) break;
+    commit((T*)((unsigned char*)xt0 + ((it + 1) & 1) * tbytes));
+    __syncthreads();
+    t = tn;
   }
 }
 
@@ -1536,6 +1750,7 @@ struct yk_model {
   std::vector<int64_t> ktab_off;
   int* ltab = nullptr;                // conv_tile_kernel K-step tables (LDS element offsets)
   bool input_valu = false;            // YK_INPUT_VALU=1: f32-VALU first conv in the bf16 build too
+  int wide_dbg = 0;                   // YK_WIDE_DBG: conv_wide_kernel diagnostics (never in production)
   std::vector<int64_t> ltab_off;
   char* arena = nullptr;      // every activation buffer (bufs[i] point into it)
   size_t arena_bytes = 0;
@@ -1590,7 +1805,9 @@ TilePlan tile_plan_geom(const yk_op& op, int esz, int B);
 
 // Geometry, then whether the whole weight slab fits LDS next to the input tile (one prologue,
 // no chunk barriers) without costing occupancy beyond ~96 KB per workgroup.
-TilePlan tile_plan(const yk_op& op, int esz, int B) {
+// big_single: keep the whole weight slab LDS-resident up to the 144 KiB cap (one workgroup
+// per CU, no chunk barriers), for the wide high-resolution convs.
+TilePlan tile_plan(const yk_op& op, int esz, int B, bool big_single = false) {
   TilePlan t = tile_plan_geom(op, esz, B);
   if (!t.ok) return t;
   t.lds = (t.lds + 15) / 16 * 16 + (size_t)op.k_steps * 16;  // + the K-step table
@@ -1598,7 +1815,7 @@ TilePlan tile_plan(const yk_op& op, int esz, int B) {
   const size_t slab = (size_t)t.nnt * op.k_steps * 1024;
   const size_t red = t.split ? (size_t)4 * t.nnt * t.npt * 64 * 16 : 0;
   const size_t lds1 = (slab > red ? slab : red) + (tile + 15) / 16 * 16 + (size_t)op.k_steps * 16;
-  const size_t cap = t.lds > 96 * 1024 ? t.lds : 96 * 1024;
+  const size_t cap = big_single ? kTileLdsMax : t.lds > 96 * 1024 ? t.lds : 96 * 1024;
   if (lds1 <= cap && lds1 <= kTileLdsMax) {
     t.single = true;
     t.lds = lds1;
@@ -1741,9 +1958,25 @@ void set_fast_attr_w() {
   set_fast_attr_n<Tr, 3, WS>();
   set_fast_attr_n<Tr, 4, WS>();
 }
+template <class Tr, int NNT, int NW>
+void set_wide_attr_w() {
+  (void)hipFuncSetAttribute((const void*)conv_wide_kernel<Tr, NNT, 4, NW>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  (void)hipFuncSetAttribute((const void*)conv_wide_kernel<Tr, NNT, 8, NW>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  (void)hipFuncSetAttribute((const void*)conv_wide_kernel<Tr, NNT, 12, NW>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  (void)hipFuncSetAttribute((const void*)conv_wide_kernel<Tr, NNT, 16, NW>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+}
+template <class Tr, int NNT>
+void set_wide_attr_n() {
+  set_wide_attr_w<Tr, NNT, 4>();
+  set_wide_attr_w<Tr, NNT, 8>();
+}
 void set_tile_attrs() {
   set_tile_attrs_t<BF16>();
   set_tile_attrs_t<F32>();
+  set_wide_attr_n<BF16, 2>();
+  set_wide_attr_n<BF16, 4>();
+  set_wide_attr_n<F32, 2>();
+  set_wide_attr_n<F32, 4>();
   set_fast_attr_w<BF16, false>();
   set_fast_attr_w<BF16, true>();
   set_fast_attr_w<F32, false>();
@@ -1755,7 +1988,8 @@ void set_tile_attrs() {
 }
 
 // Conv kernel choice for one op at batch B.
-enum { CK_DIRECT = 0, CK_TILE = 1, CK_SPLITK = 2, CK_FAST = 3 };
+enum { CK_DIRECT = 0, CK_TILE = 1, CK_SPLITK = 2, CK_FAST = 3, CK_WIDE = 4 };
+// CK_WIDE plan: nnt in {2, 4} (output-channel tiles per workgroup), npt unused
 // CK_FAST plan: nnt in {1, 2, 3, 4}, npt = NPT | (WS << 4) with NPT in {1, 2, 4}
 struct ConvPlan {
   int kind = CK_DIRECT, nnt = 0, npt = 0;
@@ -1793,6 +2027,30 @@ ConvPlan splitk_plan(const yk_op& op, int B, int nnt_force = 0, int npt_force = 
     }
   }
   return p;
+}
+
+// conv_wide_kernel geometry of an op: 16 x 16 output tiles, input tile 15 * s + k square,
+// odd number of 16-B units per pixel; ok = fits 160 KiB of LDS with its weight slab.
+struct WidePlan {
+  bool ok = false;
+  int tih = 0, tiw = 0, ps = 0, upt = 0;
+  size_t lds = 0;
+};
+WidePlan wide_plan(const yk_op& op, int esz, int nnt, int nw = 4) {
+  WidePlan w;
+  const int cin = op.src_ch[0] + (op.n_src > 1 ? op.src_ch[1] : 0);
+  if (cin % 8 || (op.ksize != 1 && op.ksize != 3)) return w;
+  int U = cin * esz / 16;
+  const int units = U;
+  if ((U & 1) == 0) U += 1;
+  w.ps = U * 16 / esz;
+  w.tih = w.tiw = 15 * op.stride + op.ksize;
+  const int total = w.tih * w.tiw * units;
+  w.upt = (total + 64 * nw - 1) / (64 * nw);
+  w.lds = wide_lds(nnt, op.k_steps, w.tih, w.tiw, w.ps, esz);
+  w.ok = w.upt <= 16 && w.lds <= 160 * 1024 && w.tih < 128;
+  for (int sidx = 0; sidx < op.n_src; ++sidx) w.ok = w.ok && (op.ksize == 1 || op.src[sidx].up == 0);
+  return w;
 }
 
 // conv_fast_kernel geometry: the largest fragment tile (NNT x NPT) that still gives >= 1024
@@ -1833,6 +2091,14 @@ ConvPlan conv_plan(const yk_model* m, const yk_op& op, int B) {
   if (idx < m->tuned.size() && m->tuned[idx][0] >= 0 && m->tuned_batch == B) {
     const auto& t = m->tuned[idx];
     if (t[0] == CK_SPLITK) return splitk_plan(op, B, t[1], t[2]);
+    if (t[0] == CK_WIDE && m->ltab && m->ltab_off[idx] >= 0 && m->arena_bytes < 0x7fff0000ull &&
+        wide_plan(op, esz, t[1], t[2] == 8 ? 8 : 4).ok) {
+      ConvPlan p;
+      p.kind = CK_WIDE;
+      p.nnt = t[1];
+      p.npt = t[2] == 8 ? 8 : 4;  // waves per workgroup
+      return p;
+    }
     if (t[0] == CK_FAST && m->ktab && m->ktab_off[idx] >= 0 && (long)B * op.out_h * op.out_w < (1L << 22)) {
       ConvPlan p;
       p.kind = CK_FAST;
@@ -1843,7 +2109,7 @@ ConvPlan conv_plan(const yk_model* m, const yk_op& op, int B) {
     if (t[0] == CK_TILE && m->ltab && m->ltab_off[idx] >= 0) {
       ConvPlan p;
       p.kind = CK_TILE;
-      p.tp = tile_plan(op, esz, B);
+      p.tp = tile_plan(op, esz, B, t[1] == 1);
       if (p.tp.ok) return p;
     }
     return ConvPlan{};
@@ -1904,6 +2170,25 @@ template <class Tr>
 void launch_fast(const FastArgs& a, const ConvPlan& p, hipStream_t st) {
   if (p.npt >> 4) launch_fast_w<Tr, true>(a, p.nnt, p.npt & 15, st);
   else launch_fast_w<Tr, false>(a, p.nnt, p.npt & 15, st);
+}
+
+template <class Tr, int NNT, int UPT, int NW>
+void launch_wide_t(const WideArgs& a, size_t lds, hipStream_t st) {
+  const int groups = (a.n_tiles + NNT - 1) / NNT;
+  const int nsp = a.B * a.tiles_y * a.tiles_x;
+  int per_cu = (int)((160 * 1024) / lds);
+  if (per_cu < 1) per_cu = 1;
+  int gx = 256 * per_cu / groups;
+  if (gx < 1) gx = 1;
+  if (gx > nsp) gx = nsp;
+  hipLaunchKernelGGL((conv_wide_kernel<Tr, NNT, UPT, NW>), dim3(gx, groups), dim3(64 * NW), lds, st, a);
+}
+template <class Tr, int NNT, int NW>
+void launch_wide_n(const WideArgs& a, int upt, size_t lds, hipStream_t st) {
+  if (upt <= 4) launch_wide_t<Tr, NNT, 4, NW>(a, lds, st);
+  else if (upt <= 8) launch_wide_t<Tr, NNT, 8, NW>(a, lds, st);
+  else if (upt <= 12) launch_wide_t<Tr, NNT, 12, NW>(a, lds, st);
+  else launch_wide_t<Tr, NNT, 16, NW>(a, lds, st);
 }
 
 template <class Tr>
@@ -1969,7 +2254,59 @@ int launch_op(yk_model* m, const yk_op& op, const uint8_t* frames, int B, float 
         a.act = op.act;
         const ConvPlan cp = conv_plan(m, op, B);
         const TilePlan& tp = cp.tp;
-        if (cp.kind == CK_FAST) {
+        if (cp.kind == CK_WIDE) {
+          const size_t esz = sizeof(typename Tr::T);
+          const int nw = cp.npt == 8 ? 8 : 4;
+          const WidePlan wp = wide_plan(op, (int)esz, cp.nnt, nw);
+          WideArgs w;
+          w.arena = m->arena;
+          w.arena_bytes = (unsigned)m->arena_bytes;
+          w.soff0 = (unsigned)(((const char*)a.src[0].p - (const char*)m->arena) + (size_t)a.src[0].coff * esz);
+          w.soff1 = (unsigned)(((const char*)a.src[1].p - (const char*)m->arena) + (size_t)a.src[1].coff * esz);
+          w.h0 = a.src[0].h;
+          w.w0 = a.src[0].w;
+          w.cs0 = a.src[0].cstride;
+          w.up0 = a.src[0].up;
+          w.h1 = a.src[1].h;
+          w.w1 = a.src[1].w;
+          w.cs1 = a.src[1].cstride;
+          w.up1 = a.src[1].up;
+          w.c0 = a.c0;
+          w.cin = a.cin;
+          w.stride = a.stride;
+          w.pad = a.pad;
+          w.in_h = a.in_h;
+          w.in_w = a.in_w;
+          w.out_h = a.out_h;
+          w.out_w = a.out_w;
+          w.B = B;
+          w.tiles_x = (a.out_w + 15) / 16;
+          w.tiles_y = (a.out_h + 15) / 16;
+          w.tih = wp.tih;
+          w.tiw = wp.tiw;
+          w.ps = wp.ps;
+          w.wpk = a.wpk;
+          w.bias = a.bias;
+          w.ltab = m->ltab + m->ltab_off[(size_t)(&op - m->ops.data())];
+          w.k_steps = a.k_steps;
+          w.n_tiles = a.n_tiles;
+          w.dst = a.dst;
+          w.d_cstride = a.d_cstride;
+          w.d_coff = a.d_coff;
+          w.cout = a.cout;
+          w.res = a.res;
+          w.r_cstride = a.r_cstride;
+          w.r_coff = a.r_coff;
+          w.act = a.act;
+          w.dbg = m->wide_dbg;
+          if (cp.nnt == 2) {
+            if (nw == 8) launch_wide_n<Tr, 2, 8>(w, wp.upt, wp.lds, st);
+            else launch_wide_n<Tr, 2, 4>(w, wp.upt, wp.lds, st);
+          } else {
+            if (nw == 8) launch_wide_n<Tr, 4, 8>(w, wp.upt, wp.lds, st);
+            else launch_wide_n<Tr, 4, 4>(w, wp.upt, wp.lds, st);
+          }
+        } else if (cp.kind == CK_FAST) {
           FastArgs f;
           const size_t esz = sizeof(typename Tr::T);
           f.arena = m->arena;
@@ -2124,6 +2461,12 @@ const char* op_kernel_name(const yk_model* m, const yk_op& op) {
   }
   const ConvPlan cp = conv_plan(m, op, m->plan_batch);
   static thread_local char buf[96];
+  if (cp.kind == CK_WIDE) {
+    const WidePlan wp = wide_plan(op, f ? 4 : 2, cp.nnt, cp.npt);
+    const int upt = wp.upt <= 4 ? 4 : wp.upt <= 8 ? 8 : wp.upt <= 12 ? 12 : 16;
+    snprintf(buf, sizeof buf, "conv_wide_kernel<yk::det::%s, %d, %d, %d>", f ? "F32" : "BF16", cp.nnt, upt, cp.npt);
+    return buf;
+  }
   if (cp.kind == CK_FAST) {
     const int npt = cp.npt & 15, ws = cp.npt >> 4;
     const int skd = cp.nnt * npt >= 8 ? 2 : 4;
@@ -2361,8 +2704,8 @@ hipError_t build_ktabs(yk_model* m, bool fast) {
     for (int ks = 0; ks < op.k_steps; ++ks)
       for (int kg = 0; kg < 4; ++kg) {
         const int kel = ks * 4 * epl + kg * epl, q = kel >> 3, sub = kel & 7;
-        if (q >= n_chunks) {
-          lt.push_back(-1);
+        if (q >= n_chunks) {  // K padding: the packed weights are zero there, so any finite
+          lt.push_back(0);    // activation works -- the window origin's first channels
           continue;
         }
         const int tap = q / cq, c = (q - tap * cq) * 8, ky = tap / k, kx = tap - ky * k;
@@ -2482,6 +2825,7 @@ int yk_model_create(yk_ctx* ctx, const yk_model_desc* desc, const void* host_blo
   set_tile_attrs();
   if (const char* env = getenv("YK_CONV_DIRECT")) m->tiled = env[0] != '1';
   if (const char* env = getenv("YK_INPUT_VALU")) m->input_valu = env[0] == '1';
+  if (const char* env = getenv("YK_WIDE_DBG")) m->wide_dbg = atoi(env);
   if (e == hipSuccess) e = build_ktabs(m, !(getenv("YK_CONV_FAST") && getenv("YK_CONV_FAST")[0] == '0'));
   if (e == hipSuccess) e = set_schedule(m, 1, 3);
   if (e != hipSuccess) {
@@ -2625,10 +2969,13 @@ int yk_model_profile(yk_model* m, const uint8_t* frames, int batch, float conf, 
 
 int yk_model_set_plan(yk_model* m, int op_index, int batch, int kind, int nnt, int npt) {
   YK_CHECK_ARG(m && op_index >= -1 && op_index < (int)m->ops.size(), "yk_model_set_plan: bad op index");
-  YK_CHECK_ARG(kind >= -1 && kind <= CK_FAST, "yk_model_set_plan: kind must be -1 (heuristic), 0, 1, 2 or 3");
+  YK_CHECK_ARG(kind >= -1 && kind <= CK_WIDE, "yk_model_set_plan: kind must be -1 (heuristic), 0, 1, 2, 3 or 4");
+  YK_CHECK_ARG(kind != CK_WIDE || ((nnt == 2 || nnt == 4) && (npt == 0 || npt == 4 || npt == 8)),
+               "yk_model_set_plan: wide conv nnt must be 2 or 4, npt (waves) 0, 4 or 8");
   YK_CHECK_ARG(kind != CK_FAST || (nnt >= 1 && nnt <= 4 && ((npt & 15) == 1 || (npt & 15) == 2 || (npt & 15) == 4) &&
                                    (npt >> 4) <= 1),
                "yk_model_set_plan: table conv needs nnt in [1, 4], npt in {1, 2, 4} (+16: waves split K)");
+  YK_CHECK_ARG(kind != CK_TILE || nnt == 0 || nnt == 1, "yk_model_set_plan: tiled conv nnt must be 0 or 1 (LDS-resident weights)");
   YK_CHECK_ARG(kind != CK_SPLITK || ((nnt == 1 || nnt == 2 || nnt == 4) && (npt == 1 || npt == 2 || npt == 4)),
                "yk_model_set_plan: split-K fragment tile must be nnt, npt in {1, 2, 4}");
   YK_CHECK_ARG(batch >= 1 && batch <= m->desc.max_batch, "yk_model_set_plan: batch out of range");
@@ -2672,11 +3019,20 @@ int yk_model_autotune(yk_model* m, const uint8_t* frames, int batch, float conf,
     if (op.kind != YK_K_CONV) continue;
     if (op.has_res && op.res.buf == op.dst.buf && op.res.c_off == op.dst.c_off) continue;  // in place
     std::vector<std::array<int, 3>> cands = {{CK_DIRECT, 0, 0}};
-    if (tile_plan(op, esz, bt).ok && m->ltab && m->ltab_off[i] >= 0) cands.push_back({CK_TILE, 0, 0});
+    if (tile_plan(op, esz, bt).ok && m->ltab && m->ltab_off[i] >= 0) {
+      cands.push_back({CK_TILE, 0, 0});
+      if (tile_plan(op, esz, bt, true).single && !tile_plan(op, esz, bt).single) cands.push_back({CK_TILE, 1, 0});
+    }
     for (int nnt : {1, 2, 4})
       for (int npt : {1, 2, 4}) {
         if (nnt > 1 && 4 * op.n_tiles < 3 * ((op.n_tiles + nnt - 1) / nnt) * nnt) continue;
         cands.push_back({CK_SPLITK, nnt, npt});
+      }
+    if (m->ltab && m->ltab_off[i] >= 0 && m->arena_bytes < 0x7fff0000ull)
+      for (int nnt : {2, 4}) {
+        if (nnt == 4 && op.n_tiles <= 2) continue;
+        for (int nw : {4, 8})
+          if (wide_plan(op, esz, nnt, nw).ok && (long)bt * op.out_h * op.out_w >= 4096) cands.push_back({CK_WIDE, nnt, nw});
       }
     if (m->ktab && m->ktab_off[i] >= 0 && (long)bt * op.out_h * op.out_w < (1L << 22))
       for (int ws = 0; ws < 2; ++ws)
