@@ -1421,14 +1421,15 @@ __global__ void __launch_bounds__(256) detect_kernel(DetArgs a) {
     float e[4], sum = 0.f;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      e[j] = expf(v[j] - m);
+      e[j] = Tr::kExact ? expf(v[j] - m) : __expf(v[j] - m);
       sum += e[j];
     }
     sum += __shfl_xor(sum, 16);
     sum += __shfl_xor(sum, 32);
     float ex = 0.f;
+    const float rs = Tr::kExact ? 0.f : __builtin_amdgcn_rcpf(sum);  // bf16 build: v_rcp
 #pragma unroll
-    for (int j = 0; j < 4; ++j) ex += (float)(kg * 4 + j) * (e[j] / sum);
+    for (int j = 0; j < 4; ++j) ex += (float)(kg * 4 + j) * (Tr::kExact ? e[j] / sum : e[j] * rs);
     ex += __shfl_xor(ex, 16);
     ex += __shfl_xor(ex, 32);
     d[s] = ex;
