@@ -37,10 +37,11 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--config", type=int, default=3, choices=[3, 5],
-                    help="BASELINE config: 3 = 640x512, ~64 live tracks/stream (the metric's workload); "
+    ap.add_argument("--config", type=int, default=3, choices=[2, 3, 5],
+                    help="BASELINE config: 2 = 640x512 batch 1, ~16 live tracks; 3 = 640x512, ~64 live tracks/stream (the metric's workload); "
                          "5 = 1280x1024 at imgsz 1280, ~256 live tracks/stream, 150-frame occlusion bursts")
-    ap.add_argument("--streams", type=int, default=8, help="streams (= frames per forward) per GPU")
+    ap.add_argument("--streams", type=int, default=None,
+                    help="streams (= frames per forward) per GPU (default 8; 1 for config 2)")
     ap.add_argument("--targets", type=int, default=None,
                     help="synthetic targets per stream (22 -> ~64 live tracks/stream: the planted detector plus lost-track retention)")
     ap.add_argument("--scale", default="s", choices=["n", "s"])
@@ -183,10 +184,12 @@ def main():
     from importlib import import_module
 
     pipeline = import_module(PKG + ".pipeline")
+    if a.streams is None:
+        a.streams = 1 if a.config == 2 else 8
     S = a.streams
-    H, W, imgsz, max_tracks = (512, 640, 640, 512) if a.config == 3 else (1024, 1280, 1280, 2048)
+    H, W, imgsz, max_tracks = (1024, 1280, 1280, 2048) if a.config == 5 else (512, 640, 640, 512)
     if a.targets is None:
-        a.targets = 22 if a.config == 3 else 66
+        a.targets = {2: 6, 3: 22, 5: 66}[a.config]
     shard = P.shard
     my_streams = shard.stream_ids(rank, ws, S)  # this GPU's block of independent streams
     pipe = pipeline.StreamPipeline(f"yolov8{a.scale}-small.yaml", S, (H, W), a.dtype, seed=0, device=local,
