@@ -36,6 +36,22 @@ namespace det {
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
+// Workgroup -> (pixel tile, channel group), XCD-aware.  The dispatcher deals workgroups (linear id,
+// x fastest) round-robin to the 8 XCDs, each with its own 4 MiB L2 (MI355X_MICROARCH.md, "Workgroup
+// dispatch, XCD placement").  With `on`, linear id L is mapped so that XCD L % 8 owns one contiguous
+// range of work items ordered (pixel tile major, channel group minor): sibling channel groups of a
+// pixel tile and neighbouring pixel tiles (the rows a 3x3 window shares) meet in one L2 instead of
+// being fetched once per XCD.  Placement only: the mapping is a bijection either way.
+__device__ __forceinline__ int2 xcd_block(int on) {
+  if (!on) return make_int2(blockIdx.x, blockIdx.y);
+  const int gx = gridDim.x, gy = gridDim.y, n = gx * gy;
+  const int L = blockIdx.y * gx + blockIdx.x;
+  const int k = L & 7, i = L >> 3, q = n >> 3, r = n & 7;
+  const int item = k * q + (k < r ? k : r) + i;
+  const int px = item / gy;
+  return make_int2(px, item - px * gy);
+}
+
 __device__ __forceinline__ float bf2f(unsigned short h) { return __uint_as_float((unsigned)h << 16); }
 __device__ __forceinline__ unsigned short f2bf(float f) {
   unsigned u = __float_as_uint(f);
@@ -435,6 +451,7 @@ struct TileArgs {
   int r_cstride, r_coff;
   int act;
   int single;  // whole weight slab LDS-resident
+  int xcd;     // XCD-aware workgroup placement (xcd_block)
 };
 
 template <class Tr, int NNT, int NPT, bool KSPLIT>
@@ -470,12 +487,13 @@ __global__ void __launch_bounds__(256) conv_tile_kernel(TileArgs a) {
   const typename Tr::T* gbase = (const typename Tr::T*)a.src[0].p;
   const long long gdelta = rfl64((const typename Tr::T*)a.src[1].p - gbase);
   const int tpi = a.tiles_x * a.tiles_y;
-  int t = blockIdx.x;
+  const int2 blk = xcd_block(a.xcd);
+  int t = blk.x;
   const int b = t / tpi;
   t -= b * tpi;
   const int ty0 = (t / a.tiles_x) * ROWS, tx0 = (t % a.tiles_x) * 16;
   const int iy0 = ty0 * a.stride - a.pad, ix0 = tx0 * a.stride - a.pad;
-  const int nt0 = blockIdx.y * NNT;
+  const int nt0 = blk.y * NNT;
   const int wrow = KSPLIT ? 0 : wave * NPT;  // first tile row of this wave
   uint4 wreg[WPT];
   auto fetch = [&](int k0) {  // global -> registers (stays in flight over the compute)
@@ -681,6 +699,7 @@ struct FastArgs {
   const void* res;
   int r_cstride, r_coff;
   int act;
+  int xcd;
 };
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
@@ -715,8 +734,9 @@ __global__ void __launch_bounds__(256) conv_fast_kernel(FastArgs a) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int kg = lane >> 4, col = lane & 15;
-  const int nt0 = blockIdx.y * NNT;
-  const int pbase = WS ? blockIdx.x * (16 * NPT) : (blockIdx.x * 4 + wave) * (16 * NPT);
+  const int2 blk = xcd_block(a.xcd);
+  const int nt0 = blk.y * NNT;
+  const int pbase = WS ? blk.x * (16 * NPT) : (blk.x * 4 + wave) * (16 * NPT);
   const int nk = a.k_steps;
   {
     int2 tv[2];  // <= 512 entries (nk <= 128) in one round trip
@@ -903,6 +923,7 @@ struct WideArgs {
   const void* res;
   int r_cstride, r_coff;
   int act;
+  int xcd;
   int dbg;  // diagnostics (YK_WIDE_DBG): 1 = no K loop, 2 = no epilogue stores, 4 = no staging
 };
 
@@ -931,9 +952,10 @@ __global__ void __launch_bounds__(64 * NW) conv_wide_kernel(WideArgs a) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int kg = lane >> 4, col = lane & 15;
-  const int nt0 = blockIdx.y * NNT;
+  const int2 blk = xcd_block(a.xcd);
+  const int nt0 = blk.y * NNT;
   const int nsp = a.B * a.tiles_y * a.tiles_x;
-  int t = blockIdx.x;
+  int t = blk.x;
   if (t >= nsp) return;
   const __amdgpu_buffer_rsrc_t xr = make_srd(a.arena, a.arena_bytes);
   // resident weights + table
@@ -1103,6 +1125,7 @@ struct InputArgs {
   int cout;        // physical output channels (multiple of 8), weights zero-padded
   void* dst;
   int d_cstride, d_coff;
+  int xcd;
 };
 
 template <class Tr>
@@ -1119,7 +1142,7 @@ __global__ void __launch_bounds__(256) conv_input_kernel(InputArgs a) {
   __shared__ float bs[kInputCoutMax];
   __shared__ float lut[256];
   const int tiles_x = (a.out_w + 15) / 16, tiles_y = (a.out_h + 15) / 16;
-  int t = blockIdx.x;
+  int t = xcd_block(a.xcd).x;
   const int b = t / (tiles_x * tiles_y);
   t -= b * tiles_x * tiles_y;
   const int ty0 = (t / tiles_x) * 16, tx0 = (t % tiles_x) * 16;
@@ -1193,7 +1216,7 @@ __global__ void __launch_bounds__(256) conv_input_mfma_kernel(InputArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int kg = lane >> 4, col = lane & 15;
   const int tiles_x = (a.out_w + 15) / 16, tiles_y = (a.out_h + 15) / 16;
-  int t = blockIdx.x;
+  int t = xcd_block(a.xcd).x;
   const int b = t / (tiles_x * tiles_y);
   t -= b * tiles_x * tiles_y;
   const int ty0 = (t / tiles_x) * 16, tx0 = (t % tiles_x) * 16;
@@ -1750,6 +1773,7 @@ struct yk_model {
   int2* ktab = nullptr;
   std::vector<int64_t> ktab_off;
   int* ltab = nullptr;                // conv_tile_kernel K-step tables (LDS element offsets)
+  int xcd = 1;                        // YK_XCD=0: plain blockIdx order (A/B of the XCD-aware placement)
   bool input_valu = false;            // YK_INPUT_VALU=1: f32-VALU first conv in the bf16 build too
   int wide_dbg = 0;                   // YK_WIDE_DBG: conv_wide_kernel diagnostics (never in production)
   std::vector<int64_t> ltab_off;
@@ -2219,6 +2243,7 @@ int launch_op(yk_model* m, const yk_op& op, const uint8_t* frames, int B, float 
         a.dst = img_ptr(m, op.dst.buf, op.out_h, op.out_w, op.dst.c_stride, b0);
         a.d_cstride = op.dst.c_stride;
         a.d_coff = op.dst.c_off;
+        a.xcd = m->xcd;
         const int tiles = B * ((op.out_h + 15) / 16) * ((op.out_w + 15) / 16);
         if (!Tr::kExact && op.cout <= 32 && !m->input_valu)
           hipLaunchKernelGGL(conv_input_mfma_kernel, dim3(tiles), dim3(256), 0, st, a);
@@ -2300,6 +2325,7 @@ int launch_op(yk_model* m, const yk_op& op, const uint8_t* frames, int B, float 
           w.r_coff = a.r_coff;
           w.act = a.act;
           w.dbg = m->wide_dbg;
+          w.xcd = m->xcd;
           if (cp.nnt == 2) {
             if (nw == 8) launch_wide_n<Tr, 2, 8>(w, wp.upt, wp.lds, st);
             else launch_wide_n<Tr, 2, 4>(w, wp.upt, wp.lds, st);
@@ -2346,6 +2372,7 @@ int launch_op(yk_model* m, const yk_op& op, const uint8_t* frames, int B, float 
           f.r_cstride = a.r_cstride;
           f.r_coff = a.r_coff;
           f.act = a.act;
+          f.xcd = m->xcd;
           launch_fast<Tr>(f, cp, st);
         } else if (cp.kind == CK_SPLITK) {
           launch_splitk<Tr>(a, cp, st);
@@ -2382,6 +2409,7 @@ int launch_op(yk_model* m, const yk_op& op, const uint8_t* frames, int B, float 
           t.r_coff = a.r_coff;
           t.act = a.act;
           t.single = tp.single ? 1 : 0;
+          t.xcd = m->xcd;
           launch_tile<Tr>(t, tp, B, st);
         } else {
           launch_conv<Tr>(a, st);
@@ -2826,6 +2854,7 @@ int yk_model_create(yk_ctx* ctx, const yk_model_desc* desc, const void* host_blo
   set_tile_attrs();
   if (const char* env = getenv("YK_CONV_DIRECT")) m->tiled = env[0] != '1';
   if (const char* env = getenv("YK_INPUT_VALU")) m->input_valu = env[0] == '1';
+  if (const char* env = getenv("YK_XCD")) m->xcd = atoi(env);
   if (const char* env = getenv("YK_WIDE_DBG")) m->wide_dbg = atoi(env);
   if (e == hipSuccess) e = build_ktabs(m, !(getenv("YK_CONV_FAST") && getenv("YK_CONV_FAST")[0] == '0'));
   if (e == hipSuccess) e = set_schedule(m, 1, 3);
