@@ -17,3 +17,10 @@ _, cc = dm.candidates(B)
 print("candidates per image", cc.tolist(), "kept", counts.cpu().tolist())
 prof = dm.profile(fr, reps=20)
 print("nms us", round(prof[-1][3] * 1e3, 2), "detect P2 us", [round(p[3] * 1e3, 2) for p in prof if "detect" in p[2]])
+if os.environ.get("YK_NMS_DBG"):
+    dets, counts = dm.detect(fr)
+    torch.cuda.synchronize()
+    ph = dets[:, -1].cpu()
+    for b in range(B):
+        print("image", b, "n", int(ph[b, 5]), "us: load", round(float(ph[b, 0]), 2), "sort", round(float(ph[b, 1]), 2),
+              "gather+mask", round(float(ph[b, 2]), 2), "walk", round(float(ph[b, 3]), 2), "out", round(float(ph[b, 4]), 2), "clock MHz", round(float(dets[b, -2, 0]), 0))

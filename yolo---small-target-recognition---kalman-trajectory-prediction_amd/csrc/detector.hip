@@ -1344,17 +1344,21 @@ __global__ void __launch_bounds__(256) sppf_lds_kernel(void* buf, int cstride, i
     *(float4*)(x + p * 8 + h) = make_float4(v[0], v[1], v[2], v[3]);
   }
   __syncthreads();
+  // Window indices are clamped to the plane instead of skipped: a clamped index is the border
+  // element, which lies inside the same window, and max is idempotent -- so the 13 reads of a
+  // window are branch-free and issue back to back.
   for (int i = threadIdx.x; i < HW * 8; i += blockDim.x) {
     const int p = i >> 3, c = i & 7, yy = p / W, xx = p - yy * W;
-    float m5 = -INFINITY, m9 = -INFINITY, m13 = -INFINITY;
-    for (int dx = -6; dx <= 6; ++dx) {
-      const int u = xx + dx;
-      if (u < 0 || u >= W) continue;
-      const float v = x[(yy * W + u) * 8 + c];
-      m13 = fmaxf(m13, v);
-      if (dx >= -4 && dx <= 4) m9 = fmaxf(m9, v);
-      if (dx >= -2 && dx <= 2) m5 = fmaxf(m5, v);
+    const float* row = x + yy * W * 8 + c;
+    float v[13];
+#pragma unroll
+    for (int d = 0; d < 13; ++d) {
+      const int u = min(max(xx + d - 6, 0), W - 1);
+      v[d] = row[u * 8];
     }
+    float m5 = fmaxf(fmaxf(fmaxf(v[4], v[5]), fmaxf(v[6], v[7])), v[8]);
+    float m9 = fmaxf(fmaxf(m5, fmaxf(v[2], v[3])), fmaxf(v[9], v[10]));
+    float m13 = fmaxf(fmaxf(m9, fmaxf(v[0], v[1])), fmaxf(v[11], v[12]));
     r5[i] = m5;
     r9[i] = m9;
     r13[i] = m13;
@@ -1363,15 +1367,23 @@ __global__ void __launch_bounds__(256) sppf_lds_kernel(void* buf, int cstride, i
   for (int i = threadIdx.x; i < HW * 2; i += blockDim.x) {
     const int p = i >> 1, h = (i & 1) * 4, yy = p / W, xx = p - yy * W;
     float m5[4], m9[4], m13[4];
+#pragma unroll
     for (int j = 0; j < 4; ++j) m5[j] = m9[j] = m13[j] = -INFINITY;
-    for (int dy = -6; dy <= 6; ++dy) {
-      const int v = yy + dy;
-      if (v < 0 || v >= H) continue;
-      const int q = (v * W + xx) * 8 + h;
-      for (int j = 0; j < 4; ++j) {
-        m13[j] = fmaxf(m13[j], r13[q + j]);
-        if (dy >= -4 && dy <= 4) m9[j] = fmaxf(m9[j], r9[q + j]);
-        if (dy >= -2 && dy <= 2) m5[j] = fmaxf(m5[j], r5[q + j]);
+#pragma unroll
+    for (int d = 0; d < 13; ++d) {
+      const int q = (min(max(yy + d - 6, 0), H - 1) * W + xx) * 8 + h;
+      const float4 a13 = *(const float4*)(r13 + q);
+      m13[0] = fmaxf(m13[0], a13.x); m13[1] = fmaxf(m13[1], a13.y);
+      m13[2] = fmaxf(m13[2], a13.z); m13[3] = fmaxf(m13[3], a13.w);
+      if (d >= 2 && d <= 10) {
+        const float4 a9 = *(const float4*)(r9 + q);
+        m9[0] = fmaxf(m9[0], a9.x); m9[1] = fmaxf(m9[1], a9.y);
+        m9[2] = fmaxf(m9[2], a9.z); m9[3] = fmaxf(m9[3], a9.w);
+      }
+      if (d >= 4 && d <= 8) {
+        const float4 a5 = *(const float4*)(r5 + q);
+        m5[0] = fmaxf(m5[0], a5.x); m5[1] = fmaxf(m5[1], a5.y);
+        m5[2] = fmaxf(m5[2], a5.z); m5[3] = fmaxf(m5[3], a5.w);
       }
     }
     T* o = base + (size_t)p * cstride + h;
@@ -1481,6 +1493,9 @@ __global__ void __launch_bounds__(256) detect_kernel(DetArgs a) {
 }
 
 // ---------------------------------------------------------------- NMS + scale/clip
+// IoU decisions must round like the reference's separate torch ops (inter = w * h rounded, then
+// (area_i + area_j) - inter): no a*b+c contraction anywhere in the NMS code.
+#pragma clang fp contract(off)
 constexpr int NMS_NT = 512;
 constexpr int NMS_LDS_N = 2048;   // candidates sorted in LDS; more -> global scratch
 constexpr int NMS_MASK_N = 512;   // bitmask suppression in LDS up to this many candidates
@@ -1506,6 +1521,7 @@ struct NmsArgs {
   float* dets;                  // [B][max_det][6]
   int* counts;
   float pad_x, pad_y, gain, clip_w, clip_h;
+  int dbg;  // YK_NMS_DBG=1: phase times (us, s_memrealtime) in dets[b][max_det-1] (diagnostics only)
 };
 
 __device__ __forceinline__ void bitonic_sort(unsigned long long* k, int n2) {
@@ -1526,12 +1542,91 @@ __device__ __forceinline__ void bitonic_sort(unsigned long long* k, int n2) {
   }
 }
 
+// the same network carrying a 32-bit payload (the candidate's slot) with each key
+__device__ __forceinline__ void bitonic_sort_kv(unsigned long long* k, int* pay, int n2) {
+  for (int size = 2; size <= n2; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int i = threadIdx.x; i < (n2 >> 1); i += blockDim.x) {
+        const int lo = 2 * i - (i & (stride - 1));
+        const int hi = lo + stride;
+        const bool up = (lo & size) == 0;
+        const unsigned long long a = k[lo], b = k[hi];
+        if ((a > b) == up) {
+          const int pa = pay[lo];
+          k[lo] = b;
+          k[hi] = a;
+          pay[lo] = pay[hi];
+          pay[hi] = pa;
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
 // bits of word `w` (candidates w*64 .. w*64+63) that lie strictly after candidate i
 __device__ __forceinline__ unsigned long long after_mask(int w, int i) {
   const int base = w * 64;
   if (i < base) return ~0ull;
   if (i >= base + 63) return 0ull;
   return ~0ull << (i - base + 1);
+}
+
+// The greedy walk over precomputed masks (one wave).  Both mask rows of the picked box are read
+// together, so an iteration waits on one LDS round trip.
+__device__ int nms_walk(int n, int max_det, const unsigned long long* sup, const unsigned long long* ovl, int* keep,
+                        int* k_out) {
+  const int W = (n + 63) / 64;
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    unsigned long long R = ~0ull;  // removed (or beyond n)
+    if (lane < W) {
+      const int rem = n - lane * 64;
+      R = rem >= 64 ? 0ull : ~0ull << rem;
+    }
+    int k = 0, i = -1;
+    while (k < max_det) {
+      const unsigned long long cand = lane < W ? (~R & after_mask(lane, i)) : 0ull;
+      const unsigned long long bal = __ballot(cand != 0ull);
+      if (bal == 0ull) break;
+      const int fl = __ffsll((long long)bal) - 1;
+      // fl is wave-uniform (from a ballot): two v_readlane instead of an LDS permute
+      const unsigned long long word = ((unsigned long long)__builtin_amdgcn_readlane((unsigned)(cand >> 32), fl) << 32) |
+                                      __builtin_amdgcn_readlane((unsigned)cand, fl);
+      i = fl * 64 + __ffsll((long long)word) - 1;
+      const unsigned long long orow = lane < W ? ovl[i * NMS_W + lane] : 0ull;
+      const unsigned long long srow = lane < W ? sup[i * NMS_W + lane] : 0ull;
+      if (lane == 0) keep[k] = i;
+      ++k;
+      if (k >= max_det) break;
+      const unsigned long long o = orow & ~R;
+      if (__ballot(o != 0ull) == 0ull) {
+        // keep every remaining candidate after i, in order
+        const unsigned long long rem = lane < W ? (~R & after_mask(lane, i)) : 0ull;
+        const int c = __popcll(rem);
+        int incl = c;
+        for (int d = 1; d < 64; d <<= 1) {
+          const int v = __shfl_up(incl, d);
+          if (lane >= d) incl += v;
+        }
+        int r = k + incl - c;
+        unsigned long long bits = rem;
+        while (bits) {
+          const int bpos = __ffsll((long long)bits) - 1;
+          bits &= bits - 1;
+          if (r < max_det) keep[r] = lane * 64 + bpos;
+          ++r;
+        }
+        const int total = __shfl(incl, 63);
+        k = k + total < max_det ? k + total : max_det;
+        break;
+      }
+      R |= srow;
+    }
+    if (lane == 0) *k_out = k;
+  }
+  __syncthreads();
+  return *k_out;
 }
 
 // TorchNMS.nms on one image's sorted candidates as bitmasks (utils/nms.py:237-304):
@@ -1563,47 +1658,85 @@ __device__ int nms_bitmask(const float* box, int n, float thr, int max_det, unsi
     ovl[i * NMS_W + w] = om;
   }
   __syncthreads();
+  return nms_walk(n, max_det, sup, ovl, keep, k_out);
+}
+
+// TorchNMS.nms (utils/nms.py:237-304) on up to NMS_GW*64 sorted candidates by ONE wave, with no
+// LDS in the loop: lane l holds columns w*64 + l (box, area, alive flag) in registers.  Each
+// iteration keeps the first alive column i (ballots), fetches box i by v_readlane, and tests it
+// against every alive column: all intersections zero -> keep every alive column in order and stop
+// (:291-296); otherwise drop the columns with !(iou <= thr).  Work = kept x n pairs instead of the
+// n^2/2 of the mask build, on one SIMD.
+constexpr int NMS_GW = 4;
+__device__ int nms_greedy_wave(const float4* bx, const float* ar, int n, float thr, int max_det, int* keep,
+                               int* k_out) {
   if (threadIdx.x < 64) {
     const int lane = threadIdx.x;
-    unsigned long long R = ~0ull;  // removed (or beyond n)
-    if (lane < W) {
-      const int rem = n - lane * 64;
-      R = rem >= 64 ? 0ull : ~0ull << rem;
+    const int W = (n + 63) / 64;
+    float4 bj[NMS_GW];
+    float aj[NMS_GW];
+    bool al[NMS_GW];
+#pragma unroll
+    for (int w = 0; w < NMS_GW; ++w) {
+      const int j = w * 64 + lane;
+      al[w] = j < n;
+      bj[w] = al[w] ? bx[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+      aj[w] = al[w] ? ar[j] : 0.f;
     }
-    int k = 0, i = -1;
+    int k = 0;
     while (k < max_det) {
-      const unsigned long long cand = lane < W ? (~R & after_mask(lane, i)) : 0ull;
-      const unsigned long long bal = __ballot(cand != 0ull);
-      if (bal == 0ull) break;
-      const int fl = __ffsll((long long)bal) - 1;
-      const unsigned long long word = __shfl(cand, fl);
-      i = fl * 64 + __ffsll((long long)word) - 1;
+      int i = -1;
+#pragma unroll
+      for (int w = 0; w < NMS_GW; ++w) {
+        const unsigned long long b = __ballot(al[w]);
+        if (i < 0 && b != 0ull) i = w * 64 + __ffsll((long long)b) - 1;
+      }
+      if (i < 0) break;
       if (lane == 0) keep[k] = i;
       ++k;
       if (k >= max_det) break;
-      const unsigned long long o = lane < W ? (ovl[i * NMS_W + lane] & ~R) : 0ull;
-      if (__ballot(o != 0ull) == 0ull) {
-        // keep every remaining candidate after i, in order
-        const unsigned long long rem = lane < W ? (~R & after_mask(lane, i)) : 0ull;
-        const int c = __popcll(rem);
-        int incl = c;
-        for (int d = 1; d < 64; d <<= 1) {
-          const int v = __shfl_up(incl, d);
-          if (lane >= d) incl += v;
+      const int wi = i >> 6, li = i & 63;
+      float4 bi = make_float4(0.f, 0.f, 0.f, 0.f);
+      float ai = 0.f;
+#pragma unroll
+      for (int w = 0; w < NMS_GW; ++w)
+        if (w == wi) {
+          bi.x = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(bj[w].x), li));
+          bi.y = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(bj[w].y), li));
+          bi.z = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(bj[w].z), li));
+          bi.w = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(bj[w].w), li));
+          ai = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(aj[w]), li));
+          if (lane == li) al[w] = false;
         }
-        int r = k + incl - c;
-        unsigned long long bits = rem;
-        while (bits) {
-          const int bpos = __ffsll((long long)bits) - 1;
-          bits &= bits - 1;
-          if (r < max_det) keep[r] = lane * 64 + bpos;
-          ++r;
+      bool any = false;
+      bool sup[NMS_GW];
+#pragma unroll
+      for (int w = 0; w < NMS_GW; ++w) {
+        sup[w] = false;
+        if (w < W && al[w]) {
+          const float ww = fmaxf(fminf(bi.z, bj[w].z) - fmaxf(bi.x, bj[w].x), 0.f);
+          const float hh = fmaxf(fminf(bi.w, bj[w].w) - fmaxf(bi.y, bj[w].y), 0.f);
+          const float inter = ww * hh;
+          any |= inter != 0.f;
+          const float iou = inter / (ai + aj[w] - inter);
+          sup[w] = !(iou <= thr);
         }
-        const int total = __shfl(incl, 63);
-        k = k + total < max_det ? k + total : max_det;
+      }
+      if (__ballot(any) == 0ull) {
+        // keep every alive column, in order
+        int base = k;
+#pragma unroll
+        for (int w = 0; w < NMS_GW; ++w) {
+          const unsigned long long b = __ballot(al[w]);
+          const int r = base + __popcll(b & ((1ull << lane) - 1ull));
+          if (al[w] && r < max_det) keep[r] = w * 64 + lane;
+          base += __popcll(b);
+        }
+        k = base < max_det ? base : max_det;
         break;
       }
-      if (lane < W) R |= sup[i * NMS_W + lane];
+#pragma unroll
+      for (int w = 0; w < NMS_GW; ++w) al[w] = al[w] && !sup[w];
     }
     if (lane == 0) *k_out = k;
   }
@@ -1611,11 +1744,171 @@ __device__ int nms_bitmask(const float* box, int n, float thr, int max_det, unsi
   return *k_out;
 }
 
+// Candidate counts up to NMS_MASK_N (the common case): the rows are read from HBM once, in one
+// coalesced pass, and everything after -- sort (key + slot payload), box gather, masks, walk,
+// output rows -- works on LDS copies.  Same arithmetic as the general path below.
+constexpr size_t NS_PAY = (size_t)NMS_MASK_N * 8;
+constexpr size_t NS_STG = NS_PAY + (size_t)NMS_MASK_N * 8;  // slot by input index, then by sorted position
+constexpr size_t NS_BX = NS_STG + (size_t)NMS_MASK_N * 20;
+constexpr size_t NS_AR = NS_BX + (size_t)NMS_MASK_N * 16;
+constexpr size_t NS_KEEP = NS_AR + (size_t)NMS_MASK_N * 4;
+constexpr size_t NS_MISC = NS_KEEP + (size_t)NMS_MASK_N * 4;
+constexpr size_t NS_MASK = NS_MISC + 64;
+static_assert(NS_BX % 16 == 0 && NS_MASK % 8 == 0, "NMS LDS alignment");
+static_assert(NS_MASK + (size_t)NMS_MASK_N * NMS_W * 16 <= NMS_LDS, "NMS small-path LDS");
+
+__device__ void nms_small(const NmsArgs& a, int b, int n, unsigned char* smem) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const float* cand = a.cand + (size_t)b * a.cap * 6;
+  unsigned long long* keys = (unsigned long long*)smem;
+  int* pay = (int*)(smem + NS_PAY);
+  float* stg = (float*)(smem + NS_STG);
+  float4* bx = (float4*)(smem + NS_BX);
+  float* ar = (float*)(smem + NS_AR);
+  int* keep = (int*)(smem + NS_KEEP);
+  int* misc = (int*)(smem + NS_MISC);
+  unsigned long long* sup = (unsigned long long*)(smem + NS_MASK);
+  unsigned long long* ovl = sup + NMS_MASK_N * NMS_W;
+  unsigned long long t[6], c0 = 0;
+  if (a.dbg) {
+    t[0] = __builtin_amdgcn_s_memrealtime();
+    c0 = __builtin_amdgcn_s_memtime();
+  }
+  int n2 = 1;
+  while (n2 < n) n2 <<= 1;
+  for (int i = tid; i < n2; i += NMS_NT) {
+    unsigned long long k = ~0ull;
+    if (i < n) {
+      const float2* c = (const float2*)(cand + (size_t)i * 6);  // rows are 8-byte aligned
+      const float2 v01 = c[0], v23 = c[1], v45 = c[2];
+      stg[i * 5 + 0] = v01.x;
+      stg[i * 5 + 1] = v01.y;
+      stg[i * 5 + 2] = v23.x;
+      stg[i * 5 + 3] = v23.y;
+      stg[i * 5 + 4] = v45.x;
+      k = ((unsigned long long)(0xffffffffu - __float_as_uint(v45.x)) << 32) | (unsigned)__float_as_int(v45.y);
+    }
+    keys[i] = k;
+  }
+  __syncthreads();
+  if (a.dbg) t[1] = __builtin_amdgcn_s_memrealtime();
+  // rank sort: keys are unique (one candidate per anchor), so a candidate's sorted position is
+  // the number of smaller keys -- no barrier stages; every lane of a wave reads the same key
+  // (an LDS broadcast)
+  if (tid < n) {
+    const unsigned long long mine = keys[tid];
+    int r = 0;
+#pragma unroll 8
+    for (int j = 0; j < n; ++j) r += keys[j] < mine ? 1 : 0;
+    pay[NMS_MASK_N + r] = tid;  // second half of the payload area: slot at sorted position r
+  }
+  __syncthreads();
+  if (a.dbg) t[2] = __builtin_amdgcn_s_memrealtime();
+  if (n > a.max_nms) n = a.max_nms;  // nms.py:138-142
+  const int* spay = pay + NMS_MASK_N;
+  for (int i = tid; i < n; i += NMS_NT) {
+    const int s = spay[i];
+    const float x1 = stg[s * 5], y1 = stg[s * 5 + 1], x2 = stg[s * 5 + 2], y2 = stg[s * 5 + 3];
+    bx[i] = make_float4(x1, y1, x2, y2);
+    ar[i] = (x2 - x1) * (y2 - y1);
+  }
+  __syncthreads();
+  int k;
+  if (n <= NMS_GW * 64) {
+    if (a.dbg) t[3] = __builtin_amdgcn_s_memrealtime();
+    k = nms_greedy_wave(bx, ar, n, a.iou, a.max_det, keep, misc + 15);
+    if (a.dbg) t[4] = __builtin_amdgcn_s_memrealtime();
+  } else {
+  // sup / ovl words: each wave holds every column box in registers (lane = column within a
+  // word), then per row i one broadcast read of box i and W ballots form the row's words
+  const int W = (n + 63) / 64;
+  const float thr = a.iou;
+  float4 bj[NMS_W];
+  float aj[NMS_W];
+#pragma unroll
+  for (int w = 0; w < NMS_W; ++w) {
+    const int j = w * 64 + lane;
+    bj[w] = j < n ? bx[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+    aj[w] = j < n ? ar[j] : 0.f;
+  }
+  for (int i = wave; i < n; i += NMS_NT / 64) {
+    const float4 bi = bx[i];
+    const float ai = ar[i];
+    unsigned long long smw = 0ull, omw = 0ull;  // lane w keeps word w
+    const int w0 = i >> 6;                       // words below hold only columns j <= i: zero
+#pragma unroll
+    for (int w = 0; w < NMS_W; ++w) {
+      if (w >= W) break;
+      if (w < w0) continue;
+      const int j = w * 64 + lane;
+      bool sb = false, ob = false;
+      if (j > i && j < n) {
+        const float ww = fmaxf(fminf(bi.z, bj[w].z) - fmaxf(bi.x, bj[w].x), 0.f);
+        const float hh = fmaxf(fminf(bi.w, bj[w].w) - fmaxf(bi.y, bj[w].y), 0.f);
+        const float inter = ww * hh;
+        const float un = ai + aj[w] - inter;
+        // iou <= thr decided on v_rcp (~1 ulp) unless within 1e-5 relative of thr; the rest (and a
+        // zero or tiny union, where iou is NaN or inf) take the exact IEEE division
+        const float q = inter * __builtin_amdgcn_rcpf(un);
+        if (un > 1e-30f && fabsf(q - thr) > 1e-5f * thr) {
+          sb = q > thr;
+        } else {
+          const float iou = inter / un;
+          sb = !(iou <= thr);
+        }
+        ob = inter != 0.f;
+      }
+      const unsigned long long sm = __ballot(sb), om = __ballot(ob);
+      if (lane == w) {
+        smw = sm;
+        omw = om;
+      }
+    }
+    if (lane < W) {
+      sup[i * NMS_W + lane] = smw;
+      ovl[i * NMS_W + lane] = omw;
+    }
+  }
+  __syncthreads();
+  if (a.dbg) t[3] = __builtin_amdgcn_s_memrealtime();
+  k = nms_walk(n, a.max_det, sup, ovl, keep, misc + 15);
+  if (a.dbg) t[4] = __builtin_amdgcn_s_memrealtime();
+  }
+  // outputs: x[i] rows, then scale_boxes (x - pad) / gain and clip (ops.py:105-184)
+  for (int r = tid; r < k; r += NMS_NT) {
+    const float* c = stg + pay[NMS_MASK_N + keep[r]] * 5;
+    float* o = a.dets + ((size_t)b * a.max_det + r) * 6;
+    const float x1 = (c[0] - a.pad_x) / a.gain, y1 = (c[1] - a.pad_y) / a.gain;
+    const float x2 = (c[2] - a.pad_x) / a.gain, y2 = (c[3] - a.pad_y) / a.gain;
+    o[0] = fminf(fmaxf(x1, 0.f), a.clip_w);
+    o[1] = fminf(fmaxf(y1, 0.f), a.clip_h);
+    o[2] = fminf(fmaxf(x2, 0.f), a.clip_w);
+    o[3] = fminf(fmaxf(y2, 0.f), a.clip_h);
+    o[4] = c[4];
+    o[5] = 0.f;
+  }
+  if (tid == 0) a.counts[b] = k;
+  if (a.dbg) {
+    __syncthreads();
+    t[5] = __builtin_amdgcn_s_memrealtime();
+    if (tid == 0) {
+      float* o = a.dets + ((size_t)b * a.max_det + a.max_det - 1) * 6;
+      for (int q = 0; q < 5; ++q) o[q] = (float)(t[q + 1] - t[q]) * 0.01f;  // 100 MHz counter -> us
+      o[5] = (float)n;
+      o[-6] = (float)(__builtin_amdgcn_s_memtime() - c0) / ((float)(t[5] - t[0]) * 0.01f);  // core MHz
+    }
+  }
+}
+
 __global__ void __launch_bounds__(NMS_NT) nms_kernel(NmsArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int b = blockIdx.x, tid = threadIdx.x;
   int n = a.cand_count[b];
   if (n > a.cap) n = a.cap;
+  if (n <= NMS_MASK_N) {
+    nms_small(a, b, n, smem);
+    return;
+  }
   const float* cand = a.cand + (size_t)b * a.cap * 6;
   const bool in_lds = n <= NMS_LDS_N;
   int n2 = 1;
@@ -1725,6 +2018,8 @@ __global__ void __launch_bounds__(NMS_NT) nms_kernel(NmsArgs a) {
   if (tid == 0) a.counts[b] = k;
 }
 
+#pragma clang fp contract(fast)
+
 size_t nms_lds_bytes() { return NMS_LDS; }
 
 }  // namespace det
@@ -1775,6 +2070,7 @@ struct yk_model {
   int* ltab = nullptr;                // conv_tile_kernel K-step tables (LDS element offsets)
   int xcd = 1;                        // YK_XCD=0: plain blockIdx order (A/B of the XCD-aware placement)
   bool input_valu = false;            // YK_INPUT_VALU=1: f32-VALU first conv in the bf16 build too
+  int nms_dbg = 0;                    // YK_NMS_DBG: nms_kernel phase timing (never in production)
   int wide_dbg = 0;                   // YK_WIDE_DBG: conv_wide_kernel diagnostics (never in production)
   std::vector<int64_t> ltab_off;
   char* arena = nullptr;      // every activation buffer (bufs[i] point into it)
@@ -2678,6 +2974,7 @@ int launch_nms(yk_model* m, int B, float iou, int max_det, float* dets, int32_t*
   a.gain = 1.0f;
   a.clip_w = (float)D.frame_w;
   a.clip_h = (float)D.frame_h;
+  a.dbg = m->nms_dbg;
   hipLaunchKernelGGL(nms_kernel, dim3(B), dim3(NMS_NT), nms_lds_bytes(), st, a);
   YK_HIP(hipGetLastError());
   return YK_OK;
@@ -2856,6 +3153,7 @@ int yk_model_create(yk_ctx* ctx, const yk_model_desc* desc, const void* host_blo
   if (const char* env = getenv("YK_INPUT_VALU")) m->input_valu = env[0] == '1';
   if (const char* env = getenv("YK_XCD")) m->xcd = atoi(env);
   if (const char* env = getenv("YK_WIDE_DBG")) m->wide_dbg = atoi(env);
+  if (const char* env = getenv("YK_NMS_DBG")) m->nms_dbg = atoi(env);
   if (e == hipSuccess) e = build_ktabs(m, !(getenv("YK_CONV_FAST") && getenv("YK_CONV_FAST")[0] == '0'));
   if (e == hipSuccess) e = set_schedule(m, 1, 3);
   if (e != hipSuccess) {
