@@ -236,7 +236,7 @@ def test_bf16_first_conv_mfma_close_to_oracle(frame_hw):
 
 
 
-@pytest.mark.parametrize("count", [150, 300, 1200, 3000])
+@pytest.mark.parametrize("count", [40, 100, 150, 230, 300, 1200, 3000])
 def test_fp32_nms_paths_match_oracle(count):
     """nms_kernel's paths -- one-wave register greedy loop (<= 256 candidates), all-LDS bitmask (<= 512), LDS-sorted general loop
     (<= 2048) and global-scratch sort (> 2048) -- against the oracle's NMS (torch_nms with the

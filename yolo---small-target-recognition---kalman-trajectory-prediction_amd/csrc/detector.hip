@@ -1668,16 +1668,17 @@ __device__ int nms_bitmask(const float* box, int n, float thr, int max_det, unsi
 // (:291-296); otherwise drop the columns with !(iou <= thr).  Work = kept x n pairs instead of the
 // n^2/2 of the mask build, on one SIMD.
 constexpr int NMS_GW = 4;
+template <int GW>
 __device__ int nms_greedy_wave(const float4* bx, const float* ar, int n, float thr, int max_det, int* keep,
                                int* k_out) {
   if (threadIdx.x < 64) {
     const int lane = threadIdx.x;
     const int W = (n + 63) / 64;
-    float4 bj[NMS_GW];
-    float aj[NMS_GW];
-    bool al[NMS_GW];
+    float4 bj[GW];
+    float aj[GW];
+    bool al[GW];
 #pragma unroll
-    for (int w = 0; w < NMS_GW; ++w) {
+    for (int w = 0; w < GW; ++w) {
       const int j = w * 64 + lane;
       al[w] = j < n;
       bj[w] = al[w] ? bx[j] : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -1687,7 +1688,7 @@ __device__ int nms_greedy_wave(const float4* bx, const float* ar, int n, float t
     while (k < max_det) {
       int i = -1;
 #pragma unroll
-      for (int w = 0; w < NMS_GW; ++w) {
+      for (int w = 0; w < GW; ++w) {
         const unsigned long long b = __ballot(al[w]);
         if (i < 0 && b != 0ull) i = w * 64 + __ffsll((long long)b) - 1;
       }
@@ -1699,7 +1700,7 @@ __device__ int nms_greedy_wave(const float4* bx, const float* ar, int n, float t
       float4 bi = make_float4(0.f, 0.f, 0.f, 0.f);
       float ai = 0.f;
 #pragma unroll
-      for (int w = 0; w < NMS_GW; ++w)
+      for (int w = 0; w < GW; ++w)
         if (w == wi) {
           bi.x = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(bj[w].x), li));
           bi.y = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(bj[w].y), li));
@@ -1709,9 +1710,9 @@ __device__ int nms_greedy_wave(const float4* bx, const float* ar, int n, float t
           if (lane == li) al[w] = false;
         }
       bool any = false;
-      bool sup[NMS_GW];
+      bool sup[GW];
 #pragma unroll
-      for (int w = 0; w < NMS_GW; ++w) {
+      for (int w = 0; w < GW; ++w) {
         sup[w] = false;
         if (w < W && al[w]) {
           const float ww = fmaxf(fminf(bi.z, bj[w].z) - fmaxf(bi.x, bj[w].x), 0.f);
@@ -1726,7 +1727,7 @@ __device__ int nms_greedy_wave(const float4* bx, const float* ar, int n, float t
         // keep every alive column, in order
         int base = k;
 #pragma unroll
-        for (int w = 0; w < NMS_GW; ++w) {
+        for (int w = 0; w < GW; ++w) {
           const unsigned long long b = __ballot(al[w]);
           const int r = base + __popcll(b & ((1ull << lane) - 1ull));
           if (al[w] && r < max_det) keep[r] = w * 64 + lane;
@@ -1736,7 +1737,7 @@ __device__ int nms_greedy_wave(const float4* bx, const float* ar, int n, float t
         break;
       }
 #pragma unroll
-      for (int w = 0; w < NMS_GW; ++w) al[w] = al[w] && !sup[w];
+      for (int w = 0; w < GW; ++w) al[w] = al[w] && !sup[w];
     }
     if (lane == 0) *k_out = k;
   }
@@ -1816,7 +1817,11 @@ __device__ void nms_small(const NmsArgs& a, int b, int n, unsigned char* smem) {
   int k;
   if (n <= NMS_GW * 64) {
     if (a.dbg) t[3] = __builtin_amdgcn_s_memrealtime();
-    k = nms_greedy_wave(bx, ar, n, a.iou, a.max_det, keep, misc + 15);
+    // specialised on the live word count: the unrolled word loops carry no dead blocks
+    if (n <= 64) k = nms_greedy_wave<1>(bx, ar, n, a.iou, a.max_det, keep, misc + 15);
+    else if (n <= 128) k = nms_greedy_wave<2>(bx, ar, n, a.iou, a.max_det, keep, misc + 15);
+    else if (n <= 192) k = nms_greedy_wave<3>(bx, ar, n, a.iou, a.max_det, keep, misc + 15);
+    else k = nms_greedy_wave<NMS_GW>(bx, ar, n, a.iou, a.max_det, keep, misc + 15);
     if (a.dbg) t[4] = __builtin_amdgcn_s_memrealtime();
   } else {
   // sup / ovl words: each wave holds every column box in registers (lane = column within a
