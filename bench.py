@@ -28,7 +28,7 @@ sys.path.insert(0, REPO)
 PKG = "yolo---small-target-recognition---kalman-trajectory-prediction_amd"
 
 METRIC = "end-to-end frames/sec (640×512 YOLOv8s+P2, 64 tracks) at 1/2/4/8 GPUs"
-PEAK = {"bf16": 2500.0, "fp32": 157.3}  # dense MFMA TFLOP/s (MI355X_MICROARCH.md)
+PEAK = {"bf16": 2500.0, "fp32": 157.3, "fp8": 5000.0}  # dense MFMA TFLOP/s (MI355X_MICROARCH.md)
 HBM_PEAK = 8000.0  # GB/s
 
 
@@ -45,7 +45,8 @@ def parse():
     ap.add_argument("--targets", type=int, default=None,
                     help="synthetic targets per stream (22 -> ~64 live tracks/stream: the planted detector plus lost-track retention)")
     ap.add_argument("--scale", default="s", choices=["n", "s"])
-    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--dtype", default=None, choices=["bf16", "fp32", "fp8"],
+                    help="activation/weight dtype (default: fp8 for --config 5, else bf16)")
     ap.add_argument("--frames", type=int, default=120, help="pre-rendered frames per stream (cycled)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--frame-copy", default="copy", choices=["copy", "none"],
@@ -186,6 +187,8 @@ def main():
     pipeline = import_module(PKG + ".pipeline")
     if a.streams is None:
         a.streams = 1 if a.config == 2 else 8
+    if a.dtype is None:
+        a.dtype = "fp8" if a.config == 5 else "bf16"
     S = a.streams
     H, W, imgsz, max_tracks = (1024, 1280, 1280, 2048) if a.config == 5 else (512, 640, 640, 512)
     if a.targets is None:

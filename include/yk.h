@@ -184,7 +184,7 @@ int yk_track_create(yk_tracker* trk, int stream_index, const double* host_bbox, 
  * (utils/ops.py:105-184).  The host builds the program (parse_model rules + weight
  * packing, see arch.py / model.py); the library executes it.
  */
-enum yk_act_dtype { YK_ACT_BF16 = 0, YK_ACT_F32 = 1 };
+enum yk_act_dtype { YK_ACT_BF16 = 0, YK_ACT_F32 = 1, YK_ACT_FP8 = 2 };  /* FP8: OCP e4m3 activations + weights */
 enum yk_op_kind {
   YK_K_CONV_INPUT = 0, /* first conv, reads uint8 BGR frames (fused letterbox/RGB//255)    */
   YK_K_CONV = 1,       /* implicit-GEMM conv (+bias, SiLU, residual, concat/upsample read)   */
@@ -205,14 +205,15 @@ typedef struct {
   int32_t ksize, stride, act; /* act: 0 none, 1 SiLU                                   */
   int32_t n_src;
   yk_view src[2];
-  int32_t src_ch[2];          /* physical channels of each source (multiples of 8)     */
+  int32_t src_ch[2];          /* physical channels of each source (multiples of 8; FP8 16) */
   yk_view dst;
   int32_t cout;               /* physical output channels written                      */
   int32_t has_res;
   yk_view res;                /* residual added after the activation (Bottleneck add)  */
   int32_t out_h, out_w;
   int32_t k_steps, n_tiles;   /* packed weights: [n_tiles][k_steps][64 lanes][16 B]    */
-  int64_t w_off, b_off, t_off;/* blob offsets: packed weights, f32 bias, int32 K-chunk table */
+  int64_t w_off, b_off, t_off;/* blob offsets: packed weights, f32 bias (FP8: then f32 per-  *
+                               * channel dequant scales), int32 K-chunk table             */
   /* YK_K_DETECT */
   int32_t det_stride;         /* level stride in input pixels                           */
   int32_t det_anchor_off;     /* index of this level's first anchor                     */

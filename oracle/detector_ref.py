@@ -241,3 +241,83 @@ def predict(det: RefDetector, frames, conf=0.25, iou=0.7, max_det=300, imgsz=640
     y, _ = det.forward(im)
     out = non_max_suppression(y, conf, iou, max_det)
     return [scale_clip(p, im.shape[2:], frames[0].shape[:2]) for p in out], y
+
+
+# ---------------------------------------------------------------- FP8 build restatement
+def e4m3(t):
+    """Round to OCP e4m3 (float8_e4m3fn), saturating at +-448, as the FP8 build stores
+    every activation; returns float32 values."""
+    return t.float().clamp(-448.0, 448.0).to(torch.float8_e4m3fn).float()
+
+
+def fp8_weights(w):
+    """Per-output-channel e4m3 weights of the FP8 build: scale = 448 / max|w[o]| (f32),
+    Wq = e4m3(w * scale), dequant dq = 1 / scale (f32).  Returns (Wq, dq)."""
+    amax = w.abs().flatten(1).amax(1)
+    # true f32 divisions (a python scalar over a tensor is reciprocal() * scalar in torch)
+    scale = torch.where(amax > 0, torch.full_like(amax, 448.0) / amax.clamp_min(1e-30), torch.ones_like(amax)).float()
+    dq = (torch.ones_like(scale) / scale).float()
+    return e4m3(w * scale.view(-1, 1, 1, 1)), dq
+
+
+class RefDetectorFP8(RefDetector):
+    """The reference graph (same modules as RefDetector) in the FP8 build's arithmetic, the
+    checker for the MI355X fp8 path (BASELINE config 5).  Not a reference-parity claim: the
+    reference is fp32; this restates the quantisation the fp8 build applies on top of it:
+
+      * conv weights: per-output-channel e4m3 (fp8_weights), y = conv(x, Wq) * dq + b;
+      * every stored activation (conv output after SiLU and the Bottleneck add) is e4m3;
+      * layer 0 keeps the bf16 first conv of the production build (raw uint8 values x
+        bf16(w * (1/255)), f32 accumulate), its output stored e4m3;
+      * Detect: box 1x1 with e4m3 weights (not stored: f32 logits), class 1x1 in f32;
+        DFL / dist2bbox / sigmoid as RefDetector.
+    Products of e4m3 values are exact in f32, so the GPU and this restatement differ only in
+    f32 summation order and the SiLU's exp/rcp, which moves a few values across an e4m3
+    rounding boundary per layer."""
+
+    def __init__(self, layers, sd, strides):
+        super().__init__(layers, sd, strides)
+        self._q = {}
+
+    def _qw(self, p):
+        if p not in self._q:
+            if p not in self._w:
+                self._w[p] = fuse(self.sd, p)
+            w, b = self._w[p]
+            wq, dq = fp8_weights(w)
+            self._q[p] = (wq, dq, b)
+        return self._q[p]
+
+    def conv(self, x, p, k, s, act=True, res=None):
+        if p == "model.0":
+            w, b = self._w.setdefault(p, fuse(self.sd, p))
+            raw = torch.round(x * 255.0)
+            w0 = (w * torch.tensor(1.0 / 255.0, dtype=torch.float32)).to(torch.bfloat16).float()
+            y = F.conv2d(raw, w0, b, s, k // 2)
+        else:
+            wq, dq, b = self._qw(p)
+            y = F.conv2d(x, wq, None, s, k // 2) * dq.view(1, -1, 1, 1) + b.view(1, -1, 1, 1)
+        if act:
+            y = F.silu(y)
+        if res is not None:
+            y = res + y
+        return e4m3(y)
+
+    def c2f(self, x, p, n, shortcut, c):
+        y = list(self.conv(x, f"{p}.cv1", 1, 1).chunk(2, 1))
+        for j in range(n):
+            t = self.conv(y[-1], f"{p}.m.{j}.cv1", 3, 1)
+            y.append(self.conv(t, f"{p}.m.{j}.cv2", 3, 1, res=y[-1] if shortcut else None))
+        return self.conv(torch.cat(y, 1), f"{p}.cv2", 1, 1)
+
+    def detect(self, xs, p, nc):
+        outs = []
+        for li, x in enumerate(xs):
+            a = self.conv(self.conv(x, f"{p}.cv2.{li}.0", 3, 1), f"{p}.cv2.{li}.1", 3, 1)
+            wb, bb = self.sd[f"{p}.cv2.{li}.2.weight"].float(), self.sd[f"{p}.cv2.{li}.2.bias"].float()
+            wq, dq = fp8_weights(wb)
+            a = F.conv2d(a, wq) * dq.view(1, -1, 1, 1) + bb.view(1, -1, 1, 1)
+            c = self.conv(self.conv(x, f"{p}.cv3.{li}.0", 3, 1), f"{p}.cv3.{li}.1", 3, 1)
+            c = F.conv2d(c, self.sd[f"{p}.cv3.{li}.2.weight"].float(), self.sd[f"{p}.cv3.{li}.2.bias"].float())
+            outs.append(torch.cat((a, c), 1))
+        return self.inference(outs, nc, p), outs

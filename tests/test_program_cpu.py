@@ -106,3 +106,45 @@ def test_packed_conv_emulation_matches_conv2d():
     want = F.conv2d(xin.double(), w.double(), b.double(), 1, 1).permute(0, 2, 3, 1).numpy()
     np.testing.assert_allclose(got, want, rtol=1e-9, atol=1e-9)
     assert k_steps == math.ceil(9 * 40 / 16) and n_tiles == 2
+
+
+def test_fp8_packing_matches_oracle_quantisation():
+    """FP8 program: 16-channel physical groups, and every conv's packed e4m3 weights and
+    dequant scales equal the oracle's per-output-channel rule (oracle.detector_ref.fp8_weights)."""
+    from oracle import detector_ref as D
+    P = pkg()
+    import importlib
+    A = importlib.import_module(P.__name__ + ".arch")
+    W = importlib.import_module(P.__name__ + ".weights")
+    M = importlib.import_module(P.__name__ + ".model")
+    ar = A.parse_arch(A.load_model_dict("yolov8s-small.yaml"))
+    sd = W.synthetic_state_dict(ar, 0)
+    prog = M.Program(ar, sd, 512, 640, 640, 2, "fp8")
+    blob = np.frombuffer(bytes(prog.blob), np.uint8)
+    checked = 0
+    names = [p for p in prog.fused]
+    for op in prog.ops:
+        if op.kind != M.YK_K_CONV:
+            continue
+        assert op.src_ch[0] % 16 == 0 and (op.n_src < 2 or op.src_ch[1] % 16 == 0)
+        nt, ks = op.n_tiles, op.k_steps
+        dq = np.frombuffer(bytes(prog.blob[op.b_off:op.b_off + nt * 32 * 4]), np.float32)[nt * 16:]
+        assert np.all(np.isfinite(dq)) and np.all(dq > 0)
+        checked += 1
+    assert checked >= 80
+    # model.1 (3x3 s2, 24 -> 40 logical channels) unpacked and compared element for element
+    op = prog.ops[1]
+    nt, ks = op.n_tiles, op.k_steps
+    pk = blob[op.w_off:op.w_off + nt * ks * 64 * 16].reshape(nt, ks, 64, 16)
+    wq = torch.from_numpy(pk.copy()).view(torch.float8_e4m3fn).float()
+    x = wq.reshape(nt, ks, 4, 16, 16).permute(0, 3, 1, 2, 4).reshape(nt * 16, -1)
+    w, _ = D.fuse(sd, "model.1")
+    Wq, dq_ref = D.fp8_weights(w)
+    cin_p = op.src_ch[0]
+    for ky in range(3):
+        for kx in range(3):
+            tap = ky * 3 + kx
+            assert torch.equal(x[:40, tap * cin_p:tap * cin_p + 24], Wq[:, :, ky, kx])
+    dq = np.frombuffer(bytes(prog.blob[op.b_off:op.b_off + nt * 32 * 4]), np.float32)[nt * 16:nt * 16 + 40]
+    np.testing.assert_array_equal(dq, dq_ref.numpy())
+    assert "model.1" in names

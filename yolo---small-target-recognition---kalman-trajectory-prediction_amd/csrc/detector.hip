@@ -65,11 +65,24 @@ struct BF16 {
   using T = unsigned short;
   static constexpr int EPL = 8;  // k elements per lane per K-step (16x16x32: 4 groups x 8)
   static constexpr bool kExact = false;
+  static constexpr bool kScaled = false;
 };
 struct F32 {
   using T = float;
   static constexpr int EPL = 4;  // 16x16x4 issued 4x: 4 groups x 4
   static constexpr bool kExact = true;
+  static constexpr bool kScaled = false;
+};
+// OCP e4m3 (gfx950 fp8; not MI300's fnuz) activations and weights.  A 16-byte fragment holds 16
+// K elements: one K step is 64 = two 16x16x32 fp8 MFMAs (bytes 0-7 and 8-15 of every lane; A and
+// B use the same byte -> K slot map, so the dot product does not depend on the hardware's K
+// order).  Weights carry a per-output-channel scale (bias array: [bias][dequant scale]);
+// activations are unscaled e4m3, saturated to +-448 when stored.
+struct FP8 {
+  using T = unsigned char;
+  static constexpr int EPL = 16;
+  static constexpr bool kExact = false;
+  static constexpr bool kScaled = true;
 };
 
 template <class Tr>
@@ -78,6 +91,13 @@ template <>
 __device__ __forceinline__ f32x4 mma<BF16>(const uint4& w, const uint4& x, f32x4 acc) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, w), __builtin_bit_cast(bf16x8, x),
                                                  acc, 0, 0, 0);
+}
+template <>
+__device__ __forceinline__ f32x4 mma<FP8>(const uint4& w, const uint4& x, f32x4 acc) {
+  const long w0 = (long)(((unsigned long long)w.y << 32) | w.x), w1 = (long)(((unsigned long long)w.w << 32) | w.z);
+  const long x0 = (long)(((unsigned long long)x.y << 32) | x.x), x1 = (long)(((unsigned long long)x.w << 32) | x.z);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(w0, x0, acc, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(w1, x1, acc, 0, 0, 0);
 }
 template <>
 __device__ __forceinline__ f32x4 mma<F32>(const uint4& w, const uint4& x, f32x4 acc) {
@@ -108,6 +128,28 @@ __device__ __forceinline__ void store4(unsigned short* p, const float v[4]) {
   *(uint2*)p = o;
 }
 __device__ __forceinline__ void store4(float* p, const float v[4]) { *(float4*)p = make_float4(v[0], v[1], v[2], v[3]); }
+// f32 -> e4m3 with round-to-nearest-even (v_cvt_pk_fp8_f32), saturated to the finite range
+__device__ __forceinline__ float sat448(float v) { return __builtin_amdgcn_fmed3f(v, -448.f, 448.f); }
+__device__ __forceinline__ void store4(unsigned char* p, const float v[4]) {
+  int w = __builtin_amdgcn_cvt_pk_fp8_f32(sat448(v[0]), sat448(v[1]), 0, false);
+  w = __builtin_amdgcn_cvt_pk_fp8_f32(sat448(v[2]), sat448(v[3]), w, true);
+  *(int*)p = w;
+}
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void load4(const unsigned char* p, float v[4]) {
+  const int i = *(const int*)p;
+  const f32x2 lo = __builtin_amdgcn_cvt_pk_f32_fp8(i, false), hi = __builtin_amdgcn_cvt_pk_f32_fp8(i, true);
+  v[0] = lo[0];
+  v[1] = lo[1];
+  v[2] = hi[0];
+  v[3] = hi[1];
+}
+// per-output-channel dequant scale of 4 consecutive channels (FP8: stored after the bias)
+template <class Tr>
+__device__ __forceinline__ float4 dq4(const float* bias, int n_tiles, int n0) {
+  if constexpr (Tr::kScaled) return *(const float4*)(bias + n_tiles * 16 + n0);
+  else return make_float4(1.f, 1.f, 1.f, 1.f);
+}
 __device__ __forceinline__ void load4(const unsigned short* p, float v[4]) {
   const uint2 i = *(const uint2*)p;
   v[0] = bf2f(i.x & 0xffff);
@@ -778,11 +820,13 @@ __global__ void __launch_bounds__(256) conv_fast_kernel(FastArgs a) {
 #pragma unroll
     for (int t = 0; t < NPT; ++t) acc[i][t] = f32x4{0.f, 0.f, 0.f, 0.f};
   float4 bb[NNT];
+  float4 sc[NNT];  // FP8 dequant scales
   unsigned wo[NNT];
 #pragma unroll
   for (int i = 0; i < NNT; ++i) {
     const int n0 = (nt0 + i) * 16 + kg * 4;
     bb[i] = (nt0 + i < a.n_tiles && n0 < a.cout) ? *(const float4*)(a.bias + n0) : make_float4(0.f, 0.f, 0.f, 0.f);
+    if constexpr (Tr::kScaled) sc[i] = dq4<Tr>(a.bias, a.n_tiles, n0 < a.cout ? n0 : 0);
     const int nt = nt0 + i < a.n_tiles ? nt0 + i : a.n_tiles - 1;
     wo[i] = a.woff + (unsigned)(((size_t)nt * nk * 64 + lane) * 16);
   }
@@ -880,6 +924,12 @@ __global__ void __launch_bounds__(256) conv_fast_kernel(FastArgs a) {
         }
       }
       float v[4] = {v4[0] + bb[i].x, v4[1] + bb[i].y, v4[2] + bb[i].z, v4[3] + bb[i].w};
+      if constexpr (Tr::kScaled) {
+        v[0] = v4[0] * sc[i].x + bb[i].x;
+        v[1] = v4[1] * sc[i].y + bb[i].y;
+        v[2] = v4[2] * sc[i].z + bb[i].z;
+        v[3] = v4[3] * sc[i].w + bb[i].w;
+      }
       if (a.act) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) v[j] = silu<Tr::kExact>(v[j]);
@@ -993,10 +1043,12 @@ __global__ void __launch_bounds__(64 * NW) conv_wide_kernel(WideArgs a) {
 #pragma unroll
   for (int pt = 0; pt < NPT; ++pt) prow[pt] = ((wave * NPT + pt) * a.stride * a.tiw + col * a.stride) * a.ps;
   float4 bb[NNT];
+  float4 sc[NNT];  // FP8 dequant scales
 #pragma unroll
   for (int ni = 0; ni < NNT; ++ni) {
     const int n0 = (nt0 + ni) * 16 + kg * 4;
     bb[ni] = (nt0 + ni < a.n_tiles && n0 < a.cout) ? *(const float4*)(a.bias + n0) : make_float4(0.f, 0.f, 0.f, 0.f);
+    if constexpr (Tr::kScaled) sc[ni] = dq4<Tr>(a.bias, a.n_tiles, n0 < a.cout ? n0 : 0);
   }
   const int tpi = a.tiles_y * a.tiles_x;
   uint4 st[UPT];
@@ -1086,6 +1138,12 @@ __global__ void __launch_bounds__(64 * NW) conv_wide_kernel(WideArgs a) {
           const size_t p = ((size_t)b * a.out_h + oy) * a.out_w + ox;
           float v[4] = {acc[ni][pt][0] + bb[ni].x, acc[ni][pt][1] + bb[ni].y, acc[ni][pt][2] + bb[ni].z,
                         acc[ni][pt][3] + bb[ni].w};
+          if constexpr (Tr::kScaled) {
+            v[0] = acc[ni][pt][0] * sc[ni].x + bb[ni].x;
+            v[1] = acc[ni][pt][1] * sc[ni].y + bb[ni].y;
+            v[2] = acc[ni][pt][2] * sc[ni].z + bb[ni].z;
+            v[3] = acc[ni][pt][3] * sc[ni].w + bb[ni].w;
+          }
           if (a.act) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) v[j] = silu<Tr::kExact>(v[j]);
@@ -1208,6 +1266,7 @@ __global__ void __launch_bounds__(256) conv_input_kernel(InputArgs a) {
 // the 1/255 of `im /= 255` is folded into the weights (the only rounding is the bf16 weight,
 // as for every other layer).  A workgroup = a 16x16 output tile; wave w computes rows
 // 4w..4w+3: per row one B fragment (8 LDS reads per lane) and two MFMAs.
+template <class Tr>
 __global__ void __launch_bounds__(256) conv_input_mfma_kernel(InputArgs a) {
   constexpr int TI = 15 * 2 + 3;
   constexpr int TP = TI + 1;
@@ -1281,7 +1340,7 @@ __global__ void __launch_bounds__(256) conv_input_mfma_kernel(InputArgs a) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) v[j] = silu<false>(v[j]);
       const size_t p = ((size_t)b * a.out_h + oy) * a.out_w + ox;
-      store4((unsigned short*)a.dst + p * a.d_cstride + a.d_coff + n0, v);
+      store4((typename Tr::T*)a.dst + p * a.d_cstride + a.d_coff + n0, v);
     }
   }
 }
@@ -1446,10 +1505,11 @@ __global__ void __launch_bounds__(256) detect_kernel(DetArgs a) {
   for (int s = 0; s < 4; ++s) {
     float v[4];
     const float4 bb = *(const float4*)(a.bias + s * 16 + kg * 4);
-    v[0] = acc[s][0] + bb.x;
-    v[1] = acc[s][1] + bb.y;
-    v[2] = acc[s][2] + bb.z;
-    v[3] = acc[s][3] + bb.w;
+    const float4 sc = dq4<Tr>(a.bias, 4, s * 16 + kg * 4);
+    v[0] = acc[s][0] * sc.x + bb.x;
+    v[1] = acc[s][1] * sc.y + bb.y;
+    v[2] = acc[s][2] * sc.z + bb.z;
+    v[3] = acc[s][3] * sc.w + bb.w;
     float m = fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3]));
     m = fmaxf(m, __shfl_xor(m, 16));
     m = fmaxf(m, __shfl_xor(m, 32));
@@ -2085,7 +2145,10 @@ struct yk_model {
 
 namespace {
 
-size_t act_bytes(const yk_model* m) { return m->desc.act_dtype == YK_ACT_F32 ? 4 : 2; }
+int esz_of(int dtype) { return dtype == YK_ACT_F32 ? 4 : dtype == YK_ACT_FP8 ? 1 : 2; }
+size_t act_bytes(const yk_model* m) { return (size_t)esz_of(m->desc.act_dtype); }
+// trait name as rocprofv3 demangles it
+const char* tr_name(int dtype) { return dtype == YK_ACT_F32 ? "F32" : dtype == YK_ACT_FP8 ? "FP8" : "BF16"; }
 
 // Base of image b0 of a buffer whose per-image extent is h x w x c_stride elements.
 void* img_ptr(const yk_model* m, int buf, int h, int w, int cstride, int b0) {
@@ -2307,6 +2370,12 @@ void set_tile_attrs() {
   set_fast_attr_w<BF16, true>();
   set_fast_attr_w<F32, false>();
   set_fast_attr_w<F32, true>();
+  set_wide_attr_n<FP8, 2>();
+  set_wide_attr_n<FP8, 4>();
+  set_fast_attr_w<FP8, false>();
+  set_fast_attr_w<FP8, true>();
+  (void)hipFuncSetAttribute((const void*)sppf_lds_kernel<FP8>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            kSppfLdsMaxHW * 128);
   (void)hipFuncSetAttribute((const void*)sppf_lds_kernel<BF16>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             kSppfLdsMaxHW * 128);
   (void)hipFuncSetAttribute((const void*)sppf_lds_kernel<F32>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -2412,7 +2481,7 @@ ConvPlan fast_plan(const yk_op& op, int B) {
 }
 
 ConvPlan conv_plan(const yk_model* m, const yk_op& op, int B) {
-  const int esz = m->desc.act_dtype == YK_ACT_F32 ? 4 : 2;
+  const int esz = esz_of(m->desc.act_dtype);
   const size_t idx = (size_t)(&op - m->ops.data());
   if (idx < m->tuned.size() && m->tuned[idx][0] >= 0 && m->tuned_batch == B) {
     const auto& t = m->tuned[idx];
@@ -2547,7 +2616,7 @@ int launch_op(yk_model* m, const yk_op& op, const uint8_t* frames, int B, float 
         a.xcd = m->xcd;
         const int tiles = B * ((op.out_h + 15) / 16) * ((op.out_w + 15) / 16);
         if (!Tr::kExact && op.cout <= 32 && !m->input_valu)
-          hipLaunchKernelGGL(conv_input_mfma_kernel, dim3(tiles), dim3(256), 0, st, a);
+          hipLaunchKernelGGL(conv_input_mfma_kernel<Tr>, dim3(tiles), dim3(256), 0, st, a);
         else
           hipLaunchKernelGGL(conv_input_kernel<Tr>, dim3(tiles), dim3(256), 0, st, a);
         break;
@@ -2675,6 +2744,10 @@ int launch_op(yk_model* m, const yk_op& op, const uint8_t* frames, int B, float 
           f.act = a.act;
           f.xcd = m->xcd;
           launch_fast<Tr>(f, cp, st);
+        } else if constexpr (Tr::kScaled) {
+          // FP8 runs only on the table-driven and wide kernels (16-channel K chunks)
+          yk::set_error("yk_detect: FP8 conv op without a table/wide kernel plan");
+          return YK_ERR_ARG;
         } else if (cp.kind == CK_SPLITK) {
           launch_splitk<Tr>(a, cp, st);
         } else if (cp.kind == CK_TILE) {
@@ -2771,57 +2844,60 @@ int run_ops(yk_model* m, const uint8_t* frames, int B, float conf, hipStream_t s
 }
 
 int launch_any(yk_model* m, const yk_op& op, const uint8_t* frames, int B, float conf, hipStream_t st) {
-  return m->desc.act_dtype == YK_ACT_F32 ? launch_op<F32>(m, op, frames, B, conf, st)
-                                         : launch_op<BF16>(m, op, frames, B, conf, st);
+  switch (m->desc.act_dtype) {
+    case YK_ACT_F32: return launch_op<F32>(m, op, frames, B, conf, st);
+    case YK_ACT_FP8: return launch_op<FP8>(m, op, frames, B, conf, st);
+    default: return launch_op<BF16>(m, op, frames, B, conf, st);
+  }
 }
 
 // Name of the kernel instantiation an op launches (matches rocprofv3's demangled names).
 const char* op_kernel_name(const yk_model* m, const yk_op& op) {
-  const bool f = m->desc.act_dtype == YK_ACT_F32;
+  const int dt = m->desc.act_dtype;
+  const bool f = dt == YK_ACT_F32;
+  const char* tn = tr_name(dt);
+  static thread_local char buf[96];
   switch (op.kind) {
     case YK_K_CONV_INPUT:
-      return f ? "conv_input_kernel<yk::det::F32>"
-               : (op.cout <= 32 && !m->input_valu ? "conv_input_mfma_kernel" : "conv_input_kernel<yk::det::BF16>");
+      if (!f && op.cout <= 32 && !m->input_valu) snprintf(buf, sizeof buf, "conv_input_mfma_kernel<yk::det::%s>", tn);
+      else snprintf(buf, sizeof buf, "conv_input_kernel<yk::det::%s>", tn);
+      return buf;
     case YK_K_SPPF_POOL:
       if (op.src[0].h * op.src[0].w <= kSppfLdsMaxHW && op.src_ch[0] % 8 == 0)
-        return f ? "sppf_lds_kernel<yk::det::F32>" : "sppf_lds_kernel<yk::det::BF16>";
-      return f ? "sppf_pool_kernel<yk::det::F32>" : "sppf_pool_kernel<yk::det::BF16>";
-    case YK_K_DETECT: return f ? "detect_kernel<yk::det::F32>" : "detect_kernel<yk::det::BF16>";
+        snprintf(buf, sizeof buf, "sppf_lds_kernel<yk::det::%s>", tn);
+      else
+        snprintf(buf, sizeof buf, "sppf_pool_kernel<yk::det::%s>", tn);
+      return buf;
+    case YK_K_DETECT: snprintf(buf, sizeof buf, "detect_kernel<yk::det::%s>", tn); return buf;
     default: break;
   }
   const ConvPlan cp = conv_plan(m, op, m->plan_batch);
-  static thread_local char buf[96];
   if (cp.kind == CK_WIDE) {
-    const WidePlan wp = wide_plan(op, f ? 4 : 2, cp.nnt, cp.npt);
+    const WidePlan wp = wide_plan(op, esz_of(dt), cp.nnt, cp.npt);
     const int upt = wp.upt <= 4 ? 4 : wp.upt <= 8 ? 8 : wp.upt <= 12 ? 12 : 16;
-    snprintf(buf, sizeof buf, "conv_wide_kernel<yk::det::%s, %d, %d, %d>", f ? "F32" : "BF16", cp.nnt, upt, cp.npt);
+    snprintf(buf, sizeof buf, "conv_wide_kernel<yk::det::%s, %d, %d, %d>", tn, cp.nnt, upt, cp.npt);
     return buf;
   }
   if (cp.kind == CK_FAST) {
     const int npt = cp.npt & 15, ws = cp.npt >> 4;
     const int skd = cp.nnt * npt >= 8 ? 2 : 4;
-    snprintf(buf, sizeof buf, "conv_fast_kernel<yk::det::%s, %d, %d, %s, %d>", f ? "F32" : "BF16", cp.nnt, npt,
-             ws ? "true" : "false", skd);
+    snprintf(buf, sizeof buf, "conv_fast_kernel<yk::det::%s, %d, %d, %s, %d>", tn, cp.nnt, npt, ws ? "true" : "false",
+             skd);
     return buf;
   }
   if (cp.kind == CK_SPLITK) {
-    snprintf(buf, sizeof buf, "conv_splitk_kernel<yk::det::%s, %d, %d>", f ? "F32" : "BF16", cp.nnt, cp.npt);
+    snprintf(buf, sizeof buf, "conv_splitk_kernel<yk::det::%s, %d, %d>", tn, cp.nnt, cp.npt);
     return buf;
   }
   if (cp.kind == CK_TILE) {
     const TilePlan& tp = cp.tp;
-    snprintf(buf, sizeof buf, "conv_tile_kernel<yk::det::%s, %d, %d, %s>", f ? "F32" : "BF16", tp.nnt, tp.npt,
-             tp.split ? "true" : "false");
+    snprintf(buf, sizeof buf, "conv_tile_kernel<yk::det::%s, %d, %d, %s>", tn, tp.nnt, tp.npt, tp.split ? "true" : "false");
     return buf;
   }
   const int nt = op.n_tiles;
   const int nnt = nt <= 1 ? 1 : nt == 2 ? 2 : (nt == 3 || nt == 6 || nt == 9) ? 3 : 4;
-  static const char* names[2][4] = {
-      {"conv_igemm_kernel<yk::det::BF16, 1, 2>", "conv_igemm_kernel<yk::det::BF16, 2, 2>",
-       "conv_igemm_kernel<yk::det::BF16, 3, 2>", "conv_igemm_kernel<yk::det::BF16, 4, 2>"},
-      {"conv_igemm_kernel<yk::det::F32, 1, 2>", "conv_igemm_kernel<yk::det::F32, 2, 2>",
-       "conv_igemm_kernel<yk::det::F32, 3, 2>", "conv_igemm_kernel<yk::det::F32, 4, 2>"}};
-  return names[f ? 1 : 0][nnt - 1];
+  snprintf(buf, sizeof buf, "conv_igemm_kernel<yk::det::%s, %d, 2>", tn, nnt);
+  return buf;
 }
 
 int launch_nms(yk_model* m, int B, float iou, int max_det, float* dets, int32_t* counts, hipStream_t st);
@@ -2952,7 +3028,9 @@ int detect_impl(yk_model* m, const uint8_t* frames, int B, float conf, float iou
   if (!dets) dets = m->dets;
   if (!counts) counts = m->counts;
   YK_HIP(hipMemsetAsync(m->cand_count, 0, sizeof(int) * B, st));
-  int rc = D.act_dtype == YK_ACT_F32 ? run_dag<F32>(m, frames, B, conf, st) : run_dag<BF16>(m, frames, B, conf, st);
+  int rc = D.act_dtype == YK_ACT_F32   ? run_dag<F32>(m, frames, B, conf, st)
+           : D.act_dtype == YK_ACT_FP8 ? run_dag<FP8>(m, frames, B, conf, st)
+                                       : run_dag<BF16>(m, frames, B, conf, st);
   if (rc != YK_OK) return rc;
   return launch_nms(m, B, iou, max_det, dets, counts, st);
 }
@@ -2989,8 +3067,8 @@ int launch_nms(yk_model* m, int B, float iou, int max_det, float* dets, int32_t*
 // offset of the K chunk's (tap, channel) from the pixel's window origin in its source view
 // and tap | src << 4 | valid << 5.  K order = model.py Program.pack: (tap, K-space channel).
 hipError_t build_ktabs(yk_model* m, bool fast) {
-  const int epl = m->desc.act_dtype == YK_ACT_F32 ? 4 : 2 * 4;
-  const int esz = m->desc.act_dtype == YK_ACT_F32 ? 4 : 2;
+  const int esz = esz_of(m->desc.act_dtype);
+  const int epl = 16 / esz;  // K elements per lane per K step
   if (m->arena_bytes >= 0x7fff0000ull || m->blob_bytes >= 0x7fff0000ull) fast = false;  // 32-bit offsets
   std::vector<int2> all;
   m->ktab_off.assign(m->ops.size(), -1);
@@ -3089,7 +3167,8 @@ int yk_model_create(yk_ctx* ctx, const yk_model_desc* desc, const void* host_blo
   YK_CHECK_ARG(desc->max_batch >= 1 && desc->n_anchors > 0 && desc->max_det >= 1, "yk_model_create: bad sizes");
   YK_CHECK_ARG(desc->nc == 1, "yk_model_create: only single-class detection heads are supported");
   YK_CHECK_ARG(desc->max_det <= 2048, "yk_model_create: max_det must be <= 2048");
-  YK_CHECK_ARG(desc->act_dtype == YK_ACT_BF16 || desc->act_dtype == YK_ACT_F32, "yk_model_create: bad act dtype");
+  YK_CHECK_ARG(desc->act_dtype == YK_ACT_BF16 || desc->act_dtype == YK_ACT_F32 || desc->act_dtype == YK_ACT_FP8,
+               "yk_model_create: bad act dtype");
   for (int i = 0; i < desc->n_ops; ++i) {
     const yk_op& op = desc->ops[i];
     YK_CHECK_ARG(op.kind >= YK_K_CONV_INPUT && op.kind <= YK_K_DETECT, "yk_model_create: bad op kind");
@@ -3118,7 +3197,7 @@ int yk_model_create(yk_ctx* ctx, const yk_model_desc* desc, const void* host_blo
   m->buf_elems.assign(desc->buf_elems, desc->buf_elems + desc->n_bufs);
   m->desc.ops = m->ops.data();
   m->desc.buf_elems = m->buf_elems.data();
-  const size_t esz = desc->act_dtype == YK_ACT_F32 ? 4 : 2;
+  const size_t esz = (size_t)esz_of(desc->act_dtype);
   const size_t B = desc->max_batch, A = desc->n_anchors;
   hipError_t e = hipSuccess;
   auto alloc = [&](void** p, size_t bytes) {
@@ -3160,6 +3239,14 @@ int yk_model_create(yk_ctx* ctx, const yk_model_desc* desc, const void* host_blo
   if (const char* env = getenv("YK_WIDE_DBG")) m->wide_dbg = atoi(env);
   if (const char* env = getenv("YK_NMS_DBG")) m->nms_dbg = atoi(env);
   if (e == hipSuccess) e = build_ktabs(m, !(getenv("YK_CONV_FAST") && getenv("YK_CONV_FAST")[0] == '0'));
+  if (e == hipSuccess && desc->act_dtype == YK_ACT_FP8)
+    for (size_t i = 0; i < m->ops.size(); ++i)
+      if (m->ops[i].kind == YK_K_CONV && (m->ktab_off[i] < 0 || m->ops[i].src_ch[0] % 16 ||
+                                          (m->ops[i].n_src > 1 && m->ops[i].src_ch[1] % 16))) {
+        yk::set_error("yk_model_create: FP8 needs every conv on the table kernel (16-channel sources, arena < 2 GiB)");
+        yk_model_destroy(m);
+        return YK_ERR_ARG;
+      }
   if (e == hipSuccess) e = set_schedule(m, 1, 3);
   if (e != hipSuccess) {
     yk::set_error(std::string("yk_model_create: ") + hipGetErrorString(e));
@@ -3346,19 +3433,21 @@ int yk_model_autotune(yk_model* m, const uint8_t* frames, int batch, float conf,
   hipEvent_t e0, e1;
   YK_HIP(hipEventCreate(&e0));
   YK_HIP(hipEventCreate(&e1));
-  const int esz = m->desc.act_dtype == YK_ACT_F32 ? 4 : 2;
+  const int esz = esz_of(m->desc.act_dtype);
+  const bool fp8 = m->desc.act_dtype == YK_ACT_FP8;  // table/wide kernels only
   for (int i = 0; i < n; ++i) {
     const yk_op& op = m->ops[i];
     if (op.kind != YK_K_CONV) continue;
     if (op.has_res && op.res.buf == op.dst.buf && op.res.c_off == op.dst.c_off) continue;  // in place
-    std::vector<std::array<int, 3>> cands = {{CK_DIRECT, 0, 0}};
-    if (tile_plan(op, esz, bt).ok && m->ltab && m->ltab_off[i] >= 0) {
+    std::vector<std::array<int, 3>> cands;
+    if (!fp8) cands.push_back({CK_DIRECT, 0, 0});
+    if (!fp8 && tile_plan(op, esz, bt).ok && m->ltab && m->ltab_off[i] >= 0) {
       cands.push_back({CK_TILE, 0, 0});
       if (tile_plan(op, esz, bt, true).single && !tile_plan(op, esz, bt).single) cands.push_back({CK_TILE, 1, 0});
     }
     for (int nnt : {1, 2, 4})
       for (int npt : {1, 2, 4}) {
-        if (nnt > 1 && 4 * op.n_tiles < 3 * ((op.n_tiles + nnt - 1) / nnt) * nnt) continue;
+        if (fp8 || (nnt > 1 && 4 * op.n_tiles < 3 * ((op.n_tiles + nnt - 1) / nnt) * nnt)) continue;
         cands.push_back({CK_SPLITK, nnt, npt});
       }
     if (m->ltab && m->ltab_off[i] >= 0 && m->arena_bytes < 0x7fff0000ull)
@@ -3377,6 +3466,7 @@ int yk_model_autotune(yk_model* m, const uint8_t* frames, int batch, float conf,
             if (wgs < 64) continue;
             cands.push_back({CK_FAST, nnt, npt | (ws << 4)});
           }
+    if (cands.empty()) continue;  // (FP8 without a table: yk_model_create refuses that)
     float best = 1e30f;
     std::array<int, 3> pick = {-1, 0, 0};
     for (const auto& c : cands) {

@@ -30,11 +30,12 @@ from . import arch as A
 from . import weights as Wt
 
 YK_K_CONV_INPUT, YK_K_CONV, YK_K_SPPF_POOL, YK_K_DETECT = range(4)
-ACT = {"bf16": 0, "fp32": 1}
+ACT = {"bf16": 0, "fp32": 1, "fp8": 2}
+ESZ = {"bf16": 2, "fp32": 4, "fp8": 1}
 
 
-def phys(c: int) -> int:
-    return (c + 7) // 8 * 8
+def phys(c: int, align: int = 8) -> int:
+    return (c + align - 1) // align * align
 
 
 class View(C.Structure):
@@ -103,6 +104,17 @@ def _bf16_bits(a: np.ndarray) -> np.ndarray:
     return torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32)).to(torch.bfloat16).view(torch.int16).numpy()
 
 
+def _fp8_bits(a: np.ndarray) -> np.ndarray:
+    """float32 -> OCP e4m3 (float8_e4m3fn) bytes, round-to-nearest-even, |a| <= 448."""
+    t = torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32)).clamp(-448.0, 448.0)
+    return t.to(torch.float8_e4m3fn).view(torch.uint8).numpy()
+
+
+def fp8_round(t: torch.Tensor) -> torch.Tensor:
+    """Values as stored in an FP8 activation buffer (saturated e4m3, round-to-nearest-even)."""
+    return t.float().clamp(-448.0, 448.0).to(torch.float8_e4m3fn).float()
+
+
 class Program:
     def __init__(self, ar: A.Arch, sd: dict, frame_h: int, frame_w: int, imgsz=640, max_batch: int = 8,
                  dtype: str = "bf16", max_det: int = 300):
@@ -112,7 +124,7 @@ class Program:
         self.frame_h, self.frame_w = int(frame_h), int(frame_w)
         self.strides = A.detect_strides(ar)
         self.in_h, self.in_w, self.pad_top, self.pad_left = letterbox_geometry(frame_h, frame_w, imgsz, max(self.strides))
-        self.epl = 8 if dtype == "bf16" else 4
+        self.epl = 16 // ESZ[dtype]  # K elements per lane per 16-byte fragment
         self.fused = Wt.fused_convs(sd, ar)
         self.sd = sd
         self.buf_elems: list[int] = []
@@ -122,6 +134,11 @@ class Program:
         self.op_meta: list[int] = []  # MACs per image of each op
         self.n_anchors = 0
         self._build()
+
+    def phys(self, c: int) -> int:
+        """Physical channels of a logical group: a whole number of 16-byte... K chunks; FP8
+        fragments span 16 channels, so a chunk never straddles a tap or a concat source."""
+        return phys(c, 16 if self.dtype == "fp8" else 8)
 
     # -- resources -------------------------------------------------------------
     def new_buf(self, h, w, c) -> int:
@@ -177,11 +194,22 @@ class Program:
             for kx in range(k):
                 tap = ky * k + kx
                 Wp[np.ix_(om, tap * cin_p + im)] = w[:, :, ky, kx]
+        if self.dtype == "fp8":
+            # per-output-channel scale: the row's max |w| maps to e4m3's 448; the kernel
+            # multiplies the accumulator by the inverse (dq) before adding the bias
+            amax = np.abs(Wp).max(axis=1)
+            scale = np.where(amax > 0, 448.0 / np.maximum(amax, 1e-30), 1.0).astype(np.float32)
+            dq = (1.0 / scale).astype(np.float32)
+            Wp = Wp * scale[:, None]
         P = Wp.reshape(n_tiles, 16, k_steps, 4, self.epl).transpose(0, 2, 3, 1, 4)  # [nt][ks][kg][col][e]
         P = P.reshape(n_tiles, k_steps, 64, self.epl)
-        packed = _bf16_bits(P) if self.dtype == "bf16" else P
         bias = np.zeros(n_tiles * 16, np.float32)
         bias[om] = b
+        if self.dtype == "fp8":
+            packed = _fp8_bits(P)
+            bias = np.concatenate([bias, dq])
+        else:
+            packed = _bf16_bits(P) if self.dtype == "bf16" else P
         tab = []
         pad = k // 2
         for q in range(K // 8):
@@ -235,7 +263,7 @@ class Program:
             if Ly.kind == "Conv" and Ly.i == 0:
                 k, s = Ly.args["k"], Ly.args["s"]
                 oh, ow = (h + 2 * (k // 2) - k) // s + 1, (w + 2 * (k // 2) - k) // s + 1
-                cp = phys(Ly.c2)
+                cp = self.phys(Ly.c2)
                 buf = self.new_buf(oh, ow, cp)
                 wf, bf, _, _, _ = self.fused["model.0"]
                 W0 = np.zeros((cp, 3, k, k), np.float32)
@@ -259,7 +287,7 @@ class Program:
                 k, s = Ly.args["k"], Ly.args["s"]
                 lh, lw = src[0].lh, src[0].lw
                 oh, ow = (lh + 2 * (k // 2) - k) // s + 1, (lw + 2 * (k // 2) - k) // s + 1
-                cp = phys(Ly.c2)
+                cp = self.phys(Ly.c2)
                 buf = self.new_buf(oh, ow, cp)
                 dst = Seg(buf, 0, cp, cp, Ly.c2, oh, ow)
                 self.conv_op(f"model.{Ly.i}", src, dst, list(range(Ly.c2)), cp)
@@ -283,7 +311,7 @@ class Program:
 
     def _c2f(self, Ly, src):
         c = int(Ly.c2 * 0.5)
-        cp = phys(c)
+        cp = self.phys(c)
         n = Ly.args["n"]
         hh, ww = src[0].lh, src[0].lw
         Y = self.new_buf(hh, ww, (2 + n) * cp)
@@ -297,7 +325,7 @@ class Program:
             self.conv_op(f"{p}.m.{j}.cv1", [ys[1 + j]], ts, list(range(c)), cp)
             self.conv_op(f"{p}.m.{j}.cv2", [ts], ys[2 + j], list(range(c)), cp,
                          res=ys[1 + j] if Ly.args["shortcut"] else None)
-        c2p = phys(Ly.c2)
+        c2p = self.phys(Ly.c2)
         ob = self.new_buf(hh, ww, c2p)
         dst = Seg(ob, 0, c2p, c2p, Ly.c2, hh, ww)
         self.conv_op(f"{p}.cv2", ys, dst, list(range(Ly.c2)), c2p)
@@ -305,7 +333,7 @@ class Program:
 
     def _sppf(self, Ly, src):
         c_ = Ly.c1 // 2
-        cp = phys(c_)
+        cp = self.phys(c_)
         hh, ww = src[0].lh, src[0].lw
         Z = self.new_buf(hh, ww, 4 * cp)
         zs = [Seg(Z, j * cp, 4 * cp, cp, c_, hh, ww) for j in range(4)]
@@ -322,7 +350,7 @@ class Program:
         assert Ly.args["k"] == 5
         self.ops.append(op)
         self.op_meta.append(0)
-        c2p = phys(Ly.c2)
+        c2p = self.phys(Ly.c2)
         ob = self.new_buf(hh, ww, c2p)
         dst = Seg(ob, 0, c2p, c2p, Ly.c2, hh, ww)
         self.conv_op(f"{p}.cv2", zs, dst, list(range(Ly.c2)), c2p)
@@ -331,7 +359,7 @@ class Program:
     def _detect(self, Ly, level_in):
         c2b, c3, nc = Ly.args["c2"], Ly.args["c3"], Ly.args["nc"]
         assert nc == 1 and c2b == 64, "decode kernel: single class, 64 box channels"
-        c3p = phys(c3)
+        c3p = self.phys(c3)
         p = f"model.{Ly.i}"
         anchor_off = 0
         for li, src in enumerate(level_in):
@@ -530,6 +558,10 @@ class DeviceModel:
             raw = np.zeros(n, np.int16)
             _memcpy_d2h(raw, ptr.value)
             out = torch.from_numpy(raw).view(torch.bfloat16).float().numpy()
+        elif self.prog.dtype == "fp8":
+            raw = np.zeros(n, np.uint8)
+            _memcpy_d2h(raw, ptr.value)
+            out = torch.from_numpy(raw).view(torch.float8_e4m3fn).float().numpy()
         else:
             out = np.zeros(n, np.float32)
             _memcpy_d2h(out, ptr.value)
