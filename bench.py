@@ -54,8 +54,11 @@ def parse():
     ap.add_argument("--no-pipeline", action="store_true",
                     help="run tracker(t) on the detector's stream instead of overlapping it with detector(t+1)")
     ap.add_argument("--no-tune", action="store_true", help="skip the per-op conv kernel autotune")
-    ap.add_argument("--lanes", type=int, default=3, help="streams per batch group the detector's op DAG runs on")
+    ap.add_argument("--lanes", type=int, default=None,
+                    help="streams per batch group the detector's op DAG runs on (default 1 with --inflight > 1, else 3)")
     ap.add_argument("--groups", type=int, default=1, help="independent sub-batches run concurrently")
+    ap.add_argument("--inflight", type=int, default=3, choices=[1, 2, 3, 4],
+                    help="detector forwards in flight (each a batch of all streams, own graph + HIP stream)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-profile", action="store_true")
@@ -187,6 +190,8 @@ def main():
     pipeline = import_module(PKG + ".pipeline")
     if a.streams is None:
         a.streams = 1 if a.config == 2 else 8
+    if a.lanes is None:
+        a.lanes = 1 if a.inflight > 1 and not a.no_pipeline else 3
     if a.dtype is None:
         a.dtype = "fp8" if a.config == 5 else "bf16"
     S = a.streams
@@ -196,7 +201,8 @@ def main():
     shard = P.shard
     my_streams = shard.stream_ids(rank, ws, S)  # this GPU's block of independent streams
     pipe = pipeline.StreamPipeline(f"yolov8{a.scale}-small.yaml", S, (H, W), a.dtype, seed=0, device=local,
-                                   pipelined=not a.no_pipeline, imgsz=imgsz, max_tracks=max_tracks)
+                                   pipelined=not a.no_pipeline, imgsz=imgsz, max_tracks=max_tracks,
+                                   inflight=1 if a.no_pipeline else a.inflight)
     # pre-render frames of every stream into HBM (inputs resident before the timed region)
     F = max(2, min(a.frames, a.warmup + a.steps))
     scenes = [P.synth.Scene(seed=shard.stream_seed(g, S), n_targets=a.targets, n_frames=F + 1, width=W, height=H)
@@ -206,7 +212,7 @@ def main():
         frames[:, s] = sc.frames_torch(0, F, dev)
     torch.cuda.synchronize()
     log("frames resident; setting schedule")
-    pipe.model.set_schedule(a.groups, a.lanes)
+    pipe.set_schedule(a.groups, a.lanes)
     pipe.frames.copy_(frames[0])
     tune = not a.no_tune
     if a.plan_in:
@@ -218,6 +224,7 @@ def main():
         pipe.capture(tune=tune)
     elif tune:
         pipe.model.autotune(pipe.frames, pipe.conf)
+        pipe.sync_plan()
     if a.plan_out and rank == 0:
         b, pl = pipe.model.get_plan()
         with open(a.plan_out, "w") as f:
@@ -288,7 +295,7 @@ def main():
                                    f"{a.targets} targets/stream, tracker(150, 1, 0.1) (BASELINE config {a.config})",
                        "streams_per_gpu": S, "global_batch": S * ws, "parallelism": f"streams sharded over {ws} GPU(s)",
                        "graph": not a.no_graph, "tracker_overlapped": not a.no_pipeline, "autotuned": not a.no_tune, "dag_lanes": a.lanes,
-                       "batch_groups": a.groups,
+                       "batch_groups": a.groups, "detector_inflight": pipe.D,
                        "live_tracks_per_stream": round(live, 1),
                        "tracks_created": int(run["total_tracks_created"]),
                        "gflop_per_frame": round(gflop, 3)},

@@ -97,14 +97,15 @@ def test_reference_driver_loop_through_compat_packages():
 
 def test_pipelined_tracker_stream_matches_serial():
     """pipelined=True (tracker(t) on its own stream, overlapping detector(t+1), double-buffered
-    detections) gives exactly the serial pipeline's tracker state."""
+    detections) and inflight=2/3 (detector graphs in flight on their own streams) give exactly the
+    serial pipeline's tracker state."""
     P = pkg()
     pipeline = importlib.import_module(P.__name__ + ".pipeline")
     S, F = 4, 24
     runs = []
-    for pipelined in (False, True):
+    for pipelined, inflight in ((False, 1), (True, 1), (True, 2), (True, 3)):
         pipe = pipeline.StreamPipeline("yolov8s-small.yaml", S, (512, 640), "bf16", seed=0, max_tracks=256,
-                                       pipelined=pipelined)
+                                       pipelined=pipelined, inflight=inflight)
         scenes = [P.synth.Scene(seed=40 + s, n_targets=16, n_frames=F) for s in range(S)]
         frames = torch.stack([sc.frames_torch(0, F, "cuda") for sc in scenes], 1)
         pipe.frames.copy_(frames[0])
@@ -114,8 +115,9 @@ def test_pipelined_tracker_stream_matches_serial():
         pipe.sync()
         rows, counts, stats = pipe.tracker.download()
         runs.append((rows.copy(), counts.copy(), stats.copy()))
-    (r0, c0, s0), (r1, c1, s1) = runs
-    np.testing.assert_array_equal(c0, c1)
-    np.testing.assert_array_equal(s0, s1)
-    for s in range(S):
-        assert r0[s][: c0[s]].tobytes() == r1[s][: c1[s]].tobytes()
+    r0, c0, s0 = runs[0]
+    for r1, c1, s1 in runs[1:]:
+        np.testing.assert_array_equal(c0, c1)
+        np.testing.assert_array_equal(s0, s1)
+        for s in range(S):
+            assert r0[s][: c0[s]].tobytes() == r1[s][: c1[s]].tobytes()

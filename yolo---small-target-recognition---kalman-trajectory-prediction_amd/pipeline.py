@@ -12,6 +12,14 @@ native hipGraph (yk_detect_graph); the tracker is one more launch.
 tracker state, so it starts while tracker(t) is still running.  Detections are
 double-buffered; detector(t+2) waits for tracker(t) to have read its buffer.  Results are
 identical to the serial order (the tracker still sees frames in order on one stream).
+
+``inflight=D`` > 1 (needs ``pipelined``) keeps D detector forwards in flight: D DeviceModels
+(same program and conv plan, each its own activation arena) replay their hipGraphs on D HIP
+streams, step t on slot t % D with its own detection buffer.  Every forward is still one batch of the S streams' frames;
+the tracker consumes the detections in frame order.  The detector's ~90 launches are each
+bound by their own latency, not by the chip (op time is nearly flat in the batch), and the
+parallel branches inside one captured graph execute one after the other, so a second
+independent graph on another stream is what fills the idle CUs (tools/inflight.py: 1.45x).
 """
 from __future__ import annotations
 
@@ -28,7 +36,7 @@ class StreamPipeline:
     def __init__(self, model_cfg: str = "yolov8s-small.yaml", n_streams: int = 8, frame_hw=(512, 640),
                  dtype: str = "bf16", weights=None, seed: int = 0, conf: float = 0.25, iou: float = 0.7,
                  max_det: int = 300, max_lost_frames: int = 150, min_hits: int = 1, iou_threshold: float = 0.1,
-                 max_tracks: int = 512, device: int = 0, pipelined: bool = False, imgsz=640):
+                 max_tracks: int = 512, device: int = 0, pipelined: bool = False, imgsz=640, inflight: int = 1):
         if conf < 0.1:
             raise ValueError("conf < 0.1 would need the driver's score > 0.1 filter on the device path")
         self.S, self.device = int(n_streams), int(device)
@@ -41,44 +49,80 @@ class StreamPipeline:
                                             self.max_det, self.device)
         dev = torch.device("cuda", self.device)
         self.frames = torch.zeros((self.S, frame_hw[0], frame_hw[1], 3), dtype=torch.uint8, device=dev)
-        self._dets = torch.zeros((2, self.S, self.max_det, 6), dtype=torch.float32, device=dev)
-        self._counts = torch.zeros((2, self.S), dtype=torch.int32, device=dev)
+        self.nb = max(2, int(inflight))  # detection buffers (= detector slots when inflight > 1)
+        self._dets = torch.zeros((self.nb, self.S, self.max_det, 6), dtype=torch.float32, device=dev)
+        self._counts = torch.zeros((self.nb, self.S), dtype=torch.int32, device=dev)
         self._k = 0  # detection buffer the next step writes
         self.pipelined = bool(pipelined)
         self.trk_stream = torch.cuda.Stream(dev) if self.pipelined else None
-        self._ev_det = [torch.cuda.Event(), torch.cuda.Event()]
-        self._ev_trk = [torch.cuda.Event(), torch.cuda.Event()]
-        self._trk_pending = [False, False]
+        self._ev_det = [torch.cuda.Event() for _ in range(self.nb)]
+        self._ev_trk = [torch.cuda.Event() for _ in range(self.nb)]
+        self._trk_pending = [False] * self.nb
         self.graph = None
+        self.D = int(inflight)
+        if not 1 <= self.D <= 4:
+            raise ValueError("inflight must be in [1, 4]")
+        if self.D > 1 and not self.pipelined:
+            raise ValueError("inflight > 1 needs pipelined=True (the tracker runs on its own stream)")
+        # slot s: detector model, input frames and launch stream (None = the caller's stream)
+        self.models = [self.model] + [M.DeviceModel(self.prog, self.device) for _ in range(self.D - 1)]
+        self.frame_slots = [self.frames] + [torch.zeros_like(self.frames) for _ in range(self.D - 1)]
+        self.det_streams = [None] + [torch.cuda.Stream(dev) for _ in range(self.D - 1)]
 
     @property
     def dets(self) -> torch.Tensor:
         """Detections [S, max_det, 6] of the most recent step."""
-        return self._dets[self._k ^ 1]
+        return self._dets[(self._k - 1) % self.nb]
 
     @property
     def counts(self) -> torch.Tensor:
-        return self._counts[self._k ^ 1]
+        return self._counts[(self._k - 1) % self.nb]
+
+    def set_schedule(self, groups: int, lanes: int):
+        for m in self.models:
+            m.set_schedule(groups, lanes)
+
+    def sync_plan(self):
+        """Give every detector slot model 0's conv plan (autotuned or loaded)."""
+        b, plan = self.model.get_plan()
+        if b:
+            for m in self.models[1:]:
+                m.load_plan(b, plan)
+
+    def _slot(self, k: int) -> int:
+        return k if self.D > 1 else 0
+
+    def _stream(self, s: int):
+        st = self.det_streams[s]
+        return torch.cuda.current_stream(self.device) if st is None else st
 
     def capture(self, tune: bool = True):
         """Autotune the conv kernels for this batch (on the current frames), then build and warm
-        the detector's native hipGraph; later steps replay it."""
+        the detector's native hipGraph(s); later steps replay them."""
         if tune:
             self.model.autotune(self.frames, self.conf)
+        self.sync_plan()
+        for fs in self.frame_slots[1:]:
+            fs.copy_(self.frames)
         self.graph = True
-        for k in range(2):  # one graph per detection buffer
-            self.model.detect(self.frames, self.conf, self.iou, self.max_det, self._dets[k], self._counts[k], graph=True)
+        for k in range(self.nb):  # one graph per detection buffer
+            s = self._slot(k)
+            with torch.cuda.stream(self._stream(s)):
+                self.models[s].detect(self.frame_slots[s], self.conf, self.iou, self.max_det, self._dets[k],
+                                      self._counts[k], graph=True)
         torch.cuda.synchronize(self.device)
         return self.graph
 
     def step(self):
         k = self._k
-        cur = torch.cuda.current_stream(self.device)
-        if self._trk_pending[k]:  # tracker(t-2) still reads buffer k
+        s = self._slot(k)
+        cur = self._stream(s)
+        if self._trk_pending[k]:  # tracker(t - nb) still reads buffer k
             cur.wait_event(self._ev_trk[k])
             self._trk_pending[k] = False
-        self.model.detect(self.frames, self.conf, self.iou, self.max_det, self._dets[k], self._counts[k],
-                          graph=bool(self.graph))
+        with torch.cuda.stream(cur):
+            self.models[s].detect(self.frame_slots[s], self.conf, self.iou, self.max_det, self._dets[k],
+                                  self._counts[k], graph=bool(self.graph))
         if self.pipelined:
             self._ev_det[k].record(cur)
             self.trk_stream.wait_event(self._ev_det[k])
@@ -88,15 +132,18 @@ class StreamPipeline:
             self._trk_pending[k] = True
         else:
             self.tracker.step_device(self._dets[k], self._counts[k])
-        self._k ^= 1
+        self._k = (k + 1) % self.nb
 
     def sync(self):
         """Wait for every launched step (detector and tracker streams)."""
         torch.cuda.synchronize(self.device)
 
     def run(self, frames: torch.Tensor):
-        """frames [S, H, W, 3] uint8 (device) -> one step."""
-        self.frames.copy_(frames, non_blocking=True)
+        """frames [S, H, W, 3] uint8 (device) -> one step.  The copy runs on the slot's detector
+        stream, after that slot's previous forward has read its frames."""
+        s = self._slot(self._k)
+        with torch.cuda.stream(self._stream(s)):
+            self.frame_slots[s].copy_(frames, non_blocking=True)
         self.step()
 
     def stats(self):
