@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define YK_ABI_VERSION 1
+#define YK_ABI_VERSION 2
 
 enum yk_status {
   YK_OK = 0,
@@ -63,7 +63,20 @@ typedef struct {
   double iou_threshold;    /* reference default 0.3 (driver uses 0.1)            */
   int32_t max_tracks;      /* capacity of live tracks per stream (<= 2048)       */
   int32_t max_dets;        /* capacity of detections per stream per frame (<= 1024) */
+  int32_t policy;          /* yk_tracker_policy                                   */
 } yk_tracker_cfg;
+
+/* Tracker policy (what update() a stream runs):
+ *   YK_POLICY_ENHANCED      kalman.EnhancedMultiTargetTracker (enhanced_multi_target_tracker.py)
+ *   YK_POLICY_MOTION_RESET  camera_motion_compensation.MotionCompensatedMultiTracker.update(dets,
+ *                           frame=None) over MotionResetKalmanTracker tracks
+ *                           (motion_compensated_multi_tracker.py:77-242,
+ *                           motion_reset_kalman_tracker.py:16-355): jump / velocity / size-change
+ *                           Kalman resets, blended predict for 10 frames after a reset, strict
+ *                           iou > thr with (iou, d, t)-descending greedy order, every live
+ *                           track reported.  The global-motion branch (needs frames + optical
+ *                           flow) is not part of this policy. */
+enum yk_tracker_policy { YK_POLICY_ENHANCED = 0, YK_POLICY_MOTION_RESET = 1 };
 
 /* Per-stream counters: EnhancedMultiTargetTracker.stats + frame_count/next_track_id
  * (enhanced_multi_target_tracker.py:28-38). */
@@ -76,6 +89,8 @@ typedef struct {
   int64_t long_term_predictions;
   int64_t successful_recoveries;
   int64_t overflow; /* detections/tracks dropped because a capacity was hit (0 in parity runs) */
+  int64_t individual_resets;   /* YK_POLICY_MOTION_RESET: stats['individual_resets']   */
+  int64_t tracking_recoveries; /* YK_POLICY_MOTION_RESET: stats['tracking_recoveries'] */
 } yk_tracker_stats;
 
 /* One output row = one reference get_track_info() dict
@@ -92,6 +107,17 @@ typedef struct {
   double velocity[2];         /* x[4:6]                                            */
   double motion_confidence, speed, direction;
   double traj[YK_TRAJ_OUT][2];/* last 30 trajectory centres, oldest first          */
+  /* YK_POLICY_MOTION_RESET (motion_reset_kalman_tracker.py:314-355); zero otherwise */
+  int32_t reset_count, frames_since_reset;
+  int32_t reason_count[3];    /* resets with a position / velocity / size reason      */
+  int32_t n_details;          /* entries of details (the last min(reset_count, 5))    */
+  double motion_consistency;
+  double reset_confidence_sum, motion_consistency_sum; /* over every reset (f64)   */
+  struct {
+    int32_t frame, reasons;   /* age at the reset; bit 0 position, 1 velocity, 2 size */
+    double value[3];          /* jump px, velocity change px/f, size-change ratio     */
+    double confidence, motion_consistency;
+  } details[5];               /* oldest first                                         */
 } yk_track_out;
 
 /* Full filter state of one live track (AircraftKalmanTracker attributes,

@@ -93,3 +93,45 @@ def test_inv_s_is_reciprocal_diagonal(seed):
     for _ in range(200):
         s = rng.uniform(10.0, 5000.0, 4)
         assert np.array_equal(np.linalg.inv(np.diag(s)), np.diag(1.0 / s))
+
+
+# ---------------------------------------------------------------- motion-reset variant
+def _still_then_jump(dx, n_still=20):
+    f = np.float32
+    still = [[f(100), f(100), f(300), f(260), f(0.9)]]  # large box: a 50 px jump keeps IoU 0.6
+    jumped = [[f(100 + dx), f(100), f(300 + dx), f(260), f(0.9)]]
+    return [still] * n_still + [jumped]
+
+
+def test_cmc_oracle_position_jump_resets():
+    """A 50 px jump of a 200x160 box after 20 still frames (IoU 0.6, still matched): distance
+    50 > 40 -> factor 1.25; the score history
+    (nine ~0 scores and 1.25) has consistency 1 - var/(mean + 0.1) = 0.375 >= 0.3, so the
+    confidence stays 1.25 > 1.0 and the filter resets to the new box with zero velocity."""
+    from oracle.cmc_ref import RefCMCMultiTracker
+    tr = RefCMCMultiTracker(150, 1, 0.1)
+    for dets in _still_then_jump(50):
+        out = tr.update(dets)
+    t = tr.trackers[0]
+    assert len(tr.trackers) == 1 and t.reset_count == 1 and tr.stats["individual_resets"] == 1
+    assert [k for k, _ in t.reset_log[0]["reasons"]] == ["position"]
+    assert abs(float(t.reset_log[0]["confidence"]) - 1.25) < 1e-3
+    assert t.x[0] == np.float32(250.0) and np.all(t.x[4:] == 0)
+    assert out[0]["frames_since_reset"] == 0 and out[0]["status_suffix"].startswith(" | ")
+
+
+def test_cmc_oracle_small_jump_keeps_filter():
+    from oracle.cmc_ref import RefCMCMultiTracker
+    tr = RefCMCMultiTracker(150, 1, 0.1)
+    for dets in _still_then_jump(8):
+        tr.update(dets)
+    assert tr.trackers[0].reset_count == 0
+
+
+def test_cmc_greedy_tie_order():
+    """(iou, d, t) tuples sorted in reverse: on an exact IoU tie the larger detection index
+    wins the track (motion_compensated_multi_tracker.py:262-274)."""
+    from oracle.cmc_ref import cmc_greedy
+    iou = np.array([[0.5, 0.2], [0.5, 0.0]])
+    assert cmc_greedy(iou, 0.1) == [(1, 0), (0, 1)]
+    assert cmc_greedy(np.array([[0.1]]), 0.1) == []  # strict >

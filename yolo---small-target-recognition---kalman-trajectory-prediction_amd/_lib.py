@@ -30,19 +30,28 @@ class YKError(RuntimeError):
 # ---------------------------------------------------------------- ABI structs
 class TrackerCfg(C.Structure):
     _fields_ = [("max_lost_frames", C.c_int32), ("min_hits", C.c_int32), ("iou_threshold", C.c_double),
-                ("max_tracks", C.c_int32), ("max_dets", C.c_int32)]
+                ("max_tracks", C.c_int32), ("max_dets", C.c_int32), ("policy", C.c_int32)]
 
+
+POLICY_ENHANCED, POLICY_MOTION_RESET = 0, 1
 
 STATS_DTYPE = np.dtype([(k, np.int64) for k in (
     "frame_count", "next_track_id", "total_tracks_created", "total_tracks_terminated",
-    "current_active_tracks", "long_term_predictions", "successful_recoveries", "overflow")])
+    "current_active_tracks", "long_term_predictions", "successful_recoveries", "overflow",
+    "individual_resets", "tracking_recoveries")])
+
+RESET_DETAIL_DTYPE = np.dtype([("frame", np.int32), ("reasons", np.int32), ("value", np.float64, (3,)),
+                               ("confidence", np.float64), ("motion_consistency", np.float64)], align=True)
 
 TRACK_OUT_DTYPE = np.dtype([
     ("track_num", np.int32), ("status", np.int32), ("age", np.int32), ("hits", np.int32),
     ("hit_streak", np.int32), ("time_since_update", np.int32), ("traj_len", np.int32),
     ("is_stable_motion", np.int32), ("bbox", np.float64, (4,)), ("confidence", np.float64),
     ("velocity", np.float64, (2,)), ("motion_confidence", np.float64), ("speed", np.float64),
-    ("direction", np.float64), ("traj", np.float64, (TRAJ_OUT, 2))], align=True)
+    ("direction", np.float64), ("traj", np.float64, (TRAJ_OUT, 2)),
+    ("reset_count", np.int32), ("frames_since_reset", np.int32), ("reason_count", np.int32, (3,)),
+    ("n_details", np.int32), ("motion_consistency", np.float64), ("reset_confidence_sum", np.float64),
+    ("motion_consistency_sum", np.float64), ("details", RESET_DETAIL_DTYPE, (5,))], align=True)
 
 TRACK_STATE_DTYPE = np.dtype([
     ("track_num", np.int32), ("age", np.int32), ("hits", np.int32), ("hit_streak", np.int32),
@@ -116,7 +125,7 @@ def lib() -> C.CDLL:
             fn = getattr(L, name)
             fn.argtypes = args
             fn.restype = res
-        if L.yk_abi_version() != 1:
+        if L.yk_abi_version() != 2:
             raise YKError("libyk.so ABI version mismatch")
         sizes = {0: C.sizeof(TrackerCfg), 1: STATS_DTYPE.itemsize, 2: TRACK_OUT_DTYPE.itemsize,
                  3: TRACK_STATE_DTYPE.itemsize}

@@ -37,6 +37,21 @@ constexpr int TH = YK_TRAJ_HIST;        // trajectory ring (deque maxlen=150)
 constexpr int TOUT = YK_TRAJ_OUT;       // trajectory points exported per row
 constexpr double kPi = 3.141592653589793;  // np.pi
 
+// YK_POLICY_MOTION_RESET numerics.  The reference's reset logic mixes numpy float32 and float64
+// scalars with python floats; NEP 50 (numpy 2) fixes every result's dtype: a numpy scalar op a
+// python float keeps the numpy dtype (the python float is cast to it), f32 op f64 is f64, and
+// np.asarray of a list is float32 only when every element is a float32 scalar.  Num carries a
+// value (exact in double) and that dtype.
+enum { K32 = 0, K64 = 1, KPY = 2 };
+struct Num {
+  double v;
+  int k;
+};
+struct ResetDetail {  // one reset_reasons entry (motion_reset_kalman_tracker.py:222-229)
+  int frame, reasons;
+  double value[3], conf, cons;
+};
+
 struct Slot {
   double x[8];
   double P[16];  // per coordinate c: [4c+0]=P[c][c] [4c+1]=P[c][c+4] [4c+2]=P[c+4][c] [4c+3]=P[c+4][c+4]
@@ -46,6 +61,18 @@ struct Slot {
   double th[TH][2];
   int age, hits, hit_streak, tsu, is_lost, lost_frames, track_num, max_lost;
   int vh_len, vh_head, th_len, th_head;
+  // YK_POLICY_MOTION_RESET (MotionResetKalmanTracker, motion_reset_kalman_tracker.py:28-65)
+  int policy;
+  int reset_count, last_reset;  // last_reset_frame: -999 at creation
+  int ph_len, ph_head, bh_len, bh_head, ms_len, ms_head, dl_len, dl_head;
+  int reason_count[3];
+  double consistency, conf_sum, cons_sum;
+  double ph[8][2];              // position_history deque(maxlen=8)
+  double bh[5][4];              // bbox_history deque(maxlen=5): detection boxes
+  double ms[10];                // motion_scores deque(maxlen=10)
+  unsigned char ph32[8];        // entry is a float32 detection centre (else a float64 state copy)
+  unsigned char mk[10];         // score dtype (K32 / K64 / KPY)
+  ResetDetail dl[5];            // the last five reset_reasons entries
 };
 
 struct Hdr {
@@ -67,6 +94,7 @@ struct Dev {
   int T, D, C;
   int max_lost, min_hits;
   double thr;
+  int policy;           // yk_tracker_policy
 };
 
 // ---------------------------------------------------------------- per-track math
@@ -129,6 +157,7 @@ __device__ void slot_init(Slot& s, const double* z, int track_num, int max_lost)
   s.max_lost = max_lost;
   s.vh_len = s.vh_head = 0;
   s.th_len = s.th_head = 0;
+  s.policy = 0;
   ring_push(s.th, TH, s.th_len, s.th_head, z[0], z[1]);
 }
 
@@ -230,6 +259,311 @@ __device__ void analyze_motion(Slot& s, const double* vx, const double* vy, cons
   s.pconf = s.stability * (1.0 < frac ? 1.0 : frac);
 }
 
+// ---------------------------------------------------------------- motion-reset policy
+// camera_motion_compensation/motion_reset_kalman_tracker.py (checker: oracle/cmc_ref.py).
+template <int CAP>
+__device__ __forceinline__ int ring_slot(int& len, int& head) {
+  int pos;
+  if (len < CAP) {
+    pos = head + len;
+    if (pos >= CAP) pos -= CAP;
+    ++len;
+  } else {
+    pos = head;
+    head = (head + 1 == CAP) ? 0 : head + 1;
+  }
+  return pos;
+}
+template <int CAP>
+__device__ __forceinline__ int ring_at(int head, int k) {
+  const int i = head + k;
+  return i >= CAP ? i - CAP : i;
+}
+
+__device__ __forceinline__ void ph_push(Slot& s, double a, double b, bool f32) {
+  const int p = ring_slot<8>(s.ph_len, s.ph_head);
+  s.ph[p][0] = a;
+  s.ph[p][1] = b;
+  s.ph32[p] = f32 ? 1 : 0;
+}
+
+// np.add.reduce of a 1-D contiguous array of n <= 16: identity 0 + numpy's pairwise sum
+// (8 accumulators from n = 8), in float32 when f32 (verified against numpy 2.2 add.reduce)
+template <typename F>
+__device__ F np_sum_t(const double* a, int n) {
+  F res;
+  if (n < 8) {
+    res = F(0);
+    for (int i = 0; i < n; ++i) res = res + (F)a[i];
+  } else {
+    F r[8];
+    for (int j = 0; j < 8; ++j) r[j] = (F)a[j];
+    int i = 8;
+    for (; i < n - (n % 8); i += 8)
+      for (int j = 0; j < 8; ++j) r[j] = r[j] + (F)a[i + j];
+    res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+    for (; i < n; ++i) res = res + (F)a[i];
+  }
+  return F(0) + res;
+}
+
+// np.mean / np.var of a python list of numpy scalars / python floats (np.asarray dtype rule)
+__device__ Num np_mean_list(const Num* a, int n) {
+  bool f32 = true;
+  double v[10];
+  for (int i = 0; i < n; ++i) {
+    f32 = f32 && a[i].k == K32;
+    v[i] = a[i].v;
+  }
+  if (f32) return Num{(double)(np_sum_t<float>(v, n) / (float)n), K32};
+  return Num{np_sum_t<double>(v, n) / (double)n, K64};
+}
+__device__ Num np_var_list(const Num* a, int n) {
+  const Num m = np_mean_list(a, n);
+  double d[10];
+  for (int i = 0; i < n; ++i) {
+    if (m.k == K32) {
+      const float x = (float)a[i].v - (float)m.v;
+      d[i] = (double)(x * x);
+    } else {
+      const double x = a[i].v - m.v;
+      d[i] = x * x;
+    }
+  }
+  if (m.k == K32) return Num{(double)(np_sum_t<float>(d, n) / (float)n), K32};
+  return Num{np_sum_t<double>(d, n) / (double)n, K64};
+}
+
+// numpy scalar (op) python float c: c takes the scalar's dtype (NEP 50)
+__device__ __forceinline__ Num div_c(Num a, double c) {
+  if (a.k == K32) return Num{(double)((float)a.v / (float)c), K32};
+  return Num{a.v / c, a.k};
+}
+__device__ __forceinline__ Num mul_c(Num a, double c) {
+  if (a.k == K32) return Num{(double)((float)a.v * (float)c), K32};
+  return Num{a.v * c, a.k};
+}
+__device__ __forceinline__ bool gt_c(Num a, double c) { return a.k == K32 ? (float)a.v > (float)c : a.v > c; }
+__device__ __forceinline__ bool lt_c(Num a, double c) { return a.k == K32 ? (float)a.v < (float)c : a.v < c; }
+// python min(a, c): c only when c < a
+__device__ __forceinline__ Num pymin_c(Num a, double c) { return gt_c(a, c) ? Num{c, KPY} : a; }
+
+// a - b of two centre coordinates (float32 when both are float32)
+__device__ __forceinline__ double sub_k(double a, double b, bool f32) {
+  return f32 ? (double)((float)a - (float)b) : a - b;
+}
+// np.linalg.norm of a 2-vector = sqrt(v.dot(v)): float32 as x*x + y*y, float64 through the
+// BLAS ddot, which contracts to fma(y, y, x*x) (both verified on numpy 2.2 + its OpenBLAS)
+__device__ __forceinline__ Num norm2(double dx, double dy, bool f32) {
+  if (f32) {
+    const float x = (float)dx, y = (float)dy;
+    return Num{(double)sqrtf(x * x + y * y), K32};
+  }
+  return Num{sqrt(fma(dy, dy, dx * dx)), K64};
+}
+
+// MotionResetKalmanTracker.__init__ on top of slot_init (:28-65): the base's position deque is
+// replaced by a maxlen-8 one holding the detection centre
+template <typename DT>
+__device__ void cmc_init(Slot& s, const DT* b) {
+  s.policy = 1;
+  s.reset_count = 0;
+  s.last_reset = -999;
+  s.ph_len = s.ph_head = s.bh_len = s.bh_head = s.ms_len = s.ms_head = s.dl_len = s.dl_head = 0;
+  s.reason_count[0] = s.reason_count[1] = s.reason_count[2] = 0;
+  s.consistency = s.conf_sum = s.cons_sum = 0.0;
+  const DT cx = (b[0] + b[2]) / DT(2), cy = (b[1] + b[3]) / DT(2);
+  ph_push(s, (double)cx, (double)cy, sizeof(DT) == 4);
+  const int p = ring_slot<5>(s.bh_len, s.bh_head);
+  for (int k = 0; k < 4; ++k) s.bh[p][k] = (double)b[k];
+}
+
+// _calculate_motion_consistency (:159-172)
+__device__ Num cmc_consistency(const Slot& s) {
+  const int n = s.ms_len;
+  if (n < 3) return Num{0.0, KPY};
+  Num sc[10];
+  for (int k = 0; k < n; ++k) {
+    const int i = ring_at<10>(s.ms_head, k);
+    sc[k] = Num{s.ms[i], (int)s.mk[i]};
+  }
+  const Num m = np_mean_list(sc, n);
+  if (!(m.v > 0.0)) return Num{1.0, KPY};
+  const Num v = np_var_list(sc, n);
+  Num c;
+  if (m.k == K32) c = Num{(double)(1.0f - (float)v.v / ((float)m.v + 0.1f)), K32};
+  else c = Num{1.0 - v.v / (m.v + 0.1), K64};
+  return c.v > 0.0 ? c : Num{0.0, KPY};  // python max(0.0, c)
+}
+
+// _should_reset_kalman (:174-214) with the three detectors (:86-157).  val / why: the
+// reasons' values and bits (1 position jump, 2 velocity change, 4 size change).
+template <typename DT>
+__device__ bool cmc_decide(Slot& s, const DT* b, double* val, int& why, Num& conf) {
+  why = 0;
+  const int since = s.age - s.last_reset;
+  if (since < 15) return false;  // reset cooldown
+  constexpr bool c32 = sizeof(DT) == 4;
+  const DT cxd = (b[0] + b[2]) / DT(2), cyd = (b[1] + b[3]) / DT(2);
+  const double cx = (double)cxd, cy = (double)cyd;
+  Num fac[3];
+  int nf = 0;
+  // 1. position jump: the centre against the mean of the last <= 3 history entries
+  if (s.ph_len >= 2) {
+    const int m = s.ph_len < 3 ? s.ph_len : 3;
+    int id[3];
+    bool all32 = true;
+    for (int k = 0; k < m; ++k) {
+      id[k] = ring_at<8>(s.ph_head, s.ph_len - m + k);
+      all32 = all32 && s.ph32[id[k]];
+    }
+    double avg[2];
+    for (int j = 0; j < 2; ++j) {  // np.mean(axis=0): rows accumulated in order
+      if (all32) {
+        float acc = (float)s.ph[id[0]][j];
+        for (int k = 1; k < m; ++k) acc = acc + (float)s.ph[id[k]][j];
+        avg[j] = (double)(acc / (float)m);
+      } else {
+        double acc = s.ph[id[0]][j];
+        for (int k = 1; k < m; ++k) acc = acc + s.ph[id[k]][j];
+        avg[j] = acc / (double)m;
+      }
+    }
+    const bool d32 = all32 && c32;
+    const Num dist = norm2(sub_k(cx, avg[0], d32), sub_k(cy, avg[1], d32), d32);
+    const Num sc = pymin_c(div_c(dist, 40.0), 3.0);
+    const int p = ring_slot<10>(s.ms_len, s.ms_head);
+    s.ms[p] = sc.v;
+    s.mk[p] = (unsigned char)sc.k;
+    if (gt_c(dist, 40.0)) {
+      why |= 1;
+      val[0] = dist.v;
+      fac[nf++] = pymin_c(div_c(dist, 40.0), 2.0);
+    }
+  }
+  // 2. velocity change: the newest step length against the mean of the two before it
+  if (s.ph_len >= 3) {
+    double px[4], py[4];
+    bool p32[4];
+    for (int k = 0; k < 3; ++k) {
+      const int i = ring_at<8>(s.ph_head, s.ph_len - 3 + k);
+      px[k] = s.ph[i][0];
+      py[k] = s.ph[i][1];
+      p32[k] = s.ph32[i] != 0;
+    }
+    px[3] = cx;
+    py[3] = cy;
+    p32[3] = c32;
+    Num sp[3];
+    for (int k = 1; k < 4; ++k) {
+      const bool f = p32[k] && p32[k - 1];
+      sp[k - 1] = norm2(sub_k(px[k], px[k - 1], f), sub_k(py[k], py[k - 1], f), f);
+    }
+    const Num avg = np_mean_list(sp, 2);
+    const bool f = sp[2].k == K32 && avg.k == K32;
+    const Num ch{fabs(sub_k(sp[2].v, avg.v, f)), f ? K32 : K64};
+    if (gt_c(ch, 60.0)) {
+      why |= 2;
+      val[1] = ch.v;
+      fac[nf++] = pymin_c(div_c(ch, 60.0), 2.0);
+    }
+  }
+  // 3. size change against the previous detection box (the detection's dtype throughout)
+  if (s.bh_len >= 2) {
+    const double* q = s.bh[ring_at<5>(s.bh_head, s.bh_len - 1)];
+    DT pw = (DT)q[2] - (DT)q[0], ph = (DT)q[3] - (DT)q[1];
+    pw = pw < DT(1) ? DT(1) : pw;  // np.maximum(prev_size, 1.0)
+    ph = ph < DT(1) ? DT(1) : ph;
+    const DT r0 = (b[2] - b[0]) / pw, r1 = (b[3] - b[1]) / ph;
+    const DT a0 = r0 - DT(1) < DT(0) ? DT(1) - r0 : r0 - DT(1);
+    const DT a1 = r1 - DT(1) < DT(0) ? DT(1) - r1 : r1 - DT(1);
+    const DT r = a1 > a0 ? a1 : a0;  // python max keeps the first on ties
+    const Num rn{(double)r, c32 ? K32 : K64};
+    if (gt_c(rn, 0.3)) {
+      why |= 4;
+      val[2] = rn.v;
+      fac[nf++] = div_c(rn, 0.3);
+    }
+  }
+  if (nf == 0) return false;
+  conf = np_mean_list(fac, nf);
+  const Num cons = cmc_consistency(s);
+  s.consistency = cons.v;
+  if (lt_c(cons, 0.3)) conf = mul_c(conf, 1.5);
+  if (s.reset_count > 0 && since < 50) conf = mul_c(conf, 0.8);  // adaptive_enabled
+  return conf.v > 1.0;
+}
+
+// _reset_kalman_filter (:216-259)
+template <typename DT>
+__device__ void cmc_reset(Slot& s, const DT* b, const double* val, int why, Num conf) {
+  s.reset_count += 1;
+  s.last_reset = s.age;
+  ResetDetail& d = s.dl[ring_slot<5>(s.dl_len, s.dl_head)];
+  d.frame = s.age;
+  d.reasons = why;
+  for (int k = 0; k < 3; ++k) {
+    d.value[k] = (why >> k) & 1 ? val[k] : 0.0;
+    s.reason_count[k] += (why >> k) & 1;
+  }
+  d.conf = conf.v;
+  d.cons = s.consistency;
+  s.conf_sum += conf.v;
+  s.cons_sum += s.consistency;
+  double z[4];
+  bbox_to_state<DT>(b, z);
+  for (int c = 0; c < 4; ++c) {
+    s.x[c] = z[c];
+    s.x[c + 4] = 0.0;
+    s.P[4 * c + 0] = s.P[4 * c + 0] * 5.0;    // P[:4, :4] *= 5 (only the diagonal is non-zero)
+    s.P[4 * c + 3] = s.P[4 * c + 3] * 100.0;  // P[4:, 4:] *= 100
+  }
+  s.th_len = s.th_head = 0;
+  ring_push(s.th, TH, s.th_len, s.th_head, z[0], z[1]);
+  s.vh_len = s.vh_head = 0;
+  s.ph_len = s.ph_head = 0;
+  ph_push(s, z[0], z[1], sizeof(DT) == 4);
+  s.ms_len = s.ms_head = 0;
+  s.hits += 1;
+  s.hit_streak += 1;
+  s.tsu = 0;
+}
+
+// update() tail (:280-285): the detection centre and box join the histories
+template <typename DT>
+__device__ void cmc_after_update(Slot& s, const DT* b) {
+  const DT cx = (b[0] + b[2]) / DT(2), cy = (b[1] + b[3]) / DT(2);
+  ph_push(s, (double)cx, (double)cy, sizeof(DT) == 4);
+  const int p = ring_slot<5>(s.bh_len, s.bh_head);
+  for (int k = 0; k < 4; ++k) s.bh[p][k] = (double)b[k];
+}
+
+// predict() (:287-312): for 10 frames after a reset the returned box's centre is blended from
+// the last history position toward the prediction (the state itself is not changed)
+__device__ void cmc_blend(const Slot& s, double* box) {
+  const int since = s.age - s.last_reset;
+  if (since >= 10 || s.ph_len == 0) return;
+  const int li = ring_at<8>(s.ph_head, s.ph_len - 1);
+  double w = (double)since / 10.0;
+  w = 1.0 < w ? 1.0 : w;
+  const double pcx = (box[0] + box[2]) / 2.0, pcy = (box[1] + box[3]) / 2.0;
+  double t0, t1;
+  if (s.ph32[li]) {  // python float x float32 array stays float32
+    const float om = (float)(1.0 - w);
+    t0 = (double)(om * (float)s.ph[li][0]);
+    t1 = (double)(om * (float)s.ph[li][1]);
+  } else {
+    t0 = (1.0 - w) * s.ph[li][0];
+    t1 = (1.0 - w) * s.ph[li][1];
+  }
+  const double ax = t0 + w * pcx, ay = t1 + w * pcy;
+  const double sw = box[2] - box[0], sh = box[3] - box[1];
+  box[0] = ax - sw / 2.0;
+  box[1] = ay - sh / 2.0;
+  box[2] = ax + sw / 2.0;
+  box[3] = ay + sh / 2.0;
+}
+
 constexpr int VS = VH + 1;  // staged entries per array (one spare for the push onto a full ring)
 
 // Chronological copy of the velocity history (before an update) into st[3][VS].
@@ -308,6 +642,7 @@ __device__ void long_term_predict(Slot& s, int k, double* box, double& conf) {
   if (k <= 1) {
     kf_predict(s);
     state_to_bbox(s.x, box);
+    if (s.policy) cmc_blend(s, box);  // the subclass's predict()
     conf = 1.0;
     return;
   }
@@ -379,6 +714,22 @@ __device__ void track_info(Slot& s, yk_track_out& o, bool copy_traj = true) {
   o.motion_confidence = s.pconf;
   o.speed = s.speed;
   o.direction = s.direction;
+  // MotionResetKalmanTracker.get_track_info / get_reset_statistics (:314-355)
+  o.reset_count = s.policy ? s.reset_count : 0;
+  o.frames_since_reset = s.policy ? s.age - s.last_reset : 0;
+  o.n_details = s.policy ? s.dl_len : 0;
+  for (int k = 0; k < 3; ++k) o.reason_count[k] = s.policy ? s.reason_count[k] : 0;
+  o.motion_consistency = s.policy ? s.consistency : 0.0;
+  o.reset_confidence_sum = s.policy ? s.conf_sum : 0.0;
+  o.motion_consistency_sum = s.policy ? s.cons_sum : 0.0;
+  for (int k = 0; k < o.n_details; ++k) {
+    const ResetDetail& d = s.dl[ring_at<5>(s.dl_head, k)];
+    o.details[k].frame = d.frame;
+    o.details[k].reasons = d.reasons;
+    for (int j = 0; j < 3; ++j) o.details[k].value[j] = d.value[j];
+    o.details[k].confidence = d.conf;
+    o.details[k].motion_consistency = d.cons;
+  }
   const int nt = s.th_len < TOUT ? s.th_len : TOUT;
   o.traj_len = nt;
   if (!copy_traj) return;  // the step kernel copies trajectories cooperatively
@@ -495,7 +846,7 @@ __device__ Lds carve(char* base, int T, int D) {
   return L;
 }
 
-enum { M_NCAND = 0, M_ACTIVE, M_RECOVER, M_LONGTERM, M_OVERFLOW, M_WSUM = 8 };
+enum { M_NCAND = 0, M_ACTIVE, M_RECOVER, M_LONGTERM, M_OVERFLOW, M_RESETS, M_TRECOV, M_WSUM = 8 };
 
 // ---------------------------------------------------------------- the step kernel
 template <typename DT>
@@ -529,6 +880,7 @@ __global__ void __launch_bounds__(NT) step_kernel(Dev g, const DT* __restrict__ 
     Slot& sl = slots[order[i]];
     kf_predict(sl);
     state_to_bbox(sl.x, &L.pb[4 * i]);
+    if (sl.policy) cmc_blend(sl, &L.pb[4 * i]);
   }
   __syncthreads();
   if (tid == 0) g.phase[s * 16 + 1] = wall_clock64();
@@ -544,7 +896,8 @@ __global__ void __launch_bounds__(NT) step_kernel(Dev g, const DT* __restrict__ 
 #pragma unroll
       for (int k = 0; k < 4; ++k) db[k] = (DT)L.det[4 * d + k];
       const double v = iou_mixed<DT>(db, &L.pb[4 * t]);
-      if (v >= g.thr) {
+      // enhanced: iou >= thr (multi:245); motion-reset: iou > thr (motion_compensated_multi_tracker.py:260)
+      if (g.policy ? v > g.thr : v >= g.thr) {
         const int c = atomicAdd(&L.misc[M_NCAND], 1);
         if (c < g.C) {
           ckey[c] = (unsigned long long)__double_as_longlong(v);
@@ -586,18 +939,22 @@ __global__ void __launch_bounds__(NT) step_kernel(Dev g, const DT* __restrict__ 
         if (tid == 0) g.phase[s * 16 + 10] = round;
         break;
       }
+      // among equal IoUs the enhanced tracker takes the lowest row-major pair first (stable
+      // argsort), the motion-reset tracker the highest (sorted (iou, d, t) tuples, reverse)
       for (int c = tid; c < nc; c += NT) {
         const int f = cflat[c], d = f / n, t = f - d * n;
         if (L.det_match[d] < 0 && L.trk_match[t] < 0) {
           const unsigned long long k = ckey[c];
-          if (k == L.row_max[d]) atomicMin(&L.row_arg[d], f);
-          if (k == L.col_max[t]) atomicMin(&L.col_arg[t], f);
+          const int rk = g.policy ? npair - 1 - f : f;
+          if (k == L.row_max[d]) atomicMin(&L.row_arg[d], rk);
+          if (k == L.col_max[t]) atomicMin(&L.col_arg[t], rk);
         }
       }
       __syncthreads();
       for (int c = tid; c < nc; c += NT) {
         const int f = cflat[c], d = f / n, t = f - d * n;
-        if (L.row_arg[d] == f && L.col_arg[t] == f) {
+        const int rk = g.policy ? npair - 1 - f : f;
+        if (L.row_arg[d] == rk && L.col_arg[t] == rk) {
           L.det_match[d] = t;
           L.trk_match[t] = d;
         }
@@ -611,7 +968,7 @@ __global__ void __launch_bounds__(NT) step_kernel(Dev g, const DT* __restrict__ 
   // tracks' velocity rings (1.2 KB each) are staged into LDS CH tracks at a time by the whole
   // workgroup (coalesced 16-B loads, all in flight at once); each track's thread then runs
   // the KF update and analyze_motion_pattern's serial reductions out of LDS.
-  int recov = 0;
+  int recov = 0, resets = 0;
   int n_upd = 0;
   for (int base = 0; base < n; base += NT) {
     const int i = base + tid;
@@ -647,12 +1004,27 @@ __global__ void __launch_bounds__(NT) step_kernel(Dev g, const DT* __restrict__ 
       DT db[4];
 #pragma unroll
       for (int k = 0; k < 4; ++k) db[k] = (DT)L.det[4 * d + k];
-      recov += sl.is_lost ? 1 : 0;
-      kf_update<DT>(sl, db, L.stage + (size_t)tid * STAGE_D);
+      if (sl.policy) {  // MotionResetKalmanTracker.update (:261-285)
+        double val[3] = {0.0, 0.0, 0.0};
+        int why = 0;
+        Num conf{0.0, KPY};
+        if (cmc_decide<DT>(sl, db, val, why, conf)) {
+          cmc_reset<DT>(sl, db, val, why, conf);
+          ++resets;
+        } else {
+          kf_update<DT>(sl, db, L.stage + (size_t)tid * STAGE_D);
+          ph_push(sl, sl.x[0], sl.x[1], false);  // the base update's position_history append
+        }
+        cmc_after_update<DT>(sl, db);
+      } else {
+        recov += sl.is_lost ? 1 : 0;
+        kf_update<DT>(sl, db, L.stage + (size_t)tid * STAGE_D);
+      }
     }
     __syncthreads();
   }
   if (recov) atomicAdd(&L.misc[M_RECOVER], recov);
+  if (resets) atomicAdd(&L.misc[M_RESETS], resets);
   __syncthreads();
   if (tid == 0) g.phase[s * 16 + 4] = wall_clock64();
 
@@ -675,6 +1047,7 @@ __global__ void __launch_bounds__(NT) step_kernel(Dev g, const DT* __restrict__ 
         double z[4];
         bbox_to_state<DT>(db, z);
         slot_init(slots[slot], z, next_num + r, g.max_lost);
+        if (g.policy) cmc_init<DT>(slots[slot], db);
         order[pos] = slot;
       } else {
         atomicAdd(&L.misc[M_OVERFLOW], 1);
@@ -721,6 +1094,8 @@ __global__ void __launch_bounds__(NT) step_kernel(Dev g, const DT* __restrict__ 
       int tot;
       const int r = pushed + block_scan(del, wsum, tot);
       if (del) fstack[nfree_after_pop + r] = slot;
+      // motion-reset stats['tracking_recoveries']: deleted trackers that had been reset
+      if (del && slots[slot].policy && slots[slot].reset_count > 0) atomicAdd(&L.misc[M_TRECOV], 1);
       pushed += tot;
     }
   }
@@ -740,14 +1115,15 @@ __global__ void __launch_bounds__(NT) step_kernel(Dev g, const DT* __restrict__ 
     Slot* sl = nullptr;
     if (i < kept) {
       sl = &slots[order[i]];
-      q = (sl->hit_streak >= g.min_hits || fc <= g.min_hits || sl->is_lost) ? 1 : 0;
+      // the motion-reset tracker reports every live tracker (motion_compensated_multi_tracker.py:369-386)
+      q = (g.policy || sl->hit_streak >= g.min_hits || fc <= g.min_hits || sl->is_lost) ? 1 : 0;
     }
     int tot;
     const int r = nout + block_scan(q, wsum, tot);
     if (q) {
       yk_track_out& o = g.rows[(size_t)s * T + r];
       track_info(*sl, o, false);
-      if (o.status == 1 && o.time_since_update > 30) ++lt;
+      if (!g.policy && o.status == 1 && o.time_since_update > 30) ++lt;
       L.order_tmp[r] = order[i];
     }
     nout += tot;
@@ -778,6 +1154,8 @@ __global__ void __launch_bounds__(NT) step_kernel(Dev g, const DT* __restrict__ 
     H.st.current_active_tracks = kept;
     H.st.long_term_predictions += L.misc[M_LONGTERM];
     H.st.successful_recoveries += L.misc[M_RECOVER];
+    H.st.individual_resets += L.misc[M_RESETS];
+    H.st.tracking_recoveries += L.misc[M_TRECOV];
     H.st.overflow += L.misc[M_OVERFLOW] + (Draw - D);
     g.counts[s] = nout;
     g.stats[s] = H.st;
@@ -862,13 +1240,23 @@ __global__ void track_op_kernel(Dev g, int s, int pos, int op, int arg, const do
     case YK_OP_PREDICT:
       kf_predict(sl);
       state_to_bbox(sl.x, out5);
+      if (sl.policy) cmc_blend(sl, out5);
       break;
     case YK_OP_UPDATE: {
       DT b[4];
       for (int k = 0; k < 4; ++k) b[k] = (DT)in_box[k];
       double st[3 * VS];
       stage_chrono(sl, st);
-      kf_update<DT>(sl, b, st);
+      double val[3] = {0.0, 0.0, 0.0};
+      int why = 0;
+      Num conf{0.0, KPY};
+      if (sl.policy && cmc_decide<DT>(sl, b, val, why, conf)) {
+        cmc_reset<DT>(sl, b, val, why, conf);
+      } else {
+        kf_update<DT>(sl, b, st);
+        if (sl.policy) ph_push(sl, sl.x[0], sl.x[1], false);
+      }
+      if (sl.policy) cmc_after_update<DT>(sl, b);
       break;
     }
     case YK_OP_MARK_LOST:
@@ -903,6 +1291,7 @@ __global__ void track_create_kernel(Dev g, int s, const double* in_box, int trac
   double z[4];
   bbox_to_state<DT>(b, z);
   slot_init(g.slots[(size_t)s * g.T + slot], z, track_num, max_lost);
+  if (g.policy) cmc_init<DT>(g.slots[(size_t)s * g.T + slot], b);
   g.order[(size_t)s * g.T + H.n_tracks] = slot;
   H.n_tracks += 1;
   *status = 0;
@@ -933,6 +1322,8 @@ int yk_tracker_create(yk_ctx* ctx, int n_streams, const yk_tracker_cfg* cfg, yk_
   YK_CHECK_ARG(cfg->max_tracks >= 1 && cfg->max_tracks <= 2048, "yk_tracker_create: max_tracks must be in [1, 2048]");
   YK_CHECK_ARG(cfg->max_dets >= 1 && cfg->max_dets <= 1024, "yk_tracker_create: max_dets must be in [1, 1024]");
   YK_CHECK_ARG(cfg->max_lost_frames >= 0, "yk_tracker_create: max_lost_frames must be >= 0");
+  YK_CHECK_ARG(cfg->policy == YK_POLICY_ENHANCED || cfg->policy == YK_POLICY_MOTION_RESET,
+               "yk_tracker_create: unknown tracker policy");
   const size_t lds = yk::trk::lds_bytes(cfg->max_tracks, cfg->max_dets);
   YK_CHECK_ARG(yk::trk::stage_chunk(cfg->max_tracks, cfg->max_dets) >= 1 && lds <= 160 * 1024,
                "yk_tracker_create: max_tracks x max_dets exceed the 160 KiB LDS budget");
@@ -949,6 +1340,7 @@ int yk_tracker_create(yk_ctx* ctx, int n_streams, const yk_tracker_cfg* cfg, yk_
   g.max_lost = cfg->max_lost_frames;
   g.min_hits = cfg->min_hits;
   g.thr = cfg->iou_threshold;
+  g.policy = cfg->policy;
   const size_t S = n_streams, T = g.T;
   hipError_t e = hipSuccess;
   auto A = [&](void** p, size_t bytes) {

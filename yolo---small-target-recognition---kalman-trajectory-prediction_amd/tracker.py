@@ -7,6 +7,10 @@ Reference surface (kalman/__init__.py:28-33):
   AircraftKalmanTracker / EnhancedAircraftKalmanTracker(initial_bbox, track_id=None,
       max_lost_frames=450)                         enhanced_aircraft_kalman_tracker.py:7-408
   MultiTargetTracker = EnhancedMultiTargetTracker
+and of the camera-motion-compensation variant:
+  MotionCompensatedMultiTracker(max_lost_frames=150, min_hits=1, iou_threshold=0.1)
+      .update(detections, frame=None)              motion_compensated_multi_tracker.py:77-242
+  over MotionResetKalmanTracker tracks             motion_reset_kalman_tracker.py:16-355
 
 All filter arithmetic, association and lifecycle run in libyk.so's HIP kernels
 (csrc/tracker.hip); this module only marshals detections in and dicts out.
@@ -81,18 +85,63 @@ def track_id_of(num: int) -> str:
     return f"T{int(num):03d}"
 
 
+_REASONS = ("position", "velocity", "size")
+
+
+def _reason_text(kind: int, value: float) -> str:
+    # the reason strings of motion_reset_kalman_tracker.py:105, :134, :155
+    return (f"position_jump_{value:.1f}px", f"velocity_change_{value:.1f}px/f", f"size_change_{value:.2f}")[kind]
+
+
+def _reset_fields(r, info: dict) -> dict:
+    """MotionResetKalmanTracker.get_track_info extras + get_reset_statistics
+    (motion_reset_kalman_tracker.py:314-355) from one yk_track_out row."""
+    n, since = int(r["reset_count"]), int(r["frames_since_reset"])
+    info["reset_count"] = n
+    info["frames_since_reset"] = since
+    info["motion_consistency"] = f"{float(r['motion_consistency']):.2f}"
+    if n == 0:
+        info["status_suffix"] = ""
+    elif since < 20:
+        info["status_suffix"] = f" | 重置({since}f前)"
+    elif n == 1:
+        info["status_suffix"] = " | 已重置1次"
+    else:
+        info["status_suffix"] = f" | 已重置{n}次"
+    if n == 0:
+        info["reset_statistics"] = {"total_resets": 0, "details": []}
+        return info
+    details = []
+    for d in r["details"][: int(r["n_details"])]:
+        reasons = [_reason_text(k, float(d["value"][k])) for k in range(3) if (int(d["reasons"]) >> k) & 1]
+        details.append({"frame": int(d["frame"]), "reasons": reasons, "confidence": float(d["confidence"]),
+                        "motion_consistency": float(d["motion_consistency"])})
+    info["reset_statistics"] = {
+        "total_resets": n,
+        "reason_distribution": {_REASONS[k]: int(r["reason_count"][k]) for k in range(3) if int(r["reason_count"][k])},
+        # averages accumulated in float64 over every reset (the reference's np.mean of the
+        # logged values; identical unless every logged value is a float32 scalar)
+        "avg_confidence": float(r["reset_confidence_sum"]) / n,
+        "avg_motion_consistency": float(r["motion_consistency_sum"]) / n,
+        "details": details,
+    }
+    return info
+
+
 class MultiStreamTracker:
     """``n_streams`` independent EnhancedMultiTargetTracker instances stepped by one
     kernel launch (one workgroup per stream).  Detections and results stay in HBM."""
 
     def __init__(self, n_streams: int = 1, max_lost_frames: int = 450, min_hits: int = 3,
                  iou_threshold: float = 0.3, max_tracks: int = 1024, max_dets: int = 1024,
-                 device: int = 0):
+                 device: int = 0, policy: int = L.POLICY_ENHANCED):
         self.n_streams, self.device = int(n_streams), int(device)
         self.max_lost_frames, self.min_hits, self.iou_threshold = int(max_lost_frames), int(min_hits), float(iou_threshold)
         self.max_tracks, self.max_dets = int(max_tracks), int(max_dets)
         ctx = L.context(self.device)
-        cfg = L.TrackerCfg(self.max_lost_frames, self.min_hits, self.iou_threshold, self.max_tracks, self.max_dets)
+        self.policy = int(policy)
+        cfg = L.TrackerCfg(self.max_lost_frames, self.min_hits, self.iou_threshold, self.max_tracks, self.max_dets,
+                           self.policy)
         h = C.c_void_p()
         L.check(L.lib().yk_tracker_create(ctx, self.n_streams, C.byref(cfg), C.byref(h)), "yk_tracker_create")
         self._h = h
@@ -427,3 +476,54 @@ class EnhancedMultiTargetTracker:
 
 
 MultiTargetTracker = EnhancedMultiTargetTracker
+
+
+class MotionCompensatedMultiTracker:
+    """Drop-in for camera_motion_compensation.MotionCompensatedMultiTracker
+    (motion_compensated_multi_tracker.py:18-394) without a frame: ``update(detections)`` runs
+    the motion-reset policy of the batched HIP tracker kernel (YK_POLICY_MOTION_RESET):
+    MotionResetKalmanTracker jump / velocity / size-change resets, blended predict after a
+    reset, strict iou > thr with the (iou, d, t)-descending greedy order, every live tracker
+    reported with its reset fields.  Global camera-motion detection needs frames and cv2
+    optical flow (global_motion_detector.py) and is not on this path: passing a frame raises.
+    Track ids are "T%03d" of the creation index (the reference draws uuid4 strings)."""
+
+    def __init__(self, max_lost_frames=150, min_hits=1, iou_threshold=0.1, motion_detection_method="optical_flow",
+                 *, max_tracks: int = 1024, max_dets: int = 1024, device: int = 0):
+        self.max_lost_frames, self.min_hits, self.iou_threshold = max_lost_frames, min_hits, iou_threshold
+        self.motion_detection_method = motion_detection_method
+        self.global_motion_compensation = True
+        self.individual_reset_enabled = True
+        self.adaptive_thresholds = True
+        self._core = MultiStreamTracker(1, max_lost_frames, min_hits, iou_threshold, max_tracks, max_dets, device,
+                                        policy=L.POLICY_MOTION_RESET)
+        self._stats = np.zeros(1, dtype=L.STATS_DTYPE)[0]
+        self.detection_stability_history = deque(maxlen=10)
+        self.frame_motion_info = None
+
+    @property
+    def frame_count(self) -> int:
+        return int(self._stats["frame_count"])
+
+    @property
+    def stats(self) -> dict:
+        s = self._stats
+        return {"total_frames": int(s["frame_count"]), "global_motion_events": 0, "global_resets": 0,
+                "individual_resets": int(s["individual_resets"]), "tracking_recoveries": int(s["tracking_recoveries"])}
+
+    def update(self, detections, frame=None):
+        if frame is not None:
+            raise NotImplementedError("global camera-motion detection (cv2 optical flow on frames) is not on the "
+                                      "MI355X path; call update(detections) for the per-track motion resets")
+        self.detection_stability_history.append(len(detections))
+        self._core.step_host([detections])
+        rows, counts, stats = self._core.download()
+        self._stats = stats[0].copy()
+        if int(self._stats["overflow"]):
+            raise L.YKError(f"tracker capacity exceeded (max_tracks={self._core.max_tracks})")
+        return [_reset_fields(r, _row_to_dict(r, track_id_of(r["track_num"]))) for r in rows[0, : int(counts[0])]]
+
+    def get_comprehensive_stats(self):
+        snap = self._core.snapshot(0)
+        return {"basic": self.stats, "motion_detection": {}, "performance": {},
+                "trackers": {"active_trackers": int(len(snap))}, "motion_history_avg": 0.0}
