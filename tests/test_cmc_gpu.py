@@ -98,10 +98,12 @@ def test_motion_reset_multi_stream_batch():
 
 
 def test_motion_reset_exact_tie_takes_highest_detection():
-    """Two identical detections over one track: the (iou, d, t)-descending order gives the
-    track to the LAST detection (the enhanced tracker gives it to the first)."""
+    """Two detections with exactly equal IoU against one track (mirror images about its
+    centre): the (iou, d, t)-descending order gives the track to the LATER detection (the
+    enhanced tracker's stable order gives it to the first)."""
     f = np.float32
-    a = [f(50), f(50), f(60), f(60), f(.9)]
-    frames = [[a], [a, list(a)], [a, list(a)]]
-    ours, ref = run_pair(frames)
-    assert len(ref.trackers) == 3
+    t0 = [f(50), f(50), f(60), f(60), f(.9)]
+    d0 = [f(49), f(50), f(59), f(60), f(.9)]
+    d1 = [f(51), f(50), f(61), f(60), f(.8)]
+    ours, ref = run_pair([[t0], [d0, d1], [d0, d1]])
+    assert ref.trackers[0].x[0] > 55.0  # track 1 moved toward d1

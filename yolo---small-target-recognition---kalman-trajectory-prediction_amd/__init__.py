@@ -16,6 +16,7 @@ from .tracker import (  # noqa: F401
     AircraftKalmanTracker,
     EnhancedAircraftKalmanTracker,
     EnhancedMultiTargetTracker,
+    MotionCompensatedMultiTracker,
     MultiStreamTracker,
     MultiTargetTracker,
 )

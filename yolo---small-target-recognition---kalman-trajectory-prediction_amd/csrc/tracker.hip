@@ -730,6 +730,11 @@ __device__ void track_info(Slot& s, yk_track_out& o, bool copy_traj = true) {
     o.details[k].confidence = d.conf;
     o.details[k].motion_consistency = d.cons;
   }
+  for (int k = o.n_details; k < 5; ++k) {  // rows are compared bytewise: no stale bytes
+    o.details[k].frame = o.details[k].reasons = 0;
+    for (int j = 0; j < 3; ++j) o.details[k].value[j] = 0.0;
+    o.details[k].confidence = o.details[k].motion_consistency = 0.0;
+  }
   const int nt = s.th_len < TOUT ? s.th_len : TOUT;
   o.traj_len = nt;
   if (!copy_traj) return;  // the step kernel copies trajectories cooperatively
