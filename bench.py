@@ -57,6 +57,9 @@ def parse():
     ap.add_argument("--lanes", type=int, default=None,
                     help="streams per batch group the detector's op DAG runs on (default 1 with --inflight > 1, else 3)")
     ap.add_argument("--groups", type=int, default=1, help="independent sub-batches run concurrently")
+    ap.add_argument("--tracker", default="enhanced", choices=["enhanced", "motion_reset"],
+                    help="tracker: kalman.EnhancedMultiTargetTracker (the driver's) or the camera_motion_compensation "
+                         "MotionCompensatedMultiTracker policy (frame-free)")
     ap.add_argument("--inflight", type=int, default=3, choices=[1, 2, 3, 4],
                     help="detector forwards in flight (each a batch of all streams, own graph + HIP stream)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -140,7 +143,7 @@ def tracker_roofline(pipe, reps=20):
             "achieved": round(gbps, 3), "peak": HBM_PEAK, "unit": "GB/s", "frac": round(gbps / HBM_PEAK, 6)}
 
 
-def cpu_baseline(P, scale, seconds, targets, seed=0, hw=(512, 640), imgsz=640):
+def cpu_baseline(P, scale, seconds, targets, seed=0, hw=(512, 640), imgsz=640, tracker="enhanced"):
     """Reference-equivalent CPU path (oracle: torch-CPU fp32 YOLOv8s+P2 + numpy tracker) on a
     bounded sample of one stream, threads as the reference's select_device: min(8, ncpu-1)."""
     from oracle import detector_ref as D
@@ -154,7 +157,11 @@ def cpu_baseline(P, scale, seconds, targets, seed=0, hw=(512, 640), imgsz=640):
               for Ly in ar.layers]
     det = D.RefDetector(layers, sd, P.arch.detect_strides(ar))
     sc = P.synth.Scene(seed=seed, n_targets=targets, n_frames=400, height=hw[0], width=hw[1])
-    trk = RefMultiTracker(150, 1, 0.1)
+    if tracker == "motion_reset":
+        from oracle.cmc_ref import RefCMCMultiTracker
+        trk = RefCMCMultiTracker(150, 1, 0.1)
+    else:
+        trk = RefMultiTracker(150, 1, 0.1)
     n, t_total = 0, 0.0
     for t in range(400):
         f = sc.frame(t)
@@ -172,7 +179,7 @@ def cpu_baseline(P, scale, seconds, targets, seed=0, hw=(512, 640), imgsz=640):
                 break
     return {"value": round(n / t_total, 3), "unit": "frames/s", "cores": threads, "kind": "port",
             "sample": f"{n} frames of one {hw[1]}x{hw[0]} stream ({targets} targets), YOLOv8{scale}+P2 fp32 torch-CPU "
-                      f"({threads} threads) + numpy tracker, after 2 warm-up frames"}
+                      f"({threads} threads) + numpy {tracker} tracker, after 2 warm-up frames"}
 
 
 def log(msg):
@@ -202,7 +209,8 @@ def main():
     my_streams = shard.stream_ids(rank, ws, S)  # this GPU's block of independent streams
     pipe = pipeline.StreamPipeline(f"yolov8{a.scale}-small.yaml", S, (H, W), a.dtype, seed=0, device=local,
                                    pipelined=not a.no_pipeline, imgsz=imgsz, max_tracks=max_tracks,
-                                   inflight=1 if a.no_pipeline else a.inflight)
+                                   inflight=1 if a.no_pipeline else a.inflight,
+                                   tracker_policy=1 if a.tracker == "motion_reset" else 0)
     # pre-render frames of every stream into HBM (inputs resident before the timed region)
     F = max(2, min(a.frames, a.warmup + a.steps))
     scenes = [P.synth.Scene(seed=shard.stream_seed(g, S), n_targets=a.targets, n_frames=F + 1, width=W, height=H)
@@ -282,7 +290,7 @@ def main():
     log("profile done")
     cpu = None
     if rank == 0 and ws == 1 and not a.no_cpu_baseline:
-        cpu = cpu_baseline(P, a.scale, a.cpu_seconds, a.targets, hw=(H, W), imgsz=imgsz)
+        cpu = cpu_baseline(P, a.scale, a.cpu_seconds, a.targets, hw=(H, W), imgsz=imgsz, tracker=a.tracker)
     if rank == 0:
         gflop = pipe.flops_per_frame() / 1e9
         out = {
@@ -292,7 +300,7 @@ def main():
             "data": f"synthetic: seeded {W}x{H} IR-like scenes rendered into HBM before timing; seeded "
                     "planted weights (no trained best.pt in the reference)",
             "config": {"workload": f"YOLOv8{a.scale}+P2 {W}x{H} (imgsz {imgsz}), {S} streams/GPU as batch {S}, "
-                                   f"{a.targets} targets/stream, tracker(150, 1, 0.1) (BASELINE config {a.config})",
+                                   f"{a.targets} targets/stream, {a.tracker} tracker(150, 1, 0.1) (BASELINE config {a.config})",
                        "streams_per_gpu": S, "global_batch": S * ws, "parallelism": f"streams sharded over {ws} GPU(s)",
                        "graph": not a.no_graph, "tracker_overlapped": not a.no_pipeline, "autotuned": not a.no_tune, "dag_lanes": a.lanes,
                        "batch_groups": a.groups, "detector_inflight": pipe.D,

@@ -36,7 +36,8 @@ class StreamPipeline:
     def __init__(self, model_cfg: str = "yolov8s-small.yaml", n_streams: int = 8, frame_hw=(512, 640),
                  dtype: str = "bf16", weights=None, seed: int = 0, conf: float = 0.25, iou: float = 0.7,
                  max_det: int = 300, max_lost_frames: int = 150, min_hits: int = 1, iou_threshold: float = 0.1,
-                 max_tracks: int = 512, device: int = 0, pipelined: bool = False, imgsz=640, inflight: int = 1):
+                 max_tracks: int = 512, device: int = 0, pipelined: bool = False, imgsz=640, inflight: int = 1,
+                 tracker_policy: int = 0):
         if conf < 0.1:
             raise ValueError("conf < 0.1 would need the driver's score > 0.1 filter on the device path")
         self.S, self.device = int(n_streams), int(device)
@@ -46,7 +47,8 @@ class StreamPipeline:
         self.prog = M.Program(ar, sd, frame_hw[0], frame_hw[1], imgsz, self.S, dtype, self.max_det)
         self.model = M.DeviceModel(self.prog, self.device)
         self.tracker = T.MultiStreamTracker(self.S, max_lost_frames, min_hits, iou_threshold, max_tracks,
-                                            self.max_det, self.device)
+                                            self.max_det, self.device,
+                                            policy=tracker_policy)
         dev = torch.device("cuda", self.device)
         self.frames = torch.zeros((self.S, frame_hw[0], frame_hw[1], 3), dtype=torch.uint8, device=dev)
         self.nb = max(2, int(inflight))  # detection buffers (= detector slots when inflight > 1)
