@@ -60,7 +60,7 @@ def parse():
     ap.add_argument("--tracker", default="enhanced", choices=["enhanced", "motion_reset"],
                     help="tracker: kalman.EnhancedMultiTargetTracker (the driver's) or the camera_motion_compensation "
                          "MotionCompensatedMultiTracker policy (frame-free)")
-    ap.add_argument("--inflight", type=int, default=3, choices=[1, 2, 3, 4],
+    ap.add_argument("--inflight", type=int, default=3, choices=range(1, 9),
                     help="detector forwards in flight (each a batch of all streams, own graph + HIP stream)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)

@@ -883,13 +883,25 @@ __global__ void __launch_bounds__(256) conv_fast_kernel(FastArgs a) {
     }
     ks += SKD;
   }
-  // short K ranges and the tail: one step at a time
-  for (; ks < k1; ++ks) {
-    load_step(ks, wb[0], xb[0]);
+  // short K ranges (the split-K waves of the low-resolution layers own 3-11 steps) and the
+  // tail: up to SKD steps of loads in flight, refilled as each step's MFMAs consume them
+  // (ks and k1 are wave-uniform: the guards are scalar branches)
+  if (ks < k1) {
 #pragma unroll
-    for (int i = 0; i < NNT; ++i)
+    for (int d = 0; d < SKD; ++d)
+      if (ks + d < k1) load_step(ks + d, wb[d], xb[d]);
+    for (; ks < k1; ks += SKD) {
 #pragma unroll
-      for (int t = 0; t < NPT; ++t) acc[i][t] = mma<Tr>(wb[0][i], xb[0][t], acc[i][t]);
+      for (int d = 0; d < SKD; ++d) {
+        if (ks + d < k1) {
+#pragma unroll
+          for (int i = 0; i < NNT; ++i)
+#pragma unroll
+            for (int t = 0; t < NPT; ++t) acc[i][t] = mma<Tr>(wb[d][i], xb[d][t], acc[i][t]);
+          if (ks + d + SKD < k1) load_step(ks + d + SKD, wb[d], xb[d]);
+        }
+      }
+    }
   }
   if constexpr (WS) {
     f32x4* red = (f32x4*)(smem + (((size_t)nk * 4 * 8 + 15) & ~(size_t)15));
@@ -2137,6 +2149,7 @@ struct yk_model {
   bool input_valu = false;            // YK_INPUT_VALU=1: f32-VALU first conv in the bf16 build too
   int nms_dbg = 0;                    // YK_NMS_DBG: nms_kernel phase timing (never in production)
   int wide_dbg = 0;                   // YK_WIDE_DBG: conv_wide_kernel diagnostics (never in production)
+  bool no_wide = false;               // YK_NO_WIDE=1: autotune without the LDS-resident wide kernel
   std::vector<int64_t> ltab_off;
   char* arena = nullptr;      // every activation buffer (bufs[i] point into it)
   size_t arena_bytes = 0;
@@ -3238,6 +3251,7 @@ int yk_model_create(yk_ctx* ctx, const yk_model_desc* desc, const void* host_blo
   if (const char* env = getenv("YK_XCD")) m->xcd = atoi(env);
   if (const char* env = getenv("YK_WIDE_DBG")) m->wide_dbg = atoi(env);
   if (const char* env = getenv("YK_NMS_DBG")) m->nms_dbg = atoi(env);
+  if (const char* env = getenv("YK_NO_WIDE")) m->no_wide = env[0] == '1';
   if (e == hipSuccess) e = build_ktabs(m, !(getenv("YK_CONV_FAST") && getenv("YK_CONV_FAST")[0] == '0'));
   if (e == hipSuccess && desc->act_dtype == YK_ACT_FP8)
     for (size_t i = 0; i < m->ops.size(); ++i)
@@ -3450,7 +3464,7 @@ int yk_model_autotune(yk_model* m, const uint8_t* frames, int batch, float conf,
         if (fp8 || (nnt > 1 && 4 * op.n_tiles < 3 * ((op.n_tiles + nnt - 1) / nnt) * nnt)) continue;
         cands.push_back({CK_SPLITK, nnt, npt});
       }
-    if (m->ltab && m->ltab_off[i] >= 0 && m->arena_bytes < 0x7fff0000ull)
+    if (m->ltab && m->ltab_off[i] >= 0 && m->arena_bytes < 0x7fff0000ull && !m->no_wide)
       for (int nnt : {2, 4}) {
         if (nnt == 4 && op.n_tiles <= 2) continue;
         for (int nw : {4, 8})

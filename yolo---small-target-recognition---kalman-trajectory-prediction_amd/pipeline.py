@@ -62,8 +62,8 @@ class StreamPipeline:
         self._trk_pending = [False] * self.nb
         self.graph = None
         self.D = int(inflight)
-        if not 1 <= self.D <= 4:
-            raise ValueError("inflight must be in [1, 4]")
+        if not 1 <= self.D <= 8:
+            raise ValueError("inflight must be in [1, 8]")
         if self.D > 1 and not self.pipelined:
             raise ValueError("inflight > 1 needs pipelined=True (the tracker runs on its own stream)")
         # slot s: detector model, input frames and launch stream (None = the caller's stream)
