@@ -259,6 +259,13 @@ typedef struct {
   const int64_t* buf_elems;   /* per-image element count of each activation buffer       */
   int32_t n_ops;
   const yk_op* ops;
+  /* LetterBox resize (data/augment.py:1717-1719, cv2.resize INTER_LINEAR) when the frame is not
+   * at the network scale: 0 none, 1 bilinear (fixed-point), 2 exact 2x (INTER_AREA fast path).
+   * The resized rs_w x rs_h image sits at (pad_left, pad_top) of the in_w x in_h input. */
+  int32_t rs_mode, rs_w, rs_h;
+  int32_t box_pad_x, box_pad_y; /* scale_boxes (utils/ops.py:123-126) padding and gain        */
+  float box_gain;
+  int64_t rs_tab_off;         /* blob: int32 xofs[rs_w], yofs[rs_h], then int16 pairs xw[rs_w][2], yw[rs_h][2] */
 } yk_model_desc;
 
 int yk_model_create(yk_ctx* ctx, const yk_model_desc* desc, const void* host_blob, int64_t blob_bytes,
@@ -322,7 +329,8 @@ int yk_model_get_plan(yk_model* m, int32_t* plan, int32_t* batch);
  * cross-lane waits (arrays of n_ops * groups). */
 int yk_model_get_schedule(yk_model* m, int32_t* lane_of, int32_t* n_waits);
 
-/* Device pointer of activation buffer `buf` (debug / parity). */
+/* Device pointer of activation buffer `buf` (debug / parity); buf = -1: the letterboxed
+ * uint8 input canvas [max_batch][in_h][in_w][3] of a resizing model (NULL otherwise). */
 int yk_model_buffer(yk_model* m, int buf, void** dev_ptr);
 
 /* Synchronous device -> host copy (bindings without their own HIP runtime access). */

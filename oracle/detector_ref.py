@@ -134,23 +134,14 @@ class RefDetector:
 
 
 def preprocess(frames, imgsz=640, stride=32):
-    """BGR HWC uint8 frames (same shape) -> (B,3,H,W) float32 RGB/255 after LetterBox(auto).
-    Returns (tensor, (gain, (padw, padh)) per LetterBox's centring)."""
-    h, w = frames[0].shape[:2]
-    r = min(imgsz / h, imgsz / w)
-    if round(w * r) != w or round(h * r) != h:
-        raise NotImplementedError("resizing letterbox needs cv2 (not available); r must be 1")
-    dw, dh = (imgsz - w) % stride, (imgsz - h) % stride
-    dw, dh = dw / 2, dh / 2
-    top, bottom = int(round(dh - 0.1)), int(round(dh + 0.1))
-    left, right = int(round(dw - 0.1)), int(round(dw + 0.1))
+    """BGR HWC uint8 frames (same shape) -> (B,3,H,W) float32 RGB/255 after LetterBox(auto)
+    (engine/predictor.py:152-204); a frame off the network scale is resized with the
+    oracle's cv2 INTER_LINEAR restatement (oracle/letterbox_ref.py, parity with cv2 unpinned)."""
     import numpy as np
 
-    ims = []
-    for f in frames:
-        if top or bottom or left or right:
-            f = np.pad(f, ((top, bottom), (left, right), (0, 0)), constant_values=114)
-        ims.append(f)
+    from .letterbox_ref import letterbox
+
+    ims = [letterbox(f, imgsz, stride) for f in frames]
     im = np.stack(ims)[..., ::-1].transpose(0, 3, 1, 2)
     t = torch.from_numpy(np.ascontiguousarray(im)).float()
     t /= 255

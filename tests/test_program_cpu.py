@@ -40,8 +40,32 @@ def test_letterbox_geometry():
     assert M.letterbox_geometry(512, 640, 640) == (512, 640, 0, 0)
     assert M.letterbox_geometry(500, 640, 640) == (512, 640, 6, 0)
     assert M.letterbox_geometry(1024, 1280, 1280) == (1024, 1280, 0, 0)
-    with pytest.raises(NotImplementedError):
-        M.letterbox_geometry(1024, 1280, 640)
+    # resizing geometries (cv2.resize INTER_LINEAR on the device, letterbox.py)
+    assert M.letterbox_geometry(1024, 1280, 640) == (512, 640, 0, 0)   # exact 2x: INTER_AREA path
+    assert M.letterbox_geometry(1080, 1920, 640) == (384, 640, 12, 0)  # 640x360 + 12 rows top/bottom
+
+
+def test_letterbox_tables_match_oracle_restatement():
+    """The device kernel's per-axis tables (letterbox.py) equal the oracle's independent
+    restatement of OpenCV's coefficient rule, and both resize paths keep flat images flat."""
+    import importlib
+    from oracle import letterbox_ref as R
+    LB = importlib.import_module(pkg().__name__ + ".letterbox")
+    for (h, w) in [(1080, 1920), (600, 800), (300, 400), (1025, 1281)]:
+        p = LB.plan(h, w, 640)
+        assert p["mode"] == LB.RS_LINEAR
+        xs, x0, x1 = R._axis(p["new_w"], w, True)
+        ys, y0, y1 = R._axis(p["new_h"], h, False)
+        np.testing.assert_array_equal(p["xofs"], xs)
+        np.testing.assert_array_equal(p["xw"][:, 0], x0)
+        np.testing.assert_array_equal(p["xw"][:, 1], x1)
+        np.testing.assert_array_equal(p["yofs"], ys)
+        np.testing.assert_array_equal(p["yw"][:, 0], y0)
+        np.testing.assert_array_equal(p["yw"][:, 1], y1)
+    assert LB.plan(1024, 1280, 640)["mode"] == LB.RS_AREA2
+    for shape in [(1080, 1920, 3), (300, 400, 3), (1024, 1280, 3)]:
+        flat = np.full(shape, 77, np.uint8)
+        assert np.all(R.letterbox(flat)[12:-12] == 77) or np.all(R.letterbox(flat) == 77)
 
 
 def _emulate(prog, op, w_blob_f32, bias, tab, src, B):

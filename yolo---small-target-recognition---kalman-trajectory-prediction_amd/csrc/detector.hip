@@ -1183,6 +1183,65 @@ inline size_t fast_lds(int k_steps, int nnt, int npt, bool ws) {
   return t + (ws ? (size_t)4 * nnt * npt * 64 * 16 : 0);
 }
 
+// ---------------------------------------------------------------- LetterBox resize
+// LetterBox (data/augment.py:1698-1729) when the frame is not at the network scale: cv2.resize
+// INTER_LINEAR of the uint8 BGR frame, restated from OpenCV 4.x's fixed-point path (see
+// letterbox.py for the rules), centred in an in_w x in_h canvas of 114.  One thread per output
+// pixel; the first conv then reads this canvas as its frame.
+struct LboxArgs {
+  const unsigned char* src;  // [B][fh][fw][3]
+  unsigned char* dst;        // [B][in_h][in_w][3]
+  int fh, fw, in_h, in_w, top, left, rs_w, rs_h, mode, vec_end;
+  const int* xofs;           // [rs_w] source column (clamped)
+  const int* yofs;           // [rs_h] source row (unclamped: the fetch clips)
+  const short2* xw;          // [rs_w] fixed-point weights (sum 2048)
+  const short2* yw;          // [rs_h]
+};
+
+__global__ void __launch_bounds__(256) letterbox_kernel(LboxArgs a, int B) {
+  const long n = (long)B * a.in_h * a.in_w;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    const int x = (int)(i % a.in_w);
+    const long t = i / a.in_w;
+    const int y = (int)(t % a.in_h), b = (int)(t / a.in_h);
+    int o[3] = {114, 114, 114};
+    const int ry = y - a.top, rx = x - a.left;
+    if (ry >= 0 && ry < a.rs_h && rx >= 0 && rx < a.rs_w) {
+      const unsigned char* S = a.src + (size_t)b * a.fh * a.fw * 3;
+      if (a.mode == 2) {  // exact 2x: INTER_AREA fast path, (a + b + c + d + 2) >> 2
+        const unsigned char* p0 = S + ((size_t)(2 * ry) * a.fw + 2 * rx) * 3;
+        const unsigned char* p1 = p0 + (size_t)a.fw * 3;
+        for (int c = 0; c < 3; ++c) o[c] = (p0[c] + p0[3 + c] + p1[c] + p1[3 + c] + 2) >> 2;
+      } else {
+        const int sx = a.xofs[rx], sx1 = sx + 1 < a.fw ? sx + 1 : a.fw - 1;
+        const short2 aw = a.xw[rx], bw = a.yw[ry];
+        const int sy = a.yofs[ry];
+        const int r0 = sy < 0 ? 0 : (sy > a.fh - 1 ? a.fh - 1 : sy);
+        const int r1 = sy + 1 < 0 ? 0 : (sy + 1 > a.fh - 1 ? a.fh - 1 : sy + 1);
+        const unsigned char* R0 = S + (size_t)r0 * a.fw * 3;
+        const unsigned char* R1 = S + (size_t)r1 * a.fw * 3;
+        for (int c = 0; c < 3; ++c) {
+          const int d0 = R0[sx * 3 + c] * aw.x + R0[sx1 * 3 + c] * aw.y;  // horizontal pass (exact)
+          const int d1 = R1[sx * 3 + c] * aw.x + R1[sx1 * 3 + c] * aw.y;
+          int v;
+          if (rx * 3 + c < a.vec_end) {  // VResizeLinearVec_32s8u: v_mul_hi of (D >> 4), then >> 2
+            const int t0 = ((int)(short)(d0 >> 4) * (int)bw.x) >> 16;
+            const int t1 = ((int)(short)(d1 >> 4) * (int)bw.y) >> 16;
+            v = (t0 + t1 + 2) >> 2;
+          } else {  // FixedPtCast<int, uchar, 22>
+            v = (d0 * bw.x + d1 * bw.y + (1 << 21)) >> 22;
+          }
+          o[c] = v < 0 ? 0 : (v > 255 ? 255 : v);
+        }
+      }
+    }
+    unsigned char* q = a.dst + (size_t)i * 3;
+    q[0] = (unsigned char)o[0];
+    q[1] = (unsigned char)o[1];
+    q[2] = (unsigned char)o[2];
+  }
+}
+
 // ---------------------------------------------------------------- first conv from uint8 frames
 constexpr int kInputCoutMax = 64;
 
@@ -2151,6 +2210,7 @@ struct yk_model {
   int wide_dbg = 0;                   // YK_WIDE_DBG: conv_wide_kernel diagnostics (never in production)
   bool no_wide = false;               // YK_NO_WIDE=1: autotune without the LDS-resident wide kernel
   std::vector<int64_t> ltab_off;
+  unsigned char* lbox = nullptr;  // letterboxed frames [max_batch][in_h][in_w][3] (resize only)
   char* arena = nullptr;      // every activation buffer (bufs[i] point into it)
   size_t arena_bytes = 0;
   size_t blob_bytes = 0;
@@ -2607,11 +2667,13 @@ int launch_op(yk_model* m, const yk_op& op, const uint8_t* frames, int B, float 
     switch (op.kind) {
       case YK_K_CONV_INPUT: {
         InputArgs a;
-        a.frames = frames + (size_t)b0 * D.frame_h * D.frame_w * 3;
-        a.fh = D.frame_h;
-        a.fw = D.frame_w;
-        a.pad_top = D.pad_top;
-        a.pad_left = D.pad_left;
+        // with a LetterBox resize the frames are already the letterboxed canvas (m->lbox)
+        const bool rs = D.rs_mode != 0;
+        a.fh = rs ? D.in_h : D.frame_h;
+        a.fw = rs ? D.in_w : D.frame_w;
+        a.frames = frames + (size_t)b0 * a.fh * a.fw * 3;
+        a.pad_top = rs ? 0 : D.pad_top;
+        a.pad_left = rs ? 0 : D.pad_left;
         a.in_h = D.in_h;
         a.in_w = D.in_w;
         a.out_h = op.out_h;
@@ -3029,6 +3091,38 @@ int run_dag(yk_model* m, const uint8_t* frames, int B, float conf, hipStream_t s
   return YK_OK;
 }
 
+// The network input: the frames themselves, or (LetterBox resize) the letterboxed canvas.
+const uint8_t* input_frames(yk_model* m, const uint8_t* frames, int B, hipStream_t st) {
+  const yk_model_desc& D = m->desc;
+  if (!D.rs_mode) return frames;
+  const int* t = (const int*)(m->blob + D.rs_tab_off);
+  LboxArgs a;
+  a.src = frames;
+  a.dst = m->lbox;
+  a.fh = D.frame_h;
+  a.fw = D.frame_w;
+  a.in_h = D.in_h;
+  a.in_w = D.in_w;
+  a.top = D.pad_top;
+  a.left = D.pad_left;
+  a.rs_w = D.rs_w;
+  a.rs_h = D.rs_h;
+  a.mode = D.rs_mode;
+  const int W = D.rs_w * 3;  // elements per resized row: 16-byte, then 8-byte SIMD blocks
+  int xv = W >= 16 ? W / 16 * 16 : 0;
+  while (xv < W - 8) xv += 8;
+  a.vec_end = xv;
+  a.xofs = t;
+  a.yofs = t + D.rs_w;
+  a.xw = (const short2*)(t + D.rs_w + D.rs_h);
+  a.yw = (const short2*)(t + 2 * D.rs_w + D.rs_h);
+  const long n = (long)B * D.in_h * D.in_w;
+  long g = (n + 255) / 256;
+  if (g > 8192) g = 8192;
+  hipLaunchKernelGGL(letterbox_kernel, dim3((unsigned)g), dim3(256), 0, st, a, B);
+  return m->lbox;
+}
+
 int detect_impl(yk_model* m, const uint8_t* frames, int B, float conf, float iou, int max_det, float* dets,
                 int32_t* counts, hipStream_t st) {
   const yk_model_desc& D = m->desc;
@@ -3041,6 +3135,7 @@ int detect_impl(yk_model* m, const uint8_t* frames, int B, float conf, float iou
   if (!dets) dets = m->dets;
   if (!counts) counts = m->counts;
   YK_HIP(hipMemsetAsync(m->cand_count, 0, sizeof(int) * B, st));
+  frames = input_frames(m, frames, B, st);
   int rc = D.act_dtype == YK_ACT_F32   ? run_dag<F32>(m, frames, B, conf, st)
            : D.act_dtype == YK_ACT_FP8 ? run_dag<FP8>(m, frames, B, conf, st)
                                        : run_dag<BF16>(m, frames, B, conf, st);
@@ -3065,9 +3160,9 @@ int launch_nms(yk_model* m, int B, float iou, int max_det, float* dets, int32_t*
   a.max_det = max_det;
   a.dets = dets;
   a.counts = counts;
-  a.pad_x = (float)D.pad_left;
-  a.pad_y = (float)D.pad_top;
-  a.gain = 1.0f;
+  a.pad_x = (float)D.box_pad_x;  // scale_boxes (utils/ops.py:123-138)
+  a.pad_y = (float)D.box_pad_y;
+  a.gain = D.box_gain;
   a.clip_w = (float)D.frame_w;
   a.clip_h = (float)D.frame_h;
   a.dbg = m->nms_dbg;
@@ -3202,6 +3297,14 @@ int yk_model_create(yk_ctx* ctx, const yk_model_desc* desc, const void* host_blo
     YK_CHECK_ARG(op.kind != YK_K_CONV_INPUT || op.cout <= kInputCoutMax,
                  "yk_model_create: the input conv must have <= 64 (padded) output channels");
   }
+  YK_CHECK_ARG(desc->rs_mode >= 0 && desc->rs_mode <= 2, "yk_model_create: bad resize mode");
+  YK_CHECK_ARG(desc->rs_mode == 0 ||
+                   (desc->rs_w >= 1 && desc->rs_h >= 1 && desc->pad_left + desc->rs_w <= desc->in_w &&
+                    desc->pad_top + desc->rs_h <= desc->in_h && desc->rs_tab_off >= 0 &&
+                    desc->rs_tab_off + (int64_t)(2 * desc->rs_w + 2 * desc->rs_h) * 4 <= blob_bytes &&
+                    (desc->rs_mode != 2 || (2 * desc->rs_w <= desc->frame_w && 2 * desc->rs_h <= desc->frame_h))),
+               "yk_model_create: inconsistent LetterBox resize geometry");
+  YK_CHECK_ARG(desc->box_gain > 0.f, "yk_model_create: box_gain must be > 0");
   yk::DeviceGuard guard(ctx->device);
   auto* m = new yk_model();
   m->ctx = ctx;
@@ -3229,6 +3332,7 @@ int yk_model_create(yk_ctx* ctx, const yk_model_desc* desc, const void* host_blo
     for (int i = 0; i < desc->n_bufs; ++i) m->bufs.push_back(m->arena ? m->arena + offs[i] : nullptr);
   }
   alloc((void**)&m->blob, (size_t)blob_bytes);
+  if (desc->rs_mode) alloc((void**)&m->lbox, B * (size_t)desc->in_h * desc->in_w * 3);
   m->blob_bytes = (size_t)blob_bytes;
   if (e == hipSuccess) e = hipMemcpy(m->blob, host_blob, (size_t)blob_bytes, hipMemcpyHostToDevice);
   int kc = 1;
@@ -3305,7 +3409,7 @@ int yk_model_destroy(yk_model* m) {
   for (hipEvent_t v : m->ev) (void)hipEventDestroy(v);
   if (m->arena) (void)hipFree(m->arena);
   void* ptrs[] = {m->blob, m->cand, m->cand_count, m->slot_of, m->gkeys, m->gbox, m->gflag, m->dets, m->counts, m->ktab,
-                  m->ltab};
+                  m->ltab, m->lbox};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   delete m;
@@ -3370,6 +3474,7 @@ int yk_model_profile(yk_model* m, const uint8_t* frames, int batch, float conf, 
   yk::DeviceGuard guard(m->ctx->device);
   hipStream_t st = (hipStream_t)stream;
   m->plan_batch = batch;
+  frames = input_frames(m, frames, batch, st);
   hipEvent_t e0, e1;
   YK_HIP(hipEventCreate(&e0));
   YK_HIP(hipEventCreate(&e1));
@@ -3531,7 +3636,11 @@ int yk_model_candidates(yk_model* m, float** cand, int32_t** counts) {
 
 int yk_model_buffer(yk_model* m, int buf, void** ptr) {
   YK_CHECK_ARG(m && ptr, "yk_model_buffer: NULL argument");
-  YK_CHECK_ARG(buf >= 0 && buf < (int)m->bufs.size(), "yk_model_buffer: index out of range");
+  YK_CHECK_ARG(buf >= -1 && buf < (int)m->bufs.size(), "yk_model_buffer: index out of range");
+  if (buf == -1) {  // the letterboxed input canvas (NULL when the frames need no resize)
+    *ptr = m->lbox;
+    return YK_OK;
+  }
   *ptr = m->bufs[buf];
   return YK_OK;
 }

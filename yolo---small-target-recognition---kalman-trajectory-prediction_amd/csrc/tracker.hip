@@ -714,26 +714,25 @@ __device__ void track_info(Slot& s, yk_track_out& o, bool copy_traj = true) {
   o.motion_confidence = s.pconf;
   o.speed = s.speed;
   o.direction = s.direction;
-  // MotionResetKalmanTracker.get_track_info / get_reset_statistics (:314-355)
-  o.reset_count = s.policy ? s.reset_count : 0;
-  o.frames_since_reset = s.policy ? s.age - s.last_reset : 0;
-  o.n_details = s.policy ? s.dl_len : 0;
-  for (int k = 0; k < 3; ++k) o.reason_count[k] = s.policy ? s.reason_count[k] : 0;
-  o.motion_consistency = s.policy ? s.consistency : 0.0;
-  o.reset_confidence_sum = s.policy ? s.conf_sum : 0.0;
-  o.motion_consistency_sum = s.policy ? s.cons_sum : 0.0;
-  for (int k = 0; k < o.n_details; ++k) {
-    const ResetDetail& d = s.dl[ring_at<5>(s.dl_head, k)];
-    o.details[k].frame = d.frame;
-    o.details[k].reasons = d.reasons;
-    for (int j = 0; j < 3; ++j) o.details[k].value[j] = d.value[j];
-    o.details[k].confidence = d.conf;
-    o.details[k].motion_consistency = d.cons;
-  }
-  for (int k = o.n_details; k < 5; ++k) {  // rows are compared bytewise: no stale bytes
-    o.details[k].frame = o.details[k].reasons = 0;
-    for (int j = 0; j < 3; ++j) o.details[k].value[j] = 0.0;
-    o.details[k].confidence = o.details[k].motion_consistency = 0.0;
+  // MotionResetKalmanTracker.get_track_info / get_reset_statistics (:314-355).  The enhanced
+  // policy never writes these fields: the rows buffer is zeroed once at creation.
+  if (s.policy) {
+    o.reset_count = s.reset_count;
+    o.frames_since_reset = s.age - s.last_reset;
+    o.n_details = s.dl_len;
+    for (int k = 0; k < 3; ++k) o.reason_count[k] = s.reason_count[k];
+    o.motion_consistency = s.consistency;
+    o.reset_confidence_sum = s.conf_sum;
+    o.motion_consistency_sum = s.cons_sum;
+    for (int k = 0; k < 5; ++k) {  // unused entries zeroed: a row position is reused by other tracks
+      const bool u = k < s.dl_len;
+      const ResetDetail& d = s.dl[ring_at<5>(s.dl_head, u ? k : 0)];
+      o.details[k].frame = u ? d.frame : 0;
+      o.details[k].reasons = u ? d.reasons : 0;
+      for (int j = 0; j < 3; ++j) o.details[k].value[j] = u ? d.value[j] : 0.0;
+      o.details[k].confidence = u ? d.conf : 0.0;
+      o.details[k].motion_consistency = u ? d.cons : 0.0;
+    }
   }
   const int nt = s.th_len < TOUT ? s.th_len : TOUT;
   o.traj_len = nt;
@@ -1358,12 +1357,14 @@ int yk_tracker_create(yk_ctx* ctx, int n_streams, const yk_tracker_cfg* cfg, yk_
   A((void**)&g.cand_key, S * (size_t)g.C * sizeof(unsigned long long));
   A((void**)&g.cand_flat, S * (size_t)g.C * sizeof(int));
   A((void**)&g.rows, S * T * sizeof(yk_track_out));
+  if (e == hipSuccess) e = hipMemset(g.rows, 0, S * T * sizeof(yk_track_out));
   A((void**)&g.counts, S * sizeof(int));
   A((void**)&g.stats, S * sizeof(yk_tracker_stats));
   A((void**)&g.phase, S * 16 * sizeof(long long));
   if (e == hipSuccess) e = hipMemset(g.phase, 0, S * 16 * sizeof(long long));
   A((void**)&t->d_snap, T * sizeof(yk_track_state));
   A((void**)&t->d_row1, sizeof(yk_track_out));
+  if (e == hipSuccess) e = hipMemset(t->d_row1, 0, sizeof(yk_track_out));
   A((void**)&t->d_box, 16 * sizeof(double));
   A((void**)&t->d_status, sizeof(int));
   if (e != hipSuccess) {

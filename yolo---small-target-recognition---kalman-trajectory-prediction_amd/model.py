@@ -27,6 +27,7 @@ import torch
 
 from . import _lib as L
 from . import arch as A
+from . import letterbox as LB
 from . import weights as Wt
 
 YK_K_CONV_INPUT, YK_K_CONV, YK_K_SPPF_POOL, YK_K_DETECT = range(4)
@@ -57,7 +58,9 @@ class ModelDesc(C.Structure):
     _fields_ = [("act_dtype", C.c_int32), ("max_batch", C.c_int32), ("frame_h", C.c_int32), ("frame_w", C.c_int32),
                 ("in_h", C.c_int32), ("in_w", C.c_int32), ("pad_top", C.c_int32), ("pad_left", C.c_int32),
                 ("n_anchors", C.c_int32), ("nc", C.c_int32), ("max_det", C.c_int32), ("n_bufs", C.c_int32),
-                ("buf_elems", C.POINTER(C.c_int64)), ("n_ops", C.c_int32), ("ops", C.POINTER(Op))]
+                ("buf_elems", C.POINTER(C.c_int64)), ("n_ops", C.c_int32), ("ops", C.POINTER(Op)),
+                ("rs_mode", C.c_int32), ("rs_w", C.c_int32), ("rs_h", C.c_int32), ("box_pad_x", C.c_int32),
+                ("box_pad_y", C.c_int32), ("box_gain", C.c_float), ("rs_tab_off", C.c_int64)]
 
 
 @dataclass(frozen=True)
@@ -83,20 +86,9 @@ class Seg:
 
 def letterbox_geometry(frame_h, frame_w, imgsz=640, stride=32):
     """LetterBox(auto=True, center=True) geometry (data/augment.py:1698-1729).  Returns
-    (in_h, in_w, pad_top, pad_left); raises if a resize would be needed (cv2 path)."""
-    if isinstance(imgsz, int):
-        imgsz = (imgsz, imgsz)
-    r = min(imgsz[0] / frame_h, imgsz[1] / frame_w)
-    new_w, new_h = int(round(frame_w * r)), int(round(frame_h * r))
-    if (new_w, new_h) != (frame_w, frame_h):
-        raise NotImplementedError(
-            f"frame {frame_w}x{frame_h} at imgsz {imgsz} needs a LetterBox resize (r={r:.4f}); only r == 1 "
-            "geometries are on the MI355X path in this round")
-    dw, dh = (imgsz[1] - new_w) % stride, (imgsz[0] - new_h) % stride
-    dw, dh = dw / 2, dh / 2
-    top, bottom = int(round(dh - 0.1)), int(round(dh + 0.1))
-    left, right = int(round(dw - 0.1)), int(round(dw + 0.1))
-    return frame_h + top + bottom, frame_w + left + right, top, left
+    (in_h, in_w, pad_top, pad_left); see letterbox.plan for the resize tables."""
+    p = LB.plan(frame_h, frame_w, imgsz, stride)
+    return p["in_h"], p["in_w"], p["top"], p["left"]
 
 
 def _bf16_bits(a: np.ndarray) -> np.ndarray:
@@ -123,7 +115,8 @@ class Program:
         self.ar, self.dtype, self.max_batch, self.max_det = ar, dtype, int(max_batch), int(max_det)
         self.frame_h, self.frame_w = int(frame_h), int(frame_w)
         self.strides = A.detect_strides(ar)
-        self.in_h, self.in_w, self.pad_top, self.pad_left = letterbox_geometry(frame_h, frame_w, imgsz, max(self.strides))
+        self.lb = LB.plan(frame_h, frame_w, imgsz, max(self.strides))
+        self.in_h, self.in_w, self.pad_top, self.pad_left = self.lb["in_h"], self.lb["in_w"], self.lb["top"], self.lb["left"]
         self.epl = 16 // ESZ[dtype]  # K elements per lane per 16-byte fragment
         self.fused = Wt.fused_convs(sd, ar)
         self.sd = sd
@@ -134,6 +127,7 @@ class Program:
         self.op_meta: list[int] = []  # MACs per image of each op
         self.n_anchors = 0
         self._build()
+        self.rs_tab_off = self.add_blob(LB.table_blob(self.lb))
 
     def phys(self, c: int) -> int:
         """Physical channels of a logical group: a whole number of 16-byte... K chunks; FP8
@@ -429,6 +423,10 @@ class Program:
         d.buf_elems = C.cast(self._bufs_arr, C.POINTER(C.c_int64))
         d.n_ops = len(self.ops)
         d.ops = C.cast(self._ops_arr, C.POINTER(Op))
+        lb = self.lb
+        d.rs_mode, d.rs_w, d.rs_h = lb["mode"], lb["new_w"], lb["new_h"]
+        d.box_pad_x, d.box_pad_y, d.box_gain = lb["pad_x"], lb["pad_y"], lb["gain"]
+        d.rs_tab_off = self.rs_tab_off
         return d
 
 
@@ -566,6 +564,17 @@ class DeviceModel:
             out = np.zeros(n, np.float32)
             _memcpy_d2h(out, ptr.value)
         return out.reshape(B, -1)
+
+    def letterboxed(self, B: int) -> np.ndarray:
+        """The letterboxed uint8 input [B, in_h, in_w, 3] of the last detect() (resizing models)."""
+        ptr = C.c_void_p()
+        L.check(L.lib().yk_model_buffer(self._h, -1, C.byref(ptr)), "yk_model_buffer")
+        if not ptr.value:
+            raise L.YKError("this model's frames need no LetterBox resize")
+        torch.cuda.synchronize(self.device)
+        out = np.zeros((B, self.prog.in_h, self.prog.in_w, 3), np.uint8)
+        _memcpy_d2h(out, ptr.value)
+        return out
 
     def layer_nchw(self, i: int, B: int) -> torch.Tensor:
         """Logical output of graph layer i as an NCHW float tensor (debug / parity)."""
