@@ -45,6 +45,9 @@ def parse():
     ap.add_argument("--targets", type=int, default=None,
                     help="synthetic targets per stream (22 -> ~64 live tracks/stream: the planted detector plus lost-track retention)")
     ap.add_argument("--scale", default="s", choices=["n", "s"])
+    ap.add_argument("--frame", default="", help="frame size WxH (e.g. 1920x1080): frames off the network scale are "
+                                                 "letterboxed with the device resize; with --imgsz")
+    ap.add_argument("--imgsz", type=int, default=0, help="network input size (default: the config's)")
     ap.add_argument("--dtype", default=None, choices=["bf16", "fp32", "fp8"],
                     help="activation/weight dtype (default: fp8 for --config 5, else bf16)")
     ap.add_argument("--frames", type=int, default=120, help="pre-rendered frames per stream (cycled)")
@@ -203,6 +206,10 @@ def main():
         a.dtype = "fp8" if a.config == 5 else "bf16"
     S = a.streams
     H, W, imgsz, max_tracks = (1024, 1280, 1280, 2048) if a.config == 5 else (512, 640, 640, 512)
+    if a.frame:
+        W, H = (int(v) for v in a.frame.lower().split("x"))
+    if a.imgsz:
+        imgsz = a.imgsz
     if a.targets is None:
         a.targets = {2: 6, 3: 22, 5: 66}[a.config]
     shard = P.shard
