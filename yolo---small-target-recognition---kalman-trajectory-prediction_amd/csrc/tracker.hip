@@ -399,7 +399,7 @@ __device__ Num cmc_consistency(const Slot& s) {
 // _should_reset_kalman (:174-214) with the three detectors (:86-157).  val / why: the
 // reasons' values and bits (1 position jump, 2 velocity change, 4 size change).
 template <typename DT>
-__device__ bool cmc_decide(Slot& s, const DT* b, double* val, int& why, Num& conf) {
+__device__ __noinline__ bool cmc_decide(Slot& s, const DT* b, double* val, int& why, Num& conf) {
   why = 0;
   const int since = s.age - s.last_reset;
   if (since < 15) return false;  // reset cooldown
@@ -853,7 +853,9 @@ __device__ Lds carve(char* base, int T, int D) {
 enum { M_NCAND = 0, M_ACTIVE, M_RECOVER, M_LONGTERM, M_OVERFLOW, M_RESETS, M_TRECOV, M_WSUM = 8 };
 
 // ---------------------------------------------------------------- the step kernel
-template <typename DT>
+// POL: yk_tracker_policy as a template constant, so the enhanced instantiation carries none of
+// the motion-reset code (registers: 122 VGPRs, no scratch).
+template <typename DT, int POL>
 __global__ void __launch_bounds__(NT) step_kernel(Dev g, const DT* __restrict__ dets, int row_stride,
                                                   const int* __restrict__ counts) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -884,7 +886,7 @@ __global__ void __launch_bounds__(NT) step_kernel(Dev g, const DT* __restrict__ 
     Slot& sl = slots[order[i]];
     kf_predict(sl);
     state_to_bbox(sl.x, &L.pb[4 * i]);
-    if (sl.policy) cmc_blend(sl, &L.pb[4 * i]);
+    if (POL && sl.policy) cmc_blend(sl, &L.pb[4 * i]);
   }
   __syncthreads();
   if (tid == 0) g.phase[s * 16 + 1] = wall_clock64();
@@ -901,7 +903,7 @@ __global__ void __launch_bounds__(NT) step_kernel(Dev g, const DT* __restrict__ 
       for (int k = 0; k < 4; ++k) db[k] = (DT)L.det[4 * d + k];
       const double v = iou_mixed<DT>(db, &L.pb[4 * t]);
       // enhanced: iou >= thr (multi:245); motion-reset: iou > thr (motion_compensated_multi_tracker.py:260)
-      if (g.policy ? v > g.thr : v >= g.thr) {
+      if (POL ? v > g.thr : v >= g.thr) {
         const int c = atomicAdd(&L.misc[M_NCAND], 1);
         if (c < g.C) {
           ckey[c] = (unsigned long long)__double_as_longlong(v);
@@ -949,7 +951,7 @@ __global__ void __launch_bounds__(NT) step_kernel(Dev g, const DT* __restrict__ 
         const int f = cflat[c], d = f / n, t = f - d * n;
         if (L.det_match[d] < 0 && L.trk_match[t] < 0) {
           const unsigned long long k = ckey[c];
-          const int rk = g.policy ? npair - 1 - f : f;
+          const int rk = POL ? npair - 1 - f : f;
           if (k == L.row_max[d]) atomicMin(&L.row_arg[d], rk);
           if (k == L.col_max[t]) atomicMin(&L.col_arg[t], rk);
         }
@@ -957,7 +959,7 @@ __global__ void __launch_bounds__(NT) step_kernel(Dev g, const DT* __restrict__ 
       __syncthreads();
       for (int c = tid; c < nc; c += NT) {
         const int f = cflat[c], d = f / n, t = f - d * n;
-        const int rk = g.policy ? npair - 1 - f : f;
+        const int rk = POL ? npair - 1 - f : f;
         if (L.row_arg[d] == rk && L.col_arg[t] == rk) {
           L.det_match[d] = t;
           L.trk_match[t] = d;
@@ -1008,7 +1010,7 @@ __global__ void __launch_bounds__(NT) step_kernel(Dev g, const DT* __restrict__ 
       DT db[4];
 #pragma unroll
       for (int k = 0; k < 4; ++k) db[k] = (DT)L.det[4 * d + k];
-      if (sl.policy) {  // MotionResetKalmanTracker.update (:261-285)
+      if (POL && sl.policy) {  // MotionResetKalmanTracker.update (:261-285)
         double val[3] = {0.0, 0.0, 0.0};
         int why = 0;
         Num conf{0.0, KPY};
@@ -1051,7 +1053,7 @@ __global__ void __launch_bounds__(NT) step_kernel(Dev g, const DT* __restrict__ 
         double z[4];
         bbox_to_state<DT>(db, z);
         slot_init(slots[slot], z, next_num + r, g.max_lost);
-        if (g.policy) cmc_init<DT>(slots[slot], db);
+        if (POL) cmc_init<DT>(slots[slot], db);
         order[pos] = slot;
       } else {
         atomicAdd(&L.misc[M_OVERFLOW], 1);
@@ -1099,7 +1101,7 @@ __global__ void __launch_bounds__(NT) step_kernel(Dev g, const DT* __restrict__ 
       const int r = pushed + block_scan(del, wsum, tot);
       if (del) fstack[nfree_after_pop + r] = slot;
       // motion-reset stats['tracking_recoveries']: deleted trackers that had been reset
-      if (del && slots[slot].policy && slots[slot].reset_count > 0) atomicAdd(&L.misc[M_TRECOV], 1);
+      if (POL && del && slots[slot].policy && slots[slot].reset_count > 0) atomicAdd(&L.misc[M_TRECOV], 1);
       pushed += tot;
     }
   }
@@ -1120,14 +1122,14 @@ __global__ void __launch_bounds__(NT) step_kernel(Dev g, const DT* __restrict__ 
     if (i < kept) {
       sl = &slots[order[i]];
       // the motion-reset tracker reports every live tracker (motion_compensated_multi_tracker.py:369-386)
-      q = (g.policy || sl->hit_streak >= g.min_hits || fc <= g.min_hits || sl->is_lost) ? 1 : 0;
+      q = (POL || sl->hit_streak >= g.min_hits || fc <= g.min_hits || sl->is_lost) ? 1 : 0;
     }
     int tot;
     const int r = nout + block_scan(q, wsum, tot);
     if (q) {
       yk_track_out& o = g.rows[(size_t)s * T + r];
       track_info(*sl, o, false);
-      if (!g.policy && o.status == 1 && o.time_since_update > 30) ++lt;
+      if (!POL && o.status == 1 && o.time_since_update > 30) ++lt;
       L.order_tmp[r] = order[i];
     }
     nout += tot;
@@ -1372,9 +1374,13 @@ int yk_tracker_create(yk_ctx* ctx, int n_streams, const yk_tracker_cfg* cfg, yk_
     yk_tracker_destroy(t);
     return YK_ERR_HIP;
   }
-  if (hipFuncSetAttribute((const void*)yk::trk::step_kernel<float>,
+  if (hipFuncSetAttribute((const void*)yk::trk::step_kernel<float, 0>,
                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess ||
-      hipFuncSetAttribute((const void*)yk::trk::step_kernel<double>,
+      hipFuncSetAttribute((const void*)yk::trk::step_kernel<double, 0>,
+                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess ||
+      hipFuncSetAttribute((const void*)yk::trk::step_kernel<float, 1>,
+                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess ||
+      hipFuncSetAttribute((const void*)yk::trk::step_kernel<double, 1>,
                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) {
     (void)hipGetLastError();
   }
@@ -1414,12 +1420,22 @@ int yk_tracker_step(yk_tracker* t, const void* dets, int dtype, int row_stride, 
   YK_CHECK_ARG(row_stride >= 4, "yk_tracker_step: row_stride must be >= 4");
   YK_CHECK_ARG(dtype == YK_F32 || dtype == YK_F64, "yk_tracker_step: dtype must be YK_F32 or YK_F64");
   yk::DeviceGuard guard(t->ctx->device);
-  if (dtype == YK_F32)
-    hipLaunchKernelGGL(yk::trk::step_kernel<float>, dim3(t->S), dim3(yk::trk::NT), t->lds,
-                       (hipStream_t)stream, t->dev, (const float*)dets, row_stride, counts);
-  else
-    hipLaunchKernelGGL(yk::trk::step_kernel<double>, dim3(t->S), dim3(yk::trk::NT), t->lds,
-                       (hipStream_t)stream, t->dev, (const double*)dets, row_stride, counts);
+  const bool mr = t->cfg.policy == YK_POLICY_MOTION_RESET;
+  if (dtype == YK_F32) {
+    if (mr)
+      hipLaunchKernelGGL((yk::trk::step_kernel<float, 1>), dim3(t->S), dim3(yk::trk::NT), t->lds,
+                         (hipStream_t)stream, t->dev, (const float*)dets, row_stride, counts);
+    else
+      hipLaunchKernelGGL((yk::trk::step_kernel<float, 0>), dim3(t->S), dim3(yk::trk::NT), t->lds,
+                         (hipStream_t)stream, t->dev, (const float*)dets, row_stride, counts);
+  } else {
+    if (mr)
+      hipLaunchKernelGGL((yk::trk::step_kernel<double, 1>), dim3(t->S), dim3(yk::trk::NT), t->lds,
+                         (hipStream_t)stream, t->dev, (const double*)dets, row_stride, counts);
+    else
+      hipLaunchKernelGGL((yk::trk::step_kernel<double, 0>), dim3(t->S), dim3(yk::trk::NT), t->lds,
+                         (hipStream_t)stream, t->dev, (const double*)dets, row_stride, counts);
+  }
   YK_HIP(hipGetLastError());
   return YK_OK;
 }
