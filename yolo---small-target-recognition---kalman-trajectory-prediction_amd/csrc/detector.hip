@@ -742,6 +742,7 @@ struct FastArgs {
   int r_cstride, r_coff;
   int act;
   int xcd;
+  unsigned long long* tstamp;  // diagnostics (YK_FAST_TS): per-workgroup [start, end] wall clock
 };
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
@@ -780,6 +781,8 @@ __global__ void __launch_bounds__(256) conv_fast_kernel(FastArgs a) {
   const int nt0 = blk.y * NNT;
   const int pbase = WS ? blk.x * (16 * NPT) : (blk.x * 4 + wave) * (16 * NPT);
   const int nk = a.k_steps;
+  const int wg_lin = blockIdx.y * gridDim.x + blockIdx.x;
+  if (a.tstamp && tid == 0) a.tstamp[3 * wg_lin] = wall_clock64();
   {
     int2 tv[2];  // <= 512 entries (nk <= 128) in one round trip
 #pragma unroll
@@ -903,6 +906,7 @@ __global__ void __launch_bounds__(256) conv_fast_kernel(FastArgs a) {
       }
     }
   }
+  if (a.tstamp && tid == 0) a.tstamp[3 * wg_lin + 1] = wall_clock64();
   if constexpr (WS) {
     f32x4* red = (f32x4*)(smem + (((size_t)nk * 4 * 8 + 15) & ~(size_t)15));
 #pragma unroll
@@ -955,6 +959,7 @@ __global__ void __launch_bounds__(256) conv_fast_kernel(FastArgs a) {
       store4((T*)a.dst + (size_t)p * a.d_cstride + a.d_coff + n0, v);
     }
   }
+  if (a.tstamp && tid == 0) a.tstamp[3 * wg_lin + 2] = wall_clock64();
 }
 
 // ---------------------------------------------------------------- persistent LDS-tiled conv (wide layers)
@@ -2209,6 +2214,8 @@ struct yk_model {
   int nms_dbg = 0;                    // YK_NMS_DBG: nms_kernel phase timing (never in production)
   int wide_dbg = 0;                   // YK_WIDE_DBG: conv_wide_kernel diagnostics (never in production)
   bool no_wide = false;               // YK_NO_WIDE=1: autotune without the LDS-resident wide kernel
+  int ts_op = -1;                     // YK_FAST_TS=<op>: per-workgroup timestamps of that conv_fast op
+  unsigned long long* ts = nullptr;   // [3 * 65536] start, after K loop, end (wall_clock64, 100 MHz)
   std::vector<int64_t> ltab_off;
   unsigned char* lbox = nullptr;  // letterboxed frames [max_batch][in_h][in_w][3] (resize only)
   char* arena = nullptr;      // every activation buffer (bufs[i] point into it)
@@ -2818,6 +2825,7 @@ int launch_op(yk_model* m, const yk_op& op, const uint8_t* frames, int B, float 
           f.r_coff = a.r_coff;
           f.act = a.act;
           f.xcd = m->xcd;
+          f.tstamp = (m->ts && (int)(&op - m->ops.data()) == m->ts_op) ? m->ts : nullptr;
           launch_fast<Tr>(f, cp, st);
         } else if constexpr (Tr::kScaled) {
           // FP8 runs only on the table-driven and wide kernels (16-channel K chunks)
@@ -3356,6 +3364,11 @@ int yk_model_create(yk_ctx* ctx, const yk_model_desc* desc, const void* host_blo
   if (const char* env = getenv("YK_WIDE_DBG")) m->wide_dbg = atoi(env);
   if (const char* env = getenv("YK_NMS_DBG")) m->nms_dbg = atoi(env);
   if (const char* env = getenv("YK_NO_WIDE")) m->no_wide = env[0] == '1';
+  if (const char* env = getenv("YK_FAST_TS")) {
+    m->ts_op = atoi(env);
+    if (e == hipSuccess) e = hipMalloc((void**)&m->ts, 3 * 65536 * sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipMemset(m->ts, 0, 3 * 65536 * sizeof(unsigned long long));
+  }
   if (e == hipSuccess) e = build_ktabs(m, !(getenv("YK_CONV_FAST") && getenv("YK_CONV_FAST")[0] == '0'));
   if (e == hipSuccess && desc->act_dtype == YK_ACT_FP8)
     for (size_t i = 0; i < m->ops.size(); ++i)
@@ -3409,7 +3422,7 @@ int yk_model_destroy(yk_model* m) {
   for (hipEvent_t v : m->ev) (void)hipEventDestroy(v);
   if (m->arena) (void)hipFree(m->arena);
   void* ptrs[] = {m->blob, m->cand, m->cand_count, m->slot_of, m->gkeys, m->gbox, m->gflag, m->dets, m->counts, m->ktab,
-                  m->ltab, m->lbox};
+                  m->ltab, m->lbox, m->ts};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   delete m;
@@ -3636,9 +3649,13 @@ int yk_model_candidates(yk_model* m, float** cand, int32_t** counts) {
 
 int yk_model_buffer(yk_model* m, int buf, void** ptr) {
   YK_CHECK_ARG(m && ptr, "yk_model_buffer: NULL argument");
-  YK_CHECK_ARG(buf >= -1 && buf < (int)m->bufs.size(), "yk_model_buffer: index out of range");
+  YK_CHECK_ARG(buf >= -2 && buf < (int)m->bufs.size(), "yk_model_buffer: index out of range");
   if (buf == -1) {  // the letterboxed input canvas (NULL when the frames need no resize)
     *ptr = m->lbox;
+    return YK_OK;
+  }
+  if (buf == -2) {  // YK_FAST_TS diagnostics buffer (NULL unless enabled)
+    *ptr = m->ts;
     return YK_OK;
   }
   *ptr = m->bufs[buf];
