@@ -3,11 +3,25 @@
 
 One step = one frame of every stream on this GPU through the whole hot path
 (kalman/aircraft_detection_tracking.py:96-109): uint8 BGR frame in HBM -> letterbox/normalise
--> YOLOv8s+P2 forward -> Detect decode -> NMS -> EnhancedMultiTargetTracker.update per stream,
-captured as one hipGraph.  Default workload = BASELINE config 3: 8 independent 640x512 streams
-per GPU (batch 8), ~64 live tracks per stream, bf16 convs.  Multi-GPU (torchrun): streams are
-sharded one group per GPU with no data-path collective (weak scaling); RCCL only reduces the
-end-of-run counters and the max wall time.
+-> YOLOv8s+P2 forward -> Detect decode -> NMS -> EnhancedMultiTargetTracker.update per stream.
+
+Workloads (BASELINE.json configs; the default is config 3, the metric's workload):
+  2  640x512, 1 stream (batch 1), bf16 convs (BASELINE names bf16), >= 16 live tracks
+  3  640x512, 8 streams per GPU as one batch-8 forward, fp32 convs (the reference's
+     arithmetic; bf16 reported beside it as a labelled secondary leg), >= 64 live tracks/stream
+  4  640x512, ONE stream per GPU (8 GPUs x 1 stream at --gpus 8), fp32, >= 64 live tracks
+  5  1280x1024 at imgsz 1280, 8 streams, fp8 convs (bf16 secondary), >= 256 live tracks/stream,
+     150-frame occlusion bursts
+
+Protocol: frames are rendered into HBM before anything is timed; the committed conv plan
+(plans/*.json) is loaded instead of autotuning; an untimed tracker pre-roll of --preroll frames
+(independent of --steps/--warmup) brings every stream to its steady-state track load; then
+--warmup untimed steps and exactly --steps timed steps between barrier + synchronize.  The run
+fails if the tracker dropped anything (stats.overflow != 0).
+
+Multi-GPU: `torchrun --nproc-per-node N bench.py --gpus N`, or `bench.py --gpus N` alone, which
+starts the N rank processes itself.  Streams are sharded one block per GPU with no data-path
+collective (weak scaling); RCCL only reduces the end-of-run counters and the max wall time.
 
 Prints ONE JSON line on rank 0.
 """
@@ -17,6 +31,9 @@ import argparse
 import importlib
 import json
 import os
+import socket
+import statistics
+import subprocess
 import sys
 import time
 
@@ -30,6 +47,19 @@ PKG = "yolo---small-target-recognition---kalman-trajectory-prediction_amd"
 METRIC = "end-to-end frames/sec (640×512 YOLOv8s+P2, 64 tracks) at 1/2/4/8 GPUs"
 PEAK = {"bf16": 2500.0, "fp32": 157.3, "fp8": 5000.0}  # dense MFMA TFLOP/s (MI355X_MICROARCH.md)
 HBM_PEAK = 8000.0  # GB/s
+TRACK_STEP_BYTES = 1216  # R+W of x (8 f64) and dense P (64 f64), z, box
+
+# BASELINE.json configs -> workload.  live_floor: the live tracks per stream the config names.
+# Targets per stream are set so the steady-state LIVE track count (detected + lost-but-retained
+# tracks, max_lost_frames=150) meets the floor: the planted detector's ~96-px boxes merge nearby
+# targets and crossing targets churn IDs, so live tracks != targets (40 targets -> ~70-150 live).
+CONFIGS = {
+    2: dict(S=1, H=512, W=640, imgsz=640, max_tracks=512, targets=12, dtype="bf16", secondary="", live_floor=16),
+    3: dict(S=8, H=512, W=640, imgsz=640, max_tracks=512, targets=40, dtype="fp32", secondary="bf16", live_floor=64),
+    4: dict(S=1, H=512, W=640, imgsz=640, max_tracks=512, targets=40, dtype="fp32", secondary="", live_floor=64),
+    5: dict(S=8, H=1024, W=1280, imgsz=1280, max_tracks=2048, targets=96, dtype="fp8", secondary="bf16",
+            live_floor=256),
+}
 
 
 def parse():
@@ -37,41 +67,62 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--config", type=int, default=3, choices=[2, 3, 5],
-                    help="BASELINE config: 2 = 640x512 batch 1, ~16 live tracks; 3 = 640x512, ~64 live tracks/stream (the metric's workload); "
-                         "5 = 1280x1024 at imgsz 1280, ~256 live tracks/stream, 150-frame occlusion bursts")
-    ap.add_argument("--streams", type=int, default=None,
-                    help="streams (= frames per forward) per GPU (default 8; 1 for config 2)")
-    ap.add_argument("--targets", type=int, default=None,
-                    help="synthetic targets per stream (22 -> ~64 live tracks/stream: the planted detector plus lost-track retention)")
+    ap.add_argument("--config", type=int, default=3, choices=sorted(CONFIGS))
+    ap.add_argument("--streams", type=int, default=None, help="streams (= frames per forward) per GPU")
+    ap.add_argument("--targets", type=int, default=None, help="synthetic targets per stream")
     ap.add_argument("--scale", default="s", choices=["n", "s"])
     ap.add_argument("--frame", default="", help="frame size WxH (e.g. 1920x1080): frames off the network scale are "
                                                  "letterboxed with the device resize; with --imgsz")
     ap.add_argument("--imgsz", type=int, default=0, help="network input size (default: the config's)")
-    ap.add_argument("--dtype", default=None, choices=["bf16", "fp32", "fp8"],
-                    help="activation/weight dtype (default: fp8 for --config 5, else bf16)")
-    ap.add_argument("--frames", type=int, default=120, help="pre-rendered frames per stream (cycled)")
+    ap.add_argument("--dtype", default=None, choices=["bf16", "fp32", "fp8"], help="conv dtype of the headline leg")
+    ap.add_argument("--secondary", default=None,
+                    help="comma list of dtypes timed after the headline leg with the same protocol (default: the "
+                         "config's; 'none' to skip)")
+    ap.add_argument("--preroll", type=int, default=160,
+                    help="untimed tracker pre-roll frames before warm-up (steady-state track load)")
+    ap.add_argument("--max-frames", type=int, default=1200, help="pre-rendered frames per stream (cycled beyond)")
     ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--frame-copy", default="copy", choices=["copy", "none"],
-                    help="how each step's frames reach the detector's input buffer (none: diagnostic only)")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="run tracker(t) on the detector's stream instead of overlapping it with detector(t+1)")
-    ap.add_argument("--no-tune", action="store_true", help="skip the per-op conv kernel autotune")
-    ap.add_argument("--lanes", type=int, default=None,
-                    help="streams per batch group the detector's op DAG runs on (default 1 with --inflight > 1, else 3)")
+    ap.add_argument("--autotune", action="store_true", help="autotune the conv plan instead of loading plans/*.json")
+    ap.add_argument("--lanes", type=int, default=None)
     ap.add_argument("--groups", type=int, default=1, help="independent sub-batches run concurrently")
-    ap.add_argument("--tracker", default="enhanced", choices=["enhanced", "motion_reset"],
-                    help="tracker: kalman.EnhancedMultiTargetTracker (the driver's) or the camera_motion_compensation "
-                         "MotionCompensatedMultiTracker policy (frame-free)")
+    ap.add_argument("--tracker", default="enhanced", choices=["enhanced", "motion_reset"])
     ap.add_argument("--inflight", type=int, default=3, choices=range(1, 9),
                     help="detector forwards in flight (each a batch of all streams, own graph + HIP stream)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--cpu-seconds", type=float, default=25.0, help="CPU-baseline sample bound (default threads)")
+    ap.add_argument("--cpu-all-seconds", type=float, default=10.0, help="CPU-baseline sample bound (all cores)")
     ap.add_argument("--no-profile", action="store_true")
-    ap.add_argument("--plan-out", default="", help="write the autotuned conv plan (json) here")
-    ap.add_argument("--plan-in", default="", help="load a conv plan (json) instead of autotuning")
+    ap.add_argument("--plan-out", default="", help="write the headline leg's conv plan (json) here")
+    ap.add_argument("--save-plans", action="store_true", help="write every leg's conv plan to plans/<workload>.json")
+    ap.add_argument("--plan-in", default="", help="conv plan (json) of the headline leg (default: plans/<workload>.json)")
     ap.add_argument("--dump-ops", default="", help="write per-op device times (json) to this path")
     return ap.parse_args()
+
+
+# ---------------------------------------------------------------------------- ranks
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n: int) -> int:
+    """`bench.py --gpus N` without a launcher: start N rank processes (one per GPU) like
+    torch.distributed.run does, before this process touches any GPU; exit with the first
+    non-zero child status."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    for p in procs:
+        c = p.wait()
+        rc = rc or c
+    return rc
 
 
 def dist_setup():
@@ -87,10 +138,21 @@ def dist_setup():
     return ws, rank, local
 
 
+def barrier(ws):
+    if ws > 1:
+        import torch.distributed as dist
+
+        dist.barrier()
+
+
+# ---------------------------------------------------------------------------- measurement helpers
 def roofline(pipe, frames, dtype, B):
-    """Per-op device times (hipEvents on the launch stream), grouped by kernel instantiation;
-    the dominant one gives the roofline entry."""
+    """Per-op device times of one forward at a time (hipEvents on the launch stream, `reps`
+    back-to-back launches per op), grouped by kernel instantiation; the dominant one gives the
+    roofline entry.  Returns (entry, by_kernel, per-op list, [t0_ns, t1_ns] of the pass)."""
+    t0 = time.clock_gettime_ns(time.CLOCK_MONOTONIC)
     prof = pipe.model.profile(frames, pipe.conf, pipe.iou, pipe.max_det, reps=5)
+    t1 = time.clock_gettime_ns(time.CLOCK_MONOTONIC)
     flops = pipe.prog.op_flops(B)
     by = {}
     for (i, kind, name, ms), fl in zip(prof, flops):
@@ -98,229 +160,328 @@ def roofline(pipe, frames, dtype, B):
         d["ms"] += ms
         d["flops"] += fl
         d["launches"] += 1
-    dom = max(by, key=lambda k: by[k]["ms"])
+    conv = {k: v for k, v in by.items() if v["flops"] > 0}
+    dom = max(conv, key=lambda k: conv[k]["ms"])
     d = by[dom]
     avg_ms = d["ms"] / d["launches"]
     ach = d["flops"] / (d["ms"] * 1e-3) / 1e12 if d["ms"] > 0 else 0.0
     total_ms = sum(v["ms"] for v in by.values())
     return {
         "kernel": dom, "bound": "mfma", "achieved": round(ach, 2), "peak": PEAK[dtype], "unit": "TFLOP/s",
-        "frac": round(ach / PEAK[dtype], 5), "traffic": pmc_traffic(dom), "traffic_unit": "bytes/launch", "avg_launch_us": round(avg_ms * 1e3, 2),
-        "launches_per_step": d["launches"], "flops_per_launch": int(d["flops"] / d["launches"]),
-        "share_of_detect_time": round(d["ms"] / total_ms, 3),
-    }, by, prof
+        "frac": round(ach / PEAK[dtype], 5), "traffic": pmc_traffic(dom, dtype), "traffic_unit": "bytes/launch",
+        "avg_launch_us": round(avg_ms * 1e3, 2), "launches_per_step": d["launches"],
+        "flops_per_launch": int(d["flops"] / d["launches"]), "share_of_detect_time": round(d["ms"] / total_ms, 3),
+        "timing": "hipEvents around 5 back-to-back launches of each op, one forward at a time",
+    }, by, prof, [t0, t1]
 
 
-def pmc_traffic(kernel):
+def pmc_traffic(kernel, dtype):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
-    (tools/pmc_summary.py: FETCH_SIZE x2 + WRITE_SIZE, separate passes), or None."""
-    path = os.path.join(REPO, "profiles", "pmc_traffic.json")
-    try:
-        with open(path) as f:
-            k = json.load(f)["kernels"]
-    except (OSError, ValueError, KeyError):
-        return None
-    short = kernel.replace("yk::det::", "").replace("yk::trk::", "")
-    v = k.get(short)
-    return None if v is None else round(v["hbm_bytes_per_launch"])
+    (tools/pmc_summary.py: FETCH_SIZE + WRITE_SIZE, separate passes), or None."""
+    for path in (os.path.join(REPO, "profiles", f"pmc_traffic_{dtype}.json"),
+                 os.path.join(REPO, "profiles", "pmc_traffic.json")):
+        try:
+            with open(path) as f:
+                k = json.load(f)["kernels"]
+        except (OSError, ValueError, KeyError):
+            continue
+        short = kernel.replace("yk::det::", "").replace("yk::trk::", "")
+        v = k.get(short)
+        if v is not None:
+            return round(v["hbm_bytes_per_launch"])
+    return None
 
 
 def tracker_roofline(pipe, reps=20):
     """Tracker step kernel alone (events around yk_tracker_step on the launch stream); algorithmic
-    bytes per track-step from SURVEY §8d (1,216 B: R+W of x and dense P, z, box)."""
+    bytes per track-step from SURVEY §8d (1,216 B)."""
     torch.cuda.synchronize()
     _, stats = pipe.stats()
     live = int(stats["current_active_tracks"].sum())
     st = torch.cuda.current_stream()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    # replay from a snapshot-free state: timing only (the tracker keeps evolving, which is fine)
     e0.record(st)
     for _ in range(reps):
         pipe.tracker.step_device(pipe.dets, pipe.counts)
     e1.record(st)
     torch.cuda.synchronize()
     us = e0.elapsed_time(e1) * 1e3 / reps
-    by = live * 1216
+    by = live * TRACK_STEP_BYTES
     gbps = by / (us * 1e-6) / 1e9 if us > 0 else 0.0
     return {"kernel": "step_kernel", "bound": "hbm", "avg_launch_us": round(us, 2), "live_tracks": live,
             "achieved": round(gbps, 3), "peak": HBM_PEAK, "unit": "GB/s", "frac": round(gbps / HBM_PEAK, 6)}
 
 
-def cpu_baseline(P, scale, seconds, targets, seed=0, hw=(512, 640), imgsz=640, tracker="enhanced"):
-    """Reference-equivalent CPU path (oracle: torch-CPU fp32 YOLOv8s+P2 + numpy tracker) on a
-    bounded sample of one stream, threads as the reference's select_device: min(8, ncpu-1)."""
-    from oracle import detector_ref as D
-    from oracle.tracker_ref import RefMultiTracker
-
-    threads = min(8, (os.cpu_count() or 2) - 1)
-    torch.set_num_threads(threads)
-    ar = P.arch.parse_arch(P.arch.load_model_dict(f"yolov8{scale}-small.yaml"))
-    sd = P.weights.synthetic_state_dict(ar, seed)
-    layers = [(Ly.i, Ly.f, Ly.kind, {**Ly.args, **({"c": int(Ly.c2 * 0.5)} if Ly.kind == "C2f" else {})})
-              for Ly in ar.layers]
-    det = D.RefDetector(layers, sd, P.arch.detect_strides(ar))
-    sc = P.synth.Scene(seed=seed, n_targets=targets, n_frames=400, height=hw[0], width=hw[1])
-    if tracker == "motion_reset":
-        from oracle.cmc_ref import RefCMCMultiTracker
-        trk = RefCMCMultiTracker(150, 1, 0.1)
-    else:
-        trk = RefMultiTracker(150, 1, 0.1)
-    n, t_total = 0, 0.0
-    for t in range(400):
-        f = sc.frame(t)
-        t0 = time.perf_counter()
-        res, _ = D.predict(det, [f], 0.25, 0.7, 300, imgsz)
-        boxes = res[0][:, :4].numpy()
-        scores = res[0][:, 4].numpy()
-        dets = [[b[0], b[1], b[2], b[3], s] for b, s in zip(boxes, scores) if s > 0.1]
-        trk.update(dets)
-        dt = time.perf_counter() - t0
-        if t >= 2:  # warm-up frames
-            n += 1
-            t_total += dt
-            if t_total > seconds:
-                break
-    return {"value": round(n / t_total, 3), "unit": "frames/s", "cores": threads, "kind": "port",
-            "sample": f"{n} frames of one {hw[1]}x{hw[0]} stream ({targets} targets), YOLOv8{scale}+P2 fp32 torch-CPU "
-                      f"({threads} threads) + numpy {tracker} tracker, after 2 warm-up frames"}
+def plan_path(a, dtype, S, W, H, imgsz):
+    return os.path.join(REPO, "plans", f"{a.scale}_{W}x{H}_i{imgsz}_b{S}_{dtype}.json")
 
 
 def log(msg):
     print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
 
-def main():
-    a = parse()
-    ws, rank, local = dist_setup()
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    P = importlib.import_module(PKG)
-    from importlib import import_module
+# ---------------------------------------------------------------------------- CPU baseline
+def _cpu_quota() -> int:
+    """CPUs this process may use: affinity, capped by a cgroup v2 cpu.max quota."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            n = min(n, max(1, int(int(q) // int(p))))
+    except (OSError, ValueError):
+        pass
+    return n
 
-    pipeline = import_module(PKG + ".pipeline")
-    if a.streams is None:
-        a.streams = 1 if a.config == 2 else 8
-    if a.lanes is None:
-        a.lanes = 1 if a.inflight > 1 and not a.no_pipeline else 3
-    if a.dtype is None:
-        a.dtype = "fp8" if a.config == 5 else "bf16"
-    S = a.streams
-    H, W, imgsz, max_tracks = (1024, 1280, 1280, 2048) if a.config == 5 else (512, 640, 640, 512)
-    if a.frame:
-        W, H = (int(v) for v in a.frame.lower().split("x"))
-    if a.imgsz:
-        imgsz = a.imgsz
-    if a.targets is None:
-        a.targets = {2: 6, 3: 22, 5: 66}[a.config]
-    shard = P.shard
-    my_streams = shard.stream_ids(rank, ws, S)  # this GPU's block of independent streams
-    pipe = pipeline.StreamPipeline(f"yolov8{a.scale}-small.yaml", S, (H, W), a.dtype, seed=0, device=local,
-                                   pipelined=not a.no_pipeline, imgsz=imgsz, max_tracks=max_tracks,
+
+def cpu_baseline(P, scale, S, targets, hw, imgsz, tracker, threads, seconds, warm_frames=10, max_frames=300):
+    """Reference-equivalent CPU path (the oracle: torch-CPU fp32 YOLOv8+P2 incl. NMS with the
+    TorchNMS quirk + the numpy tracker with its Python IoU loop) on the same workload shape:
+    S frames per forward (one frame per stream) and S trackers stepped one after another, as
+    BASELINE.md's protocol says; time.perf_counter around each whole step (detector / NMS /
+    tracker split recorded), >= `warm_frames` warm-up frames, then up to `max_frames` frames or
+    `seconds` of timed steps, whichever comes first."""
+    from oracle import detector_ref as D
+    from oracle.tracker_ref import RefMultiTracker
+
+    torch.set_num_threads(threads)
+    ar = P.arch.parse_arch(P.arch.load_model_dict(f"yolov8{scale}-small.yaml"))
+    sd = P.weights.synthetic_state_dict(ar, 0)
+    layers = [(Ly.i, Ly.f, Ly.kind, {**Ly.args, **({"c": int(Ly.c2 * 0.5)} if Ly.kind == "C2f" else {})})
+              for Ly in ar.layers]
+    det = D.RefDetector(layers, sd, P.arch.detect_strides(ar))
+    warm_steps = -(-warm_frames // S)
+    max_steps = warm_steps + max(1, -(-max_frames // S))
+    scenes = [P.synth.Scene(seed=s, n_targets=targets, n_frames=max_steps + 1, height=hw[0], width=hw[1])
+              for s in range(S)]
+    frames = [sc.frames_torch(0, max_steps, "cpu").numpy() for sc in scenes]
+    if tracker == "motion_reset":
+        from oracle.cmc_ref import RefCMCMultiTracker
+        trks = [RefCMCMultiTracker(150, 1, 0.1) for _ in range(S)]
+    else:
+        trks = [RefMultiTracker(150, 1, 0.1) for _ in range(S)]
+    step_ms, split = [], np.zeros(3)
+    t_total = 0.0
+    for t in range(max_steps):
+        batch = [frames[s][t] for s in range(S)]
+        t0 = time.perf_counter()
+        with torch.no_grad():
+            im = D.preprocess(batch, imgsz)
+            y, _ = det.forward(im)
+            t1 = time.perf_counter()
+            out = D.non_max_suppression(y, 0.25, 0.7, 300)
+            res = [D.scale_clip(p, im.shape[2:], batch[0].shape[:2]) for p in out]
+        t2 = time.perf_counter()
+        for s in range(S):
+            boxes = res[s][:, :4].numpy()
+            scores = res[s][:, 4].numpy()
+            trks[s].update([[b[0], b[1], b[2], b[3], c] for b, c in zip(boxes, scores) if c > 0.1])
+        t3 = time.perf_counter()
+        if t >= warm_steps:
+            step_ms.append((t3 - t0) * 1e3)
+            split += (t1 - t0, t2 - t1, t3 - t2)
+            t_total += t3 - t0
+            if t_total > seconds:
+                break
+    n = len(step_ms)
+    live = float(np.mean([len(tr.trackers) for tr in trks]))
+    per_frame = np.asarray(step_ms) / S
+    return {"value": round(n * S / t_total, 3), "unit": "frames/s", "cores": threads, "kind": "port",
+            "median_ms_per_frame": round(float(np.median(per_frame)), 3),
+            "p90_ms_per_frame": round(float(np.percentile(per_frame, 90)), 3),
+            "split_ms_per_frame": {"detector": round(split[0] / (n * S) * 1e3, 3), "nms": round(split[1] / (n * S) * 1e3, 3),
+                                   "tracker": round(split[2] / (n * S) * 1e3, 3)},
+            "live_tracks_per_stream": round(live, 1),
+            "sample": f"{n} timed steps x {S} frames ({S} stream(s) of {hw[1]}x{hw[0]}, {targets} targets each; one "
+                      f"batch-{S} forward + {S} numpy {tracker} trackers per step) after {warm_steps * S} warm-up "
+                      f"frames; YOLOv8{scale}+P2 fp32 torch-CPU, {threads} threads"}
+
+
+# ---------------------------------------------------------------------------- one timed leg
+def run_leg(a, P, cfg, dtype, frames, dev, local, rank, ws, headline):
+    pipeline = importlib.import_module(PKG + ".pipeline")
+    S, H, W, imgsz = cfg["S"], cfg["H"], cfg["W"], cfg["imgsz"]
+    F = frames.shape[0]
+    lanes = a.lanes if a.lanes is not None else (1 if a.inflight > 1 and not a.no_pipeline else 3)
+    pipe = pipeline.StreamPipeline(f"yolov8{a.scale}-small.yaml", S, (H, W), dtype, seed=0, device=local,
+                                   pipelined=not a.no_pipeline, imgsz=imgsz, max_tracks=cfg["max_tracks"],
                                    inflight=1 if a.no_pipeline else a.inflight,
                                    tracker_policy=1 if a.tracker == "motion_reset" else 0)
-    # pre-render frames of every stream into HBM (inputs resident before the timed region)
-    F = max(2, min(a.frames, a.warmup + a.steps))
-    scenes = [P.synth.Scene(seed=shard.stream_seed(g, S), n_targets=a.targets, n_frames=F + 1, width=W, height=H)
-              for g in my_streams]
-    frames = torch.empty((F, S, H, W, 3), dtype=torch.uint8, device=dev)
-    for s, sc in enumerate(scenes):
-        frames[:, s] = sc.frames_torch(0, F, dev)
-    torch.cuda.synchronize()
-    log("frames resident; setting schedule")
-    pipe.set_schedule(a.groups, a.lanes)
+    pipe.set_schedule(a.groups, lanes)
     pipe.frames.copy_(frames[0])
-    tune = not a.no_tune
-    if a.plan_in:
-        with open(a.plan_in) as f:
+    plan_src = "heuristic"
+    pth = (a.plan_in if (headline and a.plan_in) else plan_path(a, dtype, (S + a.groups - 1) // a.groups, W, H, imgsz))
+    tune = a.autotune
+    if not tune and os.path.exists(pth):
+        with open(pth) as f:
             pl = json.load(f)
-        pipe.model.load_plan(pl["batch"], pl["plan"])
-        tune = False
+        if len(pl["plan"]) != len(pipe.prog.ops):
+            raise SystemExit(f"conv plan {pth} has {len(pl['plan'])} ops, the program {len(pipe.prog.ops)}: "
+                             "regenerate it with --autotune --plan-out")
+        for m in pipe.models:
+            m.load_plan(pl["batch"], pl["plan"])
+        plan_src = os.path.relpath(pth, REPO)
+    elif not tune:
+        log(f"no committed conv plan at {pth}: autotuning")
+        tune = True
+    if tune:
+        plan_src = "autotuned at run time"
     if not a.no_graph:
         pipe.capture(tune=tune)
     elif tune:
         pipe.model.autotune(pipe.frames, pipe.conf)
         pipe.sync_plan()
-    if a.plan_out and rank == 0:
-        b, pl = pipe.model.get_plan()
-        with open(a.plan_out, "w") as f:
-            json.dump({"batch": b, "plan": pl}, f)
-    log("graph captured; warm-up")
-    # warm-up
-    for t in range(a.warmup):
+    for out_path in ([a.plan_out] if headline and a.plan_out else []) + ([pth] if a.save_plans else []):
+        if rank == 0:
+            b, pl = pipe.model.get_plan()
+            os.makedirs(os.path.dirname(os.path.abspath(out_path)), exist_ok=True)
+            with open(out_path, "w") as f:
+                json.dump({"batch": b, "plan": pl, "dtype": dtype, "workload": os.path.basename(pth)}, f)
+    # untimed pre-roll (steady-state track load, independent of --steps/--warmup), then warm-up
+    n_pre = a.preroll
+    for t in range(n_pre + a.warmup):
         pipe.run(frames[t % F])
-    torch.cuda.synchronize()
-    if ws > 1:
-        import torch.distributed as dist
-
-        dist.barrier()
+    _, st0 = pipe.stats()
+    live_start = st0["current_active_tracks"].astype(np.float64)
+    barrier(ws)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    w0 = time.clock_gettime_ns(time.CLOCK_MONOTONIC)
     for t in range(a.steps):
-        if a.frame_copy == "none":
-            pipe.step()
-        else:
-            pipe.run(frames[(a.warmup + t) % F])
+        pipe.run(frames[(n_pre + a.warmup + t) % F])
     torch.cuda.synchronize()
-    if ws > 1:
-        dist.barrier()
+    barrier(ws)
     elapsed = time.perf_counter() - t0
-    log(f"timed {a.steps} steps in {elapsed:.3f}s")
+    w1 = time.clock_gettime_ns(time.CLOCK_MONOTONIC)
+    log(f"{dtype}: timed {a.steps} steps in {elapsed:.4f}s")
     counts, stats = pipe.stats()
-    live = float(stats["current_active_tracks"].mean())
     frames_done = S * a.steps
-    # PCIe-inclusive rate (host frames -> device each step): informational, never `value`
-    host = frames[0].cpu().pin_memory()
-    torch.cuda.synchronize()
-    tp = time.perf_counter()
-    n_pcie = min(20, a.steps)
-    for _ in range(n_pcie):
-        pipe.frames.copy_(host, non_blocking=True)
-        pipe.step()
-    torch.cuda.synchronize()
-    pcie_fps = S * n_pcie / (time.perf_counter() - tp)
-    # end-of-run exchange (RCCL): SUM of counters, MAX of wall time -- the only collective
-    run, elapsed = shard.reduce_run(shard.local_counters(frames_done, stats), elapsed, dev)
-    frames_done = int(run["frames"])
-    live = run["current_active_tracks"] / (S * ws)
-    fps = frames_done / elapsed
-    rl = None
-    trl = None
+    overflow = int(stats["overflow"].sum())
+    shard = P.shard
+    local_c = shard.local_counters(frames_done, stats)
+    local_c["live_min_start"] = float(live_start.min())
+    run, elapsed_max = shard.reduce_run(local_c, elapsed, dev)
+    fps = run["frames"] / elapsed_max
+    gflop = pipe.flops_per_frame() / 1e9
+    leg = {"dtype": dtype, "value": round(fps, 2), "ms_per_step": round(elapsed_max / a.steps * 1e3, 4),
+           "network_mfma_frac": round(fps / ws * gflop / 1e3 / PEAK[dtype], 5),
+           "live_tracks_per_stream": round(run["current_active_tracks"] / (S * ws), 1),
+           "live_tracks_per_stream_min_at_start": int(live_start.min()),
+           "overflow": int(run["overflow"]), "tracks_created": int(run["total_tracks_created"]),
+           "conv_plan": plan_src, "window_monotonic_ns": [w0, w1]}
+    if overflow:
+        log(f"tracker overflow on this rank: {overflow} detections/tracks dropped")
     if rank == 0 and not a.no_profile:
-        bg = (S + a.groups - 1) // a.groups  # the batch each group's kernels run at
-        rl, by_kernel, prof = roofline(pipe, frames[0][:bg], a.dtype, bg)
-        trl = tracker_roofline(pipe)
-        if a.dump_ops:
+        bg = (S + a.groups - 1) // a.groups
+        rl, by_kernel, prof, win = roofline(pipe, frames[0][:bg], dtype, bg)
+        rl["window_monotonic_ns"] = win
+        leg["roofline"] = rl
+        leg["tracker_roofline"] = tracker_roofline(pipe)
+        if headline and a.dump_ops:
             flops = pipe.prog.op_flops(bg)
             with open(a.dump_ops, "w") as f:
                 json.dump({"ops": [{"op": i, "kind": k, "kernel": n, "us": round(ms * 1e3, 2), "gflop": fl / 1e9}
                                    for (i, k, n, ms), fl in zip(prof, flops)], "by_kernel": by_kernel}, f, indent=1)
-    log("profile done")
+    if headline:
+        # PCIe-inclusive rate (host frames -> device each step): informational, never `value`
+        host = frames[0].cpu().pin_memory()
+        torch.cuda.synchronize()
+        tp = time.perf_counter()
+        n_pcie = min(20, a.steps)
+        for _ in range(n_pcie):
+            pipe.frames.copy_(host, non_blocking=True)
+            pipe.step()
+        torch.cuda.synchronize()
+        leg["pcie_inclusive_fps"] = round(S * n_pcie / (time.perf_counter() - tp) * ws, 2)
+    leg["gflop_per_frame"] = round(gflop, 3)
+    del pipe
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    return leg
+
+
+def main():
+    a = parse()
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(a.gpus))
+    ws, rank, local = dist_setup()
+    if ws != a.gpus:
+        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={ws}: launch one process per GPU")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    P = importlib.import_module(PKG)
+    cfg = dict(CONFIGS[a.config])
+    if a.streams is not None:
+        cfg["S"] = a.streams
+    if a.targets is not None:
+        cfg["targets"] = a.targets
+    if a.frame:
+        cfg["W"], cfg["H"] = (int(v) for v in a.frame.lower().split("x"))
+    if a.imgsz:
+        cfg["imgsz"] = a.imgsz
+    dtype = a.dtype or cfg["dtype"]
+    sec = cfg["secondary"] if a.secondary is None else ("" if a.secondary == "none" else a.secondary)
+    secondary = [d for d in sec.split(",") if d and d != dtype] if ws == 1 else []
+    S, H, W = cfg["S"], cfg["H"], cfg["W"]
+    shard = P.shard
+    my_streams = shard.stream_ids(rank, ws, S)  # this GPU's block of independent streams
+    # pre-render every stream's frames into HBM (inputs resident before anything is timed)
+    F = min(a.max_frames, a.preroll + a.warmup + a.steps)
+    frames = torch.empty((F, S, H, W, 3), dtype=torch.uint8, device=dev)
+    for s, g in enumerate(my_streams):
+        sc = P.synth.Scene(seed=shard.stream_seed(g, S), n_targets=cfg["targets"], n_frames=F + 1, width=W, height=H)
+        frames[:, s] = sc.frames_torch(0, F, dev)
+    torch.cuda.synchronize()
+    log(f"{F} frames x {S} streams resident; headline leg {dtype}, secondary {secondary or 'none'}")
+    head = run_leg(a, P, cfg, dtype, frames, dev, local, rank, ws, headline=True)
+    legs = [run_leg(a, P, cfg, d, frames, dev, local, rank, ws, headline=False) for d in secondary]
+    del frames
     cpu = None
     if rank == 0 and ws == 1 and not a.no_cpu_baseline:
-        cpu = cpu_baseline(P, a.scale, a.cpu_seconds, a.targets, hw=(H, W), imgsz=imgsz, tracker=a.tracker)
+        ncpu = os.cpu_count() or 2
+        ref_threads = max(1, min(8, ncpu - 1))  # the reference's select_device for CPU
+        cpu = cpu_baseline(P, a.scale, S, cfg["targets"], (H, W), cfg["imgsz"], a.tracker, ref_threads, a.cpu_seconds)
+        n_all = _cpu_quota()
+        if n_all != ref_threads and a.cpu_all_seconds > 0:
+            allc = cpu_baseline(P, a.scale, S, cfg["targets"], (H, W), cfg["imgsz"], a.tracker, n_all,
+                                a.cpu_all_seconds)
+            cpu["all_cores"] = {k: allc[k] for k in ("value", "cores", "median_ms_per_frame", "p90_ms_per_frame",
+                                                     "split_ms_per_frame", "sample")}
+        cpu["host_cpus"] = {"os.cpu_count": ncpu, "usable": n_all}
     if rank == 0:
-        gflop = pipe.flops_per_frame() / 1e9
+        ok_floor = head["live_tracks_per_stream_min_at_start"] >= cfg["live_floor"]
         out = {
-            "metric": METRIC, "value": round(fps, 2), "unit": "frames/s", "n_gpus": ws, "steps": a.steps,
-            "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 4), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": a.dtype,
-            "data": f"synthetic: seeded {W}x{H} IR-like scenes rendered into HBM before timing; seeded "
-                    "planted weights (no trained best.pt in the reference)",
-            "config": {"workload": f"YOLOv8{a.scale}+P2 {W}x{H} (imgsz {imgsz}), {S} streams/GPU as batch {S}, "
-                                   f"{a.targets} targets/stream, {a.tracker} tracker(150, 1, 0.1) (BASELINE config {a.config})",
-                       "streams_per_gpu": S, "global_batch": S * ws, "parallelism": f"streams sharded over {ws} GPU(s)",
-                       "graph": not a.no_graph, "tracker_overlapped": not a.no_pipeline, "autotuned": not a.no_tune, "dag_lanes": a.lanes,
-                       "batch_groups": a.groups, "detector_inflight": pipe.D,
-                       "live_tracks_per_stream": round(live, 1),
-                       "tracks_created": int(run["total_tracks_created"]),
-                       "gflop_per_frame": round(gflop, 3)},
-            "network_mfma_frac": round(fps / ws * gflop / 1e3 / PEAK[a.dtype], 5),
-            "pcie_inclusive_fps": round(pcie_fps * ws, 2),
-            "roofline": rl, "tracker_roofline": trl, "cpu_baseline": cpu,
+            "metric": METRIC, "value": head["value"], "unit": "frames/s", "n_gpus": ws, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": head["ms_per_step"], "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": dtype,
+            "data": f"synthetic: seeded {W}x{H} IR-like scenes ({cfg['targets']} targets/stream, occlusion bursts) "
+                    "rendered into HBM before timing; seeded planted weights (no trained best.pt in the reference)",
+            "config": {"workload": f"YOLOv8{a.scale}+P2 {W}x{H} (imgsz {cfg['imgsz']}), {S} stream(s)/GPU as batch {S}, "
+                                   f"{a.tracker} tracker(150, 1, 0.1), BASELINE config {a.config}",
+                       "baseline_config": a.config, "streams_per_gpu": S, "global_batch": S * ws,
+                       "parallelism": f"streams sharded over {ws} GPU(s), no data-path collective",
+                       "targets_per_stream": cfg["targets"], "tracker_preroll_frames": a.preroll,
+                       "live_tracks_per_stream": head["live_tracks_per_stream"],
+                       "live_tracks_per_stream_min_at_start": head["live_tracks_per_stream_min_at_start"],
+                       "live_tracks_floor": cfg["live_floor"], "live_tracks_floor_met": ok_floor,
+                       "tracker_overflow": head["overflow"], "tracks_created": head["tracks_created"],
+                       "conv_plan": head["conv_plan"], "graph": not a.no_graph, "tracker_overlapped": not a.no_pipeline,
+                       "detector_inflight": a.inflight, "gflop_per_frame": head["gflop_per_frame"]},
+            "network_mfma_frac": head["network_mfma_frac"],
+            "pcie_inclusive_fps": head.get("pcie_inclusive_fps"),
+            "roofline": head.get("roofline"), "tracker_roofline": head.get("tracker_roofline"),
+            "cpu_baseline": cpu,
+            "secondary": [{k: v for k, v in leg.items() if k != "window_monotonic_ns"} for leg in legs],
+            "timed_window_monotonic_ns": head["window_monotonic_ns"],
         }
-        print(json.dumps(out))
+        print(json.dumps(out), flush=True)
+    bad = head["overflow"] or any(leg["overflow"] for leg in legs)
     if ws > 1:
+        import torch.distributed as dist
+
         dist.destroy_process_group()
+    if bad:
+        log("FAIL: the tracker dropped detections/tracks (stats.overflow != 0); results would diverge from the reference")
+        sys.exit(3)
 
 
 if __name__ == "__main__":

@@ -223,6 +223,43 @@ def ref_iou(b1, b2):
     return inter / union
 
 
+def ref_iou_matrix_f32dets(dets, boxes):
+    """The D x T matrix of ``ref_iou(det, box)`` for np.float32 detections and float64 track
+    boxes, vectorised with the scalar code's exact dtype flow (a test-harness speed-up for
+    large track counts; ``ref_iou`` stays the definition and tests/test_oracle_kat.py checks
+    the two agree bit for bit):
+      * python max(a, b) returns a (the det) unless b > a; min(a, b) unless b < a -- each
+        intersection coordinate keeps its origin dtype;
+      * a difference / product of two float32 operands rounds to float32, anything with a
+        float64 operand is float64 (the float32 operand widens exactly);
+      * area1 is float32, area2 float64; union and inter/union are float64."""
+    d32 = np.asarray([[d[0], d[1], d[2], d[3]] for d in dets], dtype=np.float32).reshape(-1, 1, 4)
+    b64 = np.asarray(boxes, dtype=np.float64).reshape(1, -1, 4)
+    d64 = d32.astype(np.float64)
+    ax1, ay1, ax2, ay2 = (d64[..., i] for i in range(4))
+    bx1, by1, bx2, by2 = (b64[..., i] for i in range(4))
+    tx1, ty1 = bx1 > ax1, by1 > ay1  # the track value wins max()
+    tx2, ty2 = bx2 < ax2, by2 < ay2  # the track value wins min()
+    ix1, iy1 = np.where(tx1, bx1, ax1), np.where(ty1, by1, ay1)
+    ix2, iy2 = np.where(tx2, bx2, ax2), np.where(ty2, by2, ay2)
+    empty = (ix2 <= ix1) | (iy2 <= iy1)
+    with np.errstate(invalid="ignore", over="ignore", divide="ignore"):
+        # both operands from the det -> float32 arithmetic; else float64
+        wx32 = d32[..., 2] - d32[..., 0]
+        wy32 = d32[..., 3] - d32[..., 1]
+        wx = np.where(tx1 | tx2, ix2 - ix1, wx32.astype(np.float64))
+        wy = np.where(ty1 | ty2, iy2 - iy1, wy32.astype(np.float64))
+        f32x = ~(tx1 | tx2)
+        f32y = ~(ty1 | ty2)
+        inter32 = (wx.astype(np.float32) * wy.astype(np.float32)).astype(np.float64)
+        inter = np.where(f32x & f32y, inter32, wx * wy)
+        area1 = ((d32[..., 2] - d32[..., 0]) * (d32[..., 3] - d32[..., 1])).astype(np.float64)
+        area2 = (bx2 - bx1) * (by2 - by1)
+        union = area1 + area2 - inter
+        iou = np.where(empty | (union <= 0), 0.0, inter / np.where(union > 0, union, 1.0))
+    return iou
+
+
 def ref_greedy_assign(iou, thr, stable=False):
     """enhanced_multi_target_tracker.py:234-270.  ``stable=True`` breaks exact IoU
     ties by row-major pair index (what the HIP kernel does); the default keeps
@@ -247,11 +284,12 @@ class RefMultiTracker:
     """EnhancedMultiTargetTracker semantics (enhanced_multi_target_tracker.py:4-304)."""
 
     def __init__(self, max_lost_frames=450, min_hits=3, iou_threshold=0.3, verbose=False,
-                 stable_ties=False):
+                 stable_ties=False, fast_iou=False):
         self.trackers: list[RefTrack] = []
         self.max_lost_frames, self.min_hits, self.iou_threshold = max_lost_frames, min_hits, iou_threshold
         self.frame_count, self.next_track_id = 0, 1
         self.verbose, self.stable_ties = verbose, stable_ties
+        self.fast_iou = fast_iou  # vectorised IoU (same values) for float32 detections
         self.stats = {"total_tracks_created": 0, "total_tracks_terminated": 0,
                       "current_active_tracks": 0, "long_term_predictions": 0,
                       "successful_recoveries": 0}
@@ -260,10 +298,13 @@ class RefMultiTracker:
         self.tie_frames = 0
 
     def _associate(self, dets, boxes):
-        iou = np.zeros((len(dets), len(boxes)))
-        for d, det in enumerate(dets):
-            for t, tb in enumerate(boxes):
-                iou[d, t] = ref_iou(det[:4], tb)
+        if self.fast_iou and all(isinstance(v, np.float32) for det in dets for v in det[:4]):
+            iou = ref_iou_matrix_f32dets(dets, boxes)
+        else:
+            iou = np.zeros((len(dets), len(boxes)))
+            for d, det in enumerate(dets):
+                for t, tb in enumerate(boxes):
+                    iou[d, t] = ref_iou(det[:4], tb)
         self.last_iou = iou
         cand = iou[iou >= self.iou_threshold]
         if cand.size != np.unique(cand).size:

@@ -1,0 +1,201 @@
+#!/usr/bin/env python3
+"""Generate the golden fixtures tests/golden/*.npz from the CPU oracle (oracle/, test
+infrastructure).  Run in the build container:  python tests/golden/make_golden.py
+
+The reference itself cannot be run here (importing it was refused) and its own
+tests hold no vectors for this path, so these fixtures freeze the oracle's outputs on the
+BASELINE.json workloads (inputs are regenerated from seeds by the deterministic numpy
+generators of synth.py / tests/cmc_sequences.py; only the expected outputs are stored):
+
+  tracker_c3.npz       EnhancedMultiTargetTracker(150, 1, 0.1), 40 GT-injected targets/stream
+                       at 640x512 (config 3's tracker leg), 120 frames, float32 detections
+  tracker_c5.npz       same tracker, 256 targets at 1280x1024 (config 5's tracker leg), 24 frames
+  tracker_defaults.npz EnhancedMultiTargetTracker() defaults (450, 3, 0.3), python-float dets
+  cmc_jumpy.npz        MotionCompensatedMultiTracker(150, 1, 0.1).update(dets) on a jump / size /
+                       velocity-change sequence
+  detector_n.npz       YOLOv8n+P2 (yolov8-small.yaml) fp32 predict of two 640x512 frames
+                       (Results.boxes.data), plus the Detect candidates above conf
+  nms.npz              TorchNMS.nms keep lists (utils/nms.py:237-304, quirk C) on seeded box sets
+  letterbox.npz        LetterBox(640) canvases of a 1920x1080 and a 400x300 frame (sha256 + rows)
+"""
+from __future__ import annotations
+
+import hashlib
+import os
+import sys
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.dirname(HERE))
+
+PKG = "yolo---small-target-recognition---kalman-trajectory-prediction_amd"
+
+
+def pkg():
+    import importlib
+
+    return importlib.import_module(PKG)
+
+
+# ------------------------------------------------------------------ trackers
+TRACKER_CASES = {
+    "tracker_c3": dict(scene=dict(seed=0, n_targets=40, n_frames=120), args=(150, 1, 0.1), f64=False),
+    "tracker_c5": dict(scene=dict(seed=5, n_targets=256, n_frames=24, width=1280, height=1024), args=(150, 1, 0.1),
+                       f64=False),
+    "tracker_defaults": dict(scene=dict(seed=3, n_targets=12, n_frames=60), args=(450, 3, 0.3), f64=True),
+}
+
+
+def tracker_inputs(name):
+    c = TRACKER_CASES[name]
+    sc = pkg().synth.Scene(**c["scene"])
+    frames = [sc.detections(t) for t in range(sc.T)]
+    if c["f64"]:
+        frames = [[[float(v) for v in d] for d in f] for f in frames]
+    return frames, c["args"]
+
+
+def cmc_inputs():
+    from cmc_sequences import jumpy_sequence
+
+    return jumpy_sequence(seed=1, K=12, T=120), (150, 1, 0.1)
+
+
+def pack_tracks(outputs, stats):
+    """Per-frame lists of track dicts -> flat arrays + frame offsets."""
+    off, ints, flts = [0], [], []
+    for frame in outputs:
+        for d in frame:
+            ints.append([int(d["track_id"][1:]) if isinstance(d["track_id"], str) else int(d["track_id"]),
+                         0 if d["status"] == "detected" else 1, d["age"], d["hits"], d["hit_streak"],
+                         d["time_since_update"], d.get("reset_count", 0)])
+            flts.append([*np.asarray(d["bbox"], dtype=np.float64), float(d["confidence"])])
+        off.append(len(ints))
+    return {"off": np.asarray(off, np.int32), "ints": np.asarray(ints, np.int32).reshape(-1, 7),
+            "flts": np.asarray(flts, np.float64).reshape(-1, 5), "stats": np.asarray(stats, np.int64)}
+
+
+def run_tracker_oracle(name):
+    from oracle.tracker_ref import RefMultiTracker
+
+    frames, args = tracker_inputs(name)
+    ref = RefMultiTracker(*args, stable_ties=True)
+    outs, stats = [], []
+    for dets in frames:
+        outs.append(ref.update(dets))
+        stats.append([ref.stats[k] for k in ("total_tracks_created", "total_tracks_terminated", "current_active_tracks",
+                                             "long_term_predictions", "successful_recoveries")])
+    return pack_tracks(outs, stats)
+
+
+def run_cmc_oracle():
+    from oracle.cmc_ref import RefCMCMultiTracker
+
+    frames, args = cmc_inputs()
+    ref = RefCMCMultiTracker(*args)
+    outs, stats = [], []
+    for dets in frames:
+        outs.append(ref.update(dets))
+        stats.append([ref.stats[k] for k in ("total_frames", "individual_resets", "tracking_recoveries")])
+    return pack_tracks(outs, stats)
+
+
+# ------------------------------------------------------------------ detector
+def detector_setup():
+    P = pkg()
+    ar = P.arch.parse_arch(P.arch.load_model_dict("yolov8-small.yaml"))
+    sd = P.weights.synthetic_state_dict(ar, 0)
+    sc = P.synth.Scene(seed=0, n_targets=16, n_frames=3)
+    return P, ar, sd, [sc.frame(t) for t in range(2)]
+
+
+def run_detector_oracle():
+    from oracle import detector_ref as D
+
+    P, ar, sd, frames = detector_setup()
+    layers = [(Ly.i, Ly.f, Ly.kind, {**Ly.args, **({"c": int(Ly.c2 * 0.5)} if Ly.kind == "C2f" else {})})
+              for Ly in ar.layers]
+    ref = D.RefDetector(layers, sd, P.arch.detect_strides(ar))
+    res, y = D.predict(ref, frames, 0.25, 0.7, 300, 640)
+    out = {"n": np.asarray([len(r) for r in res], np.int32),
+           "dets": np.concatenate([r.numpy() for r in res]).astype(np.float32)}
+    for b in range(len(frames)):
+        keep = (y[b, 4] > 0.25).nonzero().flatten()
+        out[f"cand_idx{b}"] = keep.numpy().astype(np.int32)
+        out[f"cand{b}"] = y[b][:, keep].numpy().T.astype(np.float32)  # [n, 5] cx, cy, w, h, score
+    return out
+
+
+def nms_inputs():
+    rng = np.random.default_rng(7)
+    cases = []
+    for n in (1, 2, 17, 64, 300, 1000):
+        c = rng.uniform(0, 600, (n, 2))
+        wh = rng.uniform(4, 120, (n, 2))
+        boxes = np.concatenate([c - wh / 2, c + wh / 2], 1).astype(np.float32)
+        scores = rng.uniform(0.25, 1.0, n).astype(np.float32)
+        cases.append((boxes, scores, 0.7))
+    # quirk C known-answer case: A alone, then B and C overlap but no longer A
+    cases.append((np.array([[0, 0, 10, 10], [100, 0, 110, 10], [101, 0, 111, 10]], np.float32),
+                  np.array([0.9, 0.8, 0.7], np.float32), 0.7))
+    return cases
+
+
+def run_nms_oracle():
+    from oracle import detector_ref as D
+
+    out = {}
+    for i, (b, s, thr) in enumerate(nms_inputs()):
+        out[f"keep{i}"] = D.torch_nms(torch.from_numpy(b), torch.from_numpy(s), thr).numpy().astype(np.int32)
+    return out
+
+
+def letterbox_inputs():
+    P = pkg()
+    return {hw: P.synth.Scene(seed=9, n_targets=24, n_frames=2, height=hw[0], width=hw[1]).frame(0)
+            for hw in ((1080, 1920), (300, 400))}
+
+
+def run_letterbox_oracle():
+    from oracle.letterbox_ref import letterbox
+
+    out = {}
+    for (h, w), f in letterbox_inputs().items():
+        c = letterbox(f, 640, 32)
+        out[f"sha_{w}x{h}"] = np.frombuffer(hashlib.sha256(c.tobytes()).digest(), np.uint8)
+        out[f"shape_{w}x{h}"] = np.asarray(c.shape, np.int32)
+        out[f"row_{w}x{h}"] = c[c.shape[0] // 2].copy()
+    return out
+
+
+GENERATORS = {
+    "tracker_c3": lambda: run_tracker_oracle("tracker_c3"),
+    "tracker_c5": lambda: run_tracker_oracle("tracker_c5"),
+    "tracker_defaults": lambda: run_tracker_oracle("tracker_defaults"),
+    "cmc_jumpy": run_cmc_oracle,
+    "detector_n": run_detector_oracle,
+    "nms": run_nms_oracle,
+    "letterbox": run_letterbox_oracle,
+}
+
+
+def load(name):
+    with np.load(os.path.join(HERE, f"{name}.npz")) as z:
+        return {k: z[k] for k in z.files}
+
+
+def main():
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+    for name, gen in GENERATORS.items():
+        arrs = gen()
+        np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **arrs)
+        print(name, {k: v.shape for k, v in arrs.items() if not k.startswith(("cand", "keep"))},
+              os.path.getsize(os.path.join(HERE, f"{name}.npz")), "bytes")
+
+
+if __name__ == "__main__":
+    main()

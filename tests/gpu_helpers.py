@@ -1,0 +1,84 @@
+"""GPU test plumbing: record a pipelined StreamPipeline's per-step outputs without
+synchronising it, and compare track dicts against the oracle."""
+import ctypes as C
+import os
+
+import numpy as np
+import torch
+
+from conftest import pkg
+
+_hip = None
+
+
+def _hip_rt():
+    """torch's bundled HIP runtime (the one libyk.so and torch share)."""
+    global _hip
+    if _hip is None:
+        _hip = C.CDLL(os.path.join(os.path.dirname(torch.__file__), "lib", "libamdhip64.so"))
+        _hip.hipMemcpyAsync.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_void_p]
+        _hip.hipMemcpyAsync.restype = C.c_int
+    return _hip
+
+
+def d2d_async(dst: int, src: int, nbytes: int, stream) -> None:
+    rc = _hip_rt().hipMemcpyAsync(C.c_void_p(dst), C.c_void_p(src), nbytes, 3, C.c_void_p(stream.cuda_stream))
+    assert rc == 0, f"hipMemcpyAsync failed: {rc}"
+
+
+class StepRecorder:
+    """StreamPipeline.step_hook that copies, in stream order, every step's detections (on the
+    detector stream) and the tracker's output rows / counts / stats (on the tracker stream)
+    into per-step device history buffers; host() downloads them after the run."""
+
+    def __init__(self, pipe, n_steps: int):
+        L = pkg()._lib
+        self.L = L
+        S, T = pipe.S, pipe.tracker.max_tracks
+        dev = torch.device("cuda", pipe.device)
+        self.n, self.t = n_steps, 0
+        self.dets = torch.zeros((n_steps, S, pipe.max_det, 6), dtype=torch.float32, device=dev)
+        self.counts = torch.zeros((n_steps, S), dtype=torch.int32, device=dev)
+        self.row_bytes = S * T * L.TRACK_OUT_DTYPE.itemsize
+        self.stat_bytes = S * L.STATS_DTYPE.itemsize
+        self.rows = torch.zeros((n_steps, self.row_bytes), dtype=torch.uint8, device=dev)
+        self.tcounts = torch.zeros((n_steps, S), dtype=torch.int32, device=dev)
+        self.stats = torch.zeros((n_steps, self.stat_bytes), dtype=torch.uint8, device=dev)
+        self.S, self.T = S, T
+
+    def __call__(self, pipe, k, det_stream, trk_stream):
+        t = self.t
+        assert t < self.n, "more steps than the recorder holds"
+        with torch.cuda.stream(det_stream):
+            self.dets[t].copy_(pipe._dets[k])
+            self.counts[t].copy_(pipe._counts[k])
+        rows, counts, stats = pipe.tracker.device_outputs()
+        d2d_async(self.rows[t].data_ptr(), rows, self.row_bytes, trk_stream)
+        d2d_async(self.tcounts[t].data_ptr(), counts, self.S * 4, trk_stream)
+        d2d_async(self.stats[t].data_ptr(), stats, self.stat_bytes, trk_stream)
+        self.t += 1
+
+    def host(self):
+        torch.cuda.synchronize()
+        n = self.t
+        rows = self.rows[:n].cpu().numpy().view(self.L.TRACK_OUT_DTYPE).reshape(n, self.S, self.T)
+        stats = self.stats[:n].cpu().numpy().view(self.L.STATS_DTYPE).reshape(n, self.S)
+        return (self.dets[:n].cpu().numpy(), self.counts[:n].cpu().numpy(), rows, self.tcounts[:n].cpu().numpy(),
+                stats)
+
+
+def track_dicts(rows, n):
+    P = pkg()
+    return [P.tracker._row_to_dict(r, P.tracker.track_id_of(r["track_num"])) for r in rows[:n]]
+
+
+def decisions(tracks):
+    """The association decisions of one frame: (track_id, status, age, hits, tsu) per output."""
+    return [(d["track_id"], d["status"], d["age"], d["hits"], d["time_since_update"]) for d in tracks]
+
+
+def score_ties(pred: torch.Tensor, conf: float = 0.25) -> int:
+    """Exact duplicate scores among the NMS candidates (score > conf) of one image's Detect
+    output [5, A]: non_max_suppression's scores.sort (utils/nms.py:264) is unstable on them."""
+    s = pred[4][pred[4] > conf]
+    return int(s.numel() - torch.unique(s).numel())

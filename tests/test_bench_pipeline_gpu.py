@@ -1,0 +1,151 @@
+"""The exact benchmark pipeline (BASELINE config 3) against the oracle chain, every frame.
+
+bench.py's headline leg: YOLOv8s+P2 fp32, 8 streams as one batch-8 forward, three detector
+forwards in flight (inflight=3, one hipGraph per slot), the tracker on its own stream,
+EnhancedMultiTargetTracker(150, 1, 0.1) semantics, 40 targets per stream (>= 64 live tracks) with occlusion bursts
+(SURVEY §8d).  The pipeline runs unsynchronised; a step hook records every step's detections
+and tracker rows in stream order.  The oracle chain per stream is oracle/detector_ref.py
+(torch-CPU fp32) -> oracle/tracker_ref.py (numpy) on the same frames.
+
+Bars (BASELINE north_star): track-ID / association decisions identical; boxes within 1e-4
+relative (atol 1e-3 px).  The bf16 leg is measured against the same fp32 oracle chain: the
+fraction of (stream, frame) decisions that agree is reported, not asserted bit-identical.
+"""
+import json
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import pkg
+from gpu_helpers import StepRecorder, decisions, score_ties, track_dicts
+from oracle import detector_ref as D
+from oracle.tracker_ref import RefMultiTracker
+
+pytestmark = pytest.mark.gpu
+
+S, F, TARGETS = 8, 160, 40  # bench.py config 3's streams and targets
+
+
+def _layers(ar):
+    return [(Ly.i, Ly.f, Ly.kind, {**Ly.args, **({"c": int(Ly.c2 * 0.5)} if Ly.kind == "C2f" else {})})
+            for Ly in ar.layers]
+
+
+def _threads():
+    import os
+
+    n = len(os.sched_getaffinity(0))
+    return max(1, min(16, n))
+
+
+@pytest.fixture(scope="module")
+def chain():
+    """Frames (rendered once on the CPU, the same arrays for both sides) and the oracle chain's
+    per-frame detections and track dicts for every stream."""
+    P = pkg()
+    scenes = [P.synth.Scene(seed=P.shard.stream_seed(s, S), n_targets=TARGETS, n_frames=F + 1) for s in range(S)]
+    frames = torch.stack([sc.frames_torch(0, F, "cpu") for sc in scenes], 1)  # [F, S, H, W, 3]
+    ar = P.arch.parse_arch(P.arch.load_model_dict("yolov8s-small.yaml"))
+    sd = P.weights.synthetic_state_dict(ar, 0)
+    ref = D.RefDetector(_layers(ar), sd, P.arch.detect_strides(ar))
+    torch.set_num_threads(_threads())
+    trks = [RefMultiTracker(150, 1, 0.1, stable_ties=True, fast_iou=True) for _ in range(S)]
+    dets, tracks, ties = [], [], 0
+    for t in range(F):
+        fr = list(frames[t].numpy())
+        want, y = D.predict(ref, fr)
+        ties += sum(score_ties(y[s]) for s in range(S))
+        dets.append([w.numpy() for w in want])
+        tracks.append([trks[s].update([[b[0], b[1], b[2], b[3], b[4]] for b in want[s][:, :5].numpy()])
+                       for s in range(S)])
+    return {"frames": frames, "dets": dets, "tracks": tracks, "nms_score_ties": ties,
+            "tie_frames": sum(tr.tie_frames for tr in trks),
+            "terminated": sum(tr.stats["total_tracks_terminated"] for tr in trks),
+            "live": [len(tr.trackers) for tr in trks]}
+
+
+def _run_gpu(dtype, frames):
+    P = pkg()
+    import importlib
+
+    pipeline = importlib.import_module(P.__name__ + ".pipeline")
+    pipe = pipeline.StreamPipeline("yolov8s-small.yaml", S, (512, 640), dtype, seed=0, max_tracks=512,
+                                   pipelined=True, inflight=3)
+    pipe.set_schedule(1, 1)  # bench.py's schedule with 3 forwards in flight
+    fd = frames.cuda()
+    pipe.frames.copy_(fd[0])
+    pipe.capture(tune=False)
+    rec = StepRecorder(pipe, F)
+    pipe.step_hook = rec
+    for t in range(F):
+        pipe.run(fd[t])
+    pipe.sync()
+    out = rec.host()
+    del pipe
+    torch.cuda.empty_cache()
+    return out
+
+
+@pytest.mark.timeout(900)
+def test_bench_pipeline_fp32_matches_oracle_chain_every_frame(chain):
+    dets, counts, rows, tcounts, stats = _run_gpu("fp32", chain["frames"])
+    assert int(stats[-1]["overflow"].sum()) == 0
+    for t in range(F):
+        for s in range(S):
+            want = chain["dets"][t][s]
+            got = dets[t, s, : counts[t, s]]
+            assert got.shape == want.shape, (t, s, got.shape, want.shape)
+            np.testing.assert_allclose(got[:, :4], want[:, :4], rtol=1e-4, atol=1e-3, err_msg=f"frame {t} stream {s}")
+            np.testing.assert_allclose(got[:, 4], want[:, 4], rtol=1e-4, atol=1e-6)
+            ours = track_dicts(rows[t, s], int(tcounts[t, s]))
+            ref = chain["tracks"][t][s]
+            assert decisions(ours) == decisions(ref), (t, s)
+            for o, r in zip(ours, ref):
+                np.testing.assert_allclose(o["bbox"], r["bbox"], rtol=1e-4, atol=1e-3)
+                np.testing.assert_allclose(o["confidence"], r["confidence"], rtol=1e-4, atol=1e-9)
+    live = [int(tcounts[-1, s]) for s in range(S)]
+    assert min(chain["live"]) >= 40, chain["live"]  # the bench's >= 64-track load (see bench.py CONFIGS)
+    assert chain["terminated"] > 0  # the deletion path ran inside the chain
+    print("BENCH_PIPELINE_FP32", json.dumps({"frames": F, "streams": S, "live_tracks_end": live,
+                                             "oracle_tie_frames": chain["tie_frames"],
+                                             "nms_score_ties": chain["nms_score_ties"],
+                                             "terminated": chain["terminated"]}))
+
+
+@pytest.mark.timeout(900)
+def test_bench_pipeline_bf16_agreement_with_fp32_oracle(chain):
+    """How often the bf16 build's association decisions equal the fp32 oracle chain's: the
+    fraction of (stream, frame) pairs whose (id, status, age, hits, tsu) lists are identical,
+    the first diverging frame per stream, and the detection recall at IoU > 0.5."""
+    dets, counts, rows, tcounts, stats = _run_gpu("bf16", chain["frames"])
+    agree, first_div, matched, total = 0, [], 0, 0
+    for s in range(S):
+        fd = None
+        for t in range(F):
+            same = decisions(track_dicts(rows[t, s], int(tcounts[t, s]))) == decisions(chain["tracks"][t][s])
+            agree += same
+            if not same and fd is None:
+                fd = t
+            want = chain["dets"][t][s][:, :4]
+            got = dets[t, s, : counts[t, s], :4]
+            total += len(want)
+            if len(want) and len(got):
+                iou = _iou(want, got)
+                matched += int((iou.max(1) > 0.5).sum())
+        first_div.append(fd)
+    frac = agree / (S * F)
+    recall = matched / max(total, 1)
+    print("BENCH_PIPELINE_BF16_AGREEMENT", json.dumps({"frames": F, "streams": S, "decision_agreement": round(frac, 4),
+                                                        "first_divergence_frame": first_div,
+                                                        "det_recall_iou50": round(recall, 4)}))
+    assert recall > 0.9
+
+
+def _iou(a, b):
+    a, b = a[:, None, :], b[None, :, :]
+    ix = np.clip(np.minimum(a[..., 2], b[..., 2]) - np.maximum(a[..., 0], b[..., 0]), 0, None)
+    iy = np.clip(np.minimum(a[..., 3], b[..., 3]) - np.maximum(a[..., 1], b[..., 1]), 0, None)
+    inter = ix * iy
+    area = lambda z: (z[..., 2] - z[..., 0]) * (z[..., 3] - z[..., 1])  # noqa: E731
+    return inter / (area(a) + area(b) - inter)

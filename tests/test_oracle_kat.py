@@ -135,3 +135,46 @@ def test_cmc_greedy_tie_order():
     iou = np.array([[0.5, 0.2], [0.5, 0.0]])
     assert cmc_greedy(iou, 0.1) == [(1, 0), (0, 1)]
     assert cmc_greedy(np.array([[0.1]]), 0.1) == []  # strict >
+
+
+def test_fast_iou_matrix_is_the_scalar_iou_bit_for_bit():
+    """oracle.tracker_ref.ref_iou_matrix_f32dets (the vectorised test-harness IoU) equals the
+    scalar restatement of enhanced_multi_target_tracker.py:200-232 element for element,
+    including ties between a det and a track coordinate, touching / disjoint boxes and
+    degenerate (zero-area) boxes."""
+    from oracle.tracker_ref import ref_iou_matrix_f32dets
+
+    rng = np.random.default_rng(11)
+    for trial in range(20):
+        D, T = int(rng.integers(1, 40)), int(rng.integers(1, 40))
+        c = rng.uniform(0, 100, (D, 2))
+        wh = rng.uniform(0, 20, (D, 2))
+        dets = np.concatenate([c - wh / 2, c + wh / 2], 1).astype(np.float32)
+        tc = rng.uniform(0, 100, (T, 2))
+        twh = rng.uniform(0, 20, (T, 2))
+        boxes = np.concatenate([tc - twh / 2, tc + twh / 2], 1)
+        # plant exact coordinate ties, touching edges and copies
+        for k in range(min(D, T) // 2):
+            j = int(rng.integers(0, 4))
+            boxes[k, j] = float(dets[k, j])
+        if D > 2 and T > 2:
+            boxes[1] = dets[1].astype(np.float64)
+            boxes[2, 0] = float(dets[2, 2])  # touching: ix2 == ix1
+            dets[0, 2] = dets[0, 0]          # zero-width det
+        dl = [[d[0], d[1], d[2], d[3], f32(0.5)] for d in dets]
+        want = np.array([[ref_iou(d[:4], b) for b in boxes] for d in dl])
+        got = ref_iou_matrix_f32dets(dl, boxes)
+        assert got.dtype == np.float64
+        assert np.array_equal(got, want), trial
+
+
+def test_fast_iou_tracker_equals_loop_tracker():
+    from synth_helpers import scene_dets
+
+    a = RefMultiTracker(150, 1, 0.1, stable_ties=True)
+    b = RefMultiTracker(150, 1, 0.1, stable_ties=True, fast_iou=True)
+    for dets in scene_dets(seed=5, n_targets=40, n_frames=60):
+        ra, rb = a.update(dets), b.update(dets)
+        assert [x["track_id"] for x in ra] == [x["track_id"] for x in rb]
+        for x, y in zip(ra, rb):
+            assert np.array_equal(x["bbox"], y["bbox"]) and x["confidence"] == y["confidence"]

@@ -147,3 +147,38 @@ def test_multi_tracker_views_and_statistics():
         _close(a.x, b.x, "view x")
         _close(a.P, b.P, "view P")
         assert a.age == b.age and a.hits == b.hits
+
+
+@pytest.mark.timeout(900)
+def test_config5_tracker_leg_256_tracks_150_frame_bursts():
+    """BASELINE config 5's tracker leg: 256 targets per stream at 1280x1024 with 150-frame
+    predict-only occlusion bursts (GT-injected detections, option (ii)), two streams
+    stepped by one launch, every frame against the oracle; exact-IoU tie frames are counted."""
+    import json
+
+    yk = pkg()
+    S, F = 2, 330
+    scenes = [yk.synth.Scene(seed=500 + s, n_targets=256, n_frames=F, width=1280, height=1024,
+                             occlusion_lengths=(1, 30, 149, 150, 150, 150)) for s in range(S)]
+    ms = yk.MultiStreamTracker(S, 150, 1, 0.1, max_tracks=2048, max_dets=512)
+    refs = [RefMultiTracker(150, 1, 0.1, stable_ties=True, fast_iou=True) for _ in range(S)]
+    live_max = 0
+    for t in range(F):
+        per = [sc.detections(t) for sc in scenes]
+        ms.step_host(per)
+        rows, counts, stats = ms.download()
+        for s in range(S):
+            rb = refs[s].update(per[s])
+            ours = [yk.tracker._row_to_dict(r, yk.tracker.track_id_of(r["track_num"])) for r in rows[s, : counts[s]]]
+            compare_frame(ours, rb, f"stream {s} frame {t}")
+            live_max = max(live_max, len(refs[s].trackers))
+    for s in range(S):
+        for k in refs[s].stats:
+            assert int(stats[s][k]) == refs[s].stats[k], (s, k)
+        assert int(stats[s]["overflow"]) == 0
+    assert min(len(r.trackers) for r in refs) >= 256
+    assert sum(r.stats["total_tracks_terminated"] for r in refs) > 0
+    print("CONFIG5_TRACKER_LEG", json.dumps({"streams": S, "frames": F, "live_max": live_max,
+                                             "live_end": [len(r.trackers) for r in refs],
+                                             "terminated": [r.stats["total_tracks_terminated"] for r in refs],
+                                             "tie_frames": [r.tie_frames for r in refs]}))

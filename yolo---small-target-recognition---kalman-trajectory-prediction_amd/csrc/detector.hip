@@ -207,6 +207,7 @@ __device__ __forceinline__ View pick_view(const View& v0, const View& v1, bool s
 
 // ---------------------------------------------------------------- implicit-GEMM conv
 constexpr int kTabMax = 1024;
+constexpr int kTsCap = 65536;  // YK_FAST_TS diagnostics: workgroups with timestamps
 
 // Table entry of K chunk q computed arithmetically (model.py Program.pack: tap, ch =
 // divmod(8q, cin); src = ch >= c0): no table load, so no memory round trip in the K loop.
@@ -743,6 +744,7 @@ struct FastArgs {
   int act;
   int xcd;
   unsigned long long* tstamp;  // diagnostics (YK_FAST_TS): per-workgroup [start, end] wall clock
+  int tstamp_cap;              // workgroups the tstamp buffer holds (3 entries each)
 };
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
@@ -782,7 +784,7 @@ __global__ void __launch_bounds__(256) conv_fast_kernel(FastArgs a) {
   const int pbase = WS ? blk.x * (16 * NPT) : (blk.x * 4 + wave) * (16 * NPT);
   const int nk = a.k_steps;
   const int wg_lin = blockIdx.y * gridDim.x + blockIdx.x;
-  if (a.tstamp && tid == 0) a.tstamp[3 * wg_lin] = wall_clock64();
+  if (a.tstamp && tid == 0 && wg_lin < a.tstamp_cap) a.tstamp[3 * wg_lin] = wall_clock64();
   {
     int2 tv[2];  // <= 512 entries (nk <= 128) in one round trip
 #pragma unroll
@@ -906,7 +908,7 @@ __global__ void __launch_bounds__(256) conv_fast_kernel(FastArgs a) {
       }
     }
   }
-  if (a.tstamp && tid == 0) a.tstamp[3 * wg_lin + 1] = wall_clock64();
+  if (a.tstamp && tid == 0 && wg_lin < a.tstamp_cap) a.tstamp[3 * wg_lin + 1] = wall_clock64();
   if constexpr (WS) {
     f32x4* red = (f32x4*)(smem + (((size_t)nk * 4 * 8 + 15) & ~(size_t)15));
 #pragma unroll
@@ -959,7 +961,7 @@ __global__ void __launch_bounds__(256) conv_fast_kernel(FastArgs a) {
       store4((T*)a.dst + (size_t)p * a.d_cstride + a.d_coff + n0, v);
     }
   }
-  if (a.tstamp && tid == 0) a.tstamp[3 * wg_lin + 2] = wall_clock64();
+  if (a.tstamp && tid == 0 && wg_lin < a.tstamp_cap) a.tstamp[3 * wg_lin + 2] = wall_clock64();
 }
 
 // ---------------------------------------------------------------- persistent LDS-tiled conv (wide layers)
@@ -2215,7 +2217,7 @@ struct yk_model {
   int wide_dbg = 0;                   // YK_WIDE_DBG: conv_wide_kernel diagnostics (never in production)
   bool no_wide = false;               // YK_NO_WIDE=1: autotune without the LDS-resident wide kernel
   int ts_op = -1;                     // YK_FAST_TS=<op>: per-workgroup timestamps of that conv_fast op
-  unsigned long long* ts = nullptr;   // [3 * 65536] start, after K loop, end (wall_clock64, 100 MHz)
+  unsigned long long* ts = nullptr;   // [3 * kTsCap] start, after K loop, end (wall_clock64, 100 MHz)
   std::vector<int64_t> ltab_off;
   unsigned char* lbox = nullptr;  // letterboxed frames [max_batch][in_h][in_w][3] (resize only)
   char* arena = nullptr;      // every activation buffer (bufs[i] point into it)
@@ -2826,6 +2828,7 @@ int launch_op(yk_model* m, const yk_op& op, const uint8_t* frames, int B, float 
           f.act = a.act;
           f.xcd = m->xcd;
           f.tstamp = (m->ts && (int)(&op - m->ops.data()) == m->ts_op) ? m->ts : nullptr;
+          f.tstamp_cap = kTsCap;
           launch_fast<Tr>(f, cp, st);
         } else if constexpr (Tr::kScaled) {
           // FP8 runs only on the table-driven and wide kernels (16-channel K chunks)
@@ -3366,8 +3369,8 @@ int yk_model_create(yk_ctx* ctx, const yk_model_desc* desc, const void* host_blo
   if (const char* env = getenv("YK_NO_WIDE")) m->no_wide = env[0] == '1';
   if (const char* env = getenv("YK_FAST_TS")) {
     m->ts_op = atoi(env);
-    if (e == hipSuccess) e = hipMalloc((void**)&m->ts, 3 * 65536 * sizeof(unsigned long long));
-    if (e == hipSuccess) e = hipMemset(m->ts, 0, 3 * 65536 * sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipMalloc((void**)&m->ts, 3 * (size_t)kTsCap * sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipMemset(m->ts, 0, 3 * (size_t)kTsCap * sizeof(unsigned long long));
   }
   if (e == hipSuccess) e = build_ktabs(m, !(getenv("YK_CONV_FAST") && getenv("YK_CONV_FAST")[0] == '0'));
   if (e == hipSuccess && desc->act_dtype == YK_ACT_FP8)

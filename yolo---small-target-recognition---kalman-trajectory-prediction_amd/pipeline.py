@@ -61,6 +61,7 @@ class StreamPipeline:
         self._ev_trk = [torch.cuda.Event() for _ in range(self.nb)]
         self._trk_pending = [False] * self.nb
         self.graph = None
+        self.step_hook = None  # callable(pipe, k, det_stream, trk_stream), see step()
         self.D = int(inflight)
         if not 1 <= self.D <= 8:
             raise ValueError("inflight must be in [1, 8]")
@@ -134,6 +135,10 @@ class StreamPipeline:
             self._trk_pending[k] = True
         else:
             self.tracker.step_device(self._dets[k], self._counts[k])
+        if self.step_hook is not None:
+            # harness hook (tests/recorders): enqueue work after this step's launches on the
+            # detector stream (reads of detection buffer k) and the tracker stream (results)
+            self.step_hook(self, k, cur, self.trk_stream if self.pipelined else cur)
         self._k = (k + 1) % self.nb
 
     def sync(self):
@@ -142,11 +147,24 @@ class StreamPipeline:
 
     def run(self, frames: torch.Tensor):
         """frames [S, H, W, 3] uint8 (device) -> one step.  The copy runs on the slot's detector
-        stream, after that slot's previous forward has read its frames."""
+        stream, after that slot's previous forward has read its frames, and after whatever the
+        caller's current stream enqueued before this call (the producer of `frames`)."""
         s = self._slot(self._k)
-        with torch.cuda.stream(self._stream(s)):
+        st = self._stream(s)
+        cur = torch.cuda.current_stream(self.device)
+        if st != cur:
+            st.wait_stream(cur)
+            frames.record_stream(st)  # the allocator keeps `frames` alive until the copy ran
+        with torch.cuda.stream(st):
             self.frame_slots[s].copy_(frames, non_blocking=True)
         self.step()
+
+    def download(self):
+        """Tracker results of the most recent step (rows, counts, stats; host arrays).  Waits for
+        the tracker stream first, so it is safe while steps are pipelined."""
+        if self.pipelined:
+            torch.cuda.current_stream(self.device).wait_stream(self.trk_stream)
+        return self.tracker.download()
 
     def stats(self):
         self.sync()

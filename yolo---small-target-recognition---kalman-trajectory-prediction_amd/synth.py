@@ -91,28 +91,50 @@ class Scene:
         img = np.clip(np.rint(g), 0, 255).astype(np.uint8)
         return np.repeat(img[:, :, None], 3, axis=2)
 
-    def frames_torch(self, t0: int, n: int, device):
-        """n consecutive frames rendered on the GPU with torch (benchmark input setup only;
-        statistically the same scene, not bit-identical to ``frame``)."""
+    def frames_torch(self, t0: int, n: int, device, chunk: int = 32):
+        """n consecutive frames rendered with torch on `device` (benchmark / large-test input
+        setup; statistically the same scene as ``frame``, not bit-identical to it).
+
+        Vectorised over frames and targets: every target's ellipse is evaluated on a fixed
+        24x20 patch around its centre, and a pixel covered by several targets takes the one
+        with the highest index (= the last one drawn by the per-target loop of ``frame``),
+        via a scatter-max of target indices.  Deterministic on a given device."""
         import torch
 
-        H, W = self.H, self.W
+        H, W, K = self.H, self.W, self.K
         gen = torch.Generator(device=device)
         gen.manual_seed(int(self.seed) * 1000003 + int(t0))
-        yy = torch.arange(H, device=device, dtype=torch.float32)[:, None] + 0.5
-        xx = torch.arange(W, device=device, dtype=torch.float32)[None, :] + 0.5
-        grad = torch.linspace(60.0, 110.0, H, device=device)[:, None].expand(H, W)
+        grad = torch.linspace(60.0, 110.0, H, device=device)[:, None]
         out = torch.empty((n, H, W, 3), dtype=torch.uint8, device=device)
-        for i in range(n):
-            t = t0 + i
-            g = grad + 4.0 * torch.randn((H, W), generator=gen, device=device)
-            for k in np.nonzero(self.visible[t])[0]:
-                cx, cy = self.pos[t, k]
-                a, b = self.w[k] / 2, self.h[k] / 2
-                x0, x1 = max(int(cx - a) - 1, 0), min(int(cx + a) + 2, W)
-                y0, y1 = max(int(cy - b) - 1, 0), min(int(cy + b) + 2, H)
-                m = ((xx[:, x0:x1] - cx) / a) ** 2 + ((yy[y0:y1] - cy) / b) ** 2 <= 1.0
-                g[y0:y1, x0:x1] = torch.where(m, torch.tensor(float(self.intensity[k]), device=device),
-                                              g[y0:y1, x0:x1])
-            out[i] = g.round().clamp(0, 255).to(torch.uint8)[:, :, None].expand(H, W, 3)
+        PW, PH = 24, 20  # patch covers int(c - a) - 1 .. int(c + a) + 1 for a <= 10, b <= 8
+        a = torch.as_tensor(self.w / 2, dtype=torch.float32, device=device)
+        b = torch.as_tensor(self.h / 2, dtype=torch.float32, device=device)
+        inten = torch.as_tensor(self.intensity, dtype=torch.float32, device=device)
+        kidx = torch.arange(K, device=device)
+        ox = torch.arange(PW, device=device)
+        oy = torch.arange(PH, device=device)
+        for c0 in range(0, n, chunk):
+            m = min(chunk, n - c0)
+            ts = np.arange(t0 + c0, t0 + c0 + m)
+            g = grad + 4.0 * torch.randn((m, H, W), generator=gen, device=device)
+            if K:
+                pos = torch.as_tensor(self.pos[ts], dtype=torch.float32, device=device)  # [m, K, 2]
+                vis = torch.as_tensor(self.visible[ts], device=device)  # [m, K]
+                cx, cy = pos[..., 0], pos[..., 1]
+                x0 = torch.trunc(cx - a).long() - 1
+                y0 = torch.trunc(cy - b).long() - 1
+                px = x0[..., None] + ox  # [m, K, PW]
+                py = y0[..., None] + oy  # [m, K, PH]
+                ex = ((px.float() + 0.5 - cx[..., None]) / a[:, None]) ** 2
+                ey = ((py.float() + 0.5 - cy[..., None]) / b[:, None]) ** 2
+                inside = (ey[..., :, None] + ex[..., None, :]) <= 1.0  # [m, K, PH, PW]
+                inside &= ((px >= 0) & (px < W))[..., None, :] & ((py >= 0) & (py < H))[..., :, None]
+                inside &= vis[..., None, None]
+                fi = torch.arange(m, device=device)[:, None, None, None]
+                lin = (fi * H + py[..., :, None]) * W + px[..., None, :]
+                lab = torch.full((m * H * W,), -1, dtype=torch.long, device=device)
+                lab.scatter_reduce_(0, lin[inside], kidx.view(1, K, 1, 1).expand_as(lin)[inside], reduce="amax")
+                lab = lab.view(m, H, W)
+                g = torch.where(lab >= 0, inten[lab.clamp(min=0)], g)
+            out[c0:c0 + m] = g.round().clamp(0, 255).to(torch.uint8)[..., None].expand(m, H, W, 3)
         return out
