@@ -18,17 +18,18 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, S=8):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         shard = pkg().shard
-        S = 8
         ids = shard.stream_ids(rank, world, S)
         stats = np.zeros(S, dtype=[(k, np.int64) for k in shard.COUNTERS[1:]])
         stats["current_active_tracks"] = np.arange(S) + 10 * rank
         stats["total_tracks_created"] = 3 + rank
+        stats["overflow"] = rank  # bench.py fails the run when the reduced overflow is non-zero
         c = shard.local_counters(100 * S, stats)
+        c["live_min_start"] = float(stats["current_active_tracks"].min())  # bench.py's extra key
         out, el = shard.reduce_run(c, 1.0 + rank)
         q.put((rank, ids, [shard.stream_seed(i, S) for i in ids], out, el))
     finally:
@@ -63,3 +64,23 @@ def test_single_process_reduce_is_identity():
     assert shard.reduce_run(c, 0.5) == ({"frames": 5.0}, 0.5)
     with pytest.raises(ValueError):
         shard.stream_ids(2, 2, 8)
+
+
+def test_config4_one_stream_per_rank_four_ranks():
+    """bench.py --config 4: one stream per GPU; 4 gloo ranks stand in for 4 GPUs."""
+    world, port = 4, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, 1)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert [r[1] for r in res] == [[0], [1], [2], [3]]
+    assert [r[2] for r in res] == [[0], [1000], [2000], [3000]]
+    for _, _, _, out, el in res:
+        assert el == 4.0 and out["frames"] == 400.0
+        assert out["overflow"] == 0 + 1 + 2 + 3
+        assert out["current_active_tracks"] == 0 + 10 + 20 + 30

@@ -1423,6 +1423,101 @@ __global__ void __launch_bounds__(256) conv_input_mfma_kernel(InputArgs a) {
   }
 }
 
+// fp32 parity build of the first conv on the exact-f32 MFMA (v_mfma_f32_16x16x4_f32, an fmaf
+// chain in f32).  The staged patch holds v / 255 (the reference's `im /= 255`, exact f32
+// division, as conv_input_kernel's table), the weights stay the fused f32 weights, so every
+// product and sum is f32 as in the reference's fp32 conv (summation order differs within
+// rounding).  K = 27 is padded to 28 = seven K=4 MFMAs; MFMA j takes k = 4j + (lane >> 4) from
+// both operands.  A workgroup = a 16x16 output tile; wave w computes rows 4w..4w+3, two
+// 16-channel output tiles (cout <= 32).  Replaces conv_input_kernel's 27 LDS weight reads per
+// FMA (VALU + LDS issue bound).
+__global__ void __launch_bounds__(256) conv_input_f32mfma_kernel(InputArgs a) {
+  constexpr int TI = 15 * 2 + 3;
+  constexpr int TP = TI + 1;
+  __shared__ float xs[3][TI][TP];
+  __shared__ float lut[256];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int kg = lane >> 4, col = lane & 15;
+  const int tiles_x = (a.out_w + 15) / 16, tiles_y = (a.out_h + 15) / 16;
+  int t = xcd_block(a.xcd).x;
+  const int b = t / (tiles_x * tiles_y);
+  t -= b * tiles_x * tiles_y;
+  const int ty0 = (t / tiles_x) * 16, tx0 = (t % tiles_x) * 16;
+  const int s = a.stride;
+  const int ti = 15 * s + 3;
+  const int iy0 = ty0 * s - a.pad, ix0 = tx0 * s - a.pad;
+  const unsigned char* fr = a.frames + (size_t)b * a.fh * a.fw * 3;
+  lut[tid] = (float)tid / 255.0f;  // im /= 255 (exact division, as torch)
+  // A fragments straight from global (each lane 14 floats, read once per workgroup)
+  float wa[2][7];
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+    for (int j = 0; j < 7; ++j) {
+      const int k = 4 * j + kg, o = nt * 16 + col;
+      wa[nt][j] = (k < 27 && o < a.cout) ? a.w[o * 27 + k] : 0.f;
+    }
+  __syncthreads();
+  for (int i = tid; i < ti * ti; i += 256) {
+    const int ry = i / ti, rx = i - ry * ti;
+    const int iy = iy0 + ry, ix = ix0 + rx;
+    float v0 = 0.f, v1 = 0.f, v2 = 0.f;
+    if (iy >= 0 && iy < a.in_h && ix >= 0 && ix < a.in_w) {
+      const int fy = iy - a.pad_top, fx = ix - a.pad_left;
+      if (fy >= 0 && fy < a.fh && fx >= 0 && fx < a.fw) {
+        const unsigned char* px = fr + ((size_t)fy * a.fw + fx) * 3;
+        v0 = lut[px[2]];  // BGR -> RGB
+        v1 = lut[px[1]];
+        v2 = lut[px[0]];
+      } else {
+        v0 = v1 = v2 = lut[114];
+      }
+    }
+    xs[0][ry][rx] = v0;
+    xs[1][ry][rx] = v1;
+    xs[2][ry][rx] = v2;
+  }
+  __syncthreads();
+  int xoff[7];
+#pragma unroll
+  for (int j = 0; j < 7; ++j) {
+    const int k = 4 * j + kg;
+    const int c = k / 9, tap = k - c * 9, ky = tap / 3, kx = tap - ky * 3;
+    xoff[j] = k < 27 ? (c * TI + ky) * TP + col * s + kx : -1;
+  }
+  const float* xsf = &xs[0][0][0];
+  f32x4 acc[2][4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int roff = (wave * 4 + r) * s * TP;
+    acc[0][r] = f32x4{0.f, 0.f, 0.f, 0.f};
+    acc[1][r] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < 7; ++j) {
+      const float xv = xoff[j] >= 0 ? xsf[xoff[j] + roff] : 0.f;
+      acc[0][r] = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[0][j], xv, acc[0][r], 0, 0, 0);
+      acc[1][r] = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[1][j], xv, acc[1][r], 0, 0, 0);
+    }
+  }
+  const int ox = tx0 + col;
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt) {
+    const int n0 = nt * 16 + kg * 4;
+    if (n0 >= a.cout) continue;
+    const float4 bb = *(const float4*)(a.b + n0);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int oy = ty0 + wave * 4 + r;
+      if (oy >= a.out_h || ox >= a.out_w) continue;
+      float v[4] = {acc[nt][r][0] + bb.x, acc[nt][r][1] + bb.y, acc[nt][r][2] + bb.z, acc[nt][r][3] + bb.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = silu<true>(v[j]);
+      const size_t p = ((size_t)b * a.out_h + oy) * a.out_w + ox;
+      store4((float*)a.dst + p * a.d_cstride + a.d_coff + n0, v);
+    }
+  }
+}
+
 // ---------------------------------------------------------------- SPPF pooling
 // slices 1..3 of the SPPF concat buffer = max over 5x5 / 9x9 / 13x13 windows of slice 0
 // (MaxPool2d(5,1,2) applied 1/2/3 times; padding never wins a max).
@@ -2067,7 +2162,8 @@ __global__ void __launch_bounds__(NMS_NT) nms_kernel(NmsArgs a) {
     unsigned long long k = ~0ull;
     if (i < n) {
       const unsigned sb = __float_as_uint(cand[i * 6 + 4]);
-      const int anc = __float_as_int(cand[i * 6 + 5]);
+      int anc = __float_as_int(cand[i * 6 + 5]);
+      anc = (anc >= 0 && anc < a.n_anchors) ? anc : 0;  // rows are written by detect_kernel; never index outside
       k = ((unsigned long long)(0xffffffffu - sb) << 32) | (unsigned)anc;
       slot_of[anc] = i;
     }
@@ -2164,6 +2260,11 @@ __global__ void __launch_bounds__(NMS_NT) nms_kernel(NmsArgs a) {
 #pragma clang fp contract(fast)
 
 size_t nms_lds_bytes() { return NMS_LDS; }
+
+// zero n int32 counters (one wave; n <= 64 * k handled by the loop)
+__global__ void __launch_bounds__(64) zero_i32_kernel(int* p, int n) {
+  for (int i = threadIdx.x; i < n; i += 64) p[i] = 0;
+}
 
 }  // namespace det
 }  // namespace yk
@@ -2701,6 +2802,8 @@ int launch_op(yk_model* m, const yk_op& op, const uint8_t* frames, int B, float 
         const int tiles = B * ((op.out_h + 15) / 16) * ((op.out_w + 15) / 16);
         if (!Tr::kExact && op.cout <= 32 && !m->input_valu)
           hipLaunchKernelGGL(conv_input_mfma_kernel<Tr>, dim3(tiles), dim3(256), 0, st, a);
+        else if (Tr::kExact && op.cout <= 32 && !m->input_valu)
+          hipLaunchKernelGGL(conv_input_f32mfma_kernel, dim3(tiles), dim3(256), 0, st, a);
         else
           hipLaunchKernelGGL(conv_input_kernel<Tr>, dim3(tiles), dim3(256), 0, st, a);
         break;
@@ -2946,6 +3049,7 @@ const char* op_kernel_name(const yk_model* m, const yk_op& op) {
   switch (op.kind) {
     case YK_K_CONV_INPUT:
       if (!f && op.cout <= 32 && !m->input_valu) snprintf(buf, sizeof buf, "conv_input_mfma_kernel<yk::det::%s>", tn);
+      else if (f && op.cout <= 32 && !m->input_valu) snprintf(buf, sizeof buf, "conv_input_f32mfma_kernel");
       else snprintf(buf, sizeof buf, "conv_input_kernel<yk::det::%s>", tn);
       return buf;
     case YK_K_SPPF_POOL:
@@ -3145,7 +3249,11 @@ int detect_impl(yk_model* m, const uint8_t* frames, int B, float conf, float iou
   m->plan_batch = (B + m->groups - 1) / m->groups;
   if (!dets) dets = m->dets;
   if (!counts) counts = m->counts;
-  YK_HIP(hipMemsetAsync(m->cand_count, 0, sizeof(int) * B, st));
+  // candidate counters of this forward start at 0: a kernel node, not hipMemsetAsync -- a
+  // captured memset node was seen to race the detect kernels when the graph was replayed right
+  // behind other work on the launch stream (stale counters -> NMS over stale slots)
+  hipLaunchKernelGGL(zero_i32_kernel, dim3(1), dim3(64), 0, st, m->cand_count, B);
+  YK_HIP(hipGetLastError());
   frames = input_frames(m, frames, B, st);
   int rc = D.act_dtype == YK_ACT_F32   ? run_dag<F32>(m, frames, B, conf, st)
            : D.act_dtype == YK_ACT_FP8 ? run_dag<FP8>(m, frames, B, conf, st)

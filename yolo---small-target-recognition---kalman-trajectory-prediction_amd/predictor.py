@@ -112,24 +112,35 @@ class Results:
 
 
 class YOLO:
-    """YOLO(model='yolov8s-small.yaml') -> detector executed by libyk.so.
+    """YOLO(model='yolov8s-small.yaml' | 'best.pt') -> detector executed by libyk.so.
 
-    ``weights``: None (seeded synthetic weights in the reference's shapes), a
-    state dict in the reference's naming, or a path to one saved with torch.save (loaded
-    with weights_only=True).  ``dtype``: 'bf16' (production) or 'fp32' (exact-f32 MFMA,
-    parity).  Pickled ultralytics checkpoints (best.pt) need the ultralytics classes and
-    are not loaded."""
+    ``model``: a model YAML (scale from the file name, tasks.py:1703-1740) or an ultralytics
+    checkpoint (``*.pt``: architecture, scale and fp16 weights read from the pickled
+    DetectionModel without ultralytics and without executing the pickle, checkpoint.py).
+    ``weights`` (YAML models only): None (seeded synthetic weights in the reference's shapes,
+    SURVEY §8d), a state dict in the reference's naming, or a path to one saved with
+    torch.save (loaded with weights_only=True).  ``dtype``: 'fp32' (the reference's arithmetic,
+    exact-f32 MFMA), 'bf16' or 'fp8'."""
 
     def __init__(self, model: str = "yolov8s-small.yaml", task=None, verbose: bool = False, *, weights=None,
                  dtype: str = "bf16", device: int = 0, seed: int = 0, max_batch: int = 8):
         if task not in (None, "detect"):
             raise NotImplementedError(f"task {task!r}: only detection is on this path")
+        self.ckpt_meta = None
         if str(model).endswith(".pt"):
+            # ultralytics checkpoint (best.pt): the model YAML -- scale included -- comes from the
+            # pickled DetectionModel itself (tasks.py:1404-1521), loaded weights_only with inert
+            # stand-ins for its classes (checkpoint.py)
             if weights is not None:
                 raise ValueError("give either a .pt model or weights=, not both")
-            weights, model = model, os.environ.get("YK_MODEL_CFG", "yolov8s-small.yaml")
-        self.cfg = str(model)
-        self.arch = A.parse_arch(A.load_model_dict(self.cfg))
+            from . import checkpoint as CK
+
+            ydict, weights, self.ckpt_meta = CK.load_checkpoint(str(model))
+            self.cfg = str(model)
+            self.arch = A.parse_arch(ydict)
+        else:
+            self.cfg = str(model)
+            self.arch = A.parse_arch(A.load_model_dict(self.cfg))
         if weights is None:
             sd = Wt.synthetic_state_dict(self.arch, seed)
         elif isinstance(weights, dict):
@@ -171,6 +182,17 @@ class YOLO:
         max_det = self.overrides["max_det"] if max_det is None else max_det
         assert 0 <= conf <= 1, f"Invalid Confidence threshold {conf}, valid values are between 0.0 and 1.0"
         assert 0 <= iou <= 1, f"Invalid IoU {iou}, valid values are between 0.0 and 1.0"
+        if half:
+            raise NotImplementedError("half=True (fp16 weights/activations) is not built on this path; the 16-bit "
+                                      "build is YOLO(..., dtype='bf16')")
+        if self.arch.nc != 1:
+            raise NotImplementedError("only single-class detection heads are on this path")
+        # nc == 1: every candidate is class 0, so non_max_suppression's class filter (utils/nms.py:128-132),
+        # applied before NMS, keeps all candidates or none, and agnostic_nms (class offset c * max_wh with
+        # c == 0, :144) changes nothing -- both are exact here without a kernel change.
+        del agnostic_nms
+        if classes is not None:
+            classes = [int(c) for c in (classes if isinstance(classes, (list, tuple, set)) else [classes])]
         frames = self._frames(source)
         with self._lock:
             out = []
@@ -209,10 +231,9 @@ class YOLO:
         res = []
         for b in range(B):
             n = min(int(cnt[b]), max_det)
+            if classes is not None and 0 not in classes:
+                n = 0  # the class filter ran before NMS in the reference: no candidate survives
             d = dets[b, :n]
-            if classes is not None:
-                keep = torch.isin(d[:, 5], torch.tensor(classes, dtype=d.dtype, device=d.device))
-                d = d[keep]
             res.append(Results(frames[b], f"image{b}.jpg", self.names, boxes=d))
         t3 = time.perf_counter()
         sp = {"preprocess": (t1 - t0) * 1e3 / B, "inference": (t2 - t1) * 1e3 / B, "postprocess": (t3 - t2) * 1e3 / B}

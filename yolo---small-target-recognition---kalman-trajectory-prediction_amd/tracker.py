@@ -524,6 +524,16 @@ class MotionCompensatedMultiTracker:
         return [_reset_fields(r, _row_to_dict(r, track_id_of(r["track_num"]))) for r in rows[0, : int(counts[0])]]
 
     def get_comprehensive_stats(self):
-        snap = self._core.snapshot(0)
-        return {"basic": self.stats, "motion_detection": {}, "performance": {},
-                "trackers": {"active_trackers": int(len(snap))}, "motion_history_avg": 0.0}
+        """motion_compensated_multi_tracker.py:308-343.  Frame-free, so the global motion detector
+        has seen no frame (global_motion_detector.py:263-278 with total_detections == 0); the
+        reference never appends to stats['processing_times'], so 'performance' is always {}."""
+        rows, counts, _ = self._core.download()
+        live = rows[0, : int(counts[0])]
+        return {"basic": self.stats,
+                "motion_detection": {"total_detections": 0, "motion_events": 0, "reset_triggers": 0,
+                                     "motion_detection_rate": f"{0.0:.1%}", "reset_trigger_rate": f"{0.0:.1%}",
+                                     "avg_motion_magnitude": f"{0.0:.2f}px"},
+                "performance": {},
+                "trackers": {"active_trackers": int(len(live)),
+                             "total_resets_by_tracker": int(live["reset_count"].sum()) if len(live) else 0},
+                "motion_history_avg": 0.0}
