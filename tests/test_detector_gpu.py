@@ -197,7 +197,8 @@ def test_dag_schedule_matches_sequential(dtype):
 
 
 @pytest.mark.parametrize("plan", [(0, 0, 0), (1, 0, 0), (1, 1, 0), (4, 2, 0), (4, 4, 0), (4, 2, 8), (2, 1, 1), (2, 2, 4), (2, 4, 2), (3, 1, 1), (3, 2, 4), (3, 3, 2),
-                                  (3, 4, 4), (3, 1, 4 | 16), (3, 2, 2 | 16), (3, 4, 4 | 16), "tuned"])
+                                  (3, 4, 4), (3, 1, 4 | 16), (3, 2, 2 | 16), (3, 4, 4 | 16), (3, 1, 1 | 32),
+                                  (3, 2, 2 | 32), (3, 3, 1 | 32), (3, 4, 4 | 32), "tuned"])
 def test_fp32_conv_variants_match_oracle(plan):
     """Every conv kernel variant (direct, LDS-tiled, split-K fragment tiles, autotuned mix)
     forced onto every conv op reproduces the oracle's activations and detections."""
@@ -260,3 +261,27 @@ def test_fp32_nms_paths_match_oracle(count):
         n = int(counts[b])
         assert n == len(ref), (b, n, len(ref))
         np.testing.assert_array_equal(dets[b, :n].cpu().numpy(), ref.numpy())
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+@pytest.mark.parametrize("nnt,npt", [(1, 1), (3, 1), (2, 2), (4, 4)])
+def test_fastw_bit_identical_to_fast(dtype, nnt, npt):
+    """conv_fastw_kernel (weights shared through LDS) keeps conv_fast_kernel's K order and MFMA
+    sequence per accumulator: every activation buffer is bit-identical."""
+    P, A, W, M = _mods()
+    ar = A.parse_arch(A.load_model_dict("yolov8s-small.yaml"))
+    sd = W.synthetic_state_dict(ar, 0)
+    B = 4
+    prog = M.Program(ar, sd, 512, 640, 640, B, dtype)
+    sc = P.synth.Scene(seed=2, n_targets=24, n_frames=B + 1)
+    ft = torch.from_numpy(np.stack([sc.frame(t) for t in range(B)])).cuda()
+    outs = []
+    for mode in (0, 32):
+        dm = M.DeviceModel(prog)
+        dm.set_plan(B, 3, nnt, npt | mode)
+        d, c = dm.detect(ft)
+        torch.cuda.synchronize()
+        dn, cn = d.cpu().numpy(), c.cpu().numpy()  # rows past counts[b] are not written
+        outs.append([dm.buffer(i, B) for i in range(len(prog.buf_elems))] + [cn] + [dn[b, :cn[b]] for b in range(B)])
+    for a, b in zip(*outs):
+        np.testing.assert_array_equal(a, b)

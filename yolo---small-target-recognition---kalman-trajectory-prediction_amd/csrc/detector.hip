@@ -964,6 +964,169 @@ __global__ void __launch_bounds__(256) conv_fast_kernel(FastArgs a) {
   if (a.tstamp && tid == 0 && wg_lin < a.tstamp_cap) a.tstamp[3 * wg_lin + 2] = wall_clock64();
 }
 
+// ---------------------------------------------------------------- table conv, weights shared through LDS
+// conv_fast_kernel's per-wave layout (wave = NPT x 16 pixels x NNT x 16 channels, activations
+// gathered straight to registers through the K-step table), but the four waves of a workgroup
+// share one copy of the weight fragments: they are the same for all four waves (same channel
+// group), and loading them per wave made three quarters of the workgroup's vector-memory
+// instructions redundant (TA-bound: per K step NNT + NPT fragment loads per wave, against
+// NPT + NNT / 4 here).  Weights stream through a two-buffer LDS ring in chunks of 4 K steps
+// (4 x NNT fragments, one ds_read_b128 per fragment and lane); the chunk boundary is a raw
+// s_barrier behind lgkmcnt(0) -- not __syncthreads(), whose fence would drain the activation
+// loads in flight (vmcnt(0)).  Same K order and MFMA sequence per accumulator as
+// conv_fast_kernel: results are bit-identical.
+template <class Tr, int NNT, int NPT, int SKD>
+__global__ void __launch_bounds__(256) conv_fastw_kernel(FastArgs a) {
+  using T = typename Tr::T;
+  constexpr int ESZ = (int)sizeof(T);
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int nk = a.k_steps;
+  int2* tab = (int2*)smem;  // [k_steps * 4]
+  uint4* ring = (uint4*)(smem + (((size_t)nk * 4 * 8 + 15) & ~(size_t)15));  // [2][4][NNT][64]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int kg = lane >> 4, col = lane & 15;
+  const int2 blk = xcd_block(a.xcd);
+  const int nt0 = blk.y * NNT;
+  const int pbase = (blk.x * 4 + wave) * (16 * NPT);
+  for (int i = tid; i < nk * 4; i += 256) tab[i] = a.ktab[i];
+  const __amdgpu_buffer_rsrc_t xr = make_srd(a.arena, a.arena_bytes);
+  const __amdgpu_buffer_rsrc_t wr = make_srd(a.wblob, a.wbytes);
+  const int hw = a.out_h * a.out_w;
+  unsigned vo0[NPT], vo1[NPT], vm[NPT];
+#pragma unroll
+  for (int t = 0; t < NPT; ++t) {
+    const int p = pbase + t * 16 + col;
+    const bool pv = p < a.M;
+    const int pp = pv ? p : 0;
+    const int b = fdiv(pp, hw, a.inv_hw);
+    const int r = pp - b * hw;
+    const int oy = fdiv(r, a.out_w, a.inv_w);
+    const int ox = r - oy * a.out_w;
+    const int iy0 = oy * a.stride - a.pad, ix0 = ox * a.stride - a.pad;
+    vo0[t] = a.soff0 + (unsigned)(((b * a.h0 + (iy0 >> a.up0)) * a.w0 + (ix0 >> a.up0)) * a.cs0 * ESZ);
+    vo1[t] = a.soff1 + (unsigned)(((b * a.h1 + (iy0 >> a.up1)) * a.w1 + (ix0 >> a.up1)) * a.cs1 * ESZ);
+    const unsigned cm = ((unsigned)(ix0 >= 0 && ix0 < a.in_w)) | ((unsigned)(ix0 + 1 >= 0 && ix0 + 1 < a.in_w) << 1) |
+                        ((unsigned)(ix0 + 2 >= 0 && ix0 + 2 < a.in_w) << 2);
+    const unsigned m = ((iy0 >= 0 && iy0 < a.in_h) ? cm : 0u) | ((iy0 + 1 >= 0 && iy0 + 1 < a.in_h) ? cm << 3 : 0u) |
+                       ((iy0 + 2 >= 0 && iy0 + 2 < a.in_h) ? cm << 6 : 0u);
+    vm[t] = pv ? m : 0u;
+  }
+  f32x4 acc[NNT][NPT];
+#pragma unroll
+  for (int i = 0; i < NNT; ++i)
+#pragma unroll
+    for (int t = 0; t < NPT; ++t) acc[i][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float4 bb[NNT];
+  float4 sc[NNT];
+#pragma unroll
+  for (int i = 0; i < NNT; ++i) {
+    const int n0 = (nt0 + i) * 16 + kg * 4;
+    bb[i] = (nt0 + i < a.n_tiles && n0 < a.cout) ? *(const float4*)(a.bias + n0) : make_float4(0.f, 0.f, 0.f, 0.f);
+    if constexpr (Tr::kScaled) sc[i] = dq4<Tr>(a.bias, a.n_tiles, n0 < a.cout ? n0 : 0);
+  }
+  // weight staging: fragment f = wave + 4 j (j < NNT) of a chunk = (step d = f & 3, tile i = f >> 2)
+  uint4 wst[NNT];
+  auto stage_load = [&](int c) {
+#pragma unroll
+    for (int j = 0; j < NNT; ++j) {
+      const int f = wave + 4 * j, d = f & 3, i = f >> 2;
+      const int ks = 4 * c + d;
+      const int nt = nt0 + i < a.n_tiles ? nt0 + i : a.n_tiles - 1;
+      const unsigned off = a.woff + (unsigned)((((size_t)nt * nk + (ks < nk ? ks : 0)) * 64 + lane) * 16);
+      wst[j] = bload(wr, off, 0);
+    }
+  };
+  auto stage_store = [&](int buf) {
+#pragma unroll
+    for (int j = 0; j < NNT; ++j) {
+      const int f = wave + 4 * j, d = f & 3, i = f >> 2;
+      ring[((buf * 4 + d) * NNT + i) * 64 + lane] = wst[j];
+    }
+  };
+  auto act_load = [&](int ks, uint4* xf) {
+    const int2 e = tab[ks * 4 + kg];
+    const unsigned tap = (unsigned)e.y & 15u;
+    const bool s1 = (e.y & 16) != 0, ev = (e.y & 32) != 0;
+#pragma unroll
+    for (int t = 0; t < NPT; ++t) {
+      const bool ok = ev && ((vm[t] >> tap) & 1u);
+      const unsigned off = (s1 ? vo1[t] : vo0[t]) + (unsigned)e.x;
+      xf[t] = bload(xr, ok ? off : kOOB, 0);
+    }
+  };
+  stage_load(0);
+  stage_store(0);
+  __syncthreads();  // the table and chunk 0 of the ring (nothing else in flight yet)
+  uint4 xb[SKD][NPT];
+#pragma unroll
+  for (int d = 0; d < SKD; ++d)
+    if (d < nk) act_load(d, xb[d]);
+  const int nch = (nk + 3) >> 2;
+  for (int c = 0; c < nch; ++c) {
+    const bool more = c + 1 < nch;
+    if (more) stage_load(c + 1);  // in flight over this chunk's MFMAs
+    const uint4* wb = ring + (size_t)(c & 1) * 4 * NNT * 64;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      const int ks = 4 * c + d;
+      if (ks < nk) {
+        uint4 wf[NNT];
+#pragma unroll
+        for (int i = 0; i < NNT; ++i) wf[i] = wb[(d * NNT + i) * 64 + lane];
+        // step ks's activations sit in slot ks % SKD = d % SKD (SKD divides 4): a compile-time
+        // index, so the slots stay registers
+        uint4* xf = xb[d % SKD];
+#pragma unroll
+        for (int i = 0; i < NNT; ++i)
+#pragma unroll
+          for (int t = 0; t < NPT; ++t) acc[i][t] = mma<Tr>(wf[i], xf[t], acc[i][t]);
+        if (ks + SKD < nk) act_load(ks + SKD, xf);
+      }
+    }
+    if (more) {
+      stage_store((c + 1) & 1);
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's ring writes landed
+      __builtin_amdgcn_s_barrier();
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < NNT; ++i) {
+    const int nt = nt0 + i;
+    if (nt >= a.n_tiles) break;
+    const int n0 = nt * 16 + kg * 4;
+    if (n0 >= a.cout) continue;
+#pragma unroll
+    for (int t = 0; t < NPT; ++t) {
+      const int p = pbase + t * 16 + col;
+      if (p >= a.M) continue;
+      const f32x4 v4 = acc[i][t];
+      float v[4] = {v4[0] + bb[i].x, v4[1] + bb[i].y, v4[2] + bb[i].z, v4[3] + bb[i].w};
+      if constexpr (Tr::kScaled) {
+        v[0] = v4[0] * sc[i].x + bb[i].x;
+        v[1] = v4[1] * sc[i].y + bb[i].y;
+        v[2] = v4[2] * sc[i].z + bb[i].z;
+        v[3] = v4[3] * sc[i].w + bb[i].w;
+      }
+      if (a.act) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = silu<Tr::kExact>(v[j]);
+      }
+      if (a.res) {
+        float r[4];
+        load4((const T*)a.res + (size_t)p * a.r_cstride + a.r_coff + n0, r);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = r[j] + v[j];
+      }
+      store4((T*)a.dst + (size_t)p * a.d_cstride + a.d_coff + n0, v);
+    }
+  }
+}
+
+inline size_t fastw_lds(int k_steps, int nnt) {
+  return (((size_t)k_steps * 4 * 8 + 15) & ~(size_t)15) + (size_t)2 * 4 * nnt * 64 * 16;
+}
+
 // ---------------------------------------------------------------- persistent LDS-tiled conv (wide layers)
 // For the high-resolution layers (P2/P3: 20,480 / 5,120 pixels per image) the gather kernel
 // re-fetches every input pixel once per tap and every weight fragment once per wave through
@@ -2517,11 +2680,22 @@ void set_fast_attr() {
   (void)hipFuncSetAttribute((const void*)conv_fast_kernel<Tr, NNT, NPT, WS, SKD>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
 }
+template <class Tr, int NNT, int NPT>
+void set_fastw_attr() {
+  constexpr int SKD = NNT * NPT >= 8 ? 2 : 4;
+  (void)hipFuncSetAttribute((const void*)conv_fastw_kernel<Tr, NNT, NPT, SKD>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
+}
 template <class Tr, int NNT, bool WS>
 void set_fast_attr_n() {
   set_fast_attr<Tr, NNT, 1, WS>();
   set_fast_attr<Tr, NNT, 2, WS>();
   set_fast_attr<Tr, NNT, 4, WS>();
+  if constexpr (!WS) {
+    set_fastw_attr<Tr, NNT, 1>();
+    set_fastw_attr<Tr, NNT, 2>();
+    set_fastw_attr<Tr, NNT, 4>();
+  }
 }
 template <class Tr, bool WS>
 void set_fast_attr_w() {
@@ -2744,9 +2918,34 @@ void launch_fast_w(const FastArgs& a, int nnt, int npt, hipStream_t st) {
     default: launch_fast_n<Tr, 4, WS>(a, npt, st); break;
   }
 }
+template <class Tr, int NNT, int NPT>
+void launch_fastw_t(const FastArgs& a, hipStream_t st) {
+  constexpr int SKD = NNT * NPT >= 8 ? 2 : 4;
+  dim3 grid((a.M + 64 * NPT - 1) / (64 * NPT), (a.n_tiles + NNT - 1) / NNT);
+  hipLaunchKernelGGL((conv_fastw_kernel<Tr, NNT, NPT, SKD>), grid, dim3(256), fastw_lds(a.k_steps, NNT), st, a);
+}
+template <class Tr, int NNT>
+void launch_fastw_n(const FastArgs& a, int npt, hipStream_t st) {
+  if (npt == 4) launch_fastw_t<Tr, NNT, 4>(a, st);
+  else if (npt == 2) launch_fastw_t<Tr, NNT, 2>(a, st);
+  else launch_fastw_t<Tr, NNT, 1>(a, st);
+}
+template <class Tr>
+void launch_fastw(const FastArgs& a, int nnt, int npt, hipStream_t st) {
+  switch (nnt) {
+    case 1: launch_fastw_n<Tr, 1>(a, npt, st); break;
+    case 2: launch_fastw_n<Tr, 2>(a, npt, st); break;
+    case 3: launch_fastw_n<Tr, 3>(a, npt, st); break;
+    default: launch_fastw_n<Tr, 4>(a, npt, st); break;
+  }
+}
+// plan.npt = NPT | mode << 4: mode 0 per-wave pixels, 1 = the four waves split K (WS),
+// 2 = per-wave pixels with the weight fragments shared through LDS (conv_fastw_kernel)
 template <class Tr>
 void launch_fast(const FastArgs& a, const ConvPlan& p, hipStream_t st) {
-  if (p.npt >> 4) launch_fast_w<Tr, true>(a, p.nnt, p.npt & 15, st);
+  const int mode = p.npt >> 4;
+  if (mode == 2) launch_fastw<Tr>(a, p.nnt, p.npt & 15, st);
+  else if (mode == 1) launch_fast_w<Tr, true>(a, p.nnt, p.npt & 15, st);
   else launch_fast_w<Tr, false>(a, p.nnt, p.npt & 15, st);
 }
 
@@ -3069,10 +3268,13 @@ const char* op_kernel_name(const yk_model* m, const yk_op& op) {
     return buf;
   }
   if (cp.kind == CK_FAST) {
-    const int npt = cp.npt & 15, ws = cp.npt >> 4;
+    const int npt = cp.npt & 15, mode = cp.npt >> 4;
     const int skd = cp.nnt * npt >= 8 ? 2 : 4;
-    snprintf(buf, sizeof buf, "conv_fast_kernel<yk::det::%s, %d, %d, %s, %d>", tn, cp.nnt, npt, ws ? "true" : "false",
-             skd);
+    if (mode == 2)
+      snprintf(buf, sizeof buf, "conv_fastw_kernel<yk::det::%s, %d, %d, %d>", tn, cp.nnt, npt, skd);
+    else
+      snprintf(buf, sizeof buf, "conv_fast_kernel<yk::det::%s, %d, %d, %s, %d>", tn, cp.nnt, npt,
+               mode ? "true" : "false", skd);
     return buf;
   }
   if (cp.kind == CK_SPLITK) {
@@ -3636,8 +3838,8 @@ int yk_model_set_plan(yk_model* m, int op_index, int batch, int kind, int nnt, i
   YK_CHECK_ARG(kind != CK_WIDE || ((nnt == 2 || nnt == 4) && (npt == 0 || npt == 4 || npt == 8)),
                "yk_model_set_plan: wide conv nnt must be 2 or 4, npt (waves) 0, 4 or 8");
   YK_CHECK_ARG(kind != CK_FAST || (nnt >= 1 && nnt <= 4 && ((npt & 15) == 1 || (npt & 15) == 2 || (npt & 15) == 4) &&
-                                   (npt >> 4) <= 1),
-               "yk_model_set_plan: table conv needs nnt in [1, 4], npt in {1, 2, 4} (+16: waves split K)");
+                                   (npt >> 4) <= 2),
+               "yk_model_set_plan: table conv needs nnt in [1, 4], npt in {1, 2, 4} (+16: waves split K, +32: LDS-shared weights)");
   YK_CHECK_ARG(kind != CK_TILE || nnt == 0 || nnt == 1, "yk_model_set_plan: tiled conv nnt must be 0 or 1 (LDS-resident weights)");
   YK_CHECK_ARG(kind != CK_SPLITK || ((nnt == 1 || nnt == 2 || nnt == 4) && (npt == 1 || npt == 2 || npt == 4)),
                "yk_model_set_plan: split-K fragment tile must be nnt, npt in {1, 2, 4}");
@@ -3700,14 +3902,14 @@ int yk_model_autotune(yk_model* m, const uint8_t* frames, int batch, float conf,
           if (wide_plan(op, esz, nnt, nw).ok && (long)bt * op.out_h * op.out_w >= 4096) cands.push_back({CK_WIDE, nnt, nw});
       }
     if (m->ktab && m->ktab_off[i] >= 0 && (long)bt * op.out_h * op.out_w < (1L << 22))
-      for (int ws = 0; ws < 2; ++ws)
+      for (int mode = 0; mode < 3; ++mode)  // per-wave pixels / waves split K / LDS-shared weights
         for (int nnt : {1, 2, 3, 4})
           for (int npt : {1, 2, 4}) {
             if (nnt > 1 && 4 * op.n_tiles < 3 * ((op.n_tiles + nnt - 1) / nnt) * nnt) continue;
-            const long px = ws ? 16 * npt : 64 * npt;
+            const long px = mode == 1 ? 16 * npt : 64 * npt;
             const long wgs = ((long)bt * op.out_h * op.out_w + px - 1) / px * ((op.n_tiles + nnt - 1) / nnt);
             if (wgs < 64) continue;
-            cands.push_back({CK_FAST, nnt, npt | (ws << 4)});
+            cands.push_back({CK_FAST, nnt, npt | (mode << 4)});
           }
     if (cands.empty()) continue;  // (FP8 without a table: yk_model_create refuses that)
     float best = 1e30f;
