@@ -1,6 +1,6 @@
 """Per-workgroup timeline of one conv_fast op (YK_FAST_TS diagnostics): dispatch ramp (spread
 of workgroup start times), workgroup duration split into prologue+K loop and reduction+epilogue,
-and the tail.  usage: YK_FAST_TS=<op> python tools/wg_times.py <op> [<op> ...] (set for each op)"""
+and the tail.  usage: YK_FAST_TS=<op> [YK_DTYPE=fp32] [YK_PLAN=plans/x.json] python tools/wg_times.py"""
 import ctypes as C
 import importlib
 import os
@@ -19,10 +19,17 @@ L = importlib.import_module(PKG + "._lib")
 op = int(os.environ["YK_FAST_TS"])
 ar = A.parse_arch(A.load_model_dict("yolov8s-small.yaml"))
 B = 8
-dm = M.DeviceModel(M.Program(ar, W.synthetic_state_dict(ar, 0), 512, 640, 640, B, "bf16"))
+dtype = os.environ.get("YK_DTYPE", "bf16")
+dm = M.DeviceModel(M.Program(ar, W.synthetic_state_dict(ar, 0), 512, 640, 640, B, dtype))
 sc = P.synth.Scene(seed=0, n_targets=22, n_frames=B + 1)
 ft = torch.from_numpy(np.stack([sc.frame(t) for t in range(B)])).cuda()
-dm.autotune(ft, 0.25)
+plan = os.environ.get("YK_PLAN")
+if plan:  # a committed plan (plans/*.json) instead of a fresh autotune
+    import json
+    pl = json.load(open(plan))
+    dm.load_plan(pl["batch"], pl["plan"])
+else:
+    dm.autotune(ft, 0.25)
 for _ in range(3):
     dm.detect(ft)
 torch.cuda.synchronize()
@@ -31,7 +38,11 @@ L.check(L.lib().yk_model_buffer(dm._h, -2, C.byref(ptr)), "buf")
 ts = np.zeros(3 * 65536, np.uint64)
 M._memcpy_d2h(ts, ptr.value)
 ts = ts.reshape(-1, 3).astype(np.int64)
+print(f"ts buffer 0x{ptr.value or 0:x}: {(ts[:, 0] > 0).sum()} starts, {(ts[:, 1] > 0).sum()} mids, {(ts[:, 2] > 0).sum()} ends; "
+      f"plan of op {op}: {dm.get_plan()[1][op]}")
 ts = ts[ts[:, 0] > 0]
+if not len(ts):
+    sys.exit(f"op {op}: no workgroup timestamps (not a conv_fast / conv_fastw op under this plan?)")
 # the buffer keeps the last launch of every workgroup index: keep the last launch's cluster
 order = np.sort(ts[:, 0])
 gaps = np.nonzero(np.diff(order) > 300)[0]  # > 3 us between consecutive workgroup starts
@@ -44,3 +55,10 @@ print(f"op {op} {prof[op][2]} isolated {prof[op][3] * 1e3:.2f} us; {len(ts)} wor
 print(f"  start spread {st.max():.2f} us (p50 {np.median(st):.2f}); last end {en.max():.2f} us")
 print(f"  per WG: total p50 {np.median(en - st):.2f} max {np.max(en - st):.2f}; prologue+K p50 {np.median(mid - st):.2f}; "
       f"reduce+epilogue p50 {np.median(en - mid):.2f}")
+span = en.max()
+dur = en - st
+print(f"  mean resident workgroups {dur.sum() / span:.1f} (256 CUs); "
+      f"p10/p50/p90 WG duration {np.percentile(dur, 10):.2f}/{np.percentile(dur, 50):.2f}/{np.percentile(dur, 90):.2f} us")
+for q in (0.25, 0.5, 0.75, 0.95):
+    t = q * span
+    print(f"  at {q:.0%} of the span ({t:.1f} us): {int(((st <= t) & (en > t)).sum())} workgroups running")

@@ -108,6 +108,26 @@ __device__ __forceinline__ f32x4 mma<F32>(const uint4& w, const uint4& x, f32x4 
   return acc;
 }
 
+// Two consecutive K steps (fragments w0/x0 of step k, w1/x1 of step k + 1) into one accumulator.
+// FP8: ONE block-scaled v_mfma_scale_f32_16x16x128_f8f6f4 (e4m3 x e4m3, K = 128 = the 32 bytes
+// of the two steps' fragments of every lane) at unit E8M0 block scales (127 = 2^0), which runs
+// at twice the BF16 rate per clock where the non-scaled 16x16x32 fp8 form runs at the BF16 rate
+// (MI355X_MICROARCH.md, "Matrix cores").  A and B assemble their 32 bytes the same way, so the
+// byte -> K-slot pairing is consistent whatever order the hardware reads K in; the per-output-
+// channel dequantisation stays in the epilogue.  Other types: the two steps in order.
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+template <class Tr>
+__device__ __forceinline__ f32x4 mma2(const uint4& w0, const uint4& w1, const uint4& x0, const uint4& x1, f32x4 acc) {
+  if constexpr (Tr::kScaled) {
+    const i32x8 a = {(int)w0.x, (int)w0.y, (int)w0.z, (int)w0.w, (int)w1.x, (int)w1.y, (int)w1.z, (int)w1.w};
+    const i32x8 b = {(int)x0.x, (int)x0.y, (int)x0.z, (int)x0.w, (int)x1.x, (int)x1.y, (int)x1.z, (int)x1.w};
+    return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, acc, 0, 0, 0, 0x7F7F7F7F, 0, 0x7F7F7F7F);
+  } else {
+    acc = mma<Tr>(w0, x0, acc);
+    return mma<Tr>(w1, x1, acc);
+  }
+}
+
 template <bool kExact>
 __device__ __forceinline__ float silu(float v) {
   if constexpr (kExact) return v / (1.0f + expf(-v));
@@ -770,6 +790,12 @@ __device__ __forceinline__ int fdiv(int n, int d, float inv) {
   return q;
 }
 
+// K steps of loads each conv_fast wave keeps in flight (2 for the large register tiles: register
+// budget).  8 steps for the 1- and 2-fragment tiles measured no faster than 4 (round 2).
+constexpr int fast_skd(int nnt, int npt) { return nnt * npt >= 8 ? 2 : 4; }
+// conv_fastw's activation slots are indexed by the step within a 4-step weight chunk: SKD | 4
+constexpr int fastw_skd(int nnt, int npt) { return nnt * npt >= 8 ? 2 : 4; }
+
 template <class Tr, int NNT, int NPT, bool WS, int SKD>
 __global__ void __launch_bounds__(256) conv_fast_kernel(FastArgs a) {
   using T = typename Tr::T;
@@ -866,25 +892,50 @@ __global__ void __launch_bounds__(256) conv_fast_kernel(FastArgs a) {
       load_step(k0 + d, wb[d], xb[d]);
     }
     for (; ks + 2 * SKD <= k1; ks += SKD) {
+      if constexpr (Tr::kScaled) {
+        // FP8: step pairs (d, d + 1) on one block-scaled K=128 MFMA, then both refills
+#pragma unroll
+        for (int d = 0; d < SKD; d += 2) {
+          __builtin_amdgcn_sched_barrier(0);
+          const int2 e0 = tab[(ks + d + SKD) * 4 + kg], e1 = tab[(ks + d + 1 + SKD) * 4 + kg];
+#pragma unroll
+          for (int i = 0; i < NNT; ++i)
+#pragma unroll
+            for (int t = 0; t < NPT; ++t) acc[i][t] = mma2<Tr>(wb[d][i], wb[d + 1][i], xb[d][t], xb[d + 1][t], acc[i][t]);
+          __builtin_amdgcn_sched_barrier(0);
+          issue(ks + d + SKD, e0, wb[d], xb[d]);
+          issue(ks + d + 1 + SKD, e1, wb[d + 1], xb[d + 1]);
+        }
+      } else {
+#pragma unroll
+        for (int d = 0; d < SKD; ++d) {
+          __builtin_amdgcn_sched_barrier(0);
+          const int2 e = tab[(ks + d + SKD) * 4 + kg];  // LDS read in flight over the MFMAs
+#pragma unroll
+          for (int i = 0; i < NNT; ++i)
+#pragma unroll
+            for (int t = 0; t < NPT; ++t) acc[i][t] = mma<Tr>(wb[d][i], xb[d][t], acc[i][t]);
+          __builtin_amdgcn_sched_barrier(0);
+          issue(ks + d + SKD, e, wb[d], xb[d]);
+        }
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (Tr::kScaled) {
+#pragma unroll
+      for (int d = 0; d < SKD; d += 2)
+#pragma unroll
+        for (int i = 0; i < NNT; ++i)
+#pragma unroll
+          for (int t = 0; t < NPT; ++t) acc[i][t] = mma2<Tr>(wb[d][i], wb[d + 1][i], xb[d][t], xb[d + 1][t], acc[i][t]);
+    } else {
 #pragma unroll
       for (int d = 0; d < SKD; ++d) {
-        __builtin_amdgcn_sched_barrier(0);
-        const int2 e = tab[(ks + d + SKD) * 4 + kg];  // LDS read in flight over the MFMAs
 #pragma unroll
         for (int i = 0; i < NNT; ++i)
 #pragma unroll
           for (int t = 0; t < NPT; ++t) acc[i][t] = mma<Tr>(wb[d][i], xb[d][t], acc[i][t]);
-        __builtin_amdgcn_sched_barrier(0);
-        issue(ks + d + SKD, e, wb[d], xb[d]);
       }
-    }
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int d = 0; d < SKD; ++d) {
-#pragma unroll
-      for (int i = 0; i < NNT; ++i)
-#pragma unroll
-        for (int t = 0; t < NPT; ++t) acc[i][t] = mma<Tr>(wb[d][i], xb[d][t], acc[i][t]);
     }
     ks += SKD;
   }
@@ -896,14 +947,31 @@ __global__ void __launch_bounds__(256) conv_fast_kernel(FastArgs a) {
     for (int d = 0; d < SKD; ++d)
       if (ks + d < k1) load_step(ks + d, wb[d], xb[d]);
     for (; ks < k1; ks += SKD) {
+      if constexpr (Tr::kScaled) {
+        const uint4 z = make_uint4(0u, 0u, 0u, 0u);  // an odd last step pairs with zeros
 #pragma unroll
-      for (int d = 0; d < SKD; ++d) {
-        if (ks + d < k1) {
+        for (int d = 0; d < SKD; d += 2) {
+          if (ks + d < k1) {
+            const bool two = ks + d + 1 < k1;
 #pragma unroll
-          for (int i = 0; i < NNT; ++i)
+            for (int i = 0; i < NNT; ++i)
 #pragma unroll
-            for (int t = 0; t < NPT; ++t) acc[i][t] = mma<Tr>(wb[d][i], xb[d][t], acc[i][t]);
-          if (ks + d + SKD < k1) load_step(ks + d + SKD, wb[d], xb[d]);
+              for (int t = 0; t < NPT; ++t)
+                acc[i][t] = mma2<Tr>(wb[d][i], two ? wb[d + 1][i] : z, xb[d][t], two ? xb[d + 1][t] : z, acc[i][t]);
+            if (ks + d + SKD < k1) load_step(ks + d + SKD, wb[d], xb[d]);
+            if (two && ks + d + 1 + SKD < k1) load_step(ks + d + 1 + SKD, wb[d + 1], xb[d + 1]);
+          }
+        }
+      } else {
+#pragma unroll
+        for (int d = 0; d < SKD; ++d) {
+          if (ks + d < k1) {
+#pragma unroll
+            for (int i = 0; i < NNT; ++i)
+#pragma unroll
+              for (int t = 0; t < NPT; ++t) acc[i][t] = mma<Tr>(wb[d][i], xb[d][t], acc[i][t]);
+            if (ks + d + SKD < k1) load_step(ks + d + SKD, wb[d], xb[d]);
+          }
         }
       }
     }
@@ -989,6 +1057,8 @@ __global__ void __launch_bounds__(256) conv_fastw_kernel(FastArgs a) {
   const int2 blk = xcd_block(a.xcd);
   const int nt0 = blk.y * NNT;
   const int pbase = (blk.x * 4 + wave) * (16 * NPT);
+  const int wg_lin = blockIdx.y * gridDim.x + blockIdx.x;
+  if (a.tstamp && tid == 0 && wg_lin < a.tstamp_cap) a.tstamp[3 * wg_lin] = wall_clock64();
   for (int i = tid; i < nk * 4; i += 256) tab[i] = a.ktab[i];
   const __amdgpu_buffer_rsrc_t xr = make_srd(a.arena, a.arena_bytes);
   const __amdgpu_buffer_rsrc_t wr = make_srd(a.wblob, a.wbytes);
@@ -1067,21 +1137,47 @@ __global__ void __launch_bounds__(256) conv_fastw_kernel(FastArgs a) {
     const bool more = c + 1 < nch;
     if (more) stage_load(c + 1);  // in flight over this chunk's MFMAs
     const uint4* wb = ring + (size_t)(c & 1) * 4 * NNT * 64;
+    if constexpr (Tr::kScaled) {
+      // FP8: steps (d, d + 1) of the chunk on one block-scaled K=128 MFMA (odd tail: zeros)
+      const uint4 z = make_uint4(0u, 0u, 0u, 0u);
 #pragma unroll
-    for (int d = 0; d < 4; ++d) {
-      const int ks = 4 * c + d;
-      if (ks < nk) {
-        uint4 wf[NNT];
+      for (int d = 0; d < 4; d += 2) {
+        const int ks = 4 * c + d;
+        if (ks < nk) {
+          const bool two = ks + 1 < nk;
+          uint4 w0[NNT], w1[NNT];
 #pragma unroll
-        for (int i = 0; i < NNT; ++i) wf[i] = wb[(d * NNT + i) * 64 + lane];
-        // step ks's activations sit in slot ks % SKD = d % SKD (SKD divides 4): a compile-time
-        // index, so the slots stay registers
-        uint4* xf = xb[d % SKD];
+          for (int i = 0; i < NNT; ++i) {
+            w0[i] = wb[(d * NNT + i) * 64 + lane];
+            w1[i] = two ? wb[((d + 1) * NNT + i) * 64 + lane] : z;
+          }
+          uint4* x0 = xb[d % SKD];
+          uint4* x1 = xb[(d + 1) % SKD];
 #pragma unroll
-        for (int i = 0; i < NNT; ++i)
+          for (int i = 0; i < NNT; ++i)
 #pragma unroll
-          for (int t = 0; t < NPT; ++t) acc[i][t] = mma<Tr>(wf[i], xf[t], acc[i][t]);
-        if (ks + SKD < nk) act_load(ks + SKD, xf);
+            for (int t = 0; t < NPT; ++t) acc[i][t] = mma2<Tr>(w0[i], w1[i], x0[t], two ? x1[t] : z, acc[i][t]);
+          if (ks + SKD < nk) act_load(ks + SKD, x0);
+          if (two && ks + 1 + SKD < nk) act_load(ks + 1 + SKD, x1);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        const int ks = 4 * c + d;
+        if (ks < nk) {
+          uint4 wf[NNT];
+#pragma unroll
+          for (int i = 0; i < NNT; ++i) wf[i] = wb[(d * NNT + i) * 64 + lane];
+          // step ks's activations sit in slot ks % SKD = d % SKD (SKD divides 4): a compile-time
+          // index, so the slots stay registers
+          uint4* xf = xb[d % SKD];
+#pragma unroll
+          for (int i = 0; i < NNT; ++i)
+#pragma unroll
+            for (int t = 0; t < NPT; ++t) acc[i][t] = mma<Tr>(wf[i], xf[t], acc[i][t]);
+          if (ks + SKD < nk) act_load(ks + SKD, xf);
+        }
       }
     }
     if (more) {
@@ -1090,6 +1186,7 @@ __global__ void __launch_bounds__(256) conv_fastw_kernel(FastArgs a) {
       __builtin_amdgcn_s_barrier();
     }
   }
+  if (a.tstamp && tid == 0 && wg_lin < a.tstamp_cap) a.tstamp[3 * wg_lin + 1] = wall_clock64();
 #pragma unroll
   for (int i = 0; i < NNT; ++i) {
     const int nt = nt0 + i;
@@ -1121,6 +1218,7 @@ __global__ void __launch_bounds__(256) conv_fastw_kernel(FastArgs a) {
       store4((T*)a.dst + (size_t)p * a.d_cstride + a.d_coff + n0, v);
     }
   }
+  if (a.tstamp && tid == 0 && wg_lin < a.tstamp_cap) a.tstamp[3 * wg_lin + 2] = wall_clock64();
 }
 
 inline size_t fastw_lds(int k_steps, int nnt) {
@@ -1284,12 +1382,22 @@ __global__ void __launch_bounds__(64 * NW) conv_wide_kernel(WideArgs a) {
         for (int pt = 0; pt < NPT; ++pt) xf[d][pt] = *(const uint4*)(xt + prow[pt] + ev[d]);
       }
       __builtin_amdgcn_sched_barrier(0);
+      if constexpr (Tr::kScaled) {  // FP8: step pairs on one block-scaled K=128 MFMA
 #pragma unroll
-      for (int d = 0; d < 4; ++d)
+        for (int d = 0; d < 4; d += 2)
 #pragma unroll
-        for (int ni = 0; ni < NNT; ++ni)
+          for (int ni = 0; ni < NNT; ++ni)
 #pragma unroll
-          for (int pt = 0; pt < NPT; ++pt) acc[ni][pt] = mma<Tr>(wf[d][ni], xf[d][pt], acc[ni][pt]);
+            for (int pt = 0; pt < NPT; ++pt)
+              acc[ni][pt] = mma2<Tr>(wf[d][ni], wf[d + 1][ni], xf[d][pt], xf[d + 1][pt], acc[ni][pt]);
+      } else {
+#pragma unroll
+        for (int d = 0; d < 4; ++d)
+#pragma unroll
+          for (int ni = 0; ni < NNT; ++ni)
+#pragma unroll
+            for (int pt = 0; pt < NPT; ++pt) acc[ni][pt] = mma<Tr>(wf[d][ni], xf[d][pt], acc[ni][pt]);
+      }
       __builtin_amdgcn_sched_barrier(0);
     }
     for (; k4 < nkl; ++k4) {
@@ -1300,8 +1408,10 @@ __global__ void __launch_bounds__(64 * NW) conv_wide_kernel(WideArgs a) {
 #pragma unroll
       for (int ni = 0; ni < NNT; ++ni) {
         const uint4 w = wl[(ni * nk + k4) * 64 + lane];
+        const uint4 z = make_uint4(0u, 0u, 0u, 0u);
 #pragma unroll
-        for (int pt = 0; pt < NPT; ++pt) acc[ni][pt] = mma<Tr>(w, xf[pt], acc[ni][pt]);
+        for (int pt = 0; pt < NPT; ++pt)
+          acc[ni][pt] = Tr::kScaled ? mma2<Tr>(w, z, xf[pt], z, acc[ni][pt]) : mma<Tr>(w, xf[pt], acc[ni][pt]);
       }
     }
     // epilogue of tile t
@@ -1717,39 +1827,43 @@ __global__ void __launch_bounds__(256) sppf_pool_kernel(void* buf, int cstride, 
   store4(o + 3 * C, m13);
 }
 
-// One workgroup = one image x 8 channels: the plane is staged in LDS as f32, the 5/9/13-wide
-// row maxima are formed, then the column maxima (square windows are separable), so each input
-// element is read from HBM once instead of 169 times.  max is exact in any precision.
-constexpr int kSppfLdsMaxHW = 1024;
-template <class Tr>
+// One workgroup = one image x CPG channels (8, or 4 for planes of up to 2048 pixels, e.g. the P5
+// map 32 x 40 at imgsz 1280): the plane is staged in LDS as f32, the 5/9/13-wide row maxima are
+// formed, then the column maxima (square windows are separable), so each input element is read
+// from HBM once instead of 169 times.  max is exact in any precision.
+constexpr int kSppfLdsMaxHW = 1024;      // 8 channels per workgroup
+constexpr int kSppfLdsMaxHW4 = 2048;     // 4 channels per workgroup
+constexpr size_t kSppfLdsBytes = 128 * 1024;
+template <class Tr, int CPG>
 __global__ void __launch_bounds__(256) sppf_lds_kernel(void* buf, int cstride, int coff, int C, int H, int W) {
   using T = typename Tr::T;
+  constexpr int IPP = CPG / 4;  // 4-channel items per pixel
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int HW = H * W, cg = C / 8;
-  const int b = blockIdx.x / cg, c0 = (blockIdx.x - b * cg) * 8;
-  float* x = (float*)smem;  // [HW][8]
-  float* r5 = x + HW * 8;
-  float* r9 = r5 + HW * 8;
-  float* r13 = r9 + HW * 8;
+  const int HW = H * W, cg = C / CPG;
+  const int b = blockIdx.x / cg, c0 = (blockIdx.x - b * cg) * CPG;
+  float* x = (float*)smem;  // [HW][CPG]
+  float* r5 = x + HW * CPG;
+  float* r9 = r5 + HW * CPG;
+  float* r13 = r9 + HW * CPG;
   T* base = (T*)buf + (size_t)b * HW * cstride + coff + c0;
-  for (int i = threadIdx.x; i < HW * 2; i += blockDim.x) {  // 4 channels per item
-    const int p = i >> 1, h = (i & 1) * 4;
+  for (int i = threadIdx.x; i < HW * IPP; i += blockDim.x) {
+    const int p = i / IPP, h = (i % IPP) * 4;
     float v[4];
     load4(base + (size_t)p * cstride + h, v);
-    *(float4*)(x + p * 8 + h) = make_float4(v[0], v[1], v[2], v[3]);
+    *(float4*)(x + p * CPG + h) = make_float4(v[0], v[1], v[2], v[3]);
   }
   __syncthreads();
   // Window indices are clamped to the plane instead of skipped: a clamped index is the border
   // element, which lies inside the same window, and max is idempotent -- so the 13 reads of a
   // window are branch-free and issue back to back.
-  for (int i = threadIdx.x; i < HW * 8; i += blockDim.x) {
-    const int p = i >> 3, c = i & 7, yy = p / W, xx = p - yy * W;
-    const float* row = x + yy * W * 8 + c;
+  for (int i = threadIdx.x; i < HW * CPG; i += blockDim.x) {
+    const int p = i / CPG, c = i % CPG, yy = p / W, xx = p - yy * W;
+    const float* row = x + yy * W * CPG + c;
     float v[13];
 #pragma unroll
     for (int d = 0; d < 13; ++d) {
       const int u = min(max(xx + d - 6, 0), W - 1);
-      v[d] = row[u * 8];
+      v[d] = row[u * CPG];
     }
     float m5 = fmaxf(fmaxf(fmaxf(v[4], v[5]), fmaxf(v[6], v[7])), v[8]);
     float m9 = fmaxf(fmaxf(m5, fmaxf(v[2], v[3])), fmaxf(v[9], v[10]));
@@ -1759,14 +1873,14 @@ __global__ void __launch_bounds__(256) sppf_lds_kernel(void* buf, int cstride, i
     r13[i] = m13;
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < HW * 2; i += blockDim.x) {
-    const int p = i >> 1, h = (i & 1) * 4, yy = p / W, xx = p - yy * W;
+  for (int i = threadIdx.x; i < HW * IPP; i += blockDim.x) {
+    const int p = i / IPP, h = (i % IPP) * 4, yy = p / W, xx = p - yy * W;
     float m5[4], m9[4], m13[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) m5[j] = m9[j] = m13[j] = -INFINITY;
 #pragma unroll
     for (int d = 0; d < 13; ++d) {
-      const int q = (min(max(yy + d - 6, 0), H - 1) * W + xx) * 8 + h;
+      const int q = (min(max(yy + d - 6, 0), H - 1) * W + xx) * CPG + h;
       const float4 a13 = *(const float4*)(r13 + q);
       m13[0] = fmaxf(m13[0], a13.x); m13[1] = fmaxf(m13[1], a13.y);
       m13[2] = fmaxf(m13[2], a13.z); m13[3] = fmaxf(m13[3], a13.w);
@@ -2676,13 +2790,13 @@ void set_tile_attrs_t() {
 }
 template <class Tr, int NNT, int NPT, bool WS>
 void set_fast_attr() {
-  constexpr int SKD = NNT * NPT >= 8 ? 2 : 4;
+  constexpr int SKD = fast_skd(NNT, NPT);
   (void)hipFuncSetAttribute((const void*)conv_fast_kernel<Tr, NNT, NPT, WS, SKD>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
 }
 template <class Tr, int NNT, int NPT>
 void set_fastw_attr() {
-  constexpr int SKD = NNT * NPT >= 8 ? 2 : 4;
+  constexpr int SKD = fastw_skd(NNT, NPT);
   (void)hipFuncSetAttribute((const void*)conv_fastw_kernel<Tr, NNT, NPT, SKD>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
 }
@@ -2731,12 +2845,12 @@ void set_tile_attrs() {
   set_wide_attr_n<FP8, 4>();
   set_fast_attr_w<FP8, false>();
   set_fast_attr_w<FP8, true>();
-  (void)hipFuncSetAttribute((const void*)sppf_lds_kernel<FP8>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            kSppfLdsMaxHW * 128);
-  (void)hipFuncSetAttribute((const void*)sppf_lds_kernel<BF16>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            kSppfLdsMaxHW * 128);
-  (void)hipFuncSetAttribute((const void*)sppf_lds_kernel<F32>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            kSppfLdsMaxHW * 128);
+  (void)hipFuncSetAttribute((const void*)sppf_lds_kernel<FP8, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, kSppfLdsBytes);
+  (void)hipFuncSetAttribute((const void*)sppf_lds_kernel<BF16, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, kSppfLdsBytes);
+  (void)hipFuncSetAttribute((const void*)sppf_lds_kernel<F32, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, kSppfLdsBytes);
+  (void)hipFuncSetAttribute((const void*)sppf_lds_kernel<FP8, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, kSppfLdsBytes);
+  (void)hipFuncSetAttribute((const void*)sppf_lds_kernel<BF16, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, kSppfLdsBytes);
+  (void)hipFuncSetAttribute((const void*)sppf_lds_kernel<F32, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, kSppfLdsBytes);
 }
 
 // Conv kernel choice for one op at batch B.
@@ -2897,7 +3011,7 @@ void launch_splitk(const ConvArgs& a, const ConvPlan& p, hipStream_t st) {
 
 template <class Tr, int NNT, int NPT, bool WS>
 void launch_fast_t(const FastArgs& a, hipStream_t st) {
-  constexpr int SKD = NNT * NPT >= 8 ? 2 : 4;
+  constexpr int SKD = fast_skd(NNT, NPT);
   const int px = WS ? 16 * NPT : 64 * NPT;
   dim3 grid((a.M + px - 1) / px, (a.n_tiles + NNT - 1) / NNT);
   hipLaunchKernelGGL((conv_fast_kernel<Tr, NNT, NPT, WS, SKD>), grid, dim3(256), fast_lds(a.k_steps, NNT, NPT, WS), st,
@@ -2920,7 +3034,7 @@ void launch_fast_w(const FastArgs& a, int nnt, int npt, hipStream_t st) {
 }
 template <class Tr, int NNT, int NPT>
 void launch_fastw_t(const FastArgs& a, hipStream_t st) {
-  constexpr int SKD = NNT * NPT >= 8 ? 2 : 4;
+  constexpr int SKD = fastw_skd(NNT, NPT);
   dim3 grid((a.M + 64 * NPT - 1) / (64 * NPT), (a.n_tiles + NNT - 1) / NNT);
   hipLaunchKernelGGL((conv_fastw_kernel<Tr, NNT, NPT, SKD>), grid, dim3(256), fastw_lds(a.k_steps, NNT), st, a);
 }
@@ -3182,11 +3296,15 @@ int launch_op(yk_model* m, const yk_op& op, const uint8_t* frames, int B, float 
         const int M = B * op.src[0].h * op.src[0].w;
         const int C = op.src_ch[0];
         const int HW = op.src[0].h * op.src[0].w;
+        void* pb = img_ptr(m, op.src[0].buf, op.src[0].h, op.src[0].w, op.src[0].c_stride, b0);
         if (HW <= kSppfLdsMaxHW && C % 8 == 0) {
-          hipLaunchKernelGGL(sppf_lds_kernel<Tr>, dim3(B * (C / 8)), dim3(256), (size_t)HW * 8 * 4 * 4, st,
-                             img_ptr(m, op.src[0].buf, op.src[0].h, op.src[0].w, op.src[0].c_stride, b0),
-                             op.src[0].c_stride, op.src[0].c_off, C, op.src[0].h,
-                             op.src[0].w);
+          hipLaunchKernelGGL((sppf_lds_kernel<Tr, 8>), dim3(B * (C / 8)), dim3(256), (size_t)HW * 8 * 4 * 4, st, pb,
+                             op.src[0].c_stride, op.src[0].c_off, C, op.src[0].h, op.src[0].w);
+          break;
+        }
+        if (HW <= kSppfLdsMaxHW4 && C % 4 == 0) {
+          hipLaunchKernelGGL((sppf_lds_kernel<Tr, 4>), dim3(B * (C / 4)), dim3(256), (size_t)HW * 4 * 4 * 4, st, pb,
+                             op.src[0].c_stride, op.src[0].c_off, C, op.src[0].h, op.src[0].w);
           break;
         }
         const int n = M * (C / 4);
@@ -3253,7 +3371,9 @@ const char* op_kernel_name(const yk_model* m, const yk_op& op) {
       return buf;
     case YK_K_SPPF_POOL:
       if (op.src[0].h * op.src[0].w <= kSppfLdsMaxHW && op.src_ch[0] % 8 == 0)
-        snprintf(buf, sizeof buf, "sppf_lds_kernel<yk::det::%s>", tn);
+        snprintf(buf, sizeof buf, "sppf_lds_kernel<yk::det::%s, 8>", tn);
+      else if (op.src[0].h * op.src[0].w <= kSppfLdsMaxHW4 && op.src_ch[0] % 4 == 0)
+        snprintf(buf, sizeof buf, "sppf_lds_kernel<yk::det::%s, 4>", tn);
       else
         snprintf(buf, sizeof buf, "sppf_pool_kernel<yk::det::%s>", tn);
       return buf;
@@ -3269,7 +3389,7 @@ const char* op_kernel_name(const yk_model* m, const yk_op& op) {
   }
   if (cp.kind == CK_FAST) {
     const int npt = cp.npt & 15, mode = cp.npt >> 4;
-    const int skd = cp.nnt * npt >= 8 ? 2 : 4;
+    const int skd = mode == 2 ? fastw_skd(cp.nnt, npt) : fast_skd(cp.nnt, npt);
     if (mode == 2)
       snprintf(buf, sizeof buf, "conv_fastw_kernel<yk::det::%s, %d, %d, %d>", tn, cp.nnt, npt, skd);
     else
