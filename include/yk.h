@@ -161,10 +161,14 @@ int yk_tracker_outputs(yk_tracker* trk, yk_track_out** dev_rows, int32_t** dev_c
 int yk_tracker_download(yk_tracker* trk, yk_track_out* host_rows, int32_t* host_counts,
                         yk_tracker_stats* host_stats, void* stream);
 
-/* Profiling: wall_clock64 (100 MHz) timestamps of stream s's last step at its phase
- * boundaries: [0] start, [1] predict, [2] IoU candidates, [3] greedy rounds, [4] update /
- * mark_lost, [5] new tracks, [6] delete, [7] outputs; [10] = association rounds used. */
-int yk_tracker_phase_ticks(yk_tracker* trk, int stream_index, int64_t* host_ticks16, void* stream);
+/* Profiling: 32 words of stream s's last step (host_ticks holds 32).  wall_clock64 (100 MHz)
+ * timestamps at the phase boundaries -- single-workgroup step: [0] start, [1] predict, [2] IoU
+ * candidates, [3] greedy rounds, [4] update / mark_lost, [5] new tracks, [6] delete, [7] outputs;
+ * two-launch enhanced step: [0]-[4] the association kernel (boxes, candidates, rounds, decisions),
+ * [5]/[8]/[9]/[6] the first per-track workgroup (start, staged, computed, end); [10] association
+ * rounds used; [11]-[15] candidate-index counters and the association kernel's shader cycles;
+ * [16]-[19] shader cycles of the per-track waves (update / lost / new paths). */
+int yk_tracker_phase_ticks(yk_tracker* trk, int stream_index, int64_t* host_ticks, void* stream);
 
 /* Snapshot the live tracks of one stream in list order (EnhancedMultiTargetTracker.trackers).
  * host_states must hold max_tracks entries; *n_out receives the number written. */

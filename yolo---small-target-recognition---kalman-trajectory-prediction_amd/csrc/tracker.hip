@@ -36,6 +36,7 @@ constexpr int VH = YK_VEL_HIST;         // velocity ring (deque maxlen=50)
 constexpr int TH = YK_TRAJ_HIST;        // trajectory ring (deque maxlen=150)
 constexpr int TOUT = YK_TRAJ_OUT;       // trajectory points exported per row
 constexpr double kPi = 3.141592653589793;  // np.pi
+constexpr int PH = 32;                  // profiling words per stream (yk_tracker_phase_ticks)
 
 // YK_POLICY_MOTION_RESET numerics.  The reference's reset logic mixes numpy float32 and float64
 // scalars with python floats; NEP 50 (numpy 2) fixes every result's dtype: a numpy scalar op a
@@ -53,6 +54,7 @@ struct ResetDetail {  // one reset_reasons entry (motion_reset_kalman_tracker.py
 };
 
 struct Slot {
+  static constexpr bool kPol = true;  // carries the motion-reset state (LSlot below does not)
   double x[8];
   double P[16];  // per coordinate c: [4c+0]=P[c][c] [4c+1]=P[c][c+4] [4c+2]=P[c+4][c] [4c+3]=P[c+4][c+4]
   double vavg[2], vstd[2], direction, speed, stability, pconf;
@@ -75,6 +77,23 @@ struct Slot {
   ResetDetail dl[5];            // the last five reset_reasons entries
 };
 
+// Register copy of a Slot's scalar state, the rings left in global memory (pointer members, so
+// s.vh[i][0] / s.vang[i] / s.th[i][0] read the same as on a Slot).  The enhanced per-track math
+// runs on it and writes back once: on a Slot in global memory every store followed by a load of
+// another field is a memory round trip in the thread's dependency chain (no alias proof).
+struct LSlot {
+  static constexpr bool kPol = false;
+  double x[8];
+  double P[16];
+  double vavg[2], vstd[2], direction, speed, stability, pconf;
+  double (*vh)[2];
+  double* vang;
+  double (*th)[2];
+  int age, hits, hit_streak, tsu, is_lost, lost_frames, track_num, max_lost;
+  int vh_len, vh_head, th_len, th_head;
+  int policy;
+};
+
 struct Hdr {
   int n_tracks, n_free;
   yk_tracker_stats st;
@@ -90,7 +109,10 @@ struct Dev {
   yk_track_out* rows;   // [S][T]
   int* counts;          // [S]
   yk_tracker_stats* stats;  // [S]
-  long long* phase;         // [S][16] wall_clock64 at the step's phase boundaries (profiling)
+  long long* phase;         // [S][PH] wall_clock64 at the step's phase boundaries (profiling)
+  int4* items;              // [S][T] enhanced two-kernel step: {slot, det, track_num, out_row} per work item
+  int2* items_vh;           // [S][T] {vh_len, vh_head} of the item's slot before the step
+  int* n_items;             // [S]
   int T, D, C;
   int max_lost, min_hits;
   double thr;
@@ -135,7 +157,8 @@ __device__ __forceinline__ void bbox_to_state(const DT* b, double* z) {
   z[3] = (double)h;
 }
 
-__device__ void slot_init(Slot& s, const double* z, int track_num, int max_lost) {
+template <class S>
+__device__ void slot_init(S& s, const double* z, int track_num, int max_lost) {
   // AircraftKalmanTracker.__init__ (kf.py:32-101)
   for (int i = 0; i < 8; ++i) s.x[i] = 0.0;
   for (int c = 0; c < 4; ++c) {
@@ -161,7 +184,8 @@ __device__ void slot_init(Slot& s, const double* z, int track_num, int max_lost)
   ring_push(s.th, TH, s.th_len, s.th_head, z[0], z[1]);
 }
 
-__device__ void kf_predict(Slot& s) {
+template <class S>
+__device__ void kf_predict(S& s) {
   // kf.py:192-201: x = F x ; P = F P F^T + Q
   const double qp[4] = {0.1, 0.1, 0.01, 0.01};
   const double qv[4] = {0.1, 0.1, 0.001, 0.001};
@@ -201,36 +225,91 @@ __device__ double np_pairwise_sum(const double* a, int n) {
   return res;
 }
 
+// Chain-friendly forms of numpy's reductions.  The guard sits on the ADDEND: x + (-0.0) == x
+// exactly for every x (signed zeros, infinities and NaN included), so a masked-out element adds
+// -0.0 and the accumulator's dependency chain is one v_add_f64 per element.  Loops run over the
+// static ring size in chunks of 7 (inner loop unrolled, its LDS loads issued together; outer loop
+// rolled, which bounds the registers).
+constexpr int PW = 56;  // >= VH - 1, a multiple of 8
+static_assert(VH == 50, "chunking below assumes the 50-entry velocity ring");
+
+// np.add.reduce's pairwise summation (numpy/_core/src/umath/loops_utils.h.src, pairwise_sum) of
+// f(0..n-1), n <= PW: the same additions in the same order as np_pairwise_sum.
+template <class F>
+__device__ __forceinline__ double np_pairwise_sum_f(F f, int n) {
+  if (n < 8) {
+    double r = 0.0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const double v = f(i);  // unconditional: the select (not a branch) keeps the chain straight
+      r += i < n ? v : -0.0;
+    }
+    return r;
+  }
+  double r[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = f(j);
+  const int lim = n - (n % 8);
+#pragma unroll 1
+  for (int i = 8; i < lim; i += 8) {
+    double v[8];  // the block's operands first: one LDS round trip per block, not per element
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = f(i + j);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] += v[j];
+  }
+  double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+#pragma unroll
+  for (int i = 0; i < 7; ++i) {
+    const double v = f(lim + i);
+    res += lim + i < n ? v : -0.0;
+  }
+  return res;
+}
+
 // The velocity history in chronological order (oldest first), as three arrays vx, vy, ang of
-// n = s.vh_len entries: the step kernel keeps them in LDS, so the serial reductions below --
-// numpy's evaluation order, bit for bit -- run on unit-stride LDS reads.  dch (m = n - 1
-// entries) may alias vx: vx is dead once the mean and std are done.
-__device__ void analyze_motion(Slot& s, const double* vx, const double* vy, const double* ang, double* dch) {
+// n = s.vh_len entries (LDS in the step kernels); dch (>= VH - 1 entries, LDS) may alias vx.
+template <class S>
+__device__ void analyze_motion(S& s, const double* vx, const double* vy, const double* ang, double* dch) {
   // kf.py:137-182
   const int n = s.vh_len;
   if (n < 5) return;
-  double mean[2], sq[2];
-  const double* v[2] = {vx, vy};
+  double acc0 = vx[0], acc1 = vy[0];  // np.mean(axis=0): sequential over rows
+#pragma unroll 1
+  for (int c = 1; c < VH; c += 7) {
+    double a0[7], a1[7];  // the chunk's loads first (one LDS round trip), then the guarded addends
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {  // np.mean(axis=0): sequential over rows
-    const double* a = v[j];
-    double acc = a[0];
-#pragma unroll 8
-    for (int k = 1; k < n; ++k) acc += a[k];
-    mean[j] = acc / (double)n;
-  }
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {  // np.std(axis=0), ddof=0
-    const double* a = v[j];
-    double d = a[0] - mean[j];
-    double acc = d * d;
-#pragma unroll 8
-    for (int k = 1; k < n; ++k) {
-      d = a[k] - mean[j];
-      acc += d * d;
+    for (int u = 0; u < 7; ++u) {
+      a0[u] = vx[c + u];
+      a1[u] = vy[c + u];
     }
-    sq[j] = sqrt(acc / (double)n);
+#pragma unroll
+    for (int u = 0; u < 7; ++u) {
+      acc0 += c + u < n ? a0[u] : -0.0;
+      acc1 += c + u < n ? a1[u] : -0.0;
+    }
   }
+  const double mean[2] = {acc0 / (double)n, acc1 / (double)n};
+  double d0 = vx[0] - mean[0], d1 = vy[0] - mean[1];  // np.std(axis=0), ddof=0
+  double q0 = d0 * d0, q1 = d1 * d1;
+#pragma unroll 1
+  for (int c = 1; c < VH; c += 7) {
+    double a0[7], a1[7];
+#pragma unroll
+    for (int u = 0; u < 7; ++u) {
+      a0[u] = vx[c + u];
+      a1[u] = vy[c + u];
+    }
+#pragma unroll
+    for (int u = 0; u < 7; ++u) {
+      d0 = a0[u] - mean[0];
+      d1 = a1[u] - mean[1];
+      const double e0 = d0 * d0, e1 = d1 * d1;
+      q0 += c + u < n ? e0 : -0.0;
+      q1 += c + u < n ? e1 : -0.0;
+    }
+  }
+  const double sq[2] = {sqrt(q0 / (double)n), sqrt(q1 / (double)n)};
   s.vavg[0] = mean[0];
   s.vavg[1] = mean[1];
   s.vstd[0] = sq[0];
@@ -240,19 +319,30 @@ __device__ void analyze_motion(Slot& s, const double* vx, const double* vy, cons
   const double speed_stab = 1.0 / (1.0 + ((0.0 + sq[0]) + sq[1]) / 2.0);
   // _calculate_direction_consistency (kf.py:165-182); n >= 5 here, so the n<3 exit is dead
   const int m = n - 1;
-#pragma unroll 8
-  for (int k = 0; k < m; ++k) {
-    double c = ang[k + 1] - ang[k];
-    if (!(fabs(c) < kPi)) c = c - 2.0 * kPi * (c > 0.0 ? 1.0 : (c < 0.0 ? -1.0 : c));
-    dch[k] = c;
+#pragma unroll 1
+  for (int c = 0; c < m; c += 7) {
+    double a[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int k = c + u;
+      a[u] = ang[k < VH ? k : VH - 1];  // reads stay inside the ring (k >= m is discarded)
+    }
+#pragma unroll
+    for (int u = 0; u < 7; ++u) {
+      const int k = c + u;
+      double v = a[u + 1] - a[u];
+      if (!(fabs(v) < kPi)) v = v - 2.0 * kPi * (v > 0.0 ? 1.0 : (v < 0.0 ? -1.0 : v));
+      dch[k] = v;  // k >= m lands on dead vx / vy entries (k < 56 <= 3 * VS - base)
+    }
   }
-  const double dmean = np_pairwise_sum(dch, m) / (double)m;
-#pragma unroll 8
-  for (int k = 0; k < m; ++k) {
-    const double d = dch[k] - dmean;
-    dch[k] = d * d;
-  }
-  const double dstd = sqrt(np_pairwise_sum(dch, m) / (double)m);
+  const double dmean = np_pairwise_sum_f([&](int k) { return dch[k]; }, m) / (double)m;
+  const double dstd = sqrt(np_pairwise_sum_f(
+                               [&](int k) {
+                                 const double d = dch[k] - dmean;
+                                 return d * d;
+                               },
+                               m) /
+                           (double)m);
   const double dir_cons = 1.0 / (1.0 + dstd * 10.0);
   s.stability = (speed_stab + dir_cons) / 2.0;
   const double frac = (double)n / 30.0;
@@ -578,8 +668,8 @@ __device__ void stage_chrono(const Slot& s, double* st) {
 }
 
 // st: stage_chrono() of the slot before this update ([3][VS], LDS in the step kernel).
-template <typename DT>
-__device__ void kf_update(Slot& s, const DT* box, double* st) {
+template <typename DT, class S>
+__device__ void kf_update(S& s, const DT* box, double* st) {
   // kf.py:249-297 (recovery print omitted; the count is kept by the caller)
   s.tsu = 0;
   s.hits += 1;
@@ -619,7 +709,8 @@ __device__ void kf_update(Slot& s, const DT* box, double* st) {
   analyze_motion(s, st + base, st + VS + base, st + 2 * VS + base, st + base);
 }
 
-__device__ __forceinline__ void mark_lost(Slot& s) {
+template <class S>
+__device__ __forceinline__ void mark_lost(S& s) {
   // kf.py:299-317
   if (!s.is_lost) {
     s.is_lost = 1;
@@ -638,11 +729,14 @@ __device__ __forceinline__ bool should_delete(const Slot& s, int max_lost) {
 }
 
 // enhanced_long_term_predict(frames_ahead=k) (kf.py:205-247).  k <= 1 runs predict().
-__device__ void long_term_predict(Slot& s, int k, double* box, double& conf) {
+template <class S>
+__device__ void long_term_predict(S& s, int k, double* box, double& conf) {
   if (k <= 1) {
     kf_predict(s);
     state_to_bbox(s.x, box);
-    if (s.policy) cmc_blend(s, box);  // the subclass's predict()
+    if constexpr (S::kPol) {
+      if (s.policy) cmc_blend(s, box);  // the subclass's predict()
+    }
     conf = 1.0;
     return;
   }
@@ -671,7 +765,8 @@ __device__ void long_term_predict(Slot& s, int k, double* box, double& conf) {
 }
 
 // get_lost_prediction (kf.py:319-333)
-__device__ void lost_prediction(Slot& s, double* box, double& conf) {
+template <class S>
+__device__ void lost_prediction(S& s, double* box, double& conf) {
   if (!s.is_lost) {
     state_to_bbox(s.x, box);
     conf = 1.0;
@@ -682,7 +777,8 @@ __device__ void lost_prediction(Slot& s, double* box, double& conf) {
 
 // get_track_info (kf.py:335-383) including quirk A (a second predict() on the first
 // lost frame, via get_lost_prediction -> enhanced_long_term_predict(1)).
-__device__ void track_info(Slot& s, yk_track_out& o, bool copy_traj = true) {
+template <class S>
+__device__ void track_info(S& s, yk_track_out& o, bool copy_traj = true) {
   double box[4];
   double conf;
   int status;
@@ -716,7 +812,8 @@ __device__ void track_info(Slot& s, yk_track_out& o, bool copy_traj = true) {
   o.direction = s.direction;
   // MotionResetKalmanTracker.get_track_info / get_reset_statistics (:314-355).  The enhanced
   // policy never writes these fields: the rows buffer is zeroed once at creation.
-  if (s.policy) {
+  if constexpr (S::kPol) {
+   if (s.policy) {
     o.reset_count = s.reset_count;
     o.frames_since_reset = s.age - s.last_reset;
     o.n_details = s.dl_len;
@@ -733,6 +830,7 @@ __device__ void track_info(Slot& s, yk_track_out& o, bool copy_traj = true) {
       o.details[k].confidence = u ? d.conf : 0.0;
       o.details[k].motion_consistency = u ? d.cons : 0.0;
     }
+   }
   }
   const int nt = s.th_len < TOUT ? s.th_len : TOUT;
   o.traj_len = nt;
@@ -776,7 +874,9 @@ __device__ double iou_mixed(const DT* d, const double* t) {
 
 // ---------------------------------------------------------------- block helpers
 // Exclusive prefix count of `flag` over the workgroup; `total` gets the block total.
+template <int NTH = NT>
 __device__ __forceinline__ int block_scan(int flag, int* wsum, int& total) {
+  constexpr int NW = NTH / 64;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const unsigned long long m = __ballot(flag);
   const int pre = __popcll(m & ((1ull << lane) - 1ull));
@@ -850,7 +950,7 @@ __device__ Lds carve(char* base, int T, int D) {
   return L;
 }
 
-enum { M_NCAND = 0, M_ACTIVE, M_RECOVER, M_LONGTERM, M_OVERFLOW, M_RESETS, M_TRECOV, M_WSUM = 8 };
+enum { M_NCAND = 0, M_ACTIVE, M_RECOVER, M_LONGTERM, M_OVERFLOW, M_RESETS, M_TRECOV, M_WSUM = 8, M_TESTED = 12 };
 
 // ---------------------------------------------------------------- the step kernel
 // POL: yk_tracker_policy as a template constant, so the enhanced instantiation carries none of
@@ -868,7 +968,7 @@ __global__ void __launch_bounds__(NT) step_kernel(Dev g, const DT* __restrict__ 
   int* fstack = g.free_stack + (size_t)s * T;
   int* wsum = L.misc + M_WSUM;
 
-  if (tid == 0) g.phase[s * 16 + 0] = wall_clock64();
+  if (tid == 0) g.phase[s * PH + 0] = wall_clock64();
   int Draw = counts[s];
   if (Draw < 0) Draw = 0;
   const int D = Draw < g.D ? Draw : g.D;
@@ -889,7 +989,7 @@ __global__ void __launch_bounds__(NT) step_kernel(Dev g, const DT* __restrict__ 
     if (POL && sl.policy) cmc_blend(sl, &L.pb[4 * i]);
   }
   __syncthreads();
-  if (tid == 0) g.phase[s * 16 + 1] = wall_clock64();
+  if (tid == 0) g.phase[s * PH + 1] = wall_clock64();
 
   // Step 2: association (multi:61-68, 134-178)
   if (D > 0 && n > 0) {
@@ -912,7 +1012,7 @@ __global__ void __launch_bounds__(NT) step_kernel(Dev g, const DT* __restrict__ 
       }
     }
     __syncthreads();
-    if (tid == 0) g.phase[s * 16 + 2] = wall_clock64();
+    if (tid == 0) g.phase[s * PH + 2] = wall_clock64();
     int nc = L.misc[M_NCAND];
     if (nc > g.C) {
       if (tid == 0) L.misc[M_OVERFLOW] += nc - g.C;
@@ -942,7 +1042,7 @@ __global__ void __launch_bounds__(NT) step_kernel(Dev g, const DT* __restrict__ 
       if (local_active) atomicAdd(&L.misc[M_ACTIVE], local_active);
       __syncthreads();
       if (L.misc[M_ACTIVE] == 0) {
-        if (tid == 0) g.phase[s * 16 + 10] = round;
+        if (tid == 0) g.phase[s * PH + 10] = round;
         break;
       }
       // among equal IoUs the enhanced tracker takes the lowest row-major pair first (stable
@@ -969,7 +1069,7 @@ __global__ void __launch_bounds__(NT) step_kernel(Dev g, const DT* __restrict__ 
     }
   }
 
-  if (tid == 0) g.phase[s * 16 + 3] = wall_clock64();
+  if (tid == 0) g.phase[s * PH + 3] = wall_clock64();
   // Steps 3-4: update matched tracks, mark the others lost (multi:71-89).  The matched
   // tracks' velocity rings (1.2 KB each) are staged into LDS CH tracks at a time by the whole
   // workgroup (coalesced 16-B loads, all in flight at once); each track's thread then runs
@@ -1032,7 +1132,7 @@ __global__ void __launch_bounds__(NT) step_kernel(Dev g, const DT* __restrict__ 
   if (recov) atomicAdd(&L.misc[M_RECOVER], recov);
   if (resets) atomicAdd(&L.misc[M_RESETS], resets);
   __syncthreads();
-  if (tid == 0) g.phase[s * 16 + 4] = wall_clock64();
+  if (tid == 0) g.phase[s * PH + 4] = wall_clock64();
 
   // Step 5: new tracks for unmatched detections, ascending detection order (multi:92-101)
   int n_new_total = 0;
@@ -1066,7 +1166,7 @@ __global__ void __launch_bounds__(NT) step_kernel(Dev g, const DT* __restrict__ 
   if (n_new > nfree0) n_new = nfree0;
   __syncthreads();
 
-  if (tid == 0) g.phase[s * 16 + 5] = wall_clock64();
+  if (tid == 0) g.phase[s * PH + 5] = wall_clock64();
   // Step 6: delete (multi:104-113) with a stable compaction of the list
   const int n_all = n + n_new;
   int kept = 0, n_del = 0;
@@ -1109,7 +1209,7 @@ __global__ void __launch_bounds__(NT) step_kernel(Dev g, const DT* __restrict__ 
   for (int i = tid; i < kept; i += NT) order[i] = L.order_tmp[i];
   __syncthreads();
 
-  if (tid == 0) g.phase[s * 16 + 6] = wall_clock64();
+  if (tid == 0) g.phase[s * PH + 6] = wall_clock64();
   // Step 7: outputs in list order (multi:116-126), get_track_info may predict (quirk A).
   // Rows are filled one thread per track; the 30-point trajectories are then copied by the
   // whole workgroup, one 16-B point per thread (the ring reads are independent loads).
@@ -1149,7 +1249,7 @@ __global__ void __launch_bounds__(NT) step_kernel(Dev g, const DT* __restrict__ 
     *(double2*)&g.rows[(size_t)s * T + r].traj[k][0] = v;
   }
   __syncthreads();
-  if (tid == 0) g.phase[s * 16 + 7] = wall_clock64();
+  if (tid == 0) g.phase[s * PH + 7] = wall_clock64();
   if (tid == 0) {
     H.n_tracks = kept;
     H.n_free = nfree0 - n_new + n_del;
@@ -1166,6 +1266,619 @@ __global__ void __launch_bounds__(NT) step_kernel(Dev g, const DT* __restrict__ 
     g.counts[s] = nout;
     g.stats[s] = H.st;
   }
+}
+
+// ---------------------------------------------------------------- enhanced step across CUs
+// The enhanced policy's step as two launches (one workgroup per stream left the per-track work --
+// update + analyze_motion_pattern, get_track_info -- serial on S CUs):
+//  assoc_kernel   one workgroup per stream: the predicted boxes (read-only, x' = F x), candidate
+//                 pairs through an x-bin index of the predicted boxes, the locally-dominant greedy
+//                 rounds, and every list decision of the step (kept / deleted / reported tracks,
+//                 new tracks and their slots, the compacted order, the free stack, the stats).
+//                 The decisions need only the counters that predict / update / mark_lost change
+//                 deterministically (age, time_since_update, hit_streak, is_lost), so this kernel
+//                 never waits for the per-track arithmetic.  It writes one work item per track:
+//                 {slot, matched detection, new-track number (-1: existing), output row (-1: none)}.
+//  tracks_kernel  ceil(T / IPB) workgroups per stream, one thread per work item: predict and
+//                 update or mark_lost (kf.py:184-317), or __init__ for a new track, then
+//                 get_track_info into its output row; the workgroup stages the updated tracks'
+//                 velocity rings and copies the trajectories cooperatively.
+// Candidate index: a pair whose x-intervals do not overlap has IoU exactly 0 in the reference's
+// arithmetic (iou_mixed: ix2 <= ix1), so for a threshold > 0 only tracks whose left edge lies in
+// [d.x1 - max_width - margin, d.x2 + margin] can be candidates of detection d.  Tracks are
+// counting-sorted by left edge into <= NB_MAX bins (monotone bin map); the pairs in the bin range
+// get the exact IoU test.  Non-finite boxes and thresholds <= 0 fall back to all pairs.
+
+__device__ __forceinline__ void lslot_bind(LSlot& l, Slot& g) {
+  l.vh = g.vh;
+  l.vang = g.vang;
+  l.th = g.th;
+}
+__device__ __forceinline__ void lslot_load(LSlot& l, Slot& g) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) l.x[i] = g.x[i];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) l.P[i] = g.P[i];
+  l.vavg[0] = g.vavg[0];
+  l.vavg[1] = g.vavg[1];
+  l.vstd[0] = g.vstd[0];
+  l.vstd[1] = g.vstd[1];
+  l.direction = g.direction;
+  l.speed = g.speed;
+  l.stability = g.stability;
+  l.pconf = g.pconf;
+  l.age = g.age;
+  l.hits = g.hits;
+  l.hit_streak = g.hit_streak;
+  l.tsu = g.tsu;
+  l.is_lost = g.is_lost;
+  l.lost_frames = g.lost_frames;
+  l.track_num = g.track_num;
+  l.max_lost = g.max_lost;
+  l.vh_len = g.vh_len;
+  l.vh_head = g.vh_head;
+  l.th_len = g.th_len;
+  l.th_head = g.th_head;
+  l.policy = g.policy;
+  lslot_bind(l, g);
+}
+__device__ __forceinline__ void lslot_store(const LSlot& l, Slot& g) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) g.x[i] = l.x[i];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) g.P[i] = l.P[i];
+  g.vavg[0] = l.vavg[0];
+  g.vavg[1] = l.vavg[1];
+  g.vstd[0] = l.vstd[0];
+  g.vstd[1] = l.vstd[1];
+  g.direction = l.direction;
+  g.speed = l.speed;
+  g.stability = l.stability;
+  g.pconf = l.pconf;
+  g.age = l.age;
+  g.hits = l.hits;
+  g.hit_streak = l.hit_streak;
+  g.tsu = l.tsu;
+  g.is_lost = l.is_lost;
+  g.lost_frames = l.lost_frames;
+  g.track_num = l.track_num;
+  g.max_lost = l.max_lost;
+  g.vh_len = l.vh_len;
+  g.vh_head = l.vh_head;
+  g.th_len = l.th_len;
+  g.th_head = l.th_head;
+  g.policy = l.policy;
+}
+
+constexpr int NB_MAX = NT - 1;  // x bins of the candidate index (+1 for the non-finite tracks <= NT)
+constexpr int IPB = 64;      // work items per tracks_kernel workgroup
+
+struct LdsA {
+  double* pb;                   // [T][4] predicted boxes by list position
+  double* det;                  // [D][4]
+  unsigned long long* row_max;  // [D]   (decisions: int newdet[D])
+  unsigned long long* col_max;  // [T]   (decisions: int flags[T])
+  double* red;                  // [16]  block reductions
+  int* det_match;               // [D]
+  int* trk_match;               // [T]
+  int* row_arg;                 // [D]
+  int* col_arg;                 // [T]   (candidate index: tracks sorted by bin)
+  int* order_tmp;               // [T]   pre-step order, then the work items' slots
+  int* bins;                    // [2][NB_MAX + 1] bin starts, scatter cursors
+  int* misc;                    // [32] counters; [16, 32) wave sums
+};
+constexpr int NTA = 1024;  // assoc_kernel threads: one element per thread in most phases
+constexpr int MA_WSUM = 16;
+
+__host__ __device__ inline size_t assoc_lds_bytes(int T, int D) {
+  return (size_t)T * 32 + (size_t)D * 32 + (size_t)D * 8 + (size_t)T * 8 + 16 * 8 + (size_t)D * 4 +
+         (size_t)T * 4 + (size_t)D * 4 + (size_t)T * 4 + (size_t)T * 4 + 2 * (NB_MAX + 1) * 4 + 32 * 4;
+}
+__host__ __device__ inline size_t tracks_lds_bytes() { return (size_t)IPB * STAGE_D * 8 + (size_t)IPB * 36 + 16; }
+
+__device__ LdsA carve_a(char* base, int T, int D) {
+  LdsA L;
+  L.pb = (double*)base;
+  base += (size_t)T * 32;
+  L.det = (double*)base;
+  base += (size_t)D * 32;
+  L.row_max = (unsigned long long*)base;
+  base += (size_t)D * 8;
+  L.col_max = (unsigned long long*)base;
+  base += (size_t)T * 8;
+  L.red = (double*)base;
+  base += 16 * 8;
+  L.det_match = (int*)base;
+  base += (size_t)D * 4;
+  L.trk_match = (int*)base;
+  base += (size_t)T * 4;
+  L.row_arg = (int*)base;
+  base += (size_t)D * 4;
+  L.col_arg = (int*)base;
+  base += (size_t)T * 4;
+  L.order_tmp = (int*)base;
+  base += (size_t)T * 4;
+  L.bins = (int*)base;
+  base += 2 * (NB_MAX + 1) * 4;
+  L.misc = (int*)base;
+  return L;
+}
+
+// block-wide min / max of one double per thread (every thread gets the result)
+template <int NTH>
+__device__ __forceinline__ double block_min(double v, double* red) {
+  constexpr int NW = NTH / 64;
+  for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  double r = red[0];
+#pragma unroll
+  for (int i = 1; i < NW; ++i) r = fmin(r, red[i]);
+  __syncthreads();
+  return r;
+}
+template <int NTH>
+__device__ __forceinline__ double block_max(double v, double* red) { return -block_min<NTH>(-v, red); }
+
+// exclusive prefix sum of v over the workgroup; total gets the block sum
+template <int NTH>
+__device__ __forceinline__ int block_excl_sum(int v, int* wsum, int& total) {
+  constexpr int NW = NTH / 64;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int x = v;
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) wsum[w] = x;
+  __syncthreads();
+  int base = 0, tot = 0;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) {
+    base += (i < w) ? wsum[i] : 0;
+    tot += wsum[i];
+  }
+  __syncthreads();
+  total = tot;
+  return base + x - v;
+}
+
+__device__ __forceinline__ int xbin(double x, double x0, double bw, int nb) {
+  const double q = (x - x0) / bw;  // monotone in x
+  return !(q > 0.0) ? 0 : (q >= (double)(nb - 1) ? nb - 1 : (int)q);
+}
+
+// Greedy association (multi:134-178) as locally-dominant rounds (header comment) over nc
+// candidates {IoU bits, (d << 16) | t}; inlined once with LDS and once with global operands.
+__device__ __forceinline__ void assoc_rounds(const LdsA& L, const unsigned long long* ckey, const int* cpid, int nc,
+                                             int D, int n, long long* round_out) {
+  const int tid = threadIdx.x;
+  for (int round = 0; round <= D + 1; ++round) {
+    for (int d = tid; d < D; d += NTA) {
+      L.row_max[d] = 0ull;
+      L.row_arg[d] = INT_MAX;
+    }
+    for (int t = tid; t < n; t += NTA) {
+      L.col_max[t] = 0ull;
+      L.col_arg[t] = INT_MAX;
+    }
+    if (tid == 0) L.misc[M_ACTIVE] = 0;
+    __syncthreads();
+    int local_active = 0;
+    for (int c = tid; c < nc; c += NTA) {
+      const int f = cpid[c], d = f >> 16, t = f & 0xffff;
+      if (L.det_match[d] < 0 && L.trk_match[t] < 0) {
+        const unsigned long long k = ckey[c];
+        atomicMax(&L.row_max[d], k);
+        atomicMax(&L.col_max[t], k);
+        ++local_active;
+      }
+    }
+    if (local_active) atomicAdd(&L.misc[M_ACTIVE], local_active);
+    __syncthreads();
+    if (L.misc[M_ACTIVE] == 0) {
+      if (tid == 0) *round_out = round;
+      break;
+    }
+    for (int c = tid; c < nc; c += NTA) {
+      const int f = cpid[c], d = f >> 16, t = f & 0xffff;
+      if (L.det_match[d] < 0 && L.trk_match[t] < 0) {
+        const unsigned long long k = ckey[c];
+        if (k == L.row_max[d]) atomicMin(&L.row_arg[d], f);
+        if (k == L.col_max[t]) atomicMin(&L.col_arg[t], f);
+      }
+    }
+    __syncthreads();
+    for (int c = tid; c < nc; c += NTA) {
+      const int f = cpid[c], d = f >> 16, t = f & 0xffff;
+      if (L.row_arg[d] == f && L.col_arg[t] == f) {
+        L.det_match[d] = t;
+        L.trk_match[t] = d;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+template <typename DT>
+__global__ void __launch_bounds__(NTA) assoc_kernel(Dev g, const DT* __restrict__ dets, int row_stride,
+                                                   const int* __restrict__ counts) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int s = blockIdx.x, tid = threadIdx.x;
+  const int T = g.T;
+  LdsA L = carve_a(smem, T, g.D);
+  Hdr& H = g.hdr[s];
+  const Slot* slots = g.slots + (size_t)s * T;
+  int* order = g.order + (size_t)s * T;
+  int* fstack = g.free_stack + (size_t)s * T;
+  int* wsum = L.misc + MA_WSUM;
+
+  const long long cyc0 = clock64();  // shader clock: phase[15] = cycles of this kernel (clock check)
+  if (tid == 0) g.phase[s * PH + 0] = wall_clock64();
+  int Draw = counts[s];
+  if (Draw < 0) Draw = 0;
+  const int D = Draw < g.D ? Draw : g.D;
+  const int n = H.n_tracks;
+  if (tid < 16) L.misc[tid] = 0;  // counters ([16, 32): wave sums)
+  for (int i = tid; i < D * 4; i += NTA) {
+    const int d = i >> 2, k = i & 3;
+    L.det[i] = (double)dets[((size_t)s * g.D + d) * row_stride + k];
+  }
+  for (int d = tid; d < D; d += NTA) L.det_match[d] = -1;
+  // predicted boxes: predict() (kf.py:192-201) then the bbox, without changing the slot
+  double lx0 = INFINITY, lx1 = -INFINITY, lw = 0.0;
+  for (int i = tid; i < n; i += NTA) {
+    const int slot = order[i];
+    L.order_tmp[i] = slot;
+    L.trk_match[i] = -1;
+    const Slot& sl = slots[slot];
+    double xp[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) xp[c] = sl.x[c] + sl.x[c + 4];
+    double* b = &L.pb[4 * i];
+    state_to_bbox(xp, b);
+    const double w = b[2] - b[0];
+    if (isfinite(b[0]) && isfinite(b[2]) && isfinite(w)) {
+      lx0 = fmin(lx0, b[0]);
+      lx1 = fmax(lx1, b[0]);
+      lw = fmax(lw, w);
+    }
+  }
+  __syncthreads();
+  if (tid == 0) g.phase[s * PH + 1] = wall_clock64();
+
+  int nc = 0;
+  if (D > 0 && n > 0) {
+    unsigned long long* ckey = g.cand_key + (size_t)s * g.C;
+    int* cflat = g.cand_flat + (size_t)s * g.C;
+    const double x0 = block_min<NTA>(lx0, L.red), x1 = block_max<NTA>(lx1, L.red), wmax = block_max<NTA>(lw, L.red);
+    const bool index = g.thr > 0.0 && x0 <= x1;  // else every pair is tested
+    const int nb = n < NB_MAX ? n : NB_MAX;
+    double bw = (x1 - x0) / (double)nb;
+    if (!(bw > 0.0) || !isfinite(bw)) bw = 1.0;
+    int* bstart = L.bins;                // [nb + 1]: bin starts, [nb] = finite tracks
+    int* bcur = L.bins + (NB_MAX + 1);
+    int* tsorted = L.col_arg;
+    int nfin = 0;
+    if (index) {
+      for (int b = tid; b <= nb; b += NTA) bstart[b] = 0;
+      __syncthreads();
+      for (int i = tid; i < n; i += NTA) {
+        const double* b = &L.pb[4 * i];
+        const bool fin = isfinite(b[0]) && isfinite(b[2]) && isfinite(b[2] - b[0]);
+        atomicAdd(&bstart[fin ? xbin(b[0], x0, bw, nb) : nb], 1);
+      }
+      __syncthreads();
+      int tot;
+      const int v = tid <= nb ? bstart[tid] : 0;  // nb + 1 <= NTA entries
+      const int ex = block_excl_sum<NTA>(v, wsum, tot);
+      if (tid <= nb) {
+        bstart[tid] = ex;
+        bcur[tid] = ex;
+      }
+      __syncthreads();
+      nfin = bstart[nb];
+      for (int i = tid; i < n; i += NTA) {
+        const double* b = &L.pb[4 * i];
+        const bool fin = isfinite(b[0]) && isfinite(b[2]) && isfinite(b[2] - b[0]);
+        tsorted[atomicAdd(&bcur[fin ? xbin(b[0], x0, bw, nb) : nb], 1)] = i;
+      }
+      __syncthreads();
+    }
+    // candidates (multi:180-232 over the pairs the index admits).  Detection d's pairs are the
+    // tracks [k0, k0 + len) of the bin order, then the non-finite tracks; the pairs of all
+    // detections are numbered by a prefix sum and every thread walks an equal slice of them
+    // (one binary search for its first detection), so one wide detection cannot stall a wave.
+    const double margin = 1.0 + 1e-9 * (fabs(x0) + fabs(x1) + wmax);
+    int* pk0 = (int*)L.row_max;  // [D] (row_max: 8 D bytes, free until the rounds)
+    int* plen = pk0 + D;         // [D]
+    int* pbeg = L.row_arg;       // [D] first pair number of each detection
+    const int ne = index ? n - nfin : 0;
+    int total = 0;
+    for (int base = 0; base < D; base += NTA) {
+      const int d = base + tid;
+      int cnt = 0;
+      if (d < D) {
+        int k0 = 0, k1 = n;  // all pairs
+        if (index) {
+          const double dx1 = L.det[4 * d], dx2 = L.det[4 * d + 2];
+          if (isfinite(dx1) && isfinite(dx2)) {
+            const double lo = (dx1 - wmax) - margin, hi = dx2 + margin;
+            const int b0 = isfinite(lo) ? xbin(lo, x0, bw, nb) : 0;
+            const int b1 = isfinite(hi) ? xbin(hi, x0, bw, nb) : nb - 1;
+            k0 = bstart[b0];
+            k1 = b1 >= b0 ? bstart[b1 + 1] : k0;
+          } else {
+            k1 = nfin;
+          }
+        }
+        pk0[d] = k0;
+        plen[d] = k1 - k0;
+        cnt = k1 - k0 + ne;
+      }
+      int tot;
+      const int ex = block_excl_sum<NTA>(cnt, wsum, tot);
+      if (d < D) pbeg[d] = total + ex;
+      total += tot;
+    }
+    __syncthreads();
+    {
+      const int per = (total + NTA - 1) / NTA;
+      int p = tid * per;
+      const int pend = p + per < total ? p + per : total;
+      if (p < pend) {
+        int lo = 0, hi = D - 1;  // the last detection whose pairs start at or before p
+        while (lo < hi) {
+          const int mid = (lo + hi + 1) >> 1;
+          if (pbeg[mid] <= p) lo = mid;
+          else hi = mid - 1;
+        }
+        int d = lo, beg = pbeg[d], k0 = pk0[d], len = plen[d];
+        DT db[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) db[k] = (DT)L.det[4 * d + k];
+        for (; p < pend; ++p) {
+          int o = p - beg;
+          while (o >= len + ne) {  // next detection with pairs
+            ++d;
+            beg = pbeg[d];
+            k0 = pk0[d];
+            len = plen[d];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) db[k] = (DT)L.det[4 * d + k];
+            o = p - beg;
+          }
+          const int kk = o < len ? k0 + o : nfin + (o - len);
+          const int t = index ? tsorted[kk] : kk;
+          const double v = iou_mixed<DT>(db, &L.pb[4 * t]);
+          if (v >= g.thr) {  // enhanced: iou >= thr (multi:245)
+            const int c = atomicAdd(&L.misc[M_NCAND], 1);
+            if (c < g.C) {
+              ckey[c] = (unsigned long long)__double_as_longlong(v);
+              cflat[c] = (d << 16) | t;  // orders like the row-major pair index d * n + t
+            }
+          }
+        }
+      }
+    }
+    __syncthreads();
+    if (tid == 0) {
+      g.phase[s * PH + 2] = wall_clock64();
+      g.phase[s * PH + 11] = total;
+      g.phase[s * PH + 12] = L.misc[M_NCAND];
+      g.phase[s * PH + 13] = (long long)(isfinite(wmax) ? wmax : -1.0);
+      g.phase[s * PH + 14] = n - nfin;
+    }
+    nc = L.misc[M_NCAND];
+    if (nc > g.C) {
+      if (tid == 0) L.misc[M_OVERFLOW] += nc - g.C;
+      nc = g.C;
+    }
+    // the rounds read the candidates from LDS when they fit where the boxes were (dead now)
+    const int cap = (int)(((size_t)T * 32 + (size_t)g.D * 32) / 12);
+    if (nc <= cap) {
+      unsigned long long* lk = (unsigned long long*)L.pb;
+      int* lp = (int*)(lk + nc);
+      for (int c = tid; c < nc; c += NTA) {
+        lk[c] = ckey[c];
+        lp[c] = cflat[c];
+      }
+      __syncthreads();
+      assoc_rounds(L, lk, lp, nc, D, n, g.phase + s * PH + 10);
+    } else {
+      assoc_rounds(L, ckey, cflat, nc, D, n, g.phase + s * PH + 10);
+    }
+  }
+  if (tid == 0) g.phase[s * PH + 3] = wall_clock64();
+
+  // Decisions.  Post-step counters of an existing track (predict, then update or mark_lost):
+  // age + 1; matched: tsu 0, hit_streak + 1, not lost; else tsu + 1, hit_streak 0, lost.
+  // flags: 1 kept (not should_delete, kf.py:385-405), 2 reported (multi:116-126), 4 reported with
+  // status 1 and time_since_update > 30 (long_term_predictions).
+  int* flags = (int*)L.col_max;
+  int* newdet = (int*)L.row_max;
+  const int fc = (int)H.st.frame_count + 1;
+  int recov = 0;
+  int2* items_vh = g.items_vh + (size_t)s * T;
+  for (int i = tid; i < n; i += NTA) {
+    const Slot& sl = slots[L.order_tmp[i]];
+    const bool m = L.trk_match[i] >= 0;
+    items_vh[i] = make_int2(sl.vh_len, sl.vh_head);
+    const int age = sl.age + 1, tsu = m ? 0 : sl.tsu + 1, hs = m ? sl.hit_streak + 1 : 0;
+    recov += (m && sl.is_lost) ? 1 : 0;
+    const bool del = tsu > g.max_lost || (age < 5 && hs == 0 && tsu > 15) || (age < 10 && hs <= 1 && tsu > 30);
+    const bool q = hs >= g.min_hits || fc <= g.min_hits || !m;
+    flags[i] = (del ? 0 : 1) | (q ? 2 : 0) | (tsu > 30 ? 4 : 0);
+  }
+  if (recov) atomicAdd(&L.misc[M_RECOVER], recov);
+  // new tracks for unmatched detections, ascending detection order (multi:92-101)
+  int n_new_total = 0;
+  const int next_num = (int)H.st.next_track_id;
+  const int nfree0 = H.n_free;
+  for (int base = 0; base < D; base += NTA) {
+    const int d = base + tid;
+    const int flag = (d < D && L.det_match[d] < 0) ? 1 : 0;
+    int tot;
+    const int r = n_new_total + block_scan<NTA>(flag, wsum, tot);
+    if (flag) {
+      const int pos = n + r;
+      if (pos < T && r < nfree0) {
+        L.order_tmp[pos] = fstack[nfree0 - 1 - r];
+        newdet[r] = d;
+        // a new track: age 0, hit_streak 1, tsu 0, not lost (kf.py:32-101)
+        flags[pos] = 1 | ((1 >= g.min_hits || fc <= g.min_hits) ? 2 : 0);
+      } else {
+        atomicAdd(&L.misc[M_OVERFLOW], 1);
+      }
+    }
+    n_new_total += tot;
+  }
+  int n_new = n_new_total;
+  if (n + n_new > T) n_new = T - n;
+  if (n_new > nfree0) n_new = nfree0;
+  __syncthreads();  // the popped slots are read before the deleted ones are pushed
+  // work items, the compacted order (kept tracks in list order), the free stack, output rows
+  const int n_all = n + n_new;
+  const int nfree_after_pop = nfree0 - n_new;
+  int kept = 0, nout = 0, pushed = 0, lt = 0;
+  int4* items = g.items + (size_t)s * T;
+  for (int base = 0; base < n_all; base += NTA) {
+    const int j = base + tid;
+    const int f = j < n_all ? flags[j] : 0;
+    const int keep = f & 1, q = (f >> 1) & keep, del = (j < n && !keep) ? 1 : 0;
+    int tk, tq, td;
+    const int rk = kept + block_scan<NTA>(keep, wsum, tk);
+    const int rq = nout + block_scan<NTA>(q, wsum, tq);
+    const int rd = pushed + block_scan<NTA>(del, wsum, td);
+    if (j < n_all) {
+      const int slot = L.order_tmp[j];
+      if (keep) order[rk] = slot;
+      if (del) fstack[nfree_after_pop + rd] = slot;
+      if (q && (f & 4)) ++lt;
+      items[j] = make_int4(slot, j < n ? L.trk_match[j] : newdet[j - n], j < n ? -1 : next_num + (j - n), q ? rq : -1);
+    }
+    kept += tk;
+    nout += tq;
+    pushed += td;
+  }
+  if (lt) atomicAdd(&L.misc[M_LONGTERM], lt);
+  __syncthreads();
+  if (tid == 0) {
+    const long long t4 = wall_clock64();
+    for (int k = 4; k < 8; ++k) g.phase[s * PH + k] = t4;
+    g.phase[s * PH + 15] = clock64() - cyc0;
+    g.n_items[s] = n_all;
+    H.n_tracks = kept;
+    H.n_free = nfree_after_pop + pushed;
+    H.st.frame_count = fc;
+    H.st.next_track_id += n_new;
+    H.st.total_tracks_created += n_new;
+    H.st.total_tracks_terminated += pushed;
+    H.st.current_active_tracks = kept;
+    H.st.long_term_predictions += L.misc[M_LONGTERM];
+    H.st.successful_recoveries += L.misc[M_RECOVER];
+    H.st.overflow += L.misc[M_OVERFLOW] + (Draw - D);
+    g.counts[s] = nout;
+    g.stats[s] = H.st;
+  }
+}
+
+template <typename DT>
+__global__ void __launch_bounds__(NT) tracks_kernel(Dev g, const DT* __restrict__ dets, int row_stride) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int s = blockIdx.y, tid = threadIdx.x;
+  const int base = blockIdx.x * IPB;
+  const int nI = g.n_items[s];
+  if (base >= nI) return;
+  const int m = nI - base < IPB ? nI - base : IPB;
+  double* stage = (double*)smem;                           // [IPB][STAGE_D]
+  int4* it = (int4*)(smem + (size_t)IPB * STAGE_D * 8);    // [IPB]
+  int2* ivh = (int2*)(it + IPB);  // [IPB] {vh_len, vh_head} before the step, then {th_len, th_head} after it
+  int* lst = (int*)(ivh + IPB);   // [3][IPB] the block's items by path: update, lost, new
+  int* lcnt = lst + 3 * IPB;      // [3]
+  Slot* slots = g.slots + (size_t)s * g.T;
+  if (blockIdx.x == 0 && tid == 0) g.phase[s * PH + 5] = wall_clock64();
+  if (tid < m) {
+    it[tid] = g.items[(size_t)s * g.T + base + tid];
+    ivh[tid] = g.items_vh[(size_t)s * g.T + base + tid];
+  }
+  if (tid < 3) lcnt[tid] = 0;
+  __syncthreads();
+  // one path per wave (a wave runs every path its lanes take, one after the other)
+  if (tid < m) {
+    const int4 w = it[tid];
+    const int path = w.z >= 0 ? 2 : (w.y >= 0 ? 0 : 1);
+    lst[path * IPB + atomicAdd(&lcnt[path], 1)] = tid;
+  }
+  // chronological copy of each updated track's velocity ring (whole workgroup, independent loads)
+  for (int u = tid; u < m * VH; u += NT) {
+    const int j = u / VH, k = u - j * VH;
+    const int4 w = it[j];
+    if (w.z >= 0 || w.y < 0) continue;
+    const Slot& sl = slots[w.x];
+    const int2 vl = ivh[j];
+    if (k < vl.x) {
+      int idx = vl.y + k;
+      if (idx >= VH) idx -= VH;
+      const double2 v = *(const double2*)&sl.vh[idx][0];
+      double* st = stage + (size_t)j * STAGE_D;
+      st[k] = v.x;
+      st[VS + k] = v.y;
+      st[2 * VS + k] = sl.vang[idx];
+    }
+  }
+  __syncthreads();
+  if (blockIdx.x == 0 && tid == 0) g.phase[s * PH + 8] = wall_clock64();
+  const int wv = tid >> 6, ln = tid & 63;
+  const long long cw0 = clock64();
+  if (wv < 3 && ln < lcnt[wv]) {
+    const int j = lst[wv * IPB + ln];
+    const int4 w = it[j];
+    Slot& gs = slots[w.x];
+    LSlot sl;
+    if (w.z < 0) {
+      lslot_load(sl, gs);
+      kf_predict(sl);  // multi:55-58
+      if (w.y >= 0) {  // multi:71-80
+        DT db[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) db[k] = dets[((size_t)s * g.D + w.y) * row_stride + k];
+        kf_update<DT>(sl, db, stage + (size_t)j * STAGE_D);
+      } else {
+        mark_lost(sl);  // multi:83-89
+      }
+    } else {  // multi:92-101
+      DT db[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) db[k] = dets[((size_t)s * g.D + w.y) * row_stride + k];
+      double z[4];
+      bbox_to_state<DT>(db, z);
+      lslot_bind(sl, gs);
+      slot_init(sl, z, w.z, g.max_lost);
+    }
+    if (w.w >= 0) track_info(sl, g.rows[(size_t)s * g.T + w.w], false);
+    lslot_store(sl, gs);
+    ivh[j] = make_int2(sl.th_len, sl.th_head);
+  }
+  if (blockIdx.x == 0 && ln == 0 && wv < 3) g.phase[s * PH + 16 + wv] = clock64() - cw0;
+  __syncthreads();
+  if (blockIdx.x == 0 && tid == 0) g.phase[s * PH + 9] = wall_clock64();
+  for (int u = tid; u < m * TOUT; u += NT) {
+    const int j = u / TOUT, k = u - j * TOUT;
+    const int4 w = it[j];
+    if (w.w < 0) continue;
+    const Slot& sl = slots[w.x];
+    const int2 tl = ivh[j];  // th_len, th_head after the step
+    const int nt = tl.x < TOUT ? tl.x : TOUT;
+    double2 v = make_double2(0.0, 0.0);
+    if (k < nt) {
+      int idx = tl.y + (tl.x - nt) + k;
+      if (idx >= TH) idx -= TH;
+      v = *(const double2*)&sl.th[idx][0];
+    }
+    *(double2*)&g.rows[(size_t)s * g.T + w.w].traj[k][0] = v;
+  }
+  if (blockIdx.x == 0 && tid == 0) g.phase[s * PH + 6] = wall_clock64();
 }
 
 __global__ void reset_kernel(Dev g, int S) {
@@ -1314,6 +2027,8 @@ struct yk_tracker {
   yk_tracker_cfg cfg;
   Dev dev;
   size_t lds;
+  size_t lds_assoc;
+  bool split;  // enhanced policy on assoc_kernel + tracks_kernel (else one workgroup per stream)
   yk_track_state* d_snap;
   yk_track_out* d_row1;
   double* d_box;  // [8]: in[4], out[4]
@@ -1362,8 +2077,11 @@ int yk_tracker_create(yk_ctx* ctx, int n_streams, const yk_tracker_cfg* cfg, yk_
   if (e == hipSuccess) e = hipMemset(g.rows, 0, S * T * sizeof(yk_track_out));
   A((void**)&g.counts, S * sizeof(int));
   A((void**)&g.stats, S * sizeof(yk_tracker_stats));
-  A((void**)&g.phase, S * 16 * sizeof(long long));
-  if (e == hipSuccess) e = hipMemset(g.phase, 0, S * 16 * sizeof(long long));
+  A((void**)&g.items, S * T * sizeof(int4));
+  A((void**)&g.items_vh, S * T * sizeof(int2));
+  A((void**)&g.n_items, S * sizeof(int));
+  A((void**)&g.phase, S * yk::trk::PH * sizeof(long long));
+  if (e == hipSuccess) e = hipMemset(g.phase, 0, S * yk::trk::PH * sizeof(long long));
   A((void**)&t->d_snap, T * sizeof(yk_track_state));
   A((void**)&t->d_row1, sizeof(yk_track_out));
   if (e == hipSuccess) e = hipMemset(t->d_row1, 0, sizeof(yk_track_out));
@@ -1384,6 +2102,22 @@ int yk_tracker_create(yk_ctx* ctx, int n_streams, const yk_tracker_cfg* cfg, yk_
                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) {
     (void)hipGetLastError();
   }
+  // enhanced policy: the two-launch step unless its LDS does not fit or YK_TRK_SINGLE=1
+  t->lds_assoc = yk::trk::assoc_lds_bytes(cfg->max_tracks, cfg->max_dets);
+  const char* single = getenv("YK_TRK_SINGLE");
+  t->split = cfg->policy == YK_POLICY_ENHANCED && t->lds_assoc <= 160 * 1024 && !(single && single[0] == '1');
+  if (t->split) {
+    const int la = (int)t->lds_assoc, lt = (int)yk::trk::tracks_lds_bytes();
+    if (hipFuncSetAttribute((const void*)yk::trk::assoc_kernel<float>, hipFuncAttributeMaxDynamicSharedMemorySize, la) !=
+            hipSuccess ||
+        hipFuncSetAttribute((const void*)yk::trk::assoc_kernel<double>, hipFuncAttributeMaxDynamicSharedMemorySize, la) !=
+            hipSuccess ||
+        hipFuncSetAttribute((const void*)yk::trk::tracks_kernel<float>, hipFuncAttributeMaxDynamicSharedMemorySize, lt) !=
+            hipSuccess ||
+        hipFuncSetAttribute((const void*)yk::trk::tracks_kernel<double>, hipFuncAttributeMaxDynamicSharedMemorySize, lt) !=
+            hipSuccess)
+      (void)hipGetLastError();
+  }
   int rc = yk_tracker_reset(t, nullptr);
   if (rc != YK_OK) {
     yk_tracker_destroy(t);
@@ -1399,7 +2133,7 @@ int yk_tracker_destroy(yk_tracker* t) {
   yk::DeviceGuard guard(t->ctx->device);
   Dev& g = t->dev;
   void* ptrs[] = {g.slots, g.hdr, g.order, g.free_stack, g.cand_key, g.cand_flat, g.rows,
-                  g.counts, g.stats, g.phase, t->d_snap, t->d_row1, t->d_box, t->d_status};
+                  g.counts, g.stats, g.items, g.items_vh, g.n_items, g.phase, t->d_snap, t->d_row1, t->d_box, t->d_status};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   delete t;
@@ -1421,6 +2155,24 @@ int yk_tracker_step(yk_tracker* t, const void* dets, int dtype, int row_stride, 
   YK_CHECK_ARG(dtype == YK_F32 || dtype == YK_F64, "yk_tracker_step: dtype must be YK_F32 or YK_F64");
   yk::DeviceGuard guard(t->ctx->device);
   const bool mr = t->cfg.policy == YK_POLICY_MOTION_RESET;
+  if (t->split) {
+    const dim3 g2((t->dev.T + yk::trk::IPB - 1) / yk::trk::IPB, t->S);
+    const size_t l2 = yk::trk::tracks_lds_bytes();
+    hipStream_t st = (hipStream_t)stream;
+    if (dtype == YK_F32) {
+      hipLaunchKernelGGL((yk::trk::assoc_kernel<float>), dim3(t->S), dim3(yk::trk::NTA), t->lds_assoc, st, t->dev,
+                         (const float*)dets, row_stride, counts);
+      hipLaunchKernelGGL((yk::trk::tracks_kernel<float>), g2, dim3(yk::trk::NT), l2, st, t->dev, (const float*)dets,
+                         row_stride);
+    } else {
+      hipLaunchKernelGGL((yk::trk::assoc_kernel<double>), dim3(t->S), dim3(yk::trk::NTA), t->lds_assoc, st, t->dev,
+                         (const double*)dets, row_stride, counts);
+      hipLaunchKernelGGL((yk::trk::tracks_kernel<double>), g2, dim3(yk::trk::NT), l2, st, t->dev, (const double*)dets,
+                         row_stride);
+    }
+    YK_HIP(hipGetLastError());
+    return YK_OK;
+  }
   if (dtype == YK_F32) {
     if (mr)
       hipLaunchKernelGGL((yk::trk::step_kernel<float, 1>), dim3(t->S), dim3(yk::trk::NT), t->lds,
@@ -1543,13 +2295,13 @@ int yk_track_create(yk_tracker* t, int s, const double* box, int dtype, int32_t 
   return YK_OK;
 }
 
-int yk_tracker_phase_ticks(yk_tracker* t, int s, int64_t* host_ticks16, void* stream) {
-  YK_CHECK_ARG(t && host_ticks16, "yk_tracker_phase_ticks: NULL argument");
+int yk_tracker_phase_ticks(yk_tracker* t, int s, int64_t* host_ticks, void* stream) {
+  YK_CHECK_ARG(t && host_ticks, "yk_tracker_phase_ticks: NULL argument");
   YK_CHECK_ARG(s >= 0 && s < t->S, "yk_tracker_phase_ticks: stream index out of range");
   yk::DeviceGuard guard(t->ctx->device);
   hipStream_t st = (hipStream_t)stream;
-  YK_HIP(hipMemcpyAsync(host_ticks16, t->dev.phase + (size_t)s * 16, 16 * sizeof(long long), hipMemcpyDeviceToHost,
-                        st));
+  YK_HIP(hipMemcpyAsync(host_ticks, t->dev.phase + (size_t)s * yk::trk::PH, yk::trk::PH * sizeof(long long),
+                        hipMemcpyDeviceToHost, st));
   YK_HIP(hipStreamSynchronize(st));
   return YK_OK;
 }

@@ -216,13 +216,24 @@ class MultiStreamTracker:
         return rows.value, counts.value, stats.value
 
     def phase_us(self, stream_index: int = 0):
-        """Per-phase device time (µs) of the last step on one stream: predict, candidates,
-        rounds, update, create, delete, outputs; plus the association rounds used."""
-        t = np.zeros(16, np.int64)
+        """Per-phase device time (µs) of the last step on one stream (wall clock of the stream's
+        workgroup) and the association rounds used.  Single-workgroup step: predict, candidates,
+        rounds, update, create, delete, outputs.  Two-launch enhanced step: predict = predicted
+        boxes, candidates = bin index + candidate pairs (pairs_tested / n_cand / max_width /
+        n_nonfinite describe the index), rounds, update = the list decisions, create = the gap to
+        the start of tracks_kernel's first workgroup, delete = that workgroup's duration."""
+        t = np.zeros(32, np.int64)
         L.check(L.lib().yk_tracker_phase_ticks(self._h, int(stream_index), L.ptr(t), L.current_stream(self.device)),
                 "yk_tracker_phase_ticks")
         names = ["predict", "candidates", "rounds", "update", "create", "delete", "outputs"]
-        return {n: float(t[k + 1] - t[k]) / 100.0 for k, n in enumerate(names)} | {"n_rounds": int(t[10])}
+        return {n: float(t[k + 1] - t[k]) / 100.0 for k, n in enumerate(names)} | {
+            "n_rounds": int(t[10]), "pairs_tested": int(t[11]), "n_cand": int(t[12]), "max_width": int(t[13]),
+            "n_nonfinite": int(t[14]),
+            "k2_stage_us": float(t[8] - t[5]) / 100.0 if t[8] else 0.0,
+            "k2_compute_us": float(t[9] - t[8]) / 100.0 if t[9] else 0.0,
+            "k2_traj_us": float(t[6] - t[9]) / 100.0 if t[9] else 0.0,
+            "k2_wave_cycles": [int(t[16 + k]) for k in range(4)],
+            "assoc_clock_mhz": round(float(t[15]) / max(float(t[4] - t[0]) / 100.0, 1e-9), 1)}
 
     def snapshot(self, stream_index: int = 0) -> np.ndarray:
         out = np.zeros(self.max_tracks, dtype=L.TRACK_STATE_DTYPE)
