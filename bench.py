@@ -208,7 +208,7 @@ def tracker_roofline(pipe, reps=20):
     us = e0.elapsed_time(e1) * 1e3 / reps
     by = live * TRACK_STEP_BYTES
     gbps = by / (us * 1e-6) / 1e9 if us > 0 else 0.0
-    return {"kernel": "step_kernel", "bound": "hbm", "avg_launch_us": round(us, 2), "live_tracks": live,
+    return {"kernel": "assoc_kernel + tracks_kernel", "bound": "hbm", "avg_launch_us": round(us, 2), "live_tracks": live,
             "achieved": round(gbps, 3), "peak": HBM_PEAK, "unit": "GB/s", "frac": round(gbps / HBM_PEAK, 6)}
 
 

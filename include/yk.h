@@ -197,7 +197,7 @@ int yk_track_op(yk_tracker* trk, int stream_index, int pos, int op, int arg, con
 
 /* sizeof() of the ABI structs, for bindings that mirror them (0: yk_tracker_cfg,
  * 1: yk_tracker_stats, 2: yk_track_out, 3: yk_track_state, 4: yk_view, 5: yk_op,
- * 6: yk_model_desc); -1 for an unknown id. */
+ * 6: yk_model_desc, 7: yk_bt_cfg); -1 for an unknown id. */
 int64_t yk_struct_size(int which);
 
 /* Append a new track created from a box (AircraftKalmanTracker.__init__, :23-101) to the
@@ -205,6 +205,42 @@ int64_t yk_struct_size(int which);
 int yk_track_create(yk_tracker* trk, int stream_index, const double* host_bbox, int dtype,
                     int32_t track_num, int32_t max_lost_frames, void* stream);
 
+
+/* ------------------------------------------------------------------ ByteTrack / BoT-SORT
+ * Replaces the upstream model.track() trackers for this path:
+ * BYTETracker.update (ultralytics/trackers/byte_tracker.py:299-410) and BOTSORT.update without
+ * ReID / GMC (trackers/bot_sort.py:156-249), KalmanFilterXYAH / XYWH (trackers/utils/
+ * kalman_filter.py), matching.iou_distance / fuse_score / linear_assignment (trackers/utils/
+ * matching.py:20-157, scipy branch).  One tracker object holds n_streams independent trackers
+ * that share one track-id counter (BaseTrack._count, basetrack.py:67-92): each step, stream 0's
+ * new tracks get ids first, then stream 1's, ...  Thresholds compare in float32 like the
+ * reference's float32 scores. */
+enum yk_bt_kind { YK_BT_BYTETRACK = 0, YK_BT_BOTSORT = 1 };
+typedef struct yk_bt_cfg {
+  int32_t kind;              /* yk_bt_kind (cfg tracker_type)                           */
+  float track_high_thresh;   /* bytetrack.yaml / botsort.yaml defaults: 0.25           */
+  float track_low_thresh;    /* 0.1                                                    */
+  float new_track_thresh;    /* 0.25                                                   */
+  float match_thresh;        /* 0.8                                                    */
+  int32_t track_buffer;      /* 30; max_time_lost = int(frame_rate / 30 * track_buffer) */
+  int32_t frame_rate;        /* 30                                                     */
+  int32_t fuse_score;        /* 1                                                      */
+  int32_t max_tracks;        /* tracked + lost tracks per stream (<= 1024)             */
+  int32_t max_dets;          /* detections per stream and frame (<= 1024)              */
+} yk_bt_cfg;
+typedef struct yk_bt yk_bt;
+int yk_bt_create(yk_ctx* ctx, int n_streams, const yk_bt_cfg* cfg, yk_bt** out);
+int yk_bt_destroy(yk_bt* bt);
+/* BYTETracker.reset() of every stream, the shared id counter included (reset_id). */
+int yk_bt_reset(yk_bt* bt, void* stream);
+/* One update() of every stream.  dev_dets: [n_streams][max_dets][6] float32 rows x1 y1 x2 y2
+ * conf cls (Boxes.data), dev_counts: [n_streams] rows used.  Asynchronous on `stream`. */
+int yk_bt_step(yk_bt* bt, const float* dev_dets, const int32_t* dev_counts, void* stream);
+/* Device outputs of the last step: rows [n_streams][max_tracks][8] float32 = the reference's
+ * result rows (x1 y1 x2 y2 track_id score cls idx) in tracked_stracks order; counts [n_streams]. */
+int yk_bt_outputs(yk_bt* bt, float** dev_rows, int32_t** dev_counts);
+/* Copy counts (and rows when host_rows != NULL) to the host; synchronises `stream`. */
+int yk_bt_download(yk_bt* bt, float* host_rows, int32_t* host_counts, void* stream);
 
 /* ------------------------------------------------------------------ detector
  * Replaces YOLO.predict() for the detection models this path uses

@@ -35,6 +35,17 @@ class TrackerCfg(C.Structure):
 
 POLICY_ENHANCED, POLICY_MOTION_RESET = 0, 1
 
+
+class BtCfg(C.Structure):
+    """yk_bt_cfg (ByteTrack / BoT-SORT)."""
+    _fields_ = [("kind", C.c_int32), ("track_high_thresh", C.c_float), ("track_low_thresh", C.c_float),
+                ("new_track_thresh", C.c_float), ("match_thresh", C.c_float), ("track_buffer", C.c_int32),
+                ("frame_rate", C.c_int32), ("fuse_score", C.c_int32), ("max_tracks", C.c_int32),
+                ("max_dets", C.c_int32)]
+
+
+BT_BYTETRACK, BT_BOTSORT = 0, 1
+
 STATS_DTYPE = np.dtype([(k, np.int64) for k in (
     "frame_count", "next_track_id", "total_tracks_created", "total_tracks_terminated",
     "current_active_tracks", "long_term_predictions", "successful_recoveries", "overflow",
@@ -96,6 +107,12 @@ _SIGS = {
     "yk_model_autotune": ([_vp, _vp, C.c_int, C.c_float, C.c_int, _vp], C.c_int),
     "yk_model_get_schedule": ([_vp, _vp, _vp], C.c_int),
     "yk_model_get_plan": ([_vp, _vp, _vp], C.c_int),
+    "yk_bt_create": ([_vp, C.c_int, C.POINTER(BtCfg), C.POINTER(_vp)], C.c_int),
+    "yk_bt_destroy": ([_vp], C.c_int),
+    "yk_bt_reset": ([_vp, _vp], C.c_int),
+    "yk_bt_step": ([_vp, _vp, _vp, _vp], C.c_int),
+    "yk_bt_outputs": ([_vp, C.POINTER(_vp), C.POINTER(_vp)], C.c_int),
+    "yk_bt_download": ([_vp, _vp, _vp, _vp], C.c_int),
 }
 
 _lock = threading.Lock()

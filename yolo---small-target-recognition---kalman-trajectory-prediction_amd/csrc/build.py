@@ -31,6 +31,7 @@ SOURCES = [
     ("yk_capi.cpp", []),
     ("tracker.hip", ["-ffp-contract=off"]),
     ("detector.hip", []),
+    ("bytetrack.hip", ["-ffp-contract=off"]),
 ]
 HEADERS = ["yk_internal.h", os.path.join("..", "..", "include", "yk.h")]
 

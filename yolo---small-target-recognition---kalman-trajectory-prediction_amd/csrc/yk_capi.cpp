@@ -35,6 +35,7 @@ int64_t yk_struct_size(int which) {
     case 4: return (int64_t)sizeof(yk_view);
     case 5: return (int64_t)sizeof(yk_op);
     case 6: return (int64_t)sizeof(yk_model_desc);
+    case 7: return (int64_t)sizeof(yk_bt_cfg);
     default: return -1;
   }
 }
