@@ -312,6 +312,16 @@ int yk_model_create(yk_ctx* ctx, const yk_model_desc* desc, const void* host_blo
                     yk_model** out);
 int yk_model_destroy(yk_model* m);
 
+/* Load a packed detector program ("engine" file) and create the model from it: what a C / Go /
+ * Java host calls instead of building the program in Python.  The file is written once by
+ * model.Program.export_engine (tools/export_engine.py: from an ultralytics checkpoint or a
+ * state dict + the model YAML, for one frame size / dtype / max_batch, optionally with a tuned
+ * conv plan).  Layout, little-endian: "YKENGINE", int32 version (1), sizeof(yk_model_desc),
+ * sizeof(yk_op), n_bufs, n_ops, plan_batch, n_plan, pad, int64 blob_bytes; the yk_model_desc
+ * (pointer fields ignored); int64 buf_elems[n_bufs]; yk_op ops[n_ops]; the blob; int32
+ * plan[n_plan][4] = {op, kind, nnt, npt} applied with yk_model_set_plan at plan_batch. */
+int yk_model_load(yk_ctx* ctx, const char* path, yk_model** out);
+
 /* One predict() over `batch` frames resident in HBM (dev_frames: batch x frame_h x frame_w x 3
  * uint8 BGR).  Writes dev_dets[batch][max_det][6] = x1,y1,x2,y2,conf,cls (original-image pixels,
  * like Results.boxes.data) and dev_counts[batch].  NULL outputs use the model's own buffers

@@ -107,6 +107,7 @@ _SIGS = {
     "yk_model_autotune": ([_vp, _vp, C.c_int, C.c_float, C.c_int, _vp], C.c_int),
     "yk_model_get_schedule": ([_vp, _vp, _vp], C.c_int),
     "yk_model_get_plan": ([_vp, _vp, _vp], C.c_int),
+    "yk_model_load": ([_vp, C.c_char_p, C.POINTER(_vp)], C.c_int),
     "yk_bt_create": ([_vp, C.c_int, C.POINTER(BtCfg), C.POINTER(_vp)], C.c_int),
     "yk_bt_destroy": ([_vp], C.c_int),
     "yk_bt_reset": ([_vp, _vp], C.c_int),

@@ -1,4 +1,8 @@
-// Context handling and error reporting of the C ABI (include/yk.h).
+// Context handling, error reporting and the engine-file loader of the C ABI (include/yk.h).
+#include <cstring>
+#include <fstream>
+#include <vector>
+
 #include "yk_internal.h"
 
 namespace yk {
@@ -48,6 +52,53 @@ int yk_memcpy_d2h(void* host_dst, const void* dev_src, int64_t bytes) {
 
 int yk_ctx_destroy(yk_ctx* ctx) {
   delete ctx;
+  return YK_OK;
+}
+
+// Engine file (yk.h, yk_model_load): a program packed once by model.Program.export_engine.
+int yk_model_load(yk_ctx* ctx, const char* path, yk_model** out) {
+  YK_CHECK_ARG(ctx && path && out, "yk_model_load: NULL argument");
+  std::ifstream f(path, std::ios::binary);
+  YK_CHECK_ARG(f.good(), std::string("yk_model_load: cannot open ") + path);
+  struct Head {
+    char magic[8];
+    int32_t version, sizeof_desc, sizeof_op, n_bufs, n_ops, plan_batch, n_plan, pad;
+    int64_t blob_bytes;
+  } h{};
+  f.read((char*)&h, sizeof h);
+  YK_CHECK_ARG(f.good() && std::memcmp(h.magic, "YKENGINE", 8) == 0, "yk_model_load: not a YKENGINE file");
+  YK_CHECK_ARG(h.version == 1, "yk_model_load: unsupported engine version");
+  YK_CHECK_ARG(h.sizeof_desc == (int32_t)sizeof(yk_model_desc) && h.sizeof_op == (int32_t)sizeof(yk_op),
+               "yk_model_load: engine written for another ABI (struct sizes differ)");
+  YK_CHECK_ARG(h.n_bufs > 0 && h.n_bufs < (1 << 16) && h.n_ops > 0 && h.n_ops < (1 << 16) && h.blob_bytes > 0 &&
+                   h.n_plan >= 0 && h.n_plan <= h.n_ops,
+               "yk_model_load: corrupt engine header");
+  yk_model_desc d{};
+  f.read((char*)&d, sizeof d);
+  std::vector<int64_t> bufs(h.n_bufs);
+  std::vector<yk_op> ops(h.n_ops);
+  std::vector<char> blob((size_t)h.blob_bytes);
+  std::vector<int32_t> plan((size_t)h.n_plan * 4);
+  f.read((char*)bufs.data(), (std::streamsize)(bufs.size() * sizeof(int64_t)));
+  f.read((char*)ops.data(), (std::streamsize)(ops.size() * sizeof(yk_op)));
+  f.read(blob.data(), (std::streamsize)blob.size());
+  if (h.n_plan) f.read((char*)plan.data(), (std::streamsize)(plan.size() * sizeof(int32_t)));
+  YK_CHECK_ARG(f.good(), "yk_model_load: truncated engine file");
+  YK_CHECK_ARG(d.n_bufs == h.n_bufs && d.n_ops == h.n_ops, "yk_model_load: header / descriptor mismatch");
+  d.buf_elems = bufs.data();
+  d.ops = ops.data();
+  yk_model* m = nullptr;
+  const int rc = yk_model_create(ctx, &d, blob.data(), h.blob_bytes, &m);
+  if (rc != YK_OK) return rc;
+  for (int32_t i = 0; i < h.n_plan; ++i) {
+    const int32_t* p = &plan[(size_t)i * 4];
+    const int r = yk_model_set_plan(m, p[0], h.plan_batch, p[1], p[2], p[3]);
+    if (r != YK_OK) {
+      yk_model_destroy(m);
+      return r;
+    }
+  }
+  *out = m;
   return YK_OK;
 }
 

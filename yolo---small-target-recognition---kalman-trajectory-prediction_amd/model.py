@@ -430,6 +430,63 @@ class Program:
         return d
 
 
+    def export_engine(self, path: str, plan=None, plan_batch: int = 0) -> None:
+        """Write this program as an engine file (include/yk.h, yk_model_load): a C host creates
+        the model from it without Python.  plan: get_plan()-style [[kind, nnt, npt], ...] per op
+        (kind -1 entries are skipped), applied at plan_batch."""
+        import struct
+
+        d = self.desc()
+        raw = ModelDesc.from_buffer_copy(bytes(d))
+        raw.buf_elems = None
+        raw.ops = None
+        entries = []
+        if plan is not None:
+            for i, (kind, nnt, npt) in enumerate(plan):
+                if kind >= 0 and self.ops[i].kind == YK_K_CONV:
+                    entries.append((i, int(kind), int(nnt), int(npt)))
+        if entries and not 1 <= plan_batch <= self.max_batch:
+            raise ValueError(f"plan_batch must be in [1, {self.max_batch}]")
+        head = struct.pack("<8s8iq", b"YKENGINE", 1, C.sizeof(ModelDesc), C.sizeof(Op), len(self.buf_elems),
+                           len(self.ops), int(plan_batch), len(entries), 0, len(self.blob))
+        with open(path, "wb") as f:
+            f.write(head)
+            f.write(bytes(raw))
+            f.write(np.asarray(self.buf_elems, np.int64).tobytes())
+            f.write(bytes((Op * len(self.ops))(*self.ops)))
+            f.write(bytes(self.blob))
+            if entries:
+                f.write(np.asarray(entries, np.int32).tobytes())
+
+
+class EngineModel:
+    """A model created from an engine file by the library itself (yk_model_load): no Program on
+    the Python side; frame size and batch come from the file."""
+
+    def __init__(self, path: str, device: int = 0):
+        self.device = int(device)
+        h = C.c_void_p()
+        L.check(L.lib().yk_model_load(L.context(self.device), str(path).encode(), C.byref(h)), "yk_model_load")
+        self._h = h
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            try:
+                L.lib().yk_model_destroy(h)
+            except Exception:
+                pass
+            self._h = None
+
+    def detect(self, frames: torch.Tensor, conf=0.25, iou=0.7, max_det=300):
+        B = frames.shape[0]
+        dets = torch.empty((B, max_det, 6), dtype=torch.float32, device=frames.device)
+        counts = torch.empty(B, dtype=torch.int32, device=frames.device)
+        L.check(L.lib().yk_detect(self._h, L.ptr(frames), int(B), C.c_float(conf), C.c_float(iou), int(max_det),
+                                  L.ptr(dets), L.ptr(counts), L.current_stream(self.device)), "yk_detect")
+        return dets, counts
+
+
 class DeviceModel:
     """A Program instantiated on one GPU (yk_model)."""
 
