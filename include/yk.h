@@ -91,6 +91,8 @@ typedef struct {
   int64_t overflow; /* detections/tracks dropped because a capacity was hit (0 in parity runs) */
   int64_t individual_resets;   /* YK_POLICY_MOTION_RESET: stats['individual_resets']   */
   int64_t tracking_recoveries; /* YK_POLICY_MOTION_RESET: stats['tracking_recoveries'] */
+  int64_t global_motion_events;/* YK_POLICY_MOTION_RESET: stats['global_motion_events'] */
+  int64_t global_resets;       /* YK_POLICY_MOTION_RESET: stats['global_resets']        */
 } yk_tracker_stats;
 
 /* One output row = one reference get_track_info() dict
@@ -197,7 +199,7 @@ int yk_track_op(yk_tracker* trk, int stream_index, int pos, int op, int arg, con
 
 /* sizeof() of the ABI structs, for bindings that mirror them (0: yk_tracker_cfg,
  * 1: yk_tracker_stats, 2: yk_track_out, 3: yk_track_state, 4: yk_view, 5: yk_op,
- * 6: yk_model_desc, 7: yk_bt_cfg); -1 for an unknown id. */
+ * 6: yk_model_desc, 7: yk_bt_cfg, 8: yk_motion, 9: yk_gmd_stats); -1 for an unknown id. */
 int64_t yk_struct_size(int which);
 
 /* Append a new track created from a box (AircraftKalmanTracker.__init__, :23-101) to the
@@ -205,6 +207,66 @@ int64_t yk_struct_size(int which);
 int yk_track_create(yk_tracker* trk, int stream_index, const double* host_bbox, int dtype,
                     int32_t track_num, int32_t max_lost_frames, void* stream);
 
+
+/* ------------------------------------------------------------------ global camera motion
+ * Replaces GlobalMotionDetector(method='optical_flow').detect_motion(frame)
+ * (camera_motion_compensation/global_motion_detector.py:67-169, 241-261) for n_streams video
+ * streams at once: BGR->gray, goodFeaturesToTrack(maxCorners 200, quality 0.01, minDistance 15,
+ * blockSize 7) on the previous frame, pyramidal Lucas-Kanade (21x21 window, 3 levels, 30
+ * iterations / eps 0.01) into the current one, then the reference's median / 75th-percentile
+ * inlier mean, magnitude thresholds and 3-vector direction consistency.  The OpenCV stages
+ * follow OpenCV 4.x's published algorithms (cv2 is not available to pin them).
+ * 'feature_matching' and 'hybrid' (ORB + RANSAC homography) are not built. */
+enum yk_gmd_method { YK_GMD_OPTICAL_FLOW = 0, YK_GMD_FEATURE_MATCHING = 1, YK_GMD_HYBRID = 2 };
+/* One detect_motion() result (is_motion, motion_magnitude, motion_vector, should_reset). */
+typedef struct {
+  int32_t valid;           /* 1: the stream had a frame this step                            */
+  int32_t is_motion, should_reset;
+  int32_t magnitude_kind;  /* 0: the python-float 0.0 of the no-estimate returns, 1: float32  */
+  float magnitude;
+  float vector[2];         /* global motion vector (x, y), pixels per frame                  */
+  float consistency;       /* _calculate_motion_consistency of the last 3 vectors, -1: none   */
+  int32_t n_corners, n_tracked, n_inliers; /* diagnostics: corners, LK status==1, inliers     */
+  int32_t first_frame;     /* 1: no previous frame yet (the detector only stored this one)   */
+} yk_motion;
+/* GlobalMotionDetector.stats (:58-63) */
+typedef struct {
+  int64_t total_detections, motion_events, reset_triggers;
+  float avg_motion_magnitude;
+  int32_t pad;
+} yk_gmd_stats;
+typedef struct yk_gmd yk_gmd;
+/* Frames are height x width x 3 uint8 BGR (the decoder's / the detector's input buffer). */
+int yk_gmd_create(yk_ctx* ctx, int n_streams, int height, int width, int method, yk_gmd** out);
+int yk_gmd_destroy(yk_gmd* g);
+/* A fresh detector for every stream (no previous frame, zero stats, empty histories). */
+int yk_gmd_reset(yk_gmd* g, void* stream);
+/* GlobalMotionDetector.reset_stats() (:280-288) of every stream. */
+int yk_gmd_reset_stats(yk_gmd* g, void* stream);
+/* global_motion_threshold / reset_motion_threshold (:38-39; set_global_motion_sensitivity,
+ * motion_compensated_multi_tracker.py:353-360, divides both).  Compared in float32 like the
+ * reference's float32 magnitudes. */
+int yk_gmd_set_thresholds(yk_gmd* g, double global_motion_threshold, double reset_motion_threshold);
+/* detect_motion() on frame s of dev_frames ([n_streams][height][width][3] uint8) for every
+ * stream; results in dev_motion[n_streams] (device memory; NULL: the detector's own buffer,
+ * see yk_gmd_outputs).  Asynchronous on `stream`. */
+int yk_gmd_detect(yk_gmd* g, const uint8_t* dev_frames, yk_motion* dev_motion, void* stream);
+int yk_gmd_outputs(yk_gmd* g, yk_motion** dev_motion);
+/* Copy the last results (and stats when host_stats != NULL) to the host; synchronous. */
+int yk_gmd_download(yk_gmd* g, yk_motion* host_motion, yk_gmd_stats* host_stats, void* stream);
+/* Diagnostics for parity tests: stream s's last corners (x, y), LK end points (x, y) and status
+ * (host arrays of 200 entries); *n receives the corner count.  Synchronous. */
+int yk_gmd_points(yk_gmd* g, int stream_index, float* host_corners, float* host_next, uint8_t* host_status,
+                  int32_t* n, void* stream);
+
+/* MotionCompensatedMultiTracker.update(detections, frame) (motion_compensated_multi_tracker.py
+ * :75-121): yk_tracker_step of a YK_POLICY_MOTION_RESET tracker plus the global branch --
+ * global_motion_history / detection_stability_history, _should_global_reset (:123-148) and
+ * _perform_global_reset (:150-169: every tracker dropped, one new tracker per detection) --
+ * driven by dev_motion[n_streams] (yk_gmd_detect's output; a stream with valid == 0 had no
+ * frame).  dev_motion == NULL is yk_tracker_step. */
+int yk_tracker_step_motion(yk_tracker* trk, const void* dev_dets, int dtype, int row_stride,
+                           const int32_t* dev_counts, const yk_motion* dev_motion, void* stream);
 
 /* ------------------------------------------------------------------ ByteTrack / BoT-SORT
  * Replaces the upstream model.track() trackers for this path:

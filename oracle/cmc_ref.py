@@ -10,8 +10,10 @@ SURVEY §8f rank 1: the reference's subclasses of the hot path
       (:77-124, :176-242): strict `iou > thr`, (iou, d, t)-descending greedy match (:262-274),
       every live tracker reported (:369-386), stats total_frames / individual_resets /
       tracking_recoveries.
-The global-motion branch needs a frame and cv2 optical flow (global_motion_detector.py); with
-``frame=None`` -- the only mode here -- it is skipped exactly as in the reference (:97).
+With a frame, update() runs the global branch (:92-121, _should_global_reset :123-148,
+_perform_global_reset :150-169) on a motion detector: oracle/gmd_ref.py's restatement of
+GlobalMotionDetector('optical_flow') by default, or any object with detect_motion(frame)
+(the tests drive the tracker-side decision with scripted results too).
 
 Every numpy call keeps the reference's operand dtypes, so run with the same numpy (2.x, NEP 50
 scalar promotion) the values follow the reference's.  Two deliberate deviations, both outside
@@ -212,7 +214,7 @@ def cmc_greedy(iou, thr):
 class RefCMCMultiTracker:
     """MotionCompensatedMultiTracker.update(detections, frame=None) semantics."""
 
-    def __init__(self, max_lost_frames=150, min_hits=1, iou_threshold=0.1):
+    def __init__(self, max_lost_frames=150, min_hits=1, iou_threshold=0.1, motion_detector=None):
         self.trackers: list[RefResetTrack] = []
         self.max_lost_frames, self.min_hits, self.iou_threshold = max_lost_frames, min_hits, iou_threshold
         self.frame_count = 0
@@ -220,13 +222,57 @@ class RefCMCMultiTracker:
         self.stats = {"total_frames": 0, "global_motion_events": 0, "global_resets": 0,
                       "individual_resets": 0, "tracking_recoveries": 0}
         self.detection_stability_history = deque(maxlen=10)
+        self.global_motion_history = deque(maxlen=20)
+        self.frame_motion_info = None
+        if motion_detector is None:
+            from .gmd_ref import RefGlobalMotionDetector
+            motion_detector = RefGlobalMotionDetector()
+        # anything with detect_motion(frame) -> (is_motion, magnitude, vector, should_reset)
+        self.motion_detector = motion_detector
 
     def update(self, detections, frame=None):
-        if frame is not None:
-            raise NotImplementedError("global motion detection needs cv2 optical flow (out of scope)")
+        """:75-121, the global branch included (frame given -> detect_motion on it)."""
         self.frame_count += 1
         self.stats["total_frames"] += 1
+        global_motion_detected = False
+        if frame is not None:
+            is_motion, mag, vec, should_reset = self.motion_detector.detect_motion(frame)
+            self.frame_motion_info = {"is_motion": is_motion, "magnitude": mag,
+                                      "vector": vec.tolist() if hasattr(vec, "tolist") else vec,
+                                      "should_reset": should_reset}
+            self.global_motion_history.append(mag)
+            if should_reset:
+                global_motion_detected = True
+                self.stats["global_motion_events"] += 1
         self.detection_stability_history.append(len(detections))
+        if global_motion_detected and self._should_global_reset():
+            return self._perform_global_reset(detections)
+        return self._standard(detections)
+
+    def _should_global_reset(self):
+        """:123-148"""
+        if not self.frame_motion_info or not self.frame_motion_info["should_reset"]:
+            return False
+        if len(self.detection_stability_history) >= 5:
+            recent = list(self.detection_stability_history)[-5:]
+            if np.std(recent) / (np.mean(recent) + 1) > 0.5:
+                return True
+        if len(self.global_motion_history) >= 3:
+            if np.mean(list(self.global_motion_history)[-3:]) > 30.0:
+                return True
+        return self.frame_motion_info["magnitude"] > 60.0
+
+    def _perform_global_reset(self, detections):
+        """:150-169: every tracker dropped (no recovery accounting), one new tracker per detection."""
+        self.stats["global_resets"] += 1
+        self.trackers = []
+        for det in detections:
+            self.trackers.append(RefResetTrack(det[:4], self.next_num, self.max_lost_frames))
+            self.next_num += 1
+        return self._results()
+
+    def _standard(self, detections):
+        """:171-233"""
         boxes = [t.predict() for t in self.trackers]
         if len(detections) > 0 and len(self.trackers) > 0:
             iou = np.zeros((len(detections), len(boxes)))
@@ -258,6 +304,9 @@ class RefCMCMultiTracker:
             else:
                 keep.append(trk)
         self.trackers = keep
+        return self._results()
+
+    def _results(self):
         out = []
         for trk in self.trackers:
             info = trk.get_track_info()

@@ -49,7 +49,16 @@ BT_BYTETRACK, BT_BOTSORT = 0, 1
 STATS_DTYPE = np.dtype([(k, np.int64) for k in (
     "frame_count", "next_track_id", "total_tracks_created", "total_tracks_terminated",
     "current_active_tracks", "long_term_predictions", "successful_recoveries", "overflow",
-    "individual_resets", "tracking_recoveries")])
+    "individual_resets", "tracking_recoveries", "global_motion_events", "global_resets")])
+
+GMD_OPTICAL_FLOW, GMD_FEATURE_MATCHING, GMD_HYBRID = 0, 1, 2
+GMD_METHODS = {"optical_flow": GMD_OPTICAL_FLOW, "feature_matching": GMD_FEATURE_MATCHING, "hybrid": GMD_HYBRID}
+MOTION_DTYPE = np.dtype([("valid", np.int32), ("is_motion", np.int32), ("should_reset", np.int32),
+                         ("magnitude_kind", np.int32), ("magnitude", np.float32), ("vector", np.float32, (2,)),
+                         ("consistency", np.float32), ("n_corners", np.int32), ("n_tracked", np.int32),
+                         ("n_inliers", np.int32), ("first_frame", np.int32)], align=True)
+GMD_STATS_DTYPE = np.dtype([("total_detections", np.int64), ("motion_events", np.int64), ("reset_triggers", np.int64),
+                            ("avg_motion_magnitude", np.float32), ("pad", np.int32)], align=True)
 
 RESET_DETAIL_DTYPE = np.dtype([("frame", np.int32), ("reasons", np.int32), ("value", np.float64, (3,)),
                                ("confidence", np.float64), ("motion_consistency", np.float64)], align=True)
@@ -114,6 +123,16 @@ _SIGS = {
     "yk_bt_step": ([_vp, _vp, _vp, _vp], C.c_int),
     "yk_bt_outputs": ([_vp, C.POINTER(_vp), C.POINTER(_vp)], C.c_int),
     "yk_bt_download": ([_vp, _vp, _vp, _vp], C.c_int),
+    "yk_gmd_create": ([_vp, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(_vp)], C.c_int),
+    "yk_gmd_destroy": ([_vp], C.c_int),
+    "yk_gmd_reset": ([_vp, _vp], C.c_int),
+    "yk_gmd_reset_stats": ([_vp, _vp], C.c_int),
+    "yk_gmd_set_thresholds": ([_vp, C.c_double, C.c_double], C.c_int),
+    "yk_gmd_detect": ([_vp, _vp, _vp, _vp], C.c_int),
+    "yk_gmd_outputs": ([_vp, C.POINTER(_vp)], C.c_int),
+    "yk_gmd_download": ([_vp, _vp, _vp, _vp], C.c_int),
+    "yk_gmd_points": ([_vp, C.c_int, _vp, _vp, _vp, C.POINTER(_i32), _vp], C.c_int),
+    "yk_tracker_step_motion": ([_vp, _vp, C.c_int, C.c_int, _vp, _vp, _vp], C.c_int),
 }
 
 _lock = threading.Lock()
@@ -146,7 +165,8 @@ def lib() -> C.CDLL:
         if L.yk_abi_version() != 2:
             raise YKError("libyk.so ABI version mismatch")
         sizes = {0: C.sizeof(TrackerCfg), 1: STATS_DTYPE.itemsize, 2: TRACK_OUT_DTYPE.itemsize,
-                 3: TRACK_STATE_DTYPE.itemsize}
+                 3: TRACK_STATE_DTYPE.itemsize, 7: C.sizeof(BtCfg), 8: MOTION_DTYPE.itemsize,
+                 9: GMD_STATS_DTYPE.itemsize}
         for k, v in sizes.items():
             if L.yk_struct_size(k) != v:
                 raise YKError(f"ABI struct {k} size mismatch: C {L.yk_struct_size(k)} vs python {v}")

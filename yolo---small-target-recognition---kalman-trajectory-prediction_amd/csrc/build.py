@@ -32,6 +32,7 @@ SOURCES = [
     ("tracker.hip", ["-ffp-contract=off"]),
     ("detector.hip", []),
     ("bytetrack.hip", ["-ffp-contract=off"]),
+    ("gmd.hip", ["-ffp-contract=off"]),
 ]
 HEADERS = ["yk_internal.h", os.path.join("..", "..", "include", "yk.h")]
 

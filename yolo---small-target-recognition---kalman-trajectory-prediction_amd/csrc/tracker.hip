@@ -97,6 +97,12 @@ struct LSlot {
 struct Hdr {
   int n_tracks, n_free;
   yk_tracker_stats st;
+  // MotionCompensatedMultiTracker's global branch (motion_compensated_multi_tracker.py:52-53)
+  int dsh[10];                  // detection_stability_history deque(maxlen=10)
+  int dsh_len, dsh_head;
+  float gmh[20];                // global_motion_history deque(maxlen=20) ...
+  unsigned char gmk[20];        // ... entry dtype: K32 (np.float32) or KPY (python float 0.0)
+  int gmh_len, gmh_head;
 };
 
 struct Dev {
@@ -950,14 +956,79 @@ __device__ Lds carve(char* base, int T, int D) {
   return L;
 }
 
-enum { M_NCAND = 0, M_ACTIVE, M_RECOVER, M_LONGTERM, M_OVERFLOW, M_RESETS, M_TRECOV, M_WSUM = 8, M_TESTED = 12 };
+enum { M_NCAND = 0, M_ACTIVE, M_RECOVER, M_LONGTERM, M_OVERFLOW, M_RESETS, M_TRECOV, M_GRESET, M_WSUM = 8, M_TESTED = 12 };
+
+__device__ __forceinline__ int ring_slot(int cap, int& len, int& head) {  // deque(maxlen=cap).append
+  int pos;
+  if (len < cap) {
+    pos = head + len;
+    if (pos >= cap) pos -= cap;
+    ++len;
+  } else {
+    pos = head;
+    head = head + 1 == cap ? 0 : head + 1;
+  }
+  return pos;
+}
+
+// MotionCompensatedMultiTracker.update's global branch up to the reset decision (:92-118),
+// run by one thread: the two histories, stats['global_motion_events'], and
+// _should_global_reset (:123-148) with numpy's dtypes and left-to-right sums.
+__device__ bool global_branch(Hdr& H, const yk_motion* motion, int s, int n_dets) {
+  H.dsh[ring_slot(10, H.dsh_len, H.dsh_head)] = n_dets;  // (:113-114)
+  if (!motion || !motion[s].valid) return false;                // frame is None (:94)
+  const yk_motion m = motion[s];
+  const int gp = ring_slot(20, H.gmh_len, H.gmh_head);  // (:105)
+  H.gmh[gp] = m.magnitude;
+  H.gmk[gp] = m.magnitude_kind ? K32 : KPY;
+  if (!m.should_reset) return false;
+  H.st.global_motion_events += 1;  // (:107-110)
+  if (H.dsh_len >= 5) {  // np.std(recent) / (np.mean(recent) + 1) > 0.5, int64 -> float64
+    double c[5];
+    for (int i = 0; i < 5; ++i) {
+      int q = H.dsh_head + H.dsh_len - 5 + i;
+      if (q >= 10) q -= 10;
+      c[i] = (double)H.dsh[q];
+    }
+    double sum = c[0];
+    for (int i = 1; i < 5; ++i) sum += c[i];
+    const double mean = sum / 5.0;
+    double acc = (c[0] - mean) * (c[0] - mean);
+    for (int i = 1; i < 5; ++i) acc += (c[i] - mean) * (c[i] - mean);
+    const double sd = sqrt(acc / 5.0);
+    if (sd / (mean + 1.0) > 0.5) return true;
+  }
+  if (H.gmh_len >= 3) {  // np.mean(last 3) > 30.0: float32 when all three are float32 scalars
+    float v[3];
+    bool all32 = true;
+    for (int i = 0; i < 3; ++i) {
+      int q = H.gmh_head + H.gmh_len - 3 + i;
+      if (q >= 20) q -= 20;
+      v[i] = H.gmh[q];
+      all32 = all32 && H.gmk[q] == K32;
+    }
+    if (all32) {
+      float f = v[0];
+      f += v[1];
+      f += v[2];
+      if (f / 3.0f > 30.0f) return true;
+    } else {
+      double d = (double)v[0];
+      d += (double)v[1];
+      d += (double)v[2];
+      if (d / 3.0 > 30.0) return true;
+    }
+  }
+  return m.magnitude > 60.0f;
+}
 
 // ---------------------------------------------------------------- the step kernel
 // POL: yk_tracker_policy as a template constant, so the enhanced instantiation carries none of
 // the motion-reset code (registers: 122 VGPRs, no scratch).
 template <typename DT, int POL>
 __global__ void __launch_bounds__(NT) step_kernel(Dev g, const DT* __restrict__ dets, int row_stride,
-                                                  const int* __restrict__ counts) {
+                                                  const int* __restrict__ counts,
+                                                  const yk_motion* __restrict__ motion) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int s = blockIdx.x, tid = threadIdx.x;
   const int T = g.T;
@@ -972,8 +1043,21 @@ __global__ void __launch_bounds__(NT) step_kernel(Dev g, const DT* __restrict__ 
   int Draw = counts[s];
   if (Draw < 0) Draw = 0;
   const int D = Draw < g.D ? Draw : g.D;
-  const int n = H.n_tracks;
+  int greset = 0;
+  if (POL && tid == 0) greset = global_branch(H, motion, s, Draw) ? 1 : 0;
   if (tid < 8) L.misc[tid] = 0;
+  const int n_old = H.n_tracks;
+  int nfree_base = H.n_free;
+  if (POL) {
+    if (tid == 0) L.misc[M_GRESET] = greset;  // same wave as the zeroing above: program order
+    __syncthreads();
+    greset = L.misc[M_GRESET];
+    if (greset) {  // _perform_global_reset (:150-169): trackers.clear(), slots back to the stack
+      for (int i = tid; i < n_old; i += NT) fstack[nfree_base + i] = order[i];
+      nfree_base += n_old;
+    }
+  }
+  const int n = greset ? 0 : n_old;
   // load detections (rows of row_stride elements; only x1..y2 are used by the tracker)
   for (int i = tid; i < D * 4; i += NT) {
     const int d = i >> 2, k = i & 3;
@@ -1137,7 +1221,7 @@ __global__ void __launch_bounds__(NT) step_kernel(Dev g, const DT* __restrict__ 
   // Step 5: new tracks for unmatched detections, ascending detection order (multi:92-101)
   int n_new_total = 0;
   const int next_num = (int)H.st.next_track_id;
-  const int nfree0 = H.n_free;
+  const int nfree0 = nfree_base;
   for (int base = 0; base < D; base += NT) {
     const int d = base + tid;
     const int flag = (d < D && L.det_match[d] < 0) ? 1 : 0;
@@ -1256,7 +1340,8 @@ __global__ void __launch_bounds__(NT) step_kernel(Dev g, const DT* __restrict__ 
     H.st.frame_count = fc;
     H.st.next_track_id += n_new;
     H.st.total_tracks_created += n_new;
-    H.st.total_tracks_terminated += n_del;
+    H.st.total_tracks_terminated += n_del + (greset ? n_old : 0);
+    H.st.global_resets += greset;
     H.st.current_active_tracks = kept;
     H.st.long_term_predictions += L.misc[M_LONGTERM];
     H.st.successful_recoveries += L.misc[M_RECOVER];
@@ -1892,6 +1977,7 @@ __global__ void reset_kernel(Dev g, int S) {
     H.n_free = g.T;
     H.st = yk_tracker_stats{};
     H.st.next_track_id = 1;
+    H.dsh_len = H.dsh_head = H.gmh_len = H.gmh_head = 0;
     g.counts[s] = 0;
     g.stats[s] = H.st;
   }
@@ -2150,7 +2236,14 @@ int yk_tracker_reset(yk_tracker* t, void* stream) {
 
 int yk_tracker_step(yk_tracker* t, const void* dets, int dtype, int row_stride, const int32_t* counts,
                     void* stream) {
+  return yk_tracker_step_motion(t, dets, dtype, row_stride, counts, nullptr, stream);
+}
+
+int yk_tracker_step_motion(yk_tracker* t, const void* dets, int dtype, int row_stride, const int32_t* counts,
+                           const yk_motion* motion, void* stream) {
   YK_CHECK_ARG(t && dets && counts, "yk_tracker_step: NULL argument");
+  YK_CHECK_ARG(!motion || t->cfg.policy == YK_POLICY_MOTION_RESET,
+               "yk_tracker_step_motion: global camera-motion input needs the YK_POLICY_MOTION_RESET policy");
   YK_CHECK_ARG(row_stride >= 4, "yk_tracker_step: row_stride must be >= 4");
   YK_CHECK_ARG(dtype == YK_F32 || dtype == YK_F64, "yk_tracker_step: dtype must be YK_F32 or YK_F64");
   yk::DeviceGuard guard(t->ctx->device);
@@ -2176,17 +2269,17 @@ int yk_tracker_step(yk_tracker* t, const void* dets, int dtype, int row_stride, 
   if (dtype == YK_F32) {
     if (mr)
       hipLaunchKernelGGL((yk::trk::step_kernel<float, 1>), dim3(t->S), dim3(yk::trk::NT), t->lds,
-                         (hipStream_t)stream, t->dev, (const float*)dets, row_stride, counts);
+                         (hipStream_t)stream, t->dev, (const float*)dets, row_stride, counts, motion);
     else
       hipLaunchKernelGGL((yk::trk::step_kernel<float, 0>), dim3(t->S), dim3(yk::trk::NT), t->lds,
-                         (hipStream_t)stream, t->dev, (const float*)dets, row_stride, counts);
+                         (hipStream_t)stream, t->dev, (const float*)dets, row_stride, counts, motion);
   } else {
     if (mr)
       hipLaunchKernelGGL((yk::trk::step_kernel<double, 1>), dim3(t->S), dim3(yk::trk::NT), t->lds,
-                         (hipStream_t)stream, t->dev, (const double*)dets, row_stride, counts);
+                         (hipStream_t)stream, t->dev, (const double*)dets, row_stride, counts, motion);
     else
       hipLaunchKernelGGL((yk::trk::step_kernel<double, 0>), dim3(t->S), dim3(yk::trk::NT), t->lds,
-                         (hipStream_t)stream, t->dev, (const double*)dets, row_stride, counts);
+                         (hipStream_t)stream, t->dev, (const double*)dets, row_stride, counts, motion);
   }
   YK_HIP(hipGetLastError());
   return YK_OK;

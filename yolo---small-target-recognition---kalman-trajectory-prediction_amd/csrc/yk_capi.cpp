@@ -40,6 +40,8 @@ int64_t yk_struct_size(int which) {
     case 5: return (int64_t)sizeof(yk_op);
     case 6: return (int64_t)sizeof(yk_model_desc);
     case 7: return (int64_t)sizeof(yk_bt_cfg);
+    case 8: return (int64_t)sizeof(yk_motion);
+    case 9: return (int64_t)sizeof(yk_gmd_stats);
     default: return -1;
   }
 }

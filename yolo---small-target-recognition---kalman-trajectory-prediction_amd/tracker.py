@@ -170,8 +170,10 @@ class MultiStreamTracker:
     def reset(self):
         L.check(L.lib().yk_tracker_reset(self._h, L.current_stream(self.device)), "yk_tracker_reset")
 
-    def step_device(self, dets: torch.Tensor, counts: torch.Tensor, stream=None):
-        """dets: device tensor [S, max_dets, stride] (float32 or float64); counts: int32 [S]."""
+    def step_device(self, dets: torch.Tensor, counts: torch.Tensor, stream=None, motion=None):
+        """dets: device tensor [S, max_dets, stride] (float32 or float64); counts: int32 [S];
+        motion: device address of yk_motion[S] (BatchedMotionDetector.motion_ptr) for the
+        motion-reset policy's global branch, or None (no frames)."""
         if dets.dim() != 3 or dets.shape[0] != self.n_streams or dets.shape[1] != self.max_dets or dets.shape[2] < 4:
             raise ValueError(f"dets must be [{self.n_streams}, {self.max_dets}, >=4], got {tuple(dets.shape)}")
         if not dets.is_contiguous() or not counts.is_contiguous() or counts.dtype != torch.int32:
@@ -180,10 +182,10 @@ class MultiStreamTracker:
         if dt is None:
             raise ValueError("dets dtype must be float32 or float64")
         st = L.current_stream(self.device) if stream is None else C.c_void_p(stream)
-        L.check(L.lib().yk_tracker_step(self._h, L.ptr(dets), dt, int(dets.shape[2]), L.ptr(counts), st),
-                "yk_tracker_step")
+        L.check(L.lib().yk_tracker_step_motion(self._h, L.ptr(dets), dt, int(dets.shape[2]), L.ptr(counts),
+                                               C.c_void_p(motion or 0), st), "yk_tracker_step")
 
-    def step_host(self, per_stream_dets):
+    def step_host(self, per_stream_dets, motion=None):
         """Host detections (one list/array per stream) -> step.  Returns nothing; call download()."""
         arrs = [_det_array(d) for d in per_stream_dets]
         if len(arrs) != self.n_streams:
@@ -201,7 +203,7 @@ class MultiStreamTracker:
             cnt[s] = len(a)
         buf.copy_(torch.from_numpy(host))
         self._counts.copy_(torch.from_numpy(cnt))
-        self.step_device(buf, self._counts)
+        self.step_device(buf, self._counts, motion=motion)
 
     def download(self):
         st = L.current_stream(self.device)
@@ -491,26 +493,34 @@ MultiTargetTracker = EnhancedMultiTargetTracker
 
 class MotionCompensatedMultiTracker:
     """Drop-in for camera_motion_compensation.MotionCompensatedMultiTracker
-    (motion_compensated_multi_tracker.py:18-394) without a frame: ``update(detections)`` runs
-    the motion-reset policy of the batched HIP tracker kernel (YK_POLICY_MOTION_RESET):
-    MotionResetKalmanTracker jump / velocity / size-change resets, blended predict after a
-    reset, strict iou > thr with the (iou, d, t)-descending greedy order, every live tracker
-    reported with its reset fields.  Global camera-motion detection needs frames and cv2
-    optical flow (global_motion_detector.py) and is not on this path: passing a frame raises.
-    Track ids are "T%03d" of the creation index (the reference draws uuid4 strings)."""
+    (motion_compensated_multi_tracker.py:18-394) on the batched HIP kernels: the motion-reset
+    policy of the tracker kernel (YK_POLICY_MOTION_RESET: MotionResetKalmanTracker jump /
+    velocity / size-change resets, blended predict after a reset, strict iou > thr with the
+    (iou, d, t)-descending greedy order, every live tracker reported with its reset fields) and,
+    when ``update(detections, frame)`` gets a frame, the global branch: GlobalMotionDetector
+    ('optical_flow', csrc/gmd.hip) on the frame, then _should_global_reset /
+    _perform_global_reset inside the tracker step (yk_tracker_step_motion).  Track ids are
+    "T%03d" of the creation index (the reference draws uuid4 strings)."""
 
     def __init__(self, max_lost_frames=150, min_hits=1, iou_threshold=0.1, motion_detection_method="optical_flow",
-                 *, max_tracks: int = 1024, max_dets: int = 1024, device: int = 0):
+                 *, max_tracks: int = 1024, max_dets: int = 1024, device: int = 0, verbose: bool = False):
+        from .motion import GlobalMotionDetector
+
         self.max_lost_frames, self.min_hits, self.iou_threshold = max_lost_frames, min_hits, iou_threshold
         self.motion_detection_method = motion_detection_method
+        self.motion_detector = GlobalMotionDetector(motion_detection_method, device=device)
         self.global_motion_compensation = True
         self.individual_reset_enabled = True
         self.adaptive_thresholds = True
         self._core = MultiStreamTracker(1, max_lost_frames, min_hits, iou_threshold, max_tracks, max_dets, device,
                                         policy=L.POLICY_MOTION_RESET)
         self._stats = np.zeros(1, dtype=L.STATS_DTYPE)[0]
+        self._stats_base = np.zeros(1, dtype=L.STATS_DTYPE)[0]
         self.detection_stability_history = deque(maxlen=10)
+        self.global_motion_history = deque(maxlen=20)
         self.frame_motion_info = None
+        self.current_frame = None
+        self.verbose = verbose
 
     @property
     def frame_count(self) -> int:
@@ -518,33 +528,67 @@ class MotionCompensatedMultiTracker:
 
     @property
     def stats(self) -> dict:
-        s = self._stats
-        return {"total_frames": int(s["frame_count"]), "global_motion_events": 0, "global_resets": 0,
-                "individual_resets": int(s["individual_resets"]), "tracking_recoveries": int(s["tracking_recoveries"])}
+        s, b = self._stats, self._stats_base
+        return {k: int(s[src]) - int(b[src]) for k, src in (
+            ("total_frames", "frame_count"), ("global_motion_events", "global_motion_events"),
+            ("global_resets", "global_resets"), ("individual_resets", "individual_resets"),
+            ("tracking_recoveries", "tracking_recoveries"))}
 
     def update(self, detections, frame=None):
-        if frame is not None:
-            raise NotImplementedError("global camera-motion detection (cv2 optical flow on frames) is not on the "
-                                      "MI355X path; call update(detections) for the per-track motion resets")
+        """:75-121"""
+        motion = None
+        self.current_frame = frame
+        if frame is not None and self.global_motion_compensation:
+            det = self.motion_detector._detector(frame)
+            det.detect_host([frame])
+            motion = det.motion_ptr
         self.detection_stability_history.append(len(detections))
-        self._core.step_host([detections])
+        self._core.step_host([detections], motion=motion)
         rows, counts, stats = self._core.download()
         self._stats = stats[0].copy()
         if int(self._stats["overflow"]):
             raise L.YKError(f"tracker capacity exceeded (max_tracks={self._core.max_tracks})")
-        return [_reset_fields(r, _row_to_dict(r, track_id_of(r["track_num"]))) for r in rows[0, : int(counts[0])]]
+        if motion is not None:
+            from .motion import motion_tuple
+
+            m, _ = self.motion_detector._b.download()
+            is_motion, mag, vec, should_reset = motion_tuple(m[0])
+            self.frame_motion_info = {"is_motion": is_motion, "magnitude": mag,
+                                      "vector": vec.tolist() if hasattr(vec, "tolist") else vec,
+                                      "should_reset": should_reset}
+            self.global_motion_history.append(mag)
+        out = []
+        for r in rows[0, : int(counts[0])]:
+            info = _row_to_dict(r, track_id_of(r["track_num"]))
+            info = _reset_fields(r, info)
+            if self.frame_motion_info:
+                info["global_motion"] = self.frame_motion_info
+            out.append(info)
+        return out
+
+    def set_global_motion_sensitivity(self, sensitivity):
+        """:353-360"""
+        if 0.5 <= sensitivity <= 2.0:
+            self.motion_detector.global_motion_threshold /= sensitivity
+            self.motion_detector.reset_motion_threshold /= sensitivity
+
+    def enable_adaptive_mode(self, enabled=True):
+        """:345-351 (the reset trackers carry no adaptive switch; the flag is kept)"""
+        self.adaptive_thresholds = enabled
+
+    def reset_all_statistics(self):
+        """:362-374"""
+        self._stats_base = self._stats.copy()
+        self.motion_detector.reset_stats()
 
     def get_comprehensive_stats(self):
-        """motion_compensated_multi_tracker.py:308-343.  Frame-free, so the global motion detector
-        has seen no frame (global_motion_detector.py:263-278 with total_detections == 0); the
-        reference never appends to stats['processing_times'], so 'performance' is always {}."""
+        """:308-343.  The reference never appends to stats['processing_times'], so 'performance'
+        is always {}."""
         rows, counts, _ = self._core.download()
         live = rows[0, : int(counts[0])]
         return {"basic": self.stats,
-                "motion_detection": {"total_detections": 0, "motion_events": 0, "reset_triggers": 0,
-                                     "motion_detection_rate": f"{0.0:.1%}", "reset_trigger_rate": f"{0.0:.1%}",
-                                     "avg_motion_magnitude": f"{0.0:.2f}px"},
+                "motion_detection": self.motion_detector.get_stats(),
                 "performance": {},
                 "trackers": {"active_trackers": int(len(live)),
                              "total_resets_by_tracker": int(live["reset_count"].sum()) if len(live) else 0},
-                "motion_history_avg": 0.0}
+                "motion_history_avg": np.mean(self.global_motion_history) if self.global_motion_history else 0.0}
