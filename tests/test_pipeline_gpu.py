@@ -52,9 +52,10 @@ def test_stream_pipeline_fp32_matches_oracle_chain():
                 np.testing.assert_allclose(o["confidence"], r["confidence"], rtol=1e-4)
 
 
-def test_reference_driver_loop_through_compat_packages():
-    """The per-frame body of kalman/aircraft_detection_tracking.py:88-131 with the compat
-    imports; video I/O and drawing (cv2) replaced by synthetic frames."""
+def test_reference_driver_loop_through_compat_packages(tmp_path):
+    """kalman/aircraft_detection_tracking.py:58-161 with the compat imports: frames read through
+    the VideoCapture-like reader (a .npy frame stack, since no codec is in the image), the
+    per-frame body of :88-131, the visualizer and the VideoWriter-like sink."""
     sys.path.insert(0, os.path.join(REPO, pkg().__name__, "compat"))
     try:
         from kalman.enhanced_multi_target_tracker import EnhancedMultiTargetTracker
@@ -63,14 +64,23 @@ def test_reference_driver_loop_through_compat_packages():
     finally:
         sys.path.pop(0)
     P = pkg()
+    FR = P.frames
+    sc = P.synth.Scene(seed=4, n_targets=12, n_frames=8)
+    np.save(tmp_path / "short.npy", np.stack([sc.frame(t) for t in range(8)]))
     model = YOLO("yolov8s-small.yaml")
     tracker = EnhancedMultiTargetTracker(max_lost_frames=150, min_hits=1, iou_threshold=0.1)
     vis = TrajectoryVisualizer()
-    sc = P.synth.Scene(seed=4, n_targets=12, n_frames=8)
-    detection_frames = prediction_frames = state_changes = 0
+    cap = FR.VideoReader(str(tmp_path / "short.npy"))
+    fps = int(cap.get(FR.CAP_PROP_FPS))
+    width, height = int(cap.get(FR.CAP_PROP_FRAME_WIDTH)), int(cap.get(FR.CAP_PROP_FRAME_HEIGHT))
+    out = FR.VideoWriter(str(tmp_path / "result.npy"), fps, (width, height))
+    detection_frames = prediction_frames = state_changes = frame_count = 0
     last = {}
-    for t in range(8):
-        frame = sc.frame(t)
+    while True:
+        ret, frame = cap.read()
+        if not ret:
+            break
+        frame_count += 1
         results = model(frame, verbose=False)
         detections = []
         if len(results) > 0 and results[0].boxes is not None:
@@ -89,10 +99,18 @@ def test_reference_driver_loop_through_compat_packages():
             detection_frames += tr["status"] == "detected"
             prediction_frames += tr["status"] == "predicted"
         last = cur
-        assert vis.draw_tracks(frame, tracks, detections, {}) is frame
-    assert detection_frames > 0
+        frame_info = {"frame_number": frame_count, "detections": len(detections), "tracks": len(tracks),
+                      "detection_frames": detection_frames, "prediction_frames": prediction_frames,
+                      "state_changes": state_changes}
+        vis_frame = vis.draw_tracks(frame, tracks, detections, frame_info)
+        assert vis_frame.shape == frame.shape and (vis_frame != frame).any()
+        out.write(vis_frame)
+    cap.release()
+    out.release()
+    assert frame_count == 8 and detection_frames > 0
     assert tracker.frame_count == 8
     assert results[0].boxes.xyxy.is_cuda and results[0].orig_shape == (512, 640)
+    assert np.load(tmp_path / "result.npy").shape == (8, 512, 640, 3)
 
 
 def test_pipelined_tracker_stream_matches_serial():

@@ -10,7 +10,7 @@ CPU fallback: without the library or a GPU every entry point raises ``YKError``.
 ``compat/`` holds ``kalman`` and ``ultralytics`` shim packages: put that directory on
 sys.path and the reference driver's imports resolve to this package unchanged.
 """
-from . import arch, model, predictor, shard, synth, tracker, weights  # noqa: F401
+from . import arch, frames, model, predictor, shard, synth, tracker, visualize, weights  # noqa: F401
 from ._lib import YKError, exported_symbols  # noqa: F401
 from .tracker import (  # noqa: F401
     AircraftKalmanTracker,
@@ -21,5 +21,6 @@ from .tracker import (  # noqa: F401
     MultiTargetTracker,
 )
 from .predictor import YOLO, Boxes, Results  # noqa: F401
+from .visualize import TrajectoryVisualizer  # noqa: F401
 
 __version__ = "0.1.0"

@@ -1,13 +1,10 @@
-"""kalman.trajectory_visualizer stand-in.
+"""kalman.trajectory_visualizer (reference kalman/trajectory_visualizer.py:5-235).
 
-The reference's visualizer (kalman/trajectory_visualizer.py) is cv2 drawing and is outside
-the hot path.  This pass-through keeps the driver's import and call
-working: draw_tracks returns the frame unchanged."""
+Resolves to the package's host-side visualizer (visualize.py): the same colours, labels,
+flashing predicted boxes with the 0.3 / 0.7 fill, trails and velocity arrows, drawn on numpy
+BGR frames with restated OpenCV primitives (cv2 is not in this image)."""
+from ._pkg import sub
 
+TrajectoryVisualizer = sub("visualize").TrajectoryVisualizer
 
-class TrajectoryVisualizer:
-    def __init__(self, *args, **kwargs):
-        pass
-
-    def draw_tracks(self, frame, tracks, detections=None, frame_info=None):
-        return frame
+__all__ = ["TrajectoryVisualizer"]

@@ -193,28 +193,31 @@ class YOLO:
         del agnostic_nms
         if classes is not None:
             classes = [int(c) for c in (classes if isinstance(classes, (list, tuple, set)) else [classes])]
-        frames = self._frames(source)
+        items = self._frames(source)
+        paths = [p for p, _ in items]
+        frames = [f for _, f in items]
         with self._lock:
             out = []
             for i in range(0, len(frames), self.max_batch):
-                out.extend(self._predict_batch(frames[i:i + self.max_batch], conf, iou, imgsz, max_det, classes))
+                out.extend(self._predict_batch(frames[i:i + self.max_batch], conf, iou, imgsz, max_det, classes,
+                                               paths[i:i + self.max_batch]))
         return iter(out) if stream else out
 
     @staticmethod
     def _frames(source):
-        if isinstance(source, np.ndarray):
-            return [source]
-        if isinstance(source, (list, tuple)) and all(isinstance(s, np.ndarray) for s in source):
-            return list(source)
-        raise NotImplementedError("source must be an HxWx3 uint8 BGR ndarray or a list of them "
-                                  "(file/video/stream loaders are outside the hot path)")
+        """Source -> list of (path, HxWx3 uint8 BGR): ndarray(s), PIL images, image files,
+        directories, globs and .npy / .y4m frame stacks (frames.py; loaders.py:309-563)."""
+        from . import frames as FR
 
-    def _predict_batch(self, frames, conf, iou, imgsz, max_det, classes):
+        return FR.load_source(source)
+
+    def _predict_batch(self, frames, conf, iou, imgsz, max_det, classes, paths=None):
+        paths = paths or [f"image{b}.jpg" for b in range(len(frames))]
         shapes = {f.shape for f in frames}
         if len(shapes) != 1:
             out = []
-            for f in frames:
-                out.extend(self._predict_batch([f], conf, iou, imgsz, max_det, classes))
+            for f, p in zip(frames, paths):
+                out.extend(self._predict_batch([f], conf, iou, imgsz, max_det, classes, [p]))
             return out
         h, w, c = frames[0].shape
         if c != 3 or frames[0].dtype != np.uint8:
@@ -234,7 +237,7 @@ class YOLO:
             if classes is not None and 0 not in classes:
                 n = 0  # the class filter ran before NMS in the reference: no candidate survives
             d = dets[b, :n]
-            res.append(Results(frames[b], f"image{b}.jpg", self.names, boxes=d))
+            res.append(Results(frames[b], paths[b], self.names, boxes=d))
         t3 = time.perf_counter()
         sp = {"preprocess": (t1 - t0) * 1e3 / B, "inference": (t2 - t1) * 1e3 / B, "postprocess": (t3 - t2) * 1e3 / B}
         for r in res:
