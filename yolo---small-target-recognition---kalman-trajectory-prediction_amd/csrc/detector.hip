@@ -805,8 +805,11 @@ constexpr int fast_skd(int nnt, int npt) { return nnt * npt >= 8 ? 2 : 4; }
 // conv_fastw's activation slots are indexed by the step within a 4-step weight chunk: SKD | 4
 constexpr int fastw_skd(int nnt, int npt) { return nnt * npt >= 8 ? 2 : 4; }
 
-template <class Tr, int NNT, int NPT, bool WS, int SKD>
-__global__ void __launch_bounds__(256) conv_fast_kernel(FastArgs a) {
+// NE = output-channel tiles this workgroup computes: NNT, or fewer for the last channel group of
+// an op whose n_tiles is not a multiple of NNT (its missing tiles cost no loads and no MFMAs;
+// each body is straight-line code, the dispatch is one scalar branch per workgroup).
+template <class Tr, int NE, int NPT, bool WS, int SKD>
+__device__ __forceinline__ void conv_fast_body(const FastArgs& a, int2 blk, int nt0) {
   using T = typename Tr::T;
   constexpr int ESZ = (int)sizeof(T);
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -814,8 +817,6 @@ __global__ void __launch_bounds__(256) conv_fast_kernel(FastArgs a) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int kg = lane >> 4, col = lane & 15;
-  const int2 blk = xcd_block(a.xcd);
-  const int nt0 = blk.y * NNT;
   const int pbase = WS ? blk.x * (16 * NPT) : (blk.x * 4 + wave) * (16 * NPT);
   const int nk = a.k_steps;
   const int wg_lin = blockIdx.y * gridDim.x + blockIdx.x;
@@ -854,16 +855,16 @@ __global__ void __launch_bounds__(256) conv_fast_kernel(FastArgs a) {
                        ((iy0 + 2 >= 0 && iy0 + 2 < a.in_h) ? cm << 6 : 0u);
     vm[t] = pv ? m : 0u;  // 1x1 convs use tap 0 = the pixel itself
   }
-  f32x4 acc[NNT][NPT];
+  f32x4 acc[NE][NPT];
 #pragma unroll
-  for (int i = 0; i < NNT; ++i)
+  for (int i = 0; i < NE; ++i)
 #pragma unroll
     for (int t = 0; t < NPT; ++t) acc[i][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float4 bb[NNT];
-  float4 sc[NNT];  // FP8 dequant scales
-  unsigned wo[NNT];
+  float4 bb[NE];
+  float4 sc[NE];  // FP8 dequant scales
+  unsigned wo[NE];
 #pragma unroll
-  for (int i = 0; i < NNT; ++i) {
+  for (int i = 0; i < NE; ++i) {
     const int n0 = (nt0 + i) * 16 + kg * 4;
     bb[i] = (nt0 + i < a.n_tiles && n0 < a.cout) ? *(const float4*)(a.bias + n0) : make_float4(0.f, 0.f, 0.f, 0.f);
     if constexpr (Tr::kScaled) sc[i] = dq4<Tr>(a.bias, a.n_tiles, n0 < a.cout ? n0 : 0);
@@ -873,7 +874,7 @@ __global__ void __launch_bounds__(256) conv_fast_kernel(FastArgs a) {
   __syncthreads();
   auto issue = [&](int ks, int2 e, uint4* wf, uint4* xf) {
 #pragma unroll
-    for (int i = 0; i < NNT; ++i) wf[i] = bload(wr, wo[i], ks * 1024);
+    for (int i = 0; i < NE; ++i) wf[i] = bload(wr, wo[i], ks * 1024);
     const unsigned tap = (unsigned)e.y & 15u;
     const bool s1 = (e.y & 16) != 0, ev = (e.y & 32) != 0;
 #pragma unroll
@@ -890,7 +891,7 @@ __global__ void __launch_bounds__(256) conv_fast_kernel(FastArgs a) {
     k0 = wave * kq;
     k1 = k0 + kq < nk ? k0 + kq : nk;
   }
-  uint4 wb[SKD][NNT], xb[SKD][NPT];
+  uint4 wb[SKD][NE], xb[SKD][NPT];
   int ks = k0;
   if (k1 - k0 >= 2 * SKD) {
     // prologue and steady state issue the loads in the same pinned order (MFMAs of step d,
@@ -908,7 +909,7 @@ __global__ void __launch_bounds__(256) conv_fast_kernel(FastArgs a) {
           __builtin_amdgcn_sched_barrier(0);
           const int2 e0 = tab[(ks + d + SKD) * 4 + kg], e1 = tab[(ks + d + 1 + SKD) * 4 + kg];
 #pragma unroll
-          for (int i = 0; i < NNT; ++i)
+          for (int i = 0; i < NE; ++i)
 #pragma unroll
             for (int t = 0; t < NPT; ++t) acc[i][t] = mma2<Tr>(wb[d][i], wb[d + 1][i], xb[d][t], xb[d + 1][t], acc[i][t]);
           __builtin_amdgcn_sched_barrier(0);
@@ -921,7 +922,7 @@ __global__ void __launch_bounds__(256) conv_fast_kernel(FastArgs a) {
           __builtin_amdgcn_sched_barrier(0);
           const int2 e = tab[(ks + d + SKD) * 4 + kg];  // LDS read in flight over the MFMAs
 #pragma unroll
-          for (int i = 0; i < NNT; ++i)
+          for (int i = 0; i < NE; ++i)
 #pragma unroll
             for (int t = 0; t < NPT; ++t) acc[i][t] = mma<Tr>(wb[d][i], xb[d][t], acc[i][t]);
           __builtin_amdgcn_sched_barrier(0);
@@ -934,14 +935,14 @@ __global__ void __launch_bounds__(256) conv_fast_kernel(FastArgs a) {
 #pragma unroll
       for (int d = 0; d < SKD; d += 2)
 #pragma unroll
-        for (int i = 0; i < NNT; ++i)
+        for (int i = 0; i < NE; ++i)
 #pragma unroll
           for (int t = 0; t < NPT; ++t) acc[i][t] = mma2<Tr>(wb[d][i], wb[d + 1][i], xb[d][t], xb[d + 1][t], acc[i][t]);
     } else {
 #pragma unroll
       for (int d = 0; d < SKD; ++d) {
 #pragma unroll
-        for (int i = 0; i < NNT; ++i)
+        for (int i = 0; i < NE; ++i)
 #pragma unroll
           for (int t = 0; t < NPT; ++t) acc[i][t] = mma<Tr>(wb[d][i], xb[d][t], acc[i][t]);
       }
@@ -963,7 +964,7 @@ __global__ void __launch_bounds__(256) conv_fast_kernel(FastArgs a) {
           if (ks + d < k1) {
             const bool two = ks + d + 1 < k1;
 #pragma unroll
-            for (int i = 0; i < NNT; ++i)
+            for (int i = 0; i < NE; ++i)
 #pragma unroll
               for (int t = 0; t < NPT; ++t)
                 acc[i][t] = mma2<Tr>(wb[d][i], two ? wb[d + 1][i] : z, xb[d][t], two ? xb[d + 1][t] : z, acc[i][t]);
@@ -976,7 +977,7 @@ __global__ void __launch_bounds__(256) conv_fast_kernel(FastArgs a) {
         for (int d = 0; d < SKD; ++d) {
           if (ks + d < k1) {
 #pragma unroll
-            for (int i = 0; i < NNT; ++i)
+            for (int i = 0; i < NE; ++i)
 #pragma unroll
               for (int t = 0; t < NPT; ++t) acc[i][t] = mma<Tr>(wb[d][i], xb[d][t], acc[i][t]);
             if (ks + d + SKD < k1) load_step(ks + d + SKD, wb[d], xb[d]);
@@ -989,13 +990,13 @@ __global__ void __launch_bounds__(256) conv_fast_kernel(FastArgs a) {
   if constexpr (WS) {
     f32x4* red = (f32x4*)(smem + (((size_t)nk * 4 * 8 + 15) & ~(size_t)15));
 #pragma unroll
-    for (int i = 0; i < NNT; ++i)
+    for (int i = 0; i < NE; ++i)
 #pragma unroll
-      for (int t = 0; t < NPT; ++t) red[((wave * NNT + i) * NPT + t) * 64 + lane] = acc[i][t];
+      for (int t = 0; t < NPT; ++t) red[((wave * NE + i) * NPT + t) * 64 + lane] = acc[i][t];
     __syncthreads();
   }
 #pragma unroll
-  for (int i = 0; i < NNT; ++i) {
+  for (int i = 0; i < NE; ++i) {
     const int nt = nt0 + i;
     if (nt >= a.n_tiles) break;
     const int n0 = nt * 16 + kg * 4;
@@ -1008,10 +1009,10 @@ __global__ void __launch_bounds__(256) conv_fast_kernel(FastArgs a) {
       f32x4 v4 = acc[i][t];
       if constexpr (WS) {
         const f32x4* red = (const f32x4*)(smem + (((size_t)nk * 4 * 8 + 15) & ~(size_t)15));
-        v4 = red[((0 * NNT + i) * NPT + t) * 64 + lane];
+        v4 = red[((0 * NE + i) * NPT + t) * 64 + lane];
 #pragma unroll
         for (int w = 1; w < 4; ++w) {
-          const f32x4 u = red[((w * NNT + i) * NPT + t) * 64 + lane];
+          const f32x4 u = red[((w * NE + i) * NPT + t) * 64 + lane];
           v4[0] += u[0];
           v4[1] += u[1];
           v4[2] += u[2];
@@ -1040,6 +1041,28 @@ __global__ void __launch_bounds__(256) conv_fast_kernel(FastArgs a) {
   }
   if (a.tstamp && tid == 0 && wg_lin < a.tstamp_cap) a.tstamp[3 * wg_lin + 2] = wall_clock64();
 }
+
+template <class Tr, int NNT, int NPT, bool WS, int SKD>
+__global__ void __launch_bounds__(256) conv_fast_kernel(FastArgs a) {
+  const int2 blk = xcd_block(a.xcd);
+  const int nt0 = blk.y * NNT;
+  const int rem = a.n_tiles - nt0;
+  if constexpr (NNT == 1) {
+    conv_fast_body<Tr, 1, NPT, WS, SKD>(a, blk, nt0);
+  } else {
+    if (rem >= NNT) {
+      conv_fast_body<Tr, NNT, NPT, WS, SKD>(a, blk, nt0);
+    } else if (rem == 1) {
+      conv_fast_body<Tr, 1, NPT, WS, SKD>(a, blk, nt0);
+    } else if constexpr (NNT > 2) {
+      if (rem == 2 || NNT == 3)
+        conv_fast_body<Tr, 2, NPT, WS, SKD>(a, blk, nt0);
+      else
+        conv_fast_body<Tr, (NNT > 3 ? 3 : 1), NPT, WS, SKD>(a, blk, nt0);
+    }
+  }
+}
+
 
 // ---------------------------------------------------------------- table conv, weights shared through LDS
 // conv_fast_kernel's per-wave layout (wave = NPT x 16 pixels x NNT x 16 channels, activations
