@@ -88,7 +88,7 @@ def parse():
     ap.add_argument("--lanes", type=int, default=None)
     ap.add_argument("--groups", type=int, default=1, help="independent sub-batches run concurrently")
     ap.add_argument("--tracker", default="enhanced", choices=["enhanced", "motion_reset"])
-    ap.add_argument("--inflight", type=int, default=3, choices=range(1, 9),
+    ap.add_argument("--inflight", type=int, default=4, choices=range(1, 9),
                     help="detector forwards in flight (each a batch of all streams, own graph + HIP stream)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=25.0, help="CPU-baseline sample bound (default threads)")

@@ -1,7 +1,7 @@
 """The exact benchmark pipeline (BASELINE config 3) against the oracle chain, every frame.
 
-bench.py's headline leg: YOLOv8s+P2 fp32, 8 streams as one batch-8 forward, three detector
-forwards in flight (inflight=3, one hipGraph per slot), the tracker on its own stream,
+bench.py's headline leg: YOLOv8s+P2 fp32, 8 streams as one batch-8 forward, four detector
+forwards in flight (inflight=4, one hipGraph per slot), the tracker on its own stream,
 EnhancedMultiTargetTracker(150, 1, 0.1) semantics, 40 targets per stream (>= 64 live tracks) with occlusion bursts
 (SURVEY §8d).  The pipeline runs unsynchronised; a step hook records every step's detections
 and tracker rows in stream order.  The oracle chain per stream is oracle/detector_ref.py
@@ -71,7 +71,7 @@ def _run_gpu(dtype, frames):
 
     pipeline = importlib.import_module(P.__name__ + ".pipeline")
     pipe = pipeline.StreamPipeline("yolov8s-small.yaml", S, (512, 640), dtype, seed=0, max_tracks=512,
-                                   pipelined=True, inflight=3)
+                                   pipelined=True, inflight=4)
     pipe.set_schedule(1, 1)  # bench.py's schedule with 3 forwards in flight
     fd = frames.cuda()
     pipe.frames.copy_(fd[0])

@@ -115,13 +115,13 @@ def test_reference_driver_loop_through_compat_packages(tmp_path):
 
 def test_pipelined_tracker_stream_matches_serial():
     """pipelined=True (tracker(t) on its own stream, overlapping detector(t+1), double-buffered
-    detections) and inflight=2/3 (detector graphs in flight on their own streams) give exactly the
+    detections) and inflight=2/3/4 (detector graphs in flight on their own streams) give exactly the
     serial pipeline's tracker state."""
     P = pkg()
     pipeline = importlib.import_module(P.__name__ + ".pipeline")
     S, F = 4, 24
     runs = []
-    for pipelined, inflight in ((False, 1), (True, 1), (True, 2), (True, 3)):
+    for pipelined, inflight in ((False, 1), (True, 1), (True, 2), (True, 3), (True, 4)):
         pipe = pipeline.StreamPipeline("yolov8s-small.yaml", S, (512, 640), "bf16", seed=0, max_tracks=256,
                                        pipelined=pipelined, inflight=inflight)
         scenes = [P.synth.Scene(seed=40 + s, n_targets=16, n_frames=F) for s in range(S)]
