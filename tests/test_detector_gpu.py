@@ -285,3 +285,32 @@ def test_fastw_bit_identical_to_fast(dtype, nnt, npt):
         outs.append([dm.buffer(i, B) for i in range(len(prog.buf_elems))] + [cn] + [dn[b, :cn[b]] for b in range(B)])
     for a, b in zip(*outs):
         np.testing.assert_array_equal(a, b)
+
+
+def test_fp32_nms_max_nms_cap_at_1280():
+    """non_max_suppression's max_nms = 30000 cap (nms.py:138-142): at 1280x1024 / imgsz 1280
+    (108,800 anchors) with conf = 0 every anchor is a candidate, so the kernel keeps the 30,000
+    best-scored (score desc, then anchor order) before the greedy loop.  Checked exactly against
+    the oracle's cap + TorchNMS on the kernel's own candidate rows (as the NMS path test above)."""
+    P, A, W, M = _mods()
+    ar = A.parse_arch(A.load_model_dict("yolov8s-small.yaml"))
+    sd = W.synthetic_state_dict(ar, 0)
+    prog = M.Program(ar, sd, 1024, 1280, 1280, 1, "fp32")
+    dm = M.DeviceModel(prog)
+    sc = P.synth.Scene(seed=5, n_targets=64, n_frames=2, height=1024, width=1280)
+    ft = torch.from_numpy(sc.frame(0)[None].copy()).cuda()
+    dets, counts = dm.detect(ft, 0.0, 0.7, 300)
+    cand, cnt = dm.candidates(1)
+    torch.cuda.synchronize()
+    n_anchors = sum((1024 // s) * (1280 // s) for s in (4, 8, 16, 32))
+    assert int(cnt[0]) == n_anchors == 108800
+    rows = torch.from_numpy(cand[0, : int(cnt[0])].copy())
+    anchor = rows[:, 5].view(torch.int32).long()
+    x = rows[anchor.argsort()]
+    x[:, 5] = 0.0
+    x = x[x[:, 4].sort(descending=True, stable=True)[1][:30000]]  # nms.py:138-142
+    keep = D.torch_nms(x[:, :4], x[:, 4], 0.7)[:300]
+    ref = D.scale_clip(x[keep].clone(), (1024, 1280), (1024, 1280))
+    n = int(counts[0])
+    assert n == len(ref) == 300
+    np.testing.assert_array_equal(dets[0, :n].cpu().numpy(), ref.numpy())
