@@ -399,6 +399,41 @@ def run_leg(a, P, cfg, dtype, frames, dev, local, rank, ws, headline):
     return leg
 
 
+def run_leg_subprocess(dtype):
+    """One more leg (same workload and protocol, another conv dtype) as its own bench.py process;
+    returns its leg dict.  Only used at world size 1 (secondary legs)."""
+    skip = {"--dtype", "--secondary", "--dump-ops", "--plan-in", "--plan-out", "--gpus"}
+    argv, i = [], 1
+    while i < len(sys.argv):
+        t = sys.argv[i]
+        key = t.split("=", 1)[0]
+        if key in skip:
+            i += 1 if "=" in t else 2
+            continue
+        if key in ("--no-cpu-baseline", "--save-plans"):
+            i += 1
+            continue
+        argv.append(t)
+        i += 1
+    cmd = [sys.executable, os.path.abspath(__file__)] + argv + ["--dtype", dtype, "--secondary", "none",
+                                                                  "--no-cpu-baseline"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    sys.stderr.write(r.stderr)
+    if r.returncode != 0:
+        raise SystemExit(f"secondary leg {dtype} failed (exit {r.returncode})")
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    c = d["config"]
+    leg = {"dtype": dtype, "value": d["value"], "ms_per_step": d["ms_per_step"],
+           "network_mfma_frac": d["network_mfma_frac"], "live_tracks_per_stream": c["live_tracks_per_stream"],
+           "live_tracks_per_stream_min_at_start": c["live_tracks_per_stream_min_at_start"],
+           "overflow": c["tracker_overflow"], "tracks_created": c["tracks_created"], "conv_plan": c["conv_plan"],
+           "process": "own", "gflop_per_frame": c["gflop_per_frame"]}
+    for k in ("roofline", "tracker_roofline"):
+        if d.get(k) is not None:
+            leg[k] = d[k]
+    return leg
+
+
 def main():
     a = parse()
     if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -433,8 +468,11 @@ def main():
     torch.cuda.synchronize()
     log(f"{F} frames x {S} streams resident; headline leg {dtype}, secondary {secondary or 'none'}")
     head = run_leg(a, P, cfg, dtype, frames, dev, local, rank, ws, headline=True)
-    legs = [run_leg(a, P, cfg, d, frames, dev, local, rank, ws, headline=False) for d in secondary]
     del frames
+    # each secondary leg runs in a fresh process: a second StreamPipeline built in the same
+    # process after the first one was torn down measured 20-25 % slower on either dtype
+    # (bf16 12,313 as the first leg vs 9,742 as the second; fp32 4,877 vs 4,323)
+    legs = [run_leg_subprocess(d) for d in secondary]
     cpu = None
     if rank == 0 and ws == 1 and not a.no_cpu_baseline:
         ncpu = os.cpu_count() or 2
