@@ -88,6 +88,10 @@ def parse():
     ap.add_argument("--lanes", type=int, default=None)
     ap.add_argument("--groups", type=int, default=1, help="independent sub-batches run concurrently")
     ap.add_argument("--tracker", default="enhanced", choices=["enhanced", "motion_reset"])
+    ap.add_argument("--gmd", action="store_true",
+                    help="with --tracker motion_reset: also run GlobalMotionDetector('optical_flow') on every frame "
+                         "(MotionCompensatedMultiTracker.update(dets, frame)); no CPU baseline (the oracle's numpy "
+                         "restatement of cv2's optical flow is not a stand-in for cv2's speed)")
     ap.add_argument("--inflight", type=int, default=4, choices=range(1, 9),
                     help="detector forwards in flight (each a batch of all streams, own graph + HIP stream)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -305,7 +309,8 @@ def run_leg(a, P, cfg, dtype, frames, dev, local, rank, ws, headline):
     pipe = pipeline.StreamPipeline(f"yolov8{a.scale}-small.yaml", S, (H, W), dtype, seed=0, device=local,
                                    pipelined=not a.no_pipeline, imgsz=imgsz, max_tracks=cfg["max_tracks"],
                                    inflight=1 if a.no_pipeline else a.inflight,
-                                   tracker_policy=1 if a.tracker == "motion_reset" else 0)
+                                   tracker_policy=1 if a.tracker == "motion_reset" else 0,
+                                   motion_method="optical_flow" if a.gmd else None)
     pipe.set_schedule(a.groups, lanes)
     pipe.frames.copy_(frames[0])
     plan_src = "heuristic"
@@ -436,6 +441,8 @@ def run_leg_subprocess(dtype):
 
 def main():
     a = parse()
+    if a.gmd and a.tracker != "motion_reset":
+        raise SystemExit("--gmd needs --tracker motion_reset")
     if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn_ranks(a.gpus))
     ws, rank, local = dist_setup()
@@ -474,7 +481,7 @@ def main():
     # (bf16 12,313 as the first leg vs 9,742 as the second; fp32 4,877 vs 4,323)
     legs = [run_leg_subprocess(d) for d in secondary]
     cpu = None
-    if rank == 0 and ws == 1 and not a.no_cpu_baseline:
+    if rank == 0 and ws == 1 and not a.no_cpu_baseline and not a.gmd:
         ncpu = os.cpu_count() or 2
         ref_threads = max(1, min(8, ncpu - 1))  # the reference's select_device for CPU
         cpu = cpu_baseline(P, a.scale, S, cfg["targets"], (H, W), cfg["imgsz"], a.tracker, ref_threads, a.cpu_seconds)
@@ -503,7 +510,8 @@ def main():
                        "live_tracks_floor": cfg["live_floor"], "live_tracks_floor_met": ok_floor,
                        "tracker_overflow": head["overflow"], "tracks_created": head["tracks_created"],
                        "conv_plan": head["conv_plan"], "graph": not a.no_graph, "tracker_overlapped": not a.no_pipeline,
-                       "detector_inflight": a.inflight, "gflop_per_frame": head["gflop_per_frame"]},
+                       "detector_inflight": a.inflight, "gflop_per_frame": head["gflop_per_frame"],
+                       "global_motion": "optical_flow" if a.gmd else None},
             "network_mfma_frac": head["network_mfma_frac"],
             "pcie_inclusive_fps": head.get("pcie_inclusive_fps"),
             "roofline": head.get("roofline"), "tracker_roofline": head.get("tracker_roofline"),

@@ -139,3 +139,40 @@ def test_pipelined_tracker_stream_matches_serial():
         np.testing.assert_array_equal(s0, s1)
         for s in range(S):
             assert r0[s][: c0[s]].tobytes() == r1[s][: c1[s]].tobytes()
+
+
+def test_pipeline_with_global_motion_matches_serial():
+    """StreamPipeline(tracker_policy=1, motion_method='optical_flow') -- the
+    MotionCompensatedMultiTracker.update(dets, frame) loop with GlobalMotionDetector on the
+    device -- gives the serial pipeline's tracker and motion-detector state when the motion
+    detector reads each slot's frames on the tracker stream with forwards in flight.  The frames
+    are camera pans over a textured world (tests/gmd_helpers.py) with whip pans that trigger the
+    global reset branch."""
+    from gmd_helpers import camera_sequence
+
+    P = pkg()
+    pipeline = importlib.import_module(P.__name__ + ".pipeline")
+    S, F = 3, 20
+    seqs = [camera_sequence(80 + s, F, h=512, w=640, whip_at=(7, 14), n_targets=12)[0] for s in range(S)]
+    frames = torch.from_numpy(np.stack(seqs, 1)).cuda()  # [F, S, H, W, 3]
+    runs = []
+    for pipelined, inflight in ((False, 1), (True, 1), (True, 3)):
+        pipe = pipeline.StreamPipeline("yolov8s-small.yaml", S, (512, 640), "bf16", seed=0, max_tracks=256,
+                                       pipelined=pipelined, inflight=inflight, tracker_policy=1,
+                                       motion_method="optical_flow")
+        pipe.frames.copy_(frames[0])
+        pipe.capture(tune=False)
+        for t in range(F):
+            pipe.run(frames[t])
+        pipe.sync()
+        rows, counts, stats = pipe.tracker.download()
+        motion, mstats = pipe.gmd.download()
+        runs.append((rows.copy(), counts.copy(), stats.copy(), motion.copy(), mstats.copy()))
+    r0, c0, s0, m0, ms0 = runs[0]
+    assert int(ms0["reset_triggers"].sum()) > 0  # the whip pans reached the global reset branch
+    for r1, c1, s1, m1, ms1 in runs[1:]:
+        np.testing.assert_array_equal(c0, c1)
+        np.testing.assert_array_equal(s0, s1)
+        assert m0.tobytes() == m1.tobytes() and ms0.tobytes() == ms1.tobytes()
+        for s in range(S):
+            assert r0[s][: c0[s]].tobytes() == r1[s][: c1[s]].tobytes()

@@ -13,6 +13,13 @@ tracker state, so it starts while tracker(t) is still running.  D
 double-buffered; detector(t+2) waits for tracker(t) to have read its buffer.  Results are
 identical to the serial order (the tracker still sees frames in order on one stream).
 
+``motion_method='optical_flow'`` (with ``tracker_policy=1``, the camera-motion-compensation
+tracker) adds the global camera-motion branch of MotionCompensatedMultiTracker.update(dets,
+frame) (motion_compensated_multi_tracker.py:94-121): GlobalMotionDetector on every stream's
+frame (motion.BatchedMotionDetector, gmd.hip) on the tracker stream right before the tracker
+step, which consumes its device results.  The frame slot is not refilled before that detector
+has read it.
+
 ``inflight=D`` > 1 (needs ``pipelined``) keeps D detector forwards in flight: D DeviceModels
 (same program and conv plan, each its own activation arena) replay their hipGraphs on D HIP
 streams, step t on slot t % D with its own detection buffer.  Every forward is still one batch of the S streams' frames;
@@ -37,7 +44,7 @@ class StreamPipeline:
                  dtype: str = "bf16", weights=None, seed: int = 0, conf: float = 0.25, iou: float = 0.7,
                  max_det: int = 300, max_lost_frames: int = 150, min_hits: int = 1, iou_threshold: float = 0.1,
                  max_tracks: int = 512, device: int = 0, pipelined: bool = False, imgsz=640, inflight: int = 1,
-                 tracker_policy: int = 0):
+                 tracker_policy: int = 0, motion_method: str | None = None):
         if conf < 0.1:
             raise ValueError("conf < 0.1 would need the driver's score > 0.1 filter on the device path")
         self.S, self.device = int(n_streams), int(device)
@@ -71,6 +78,15 @@ class StreamPipeline:
         self.models = [self.model] + [M.DeviceModel(self.prog, self.device) for _ in range(self.D - 1)]
         self.frame_slots = [self.frames] + [torch.zeros_like(self.frames) for _ in range(self.D - 1)]
         self.det_streams = [None] + [torch.cuda.Stream(dev) for _ in range(self.D - 1)]
+        self.gmd = None
+        if motion_method is not None:
+            if tracker_policy != 1:
+                raise ValueError("motion_method needs tracker_policy=1 (the camera-motion-compensation tracker)")
+            from . import motion as Mo
+
+            self.gmd = Mo.BatchedMotionDetector(self.S, frame_hw[0], frame_hw[1], motion_method, self.device)
+        self._ev_gmd = [torch.cuda.Event() for _ in range(self.D)]  # slot's frames read by the motion detector
+        self._gmd_pending = [False] * self.D
 
     @property
     def dets(self) -> torch.Tensor:
@@ -130,16 +146,27 @@ class StreamPipeline:
             self._ev_det[k].record(cur)
             self.trk_stream.wait_event(self._ev_det[k])
             with torch.cuda.stream(self.trk_stream):
-                self.tracker.step_device(self._dets[k], self._counts[k])
+                self._track(k, s)
             self._ev_trk[k].record(self.trk_stream)
             self._trk_pending[k] = True
         else:
-            self.tracker.step_device(self._dets[k], self._counts[k])
+            self._track(k, s)
         if self.step_hook is not None:
             # harness hook (tests/recorders): enqueue work after this step's launches on the
             # detector stream (reads of detection buffer k) and the tracker stream (results)
             self.step_hook(self, k, cur, self.trk_stream if self.pipelined else cur)
         self._k = (k + 1) % self.nb
+
+    def _track(self, k: int, s: int):
+        """Tracker step of detection buffer k (frames of slot s) on the current stream."""
+        if self.gmd is None:
+            self.tracker.step_device(self._dets[k], self._counts[k])
+            return
+        self.gmd.detect_device(self.frame_slots[s])
+        if self.pipelined:
+            self._ev_gmd[s].record(torch.cuda.current_stream(self.device))
+            self._gmd_pending[s] = True
+        self.tracker.step_device(self._dets[k], self._counts[k], motion=self.gmd.motion_ptr)
 
     def sync(self):
         """Wait for every launched step (detector and tracker streams)."""
@@ -155,6 +182,9 @@ class StreamPipeline:
         if st != cur:
             st.wait_stream(cur)
             frames.record_stream(st)  # the allocator keeps `frames` alive until the copy ran
+        if self._gmd_pending[s]:  # the motion detector (tracker stream) still reads this slot's frames
+            st.wait_event(self._ev_gmd[s])
+            self._gmd_pending[s] = False
         with torch.cuda.stream(st):
             self.frame_slots[s].copy_(frames, non_blocking=True)
         self.step()
