@@ -164,23 +164,33 @@ __global__ void clear_kernel(Dev g) {
 
 // cornerMinEigenVal on a 16x16 output tile: the 22x22 Sobel-product halo (box radius 3; the
 // products outside the image are those of the reflected pixel, like boxFilter's reflect-101
-// border over the product image), 7-wide horizontal then vertical integer sums.
+// border over the product image), 7-wide horizontal then vertical integer sums.  The gray pixels
+// the Sobel taps of those products read -- rows / columns [o - 1, o + 23) of the image, each
+// product at its reflected position with Sobel's own reflect-101 neighbours -- are staged in LDS
+// once (coalesced rows), so a product costs LDS reads instead of eight global byte loads.
 __global__ void __launch_bounds__(256) eig_kernel(Dev g, int prev) {
+  __shared__ int gt[24][25];
   __shared__ int pxx[22][23], pxy[22][23], pyy[22][23];
   __shared__ int hxx[22][17], hxy[22][17], hyy[22][17];
   __shared__ unsigned wmax[4];
   const int s = blockIdx.z, W = g.geo.W, H = g.geo.H, tid = threadIdx.x;
   const unsigned char* img = g.pyr[prev] + (long long)s * g.geo.per;
   const int ox = blockIdx.x * 16 - 3, oy = blockIdx.y * 16 - 3;
+  const int gy0 = oy - 1, gx0 = ox - 1;  // LDS tile origin (image coordinates)
+  for (int i = tid; i < 24 * 24; i += 256) {
+    const int ry = i / 24, rx = i - ry * 24;
+    const int y = gy0 + ry, x = gx0 + rx;
+    gt[ry][rx] = (y >= 0 && y < H && x >= 0 && x < W) ? (int)img[(long long)y * W + x] : 0;
+  }
+  __syncthreads();
+  auto cl = [](int v) { return v < 0 ? 0 : (v > 23 ? 23 : v); };  // only outputs outside the image clamp
   for (int i = tid; i < 22 * 22; i += 256) {
     const int ry = i / 22, rx = i - ry * 22;
     const int y = refl_c(oy + ry, H), x = refl_c(ox + rx, W);
-    const unsigned char* a = img + (long long)refl(y - 1, H) * W;
-    const unsigned char* b = img + (long long)y * W;
-    const unsigned char* c = img + (long long)refl(y + 1, H) * W;
-    const int xm = refl(x - 1, W), xp = refl(x + 1, W);
-    const int ix = (a[xp] - a[xm]) + 2 * (b[xp] - b[xm]) + (c[xp] - c[xm]);
-    const int iy = (c[xm] + 2 * c[x] + c[xp]) - (a[xm] + 2 * a[x] + a[xp]);
+    const int ya = cl(refl(y - 1, H) - gy0), yb = cl(y - gy0), yc = cl(refl(y + 1, H) - gy0);
+    const int xm = cl(refl(x - 1, W) - gx0), xc = cl(x - gx0), xp = cl(refl(x + 1, W) - gx0);
+    const int ix = (gt[ya][xp] - gt[ya][xm]) + 2 * (gt[yb][xp] - gt[yb][xm]) + (gt[yc][xp] - gt[yc][xm]);
+    const int iy = (gt[yc][xm] + 2 * gt[yc][xc] + gt[yc][xp]) - (gt[ya][xm] + 2 * gt[ya][xc] + gt[ya][xp]);
     pxx[ry][rx] = ix * ix;
     pxy[ry][rx] = ix * iy;
     pyy[ry][rx] = iy * iy;
@@ -228,46 +238,72 @@ __global__ void __launch_bounds__(256) eig_kernel(Dev g, int prev) {
   if (tid == 0) {
     unsigned b = wmax[0];
     for (int i = 1; i < 4; ++i) b = wmax[i] > b ? wmax[i] : b;
-    atomicMax(&g.emax[s], b);
+    // the per-stream maximum only grows: a workgroup whose maximum does not exceed a value
+    // already there skips the atomic (1,280 same-address atomics per stream serialised at L2)
+    if (b > __hip_atomic_load(&g.emax[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(&g.emax[s], b);
   }
 }
 
+// CPX pixels per thread (a workgroup covers 256 * CPX consecutive pixels); the workgroup's
+// candidates take one global atomic (per-stream counter), not one per wave.
+constexpr int CPX = 4;
 __global__ void __launch_bounds__(256) cand_kernel(Dev g) {
-  const int s = blockIdx.y, W = g.geo.W, H = g.geo.H;
+  __shared__ int wcnt[4], wbase[4];
+  const int s = blockIdx.y, W = g.geo.W, H = g.geo.H, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const long long HW = (long long)W * H;
-  const long long p = (long long)blockIdx.x * 256 + threadIdx.x;
   const float thr = (float)((double)unord_bits(g.emax[s]) * 0.01);  // maxVal * qualityLevel
-  bool c = false;
-  unsigned long long key = 0;
-  if (p < HW) {
-    const int y = (int)(p / W), x = (int)(p - (long long)y * W);
-    if (x >= 1 && x <= W - 2 && y >= 1 && y <= H - 2) {
-      const float* e = g.eig + s * HW;
-      auto T = [&](float v) { return v > thr ? v : 0.0f; };  // THRESH_TOZERO
-      const float tp = T(e[p]);
-      if (tp != 0.0f) {
-        float m = tp;  // dilate(3x3) of the thresholded image
+  const float* e = g.eig + s * HW;
+  auto T = [&](float v) { return v > thr ? v : 0.0f; };  // THRESH_TOZERO
+  bool c[CPX];
+  unsigned long long key[CPX];
+  int mine = 0;
 #pragma unroll
-        for (int dy = -1; dy <= 1; ++dy)
+  for (int u = 0; u < CPX; ++u) {
+    const long long p = ((long long)blockIdx.x * CPX + u) * 256 + tid;
+    c[u] = false;
+    key[u] = 0;
+    if (p < HW) {
+      const int y = (int)(p / W), x = (int)(p - (long long)y * W);
+      if (x >= 1 && x <= W - 2 && y >= 1 && y <= H - 2) {
+        const float tp = T(e[p]);
+        if (tp != 0.0f) {
+          float m = tp;  // dilate(3x3) of the thresholded image
 #pragma unroll
-          for (int dx = -1; dx <= 1; ++dx) {
-            const float v = T(e[p + (long long)dy * W + dx]);
-            m = v > m ? v : m;
-          }
-        c = tp == m;
-        key = ((unsigned long long)ord_bits(tp) << 32) | (unsigned)p;
+          for (int dy = -1; dy <= 1; ++dy)
+#pragma unroll
+            for (int dx = -1; dx <= 1; ++dx) {
+              const float v = T(e[p + (long long)dy * W + dx]);
+              m = v > m ? v : m;
+            }
+          c[u] = tp == m;
+          key[u] = ((unsigned long long)ord_bits(tp) << 32) | (unsigned)p;
+        }
       }
     }
+    mine += c[u] ? 1 : 0;
   }
-  const unsigned long long mask = __ballot(c);
-  if (mask) {
-    const int lane = threadIdx.x & 63;
-    const int leader = __ffsll((long long)mask) - 1;
-    int base = 0;
-    if (lane == leader) base = atomicAdd(&g.ncand[s], __popcll(mask));
-    base = __shfl(base, leader);
-    if (c) g.cand[s * HW + base + __popcll(mask & ((1ull << lane) - 1ull))] = key;
+  // workgroup prefix of the candidate counts: lanes, then waves
+  int incl = mine;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int v = __shfl_up(incl, d);
+    if (lane >= d) incl += v;
   }
+  if (lane == 63) wcnt[wave] = incl;
+  __syncthreads();
+  if (tid == 0) {
+    const int tot = wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
+    const int base = tot ? atomicAdd(&g.ncand[s], tot) : 0;
+    wbase[0] = base;
+    wbase[1] = base + wcnt[0];
+    wbase[2] = base + wcnt[0] + wcnt[1];
+    wbase[3] = base + wcnt[0] + wcnt[1] + wcnt[2];
+  }
+  __syncthreads();
+  int o = wbase[wave] + incl - mine;
+#pragma unroll
+  for (int u = 0; u < CPX; ++u)
+    if (c[u]) g.cand[s * HW + o++] = key[u];
 }
 
 struct SelLds {
@@ -909,7 +945,8 @@ int yk_gmd_detect(yk_gmd* g, const uint8_t* frames, yk_motion* out, void* stream
   if (g->frames > 0) {
     hipLaunchKernelGGL(yk::gmd::clear_kernel, dim3((S + 255) / 256), dim3(256), 0, st, d);
     hipLaunchKernelGGL(yk::gmd::eig_kernel, dim3((G.W + 15) / 16, (G.H + 15) / 16, S), dim3(256), 0, st, d, prev);
-    hipLaunchKernelGGL(yk::gmd::cand_kernel, dim3((unsigned)((HW + 255) / 256), S), dim3(256), 0, st, d);
+    hipLaunchKernelGGL(yk::gmd::cand_kernel, dim3((unsigned)((HW + 256 * yk::gmd::CPX - 1) / (256 * yk::gmd::CPX)), S),
+                       dim3(256), 0, st, d);
     hipLaunchKernelGGL(yk::gmd::select_kernel, dim3(S), dim3(yk::gmd::NTS), yk::gmd::SEL_LDS, st, d);
     hipLaunchKernelGGL(yk::gmd::lk_kernel, dim3(yk::gmd::MAXC / 4, S), dim3(256), 0, st, d, prev, cur);
   }
