@@ -461,22 +461,45 @@ __global__ void __launch_bounds__(NTS) select_kernel(Dev g) {
       L.cy[tid] = y;
       __syncthreads();
       if (wave == 0) {  // in-chunk conflicts, in sorted order
+        // The chunk's candidates 64 at a time in registers (lane l holds candidate c0 + l); the
+        // ones that passed the test against the earlier chunks' corners are walked in order
+        // through a ballot mask, and the corners accepted in this chunk stay in registers (lane
+        // l, slot k holds accepted corner na0 + l + 64 k; at most MAXC < 256 of them).
         int na = na0;
         const int cm = m - base < NTS ? m - base : NTS;
-        for (int c = 0; c < cm && na < MAXC; ++c) {
-          if (!L.cok[c]) continue;
-          const int xc = L.cx[c], yc = L.cy[c];
-          bool conflict = false;
-          for (int q = na0 + lane; q < na; q += 64) {
-            const int dx = xc - L.ax[q], dy = yc - L.ay[q];
-            conflict |= dx * dx + dy * dy < MINDIST2;
-          }
-          if (__ballot(conflict) == 0ull) {
-            if (lane == 0) {
-              L.ax[na] = xc;
-              L.ay[na] = yc;
+        int rx[4] = {0, 0, 0, 0}, ry[4] = {0, 0, 0, 0};
+        for (int c0 = 0; c0 < cm && na < MAXC; c0 += 64) {
+          const int c = c0 + lane;
+          const bool okc = c < cm && L.cok[c] != 0;
+          const int xl = okc ? L.cx[c] : 0, yl = okc ? L.cy[c] : 0;
+          unsigned long long todo = __ballot(okc);
+          while (todo != 0ull && na < MAXC) {
+            const int b = __ffsll((long long)todo) - 1;
+            todo &= todo - 1ull;
+            const int xc = __builtin_amdgcn_readlane(xl, b), yc = __builtin_amdgcn_readlane(yl, b);
+            const int nin = na - na0;
+            bool conflict = false;
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+              if (lane + 64 * k < nin) {
+                const int dx = xc - rx[k], dy = yc - ry[k];
+                conflict |= dx * dx + dy * dy < MINDIST2;
+              }
+            if (__ballot(conflict) == 0ull) {
+              if (lane == (nin & 63)) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                  if ((nin >> 6) == k) {
+                    rx[k] = xc;
+                    ry[k] = yc;
+                  }
+              }
+              if (lane == 0) {
+                L.ax[na] = xc;
+                L.ay[na] = yc;
+              }
+              ++na;
             }
-            ++na;  // LDS operations of one wave complete in order: the next test sees it
           }
         }
         if (lane == 0) L.misc[S_NA] = na;
