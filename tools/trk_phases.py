@@ -21,11 +21,12 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--config", type=int, default=3)
 ap.add_argument("--frames", type=int, default=200)
 ap.add_argument("--streams", type=int, default=8)
+ap.add_argument("--policy", type=int, default=0, help="0 enhanced, 1 motion-reset (camera_motion_compensation)")
 a = ap.parse_args()
 c = CFG[a.config]
 S, F = a.streams, a.frames
 pipe = pipeline.StreamPipeline("yolov8s-small.yaml", S, (c["H"], c["W"]), c["dtype"], seed=0, imgsz=c["imgsz"],
-                               max_tracks=c["max_tracks"])
+                               max_tracks=c["max_tracks"], tracker_policy=a.policy)
 scenes = [P.synth.Scene(seed=s, n_targets=c["targets"], n_frames=F, width=c["W"], height=c["H"]) for s in range(S)]
 pipe.frames.copy_(torch.stack([sc.frames_torch(0, 1, "cuda")[0] for sc in scenes]))
 pipe.capture(tune=False)
