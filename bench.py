@@ -404,13 +404,13 @@ def run_leg(a, P, cfg, dtype, frames, dev, local, rank, ws, headline):
     return leg
 
 
-def run_leg_subprocess(dtype):
-    """One more leg (same workload and protocol, another conv dtype) as its own bench.py process;
-    returns its leg dict.  Only used at world size 1 (secondary legs)."""
+def leg_argv(argv, dtype):
+    """bench.py's own arguments for a secondary leg: the same workload and protocol, `dtype` as
+    the only leg, no CPU baseline, no plan / op-dump outputs, one process (no --gpus)."""
     skip = {"--dtype", "--secondary", "--dump-ops", "--plan-in", "--plan-out", "--gpus"}
-    argv, i = [], 1
-    while i < len(sys.argv):
-        t = sys.argv[i]
+    out, i = [], 0
+    while i < len(argv):
+        t = argv[i]
         key = t.split("=", 1)[0]
         if key in skip:
             i += 1 if "=" in t else 2
@@ -418,10 +418,15 @@ def run_leg_subprocess(dtype):
         if key in ("--no-cpu-baseline", "--save-plans"):
             i += 1
             continue
-        argv.append(t)
+        out.append(t)
         i += 1
-    cmd = [sys.executable, os.path.abspath(__file__)] + argv + ["--dtype", dtype, "--secondary", "none",
-                                                                  "--no-cpu-baseline"]
+    return out + ["--dtype", dtype, "--secondary", "none", "--no-cpu-baseline"]
+
+
+def run_leg_subprocess(dtype):
+    """One more leg (same workload and protocol, another conv dtype) as its own bench.py process;
+    returns its leg dict.  Only used at world size 1 (secondary legs)."""
+    cmd = [sys.executable, os.path.abspath(__file__)] + leg_argv(sys.argv[1:], dtype)
     r = subprocess.run(cmd, capture_output=True, text=True)
     sys.stderr.write(r.stderr)
     if r.returncode != 0:
