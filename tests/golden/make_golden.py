@@ -17,6 +17,11 @@ generators of synth.py / tests/cmc_sequences.py; only the expected outputs are s
                        (Results.boxes.data), plus the Detect candidates above conf
   nms.npz              TorchNMS.nms keep lists (utils/nms.py:237-304, quirk C) on seeded box sets
   letterbox.npz        LetterBox(640) canvases of a 1920x1080 and a 400x300 frame (sha256 + rows)
+  gmd_pan.npz          GlobalMotionDetector('optical_flow').detect_motion on a 12-frame camera pan
+                       with two whip pans (tests/gmd_helpers.py, 256x320): per-frame results,
+                       stats, and every frame's corners / LK end points / status
+  bytetrack.npz        BYTETracker and BOTSORT (no ReID / GMC) on a 40-frame detection sequence
+                       (tests/bt_helpers.py): every frame's output rows
 """
 from __future__ import annotations
 
@@ -172,6 +177,67 @@ def run_letterbox_oracle():
     return out
 
 
+# ------------------------------------------------------------------ global motion, ByteTrack
+def gmd_inputs():
+    from gmd_helpers import camera_sequence
+
+    frames, _ = camera_sequence(11, 12, h=256, w=320, whip_at=(5, 9), n_targets=4)
+    return frames
+
+
+def run_gmd_oracle():
+    from oracle import gmd_ref as R
+
+    det = R.RefGlobalMotionDetector()
+    res, corners, nxt, status, ncorn = [], [], [], [], []
+    for f in gmd_inputs():
+        m, mag, vec, rst = det.detect_motion(f)
+        res.append([float(bool(m)), float(mag), float(vec[0]), float(vec[1]), float(bool(rst))])
+        dbg = getattr(det, "last_debug", None) or {}
+        c = dbg.get("corners")
+        k = 0 if c is None else len(c)
+        buf_c = np.zeros((200, 2), np.float32)
+        buf_n = np.zeros((200, 2), np.float32)
+        buf_s = np.zeros(200, np.uint8)
+        if k:
+            buf_c[:k] = np.asarray(c, np.float32).reshape(-1, 2)
+            if dbg.get("next") is not None:
+                buf_n[:k] = np.asarray(dbg["next"], np.float32).reshape(-1, 2)
+                buf_s[:k] = np.asarray(dbg["status"]).reshape(-1)
+        corners.append(buf_c)
+        nxt.append(buf_n)
+        status.append(buf_s)
+        ncorn.append(k)
+        det.last_debug = None
+    st = det.stats
+    return {"res": np.array(res, np.float64), "corners": np.stack(corners), "next": np.stack(nxt),
+            "status": np.stack(status), "ncorners": np.array(ncorn, np.int32),
+            "stats": np.array([st["total_detections"], st["motion_events"], st["reset_triggers"]], np.int64),
+            "avg_mag": np.array([st["avg_motion_magnitude"]], np.float64)}
+
+
+def bytetrack_inputs():
+    from bt_helpers import scenario
+
+    return scenario(31, n_targets=30, n_frames=40)
+
+
+def run_bytetrack_oracle():
+    from oracle import bytetrack_ref as R
+
+    out = {}
+    for kind, cfg in (("bytetrack", R.BYTETRACK_CFG), ("botsort", R.BOTSORT_CFG)):
+        ref = R.RefTracker(dict(cfg), ids=R.IdCounter())
+        rows, off = [], [0]
+        for x, c, k in bytetrack_inputs():
+            r = np.asarray(ref.update(R.Dets(x, c, k)), np.float32).reshape(-1, 8)
+            rows.append(r)
+            off.append(off[-1] + len(r))
+        out[f"{kind}_rows"] = np.concatenate(rows) if rows else np.zeros((0, 8), np.float32)
+        out[f"{kind}_off"] = np.array(off, np.int64)
+    return out
+
+
 GENERATORS = {
     "tracker_c3": lambda: run_tracker_oracle("tracker_c3"),
     "tracker_c5": lambda: run_tracker_oracle("tracker_c5"),
@@ -180,6 +246,8 @@ GENERATORS = {
     "detector_n": run_detector_oracle,
     "nms": run_nms_oracle,
     "letterbox": run_letterbox_oracle,
+    "gmd_pan": run_gmd_oracle,
+    "bytetrack": run_bytetrack_oracle,
 }
 
 

@@ -40,3 +40,13 @@ def test_oracle_nms_and_letterbox_reproduce_golden():
     want, got = G.load("letterbox"), G.run_letterbox_oracle()
     for k in want:
         np.testing.assert_array_equal(got[k], want[k])
+
+
+def test_oracle_global_motion_and_bytetrack_reproduce_golden():
+    want, got = G.load("gmd_pan"), G.run_gmd_oracle()
+    for k in want:
+        np.testing.assert_array_equal(got[k], want[k], err_msg=k)
+    assert int(want["stats"][2]) >= 1  # the whip pans reach the reset branch
+    want, got = G.load("bytetrack"), G.run_bytetrack_oracle()
+    for k in want:
+        np.testing.assert_array_equal(got[k], want[k], err_msg=k)

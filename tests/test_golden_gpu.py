@@ -79,3 +79,61 @@ def test_device_letterbox_matches_golden():
         c = dm.letterboxed(1)[0]
         assert list(c.shape) == want[f"shape_{w}x{h}"].tolist()
         assert hashlib.sha256(c.tobytes()).digest() == want[f"sha_{w}x{h}"].tobytes()
+
+
+def _f32bits(x):
+    return np.asarray(x, np.float32).view(np.int32)
+
+
+def test_global_motion_kernels_match_golden():
+    """gmd.hip on the gmd_pan fixture: per-frame results bit-exact (float32 magnitude / vector),
+    corners, LK status and the end points of tracked corners bit-exact, stats exact."""
+    import importlib
+
+    M = importlib.import_module(pkg().__name__ + ".motion")
+    want = G.load("gmd_pan")
+    frames = G.gmd_inputs()
+    det = M.BatchedMotionDetector(1, frames.shape[1], frames.shape[2])
+    for t, f in enumerate(frames):
+        det.detect_host([f])
+        m, st = det.download()
+        r = want["res"][t]
+        assert bool(m[0]["is_motion"]) == bool(r[0]) and bool(m[0]["should_reset"]) == bool(r[4]), f"frame {t}"
+        if int(m[0]["magnitude_kind"]) == 1:
+            assert _f32bits(m[0]["magnitude"]) == _f32bits(r[1]), f"frame {t}"
+            assert (_f32bits(m[0]["vector"]) == _f32bits(r[2:4])).all(), f"frame {t}"
+        else:
+            assert r[1] == 0.0, f"frame {t}"
+        if t:
+            c, nx, sts = det.points(0)
+            k = int(want["ncorners"][t])
+            assert len(c) == k and (c == want["corners"][t, :k]).all(), f"frame {t}: corners"
+            if k:
+                assert (sts == want["status"][t, :k]).all(), f"frame {t}: status"
+                ok = sts == 1
+                assert (_f32bits(nx[ok]) == _f32bits(want["next"][t, :k][ok])).all(), f"frame {t}: LK end points"
+    np.testing.assert_array_equal([int(st[0]["total_detections"]), int(st[0]["motion_events"]),
+                                   int(st[0]["reset_triggers"])], want["stats"])
+
+
+@pytest.mark.parametrize("kind", ["bytetrack", "botsort"])
+def test_bytetrack_kernel_matches_golden(kind):
+    """bytetrack.hip on the bytetrack fixture: every frame's rows in order, ids / score / cls / idx
+    exact, boxes within 1e-3 px (the ByteTrack parity bar)."""
+    import importlib
+
+    from oracle import bytetrack_ref as R
+
+    BT = importlib.import_module(pkg().__name__ + ".bytetrack")
+    want = G.load("bytetrack")
+    rows, off = want[f"{kind}_rows"], want[f"{kind}_off"]
+    cfg = dict(R.BOTSORT_CFG if kind == "botsort" else R.BYTETRACK_CFG)
+    dev = BT.BatchedTracker(cfg, n_streams=1, max_tracks=256, max_dets=128)
+    for t, (x, c, k) in enumerate(G.bytetrack_inputs()):
+        dev.step([np.c_[x, c, k]])
+        got = dev.download()[0]
+        exp = rows[off[t]:off[t + 1]]
+        assert got.shape == exp.shape, f"frame {t + 1}: {got.shape} vs {exp.shape}"
+        if len(exp):
+            np.testing.assert_array_equal(got[:, 4:8], exp[:, 4:8], err_msg=f"frame {t + 1}")
+            np.testing.assert_allclose(got[:, :4], exp[:, :4], rtol=1e-6, atol=1e-3, err_msg=f"frame {t + 1}")
