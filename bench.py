@@ -481,9 +481,10 @@ def main():
     log(f"{F} frames x {S} streams resident; headline leg {dtype}, secondary {secondary or 'none'}")
     head = run_leg(a, P, cfg, dtype, frames, dev, local, rank, ws, headline=True)
     del frames
-    # each secondary leg runs in a fresh process: a second StreamPipeline built in the same
-    # process after the first one was torn down measured 20-25 % slower on either dtype
-    # (bf16 12,313 as the first leg vs 9,742 as the second; fp32 4,877 vs 4,323)
+    # each secondary leg runs in a fresh process: a second StreamPipeline in the same process
+    # measured 10-25 % slower on either dtype (bf16 12,313 as the first leg vs 9,742 as the
+    # second; fp32 4,877 vs 4,323) -- its new HIP streams land on different hardware queues
+    # (tools/second_pipe.py: the second pipeline is as fast as the first on the first one's streams)
     legs = [run_leg_subprocess(d) for d in secondary]
     cpu = None
     if rank == 0 and ws == 1 and not a.no_cpu_baseline and not a.gmd:
