@@ -3,6 +3,7 @@
   null0    slot 0 on the caller's (null) stream, slots 1..3 and the tracker on pool streams (default)
   own0     every detector slot and the tracker on pool streams
   trknull  the tracker on the null stream, the four detector slots on pool streams
+  trkhi    the tracker on a high-priority stream
 usage: stream_map.py --mode MODE [--dtype fp32] [--steps 100]"""
 import argparse
 import importlib
@@ -21,7 +22,13 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--mode", default="null0")
 ap.add_argument("--dtype", default="fp32")
 ap.add_argument("--steps", type=int, default=100)
+ap.add_argument("--shift", type=int, default=0, help="streams created and used before the pipeline's")
 a = ap.parse_args()
+_dummies = [torch.cuda.Stream() for _ in range(a.shift)]
+for _st in _dummies:
+    with torch.cuda.stream(_st):
+        torch.zeros(1, device="cuda").add_(1)
+torch.cuda.synchronize()
 S, H, W, F = 8, 512, 640, 40
 scenes = [P.synth.Scene(seed=s, n_targets=40, n_frames=F + 1) for s in range(S)]
 frames = torch.stack([sc.frames_torch(0, F, "cuda") for sc in scenes], 1).contiguous()
@@ -30,6 +37,8 @@ p = pipeline.StreamPipeline("yolov8s-small.yaml", S, (H, W), a.dtype, seed=0, pi
 null = torch.cuda.current_stream()
 if a.mode == "own0":
     p.det_streams[0] = torch.cuda.Stream()
+elif a.mode == "trkhi":
+    p.trk_stream = torch.cuda.Stream(priority=-1)
 elif a.mode == "trknull":
     p.det_streams[0] = p.trk_stream
     p.trk_stream = null
@@ -46,4 +55,4 @@ for t in range(a.steps):
     p.run(frames[t % F])
 torch.cuda.synchronize()
 dt = time.perf_counter() - t0
-print(json.dumps({"mode": a.mode, "fps": round(S * a.steps / dt, 1)}), flush=True)
+print(json.dumps({"mode": a.mode, "shift": a.shift, "fps": round(S * a.steps / dt, 1)}), flush=True)
