@@ -234,3 +234,10 @@ def test_compat_visualizer_is_the_package_one():
         assert m.TrajectoryVisualizer is V.TrajectoryVisualizer
     finally:
         sys.path.remove(compat)
+
+
+def test_load_source_names(tmp_path):
+    a = np.zeros((4, 4, 3), np.uint8)
+    FR.imwrite(str(tmp_path / "image_7.png"), a)
+    got = FR.load_source([a, str(tmp_path / "image_7.png"), a])
+    assert [p for p, _ in got] == ["image0.jpg", str(tmp_path / "image_7.png"), "image2.jpg"]

@@ -101,8 +101,11 @@ def load_source(source):
     if isinstance(source, (list, tuple)):
         out = []
         for s in source:
-            out.extend(load_source(s))
-        return [(p if not p.startswith("image") else f"image{i}.jpg", f) for i, (p, f) in enumerate(out)]
+            named = isinstance(s, (str, os.PathLike))
+            out.extend((p if named else None, f) for p, f in load_source(s))
+        # in-memory frames are named image{i}.jpg by their position in the batch, as the reference's
+        # LoadPilAndNumpy does (loaders.py:528); files keep their paths
+        return [(p if p is not None else f"image{i}.jpg", f) for i, (p, f) in enumerate(out)]
     if isinstance(source, (str, os.PathLike)):
         out = []
         for f in _expand_paths(source):
