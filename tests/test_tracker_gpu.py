@@ -107,6 +107,28 @@ def test_tracker_many_tracks_and_streams():
             assert int(stats[s]["total_tracks_created"]) == refs[s].stats["total_tracks_created"]
 
 
+@pytest.mark.parametrize("targets", [60, 100])
+def test_tracker_every_pair_candidates_beyond_lds(targets):
+    """iou_threshold 0 makes every (detection, track) pair a candidate: at 2048 x 512 the walk's
+    LDS area holds 2,005 of them, so 60 targets (~3.6k pairs) take the LDS head + global tail
+    path with the rounds on the dead box area, 100 targets (~10k) the rounds on global memory."""
+    yk = pkg()
+    sc = yk.synth.Scene(seed=20 + targets, n_targets=targets, n_frames=12)
+    ms = yk.MultiStreamTracker(1, 150, 1, 0.0, max_tracks=2048, max_dets=512)
+    ref = RefMultiTracker(150, 1, 0.0, stable_ties=True)
+    most = 0
+    for t in range(12):
+        dets = sc.detections(t)
+        ms.step_host([dets])
+        rows, counts, stats = ms.download()
+        most = max(most, len(dets) * int(stats[0]["current_active_tracks"]))
+        rb = ref.update(dets)
+        ours = [yk.tracker._row_to_dict(r, yk.tracker.track_id_of(r["track_num"])) for r in rows[0, : counts[0]]]
+        compare_frame(ours, rb, f"frame {t}")
+        assert int(stats[0]["overflow"]) == 0
+    assert most > (2005 if targets == 60 else 6826)
+
+
 def test_standalone_track_object_ops():
     yk = pkg()
     f = np.float32

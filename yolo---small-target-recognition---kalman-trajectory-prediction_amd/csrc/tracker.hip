@@ -1443,7 +1443,7 @@ struct LdsA {
   double* det;                  // [D][4]
   unsigned long long* row_max;  // [D]   (decisions: int newdet[D])
   unsigned long long* col_max;  // [T]   (decisions: int flags[T])
-  double* red;                  // [16]  block reductions
+  double* red;                  // [3][16] per-wave index bounds
   int* det_match;               // [D]
   int* trk_match;               // [T]
   int* row_arg;                 // [D]
@@ -1451,17 +1451,27 @@ struct LdsA {
   int* order_tmp;               // [T]   pre-step order, then the work items' slots
   int* bins;                    // [2][NB_MAX + 1] bin starts, scatter cursors
   int* misc;                    // [32] counters; [16, 32) wave sums
+  unsigned long long* ck;       // [ccap] candidate keys written by the pair walk (rest: global)
+  int* cp;                      // [ccap] their pairs
+  int ccap;
 };
 constexpr int NTA = 1024;  // assoc_kernel threads: one element per thread in most phases
 constexpr int MA_WSUM = 16;
 
 __host__ __device__ inline size_t assoc_lds_bytes(int T, int D) {
-  return (size_t)T * 32 + (size_t)D * 32 + (size_t)D * 8 + (size_t)T * 8 + 16 * 8 + (size_t)D * 4 +
+  return (size_t)T * 32 + (size_t)D * 32 + (size_t)D * 8 + (size_t)T * 8 + 48 * 8 + (size_t)D * 4 +
          (size_t)T * 4 + (size_t)D * 4 + (size_t)T * 4 + (size_t)T * 4 + 2 * (NB_MAX + 1) * 4 + 32 * 4;
+}
+// candidates kept in LDS: what is left of the 160 KB after the fixed arrays, at most C
+constexpr size_t LDS_CU = 160 * 1024;
+__host__ __device__ inline int assoc_lds_cand(int T, int D, int C) {
+  const size_t b = (assoc_lds_bytes(T, D) + 7) & ~(size_t)7;
+  const size_t k = b < LDS_CU ? (LDS_CU - b) / 12 : 0;
+  return (int)(k < (size_t)C ? k : (size_t)C);
 }
 __host__ __device__ inline size_t tracks_lds_bytes() { return (size_t)IPB * STAGE_D * 8 + (size_t)IPB * 36 + 16; }
 
-__device__ LdsA carve_a(char* base, int T, int D) {
+__device__ LdsA carve_a(char* base, int T, int D, int C) {
   LdsA L;
   L.pb = (double*)base;
   base += (size_t)T * 32;
@@ -1472,7 +1482,7 @@ __device__ LdsA carve_a(char* base, int T, int D) {
   L.col_max = (unsigned long long*)base;
   base += (size_t)T * 8;
   L.red = (double*)base;
-  base += 16 * 8;
+  base += 48 * 8;
   L.det_match = (int*)base;
   base += (size_t)D * 4;
   L.trk_match = (int*)base;
@@ -1486,24 +1496,12 @@ __device__ LdsA carve_a(char* base, int T, int D) {
   L.bins = (int*)base;
   base += 2 * (NB_MAX + 1) * 4;
   L.misc = (int*)base;
+  base += 32 * 4;
+  L.ccap = assoc_lds_cand(T, D, C);
+  L.ck = (unsigned long long*)(((size_t)base + 7) & ~(size_t)7);
+  L.cp = (int*)(L.ck + L.ccap);
   return L;
 }
-
-// block-wide min / max of one double per thread (every thread gets the result)
-template <int NTH>
-__device__ __forceinline__ double block_min(double v, double* red) {
-  constexpr int NW = NTH / 64;
-  for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o));
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
-  __syncthreads();
-  double r = red[0];
-#pragma unroll
-  for (int i = 1; i < NW; ++i) r = fmin(r, red[i]);
-  __syncthreads();
-  return r;
-}
-template <int NTH>
-__device__ __forceinline__ double block_max(double v, double* red) { return -block_min<NTH>(-v, red); }
 
 // exclusive prefix sum of v over the workgroup; total gets the block sum
 template <int NTH>
@@ -1528,8 +1526,8 @@ __device__ __forceinline__ int block_excl_sum(int v, int* wsum, int& total) {
   return base + x - v;
 }
 
-__device__ __forceinline__ int xbin(double x, double x0, double bw, int nb) {
-  const double q = (x - x0) / bw;  // monotone in x
+__device__ __forceinline__ int xbin(double x, double x0, double ibw, int nb) {
+  const double q = (x - x0) * ibw;  // monotone in x (ibw > 0)
   return !(q > 0.0) ? 0 : (q >= (double)(nb - 1) ? nb - 1 : (int)q);
 }
 
@@ -1591,7 +1589,7 @@ __global__ void __launch_bounds__(NTA) assoc_kernel(Dev g, const DT* __restrict_
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int s = blockIdx.x, tid = threadIdx.x;
   const int T = g.T;
-  LdsA L = carve_a(smem, T, g.D);
+  LdsA L = carve_a(smem, T, g.D, g.C);
   Hdr& H = g.hdr[s];
   const Slot* slots = g.slots + (size_t)s * T;
   int* order = g.order + (size_t)s * T;
@@ -1629,6 +1627,19 @@ __global__ void __launch_bounds__(NTA) assoc_kernel(Dev g, const DT* __restrict_
       lw = fmax(lw, w);
     }
   }
+  // the index bounds (min / max left edge, max width): per wave here, across the waves after
+  // the barrier, so the reductions add no barrier; the bin counts are cleared here as well
+  for (int o = 32; o > 0; o >>= 1) {
+    lx0 = fmin(lx0, __shfl_xor(lx0, o));
+    lx1 = fmax(lx1, __shfl_xor(lx1, o));
+    lw = fmax(lw, __shfl_xor(lw, o));
+  }
+  if ((tid & 63) == 0) {
+    L.red[tid >> 6] = lx0;
+    L.red[16 + (tid >> 6)] = lx1;
+    L.red[32 + (tid >> 6)] = lw;
+  }
+  for (int b = tid; b <= NB_MAX; b += NTA) L.bins[b] = 0;
   __syncthreads();
   if (tid == 0) g.phase[s * PH + 1] = wall_clock64();
 
@@ -1636,22 +1647,28 @@ __global__ void __launch_bounds__(NTA) assoc_kernel(Dev g, const DT* __restrict_
   if (D > 0 && n > 0) {
     unsigned long long* ckey = g.cand_key + (size_t)s * g.C;
     int* cflat = g.cand_flat + (size_t)s * g.C;
-    const double x0 = block_min<NTA>(lx0, L.red), x1 = block_max<NTA>(lx1, L.red), wmax = block_max<NTA>(lw, L.red);
+    double x0 = L.red[0], x1 = L.red[16], wmax = L.red[32];
+#pragma unroll
+    for (int w = 1; w < NTA / 64; ++w) {
+      x0 = fmin(x0, L.red[w]);
+      x1 = fmax(x1, L.red[16 + w]);
+      wmax = fmax(wmax, L.red[32 + w]);
+    }
     const bool index = g.thr > 0.0 && x0 <= x1;  // else every pair is tested
+    if (tid == 0) g.phase[s * PH + 20] = wall_clock64();
     const int nb = n < NB_MAX ? n : NB_MAX;
     double bw = (x1 - x0) / (double)nb;
     if (!(bw > 0.0) || !isfinite(bw)) bw = 1.0;
+    const double ibw = 1.0 / bw;         // bins by (x - x0) * ibw: monotone in x like the quotient
     int* bstart = L.bins;                // [nb + 1]: bin starts, [nb] = finite tracks
     int* bcur = L.bins + (NB_MAX + 1);
     int* tsorted = L.col_arg;
     int nfin = 0;
     if (index) {
-      for (int b = tid; b <= nb; b += NTA) bstart[b] = 0;
-      __syncthreads();
       for (int i = tid; i < n; i += NTA) {
         const double* b = &L.pb[4 * i];
         const bool fin = isfinite(b[0]) && isfinite(b[2]) && isfinite(b[2] - b[0]);
-        atomicAdd(&bstart[fin ? xbin(b[0], x0, bw, nb) : nb], 1);
+        atomicAdd(&bstart[fin ? xbin(b[0], x0, ibw, nb) : nb], 1);
       }
       __syncthreads();
       int tot;
@@ -1666,10 +1683,11 @@ __global__ void __launch_bounds__(NTA) assoc_kernel(Dev g, const DT* __restrict_
       for (int i = tid; i < n; i += NTA) {
         const double* b = &L.pb[4 * i];
         const bool fin = isfinite(b[0]) && isfinite(b[2]) && isfinite(b[2] - b[0]);
-        tsorted[atomicAdd(&bcur[fin ? xbin(b[0], x0, bw, nb) : nb], 1)] = i;
+        tsorted[atomicAdd(&bcur[fin ? xbin(b[0], x0, ibw, nb) : nb], 1)] = i;
       }
       __syncthreads();
     }
+    if (tid == 0) g.phase[s * PH + 21] = wall_clock64();
     // candidates (multi:180-232 over the pairs the index admits).  Detection d's pairs are the
     // tracks [k0, k0 + len) of the bin order, then the non-finite tracks; the pairs of all
     // detections are numbered by a prefix sum and every thread walks an equal slice of them
@@ -1689,8 +1707,8 @@ __global__ void __launch_bounds__(NTA) assoc_kernel(Dev g, const DT* __restrict_
           const double dx1 = L.det[4 * d], dx2 = L.det[4 * d + 2];
           if (isfinite(dx1) && isfinite(dx2)) {
             const double lo = (dx1 - wmax) - margin, hi = dx2 + margin;
-            const int b0 = isfinite(lo) ? xbin(lo, x0, bw, nb) : 0;
-            const int b1 = isfinite(hi) ? xbin(hi, x0, bw, nb) : nb - 1;
+            const int b0 = isfinite(lo) ? xbin(lo, x0, ibw, nb) : 0;
+            const int b1 = isfinite(hi) ? xbin(hi, x0, ibw, nb) : nb - 1;
             k0 = bstart[b0];
             k1 = b1 >= b0 ? bstart[b1 + 1] : k0;
           } else {
@@ -1707,6 +1725,7 @@ __global__ void __launch_bounds__(NTA) assoc_kernel(Dev g, const DT* __restrict_
       total += tot;
     }
     __syncthreads();
+    if (tid == 0) g.phase[s * PH + 22] = wall_clock64();
     {
       const int per = (total + NTA - 1) / NTA;
       int p = tid * per;
@@ -1738,9 +1757,14 @@ __global__ void __launch_bounds__(NTA) assoc_kernel(Dev g, const DT* __restrict_
           const double v = iou_mixed<DT>(db, &L.pb[4 * t]);
           if (v >= g.thr) {  // enhanced: iou >= thr (multi:245)
             const int c = atomicAdd(&L.misc[M_NCAND], 1);
-            if (c < g.C) {
-              ckey[c] = (unsigned long long)__double_as_longlong(v);
-              cflat[c] = (d << 16) | t;  // orders like the row-major pair index d * n + t
+            const unsigned long long key = (unsigned long long)__double_as_longlong(v);
+            const int f = (d << 16) | t;  // orders like the row-major pair index d * n + t
+            if (c < L.ccap) {
+              L.ck[c] = key;
+              L.cp[c] = f;
+            } else if (c < g.C) {
+              ckey[c] = key;
+              cflat[c] = f;
             }
           }
         }
@@ -1759,19 +1783,30 @@ __global__ void __launch_bounds__(NTA) assoc_kernel(Dev g, const DT* __restrict_
       if (tid == 0) L.misc[M_OVERFLOW] += nc - g.C;
       nc = g.C;
     }
-    // the rounds read the candidates from LDS when they fit where the boxes were (dead now)
-    const int cap = (int)(((size_t)T * 32 + (size_t)g.D * 32) / 12);
-    if (nc <= cap) {
-      unsigned long long* lk = (unsigned long long*)L.pb;
-      int* lp = (int*)(lk + nc);
-      for (int c = tid; c < nc; c += NTA) {
-        lk[c] = ckey[c];
-        lp[c] = cflat[c];
+    // the rounds read the candidates from the walk's LDS area when it held them all; else the
+    // LDS head joins the global tail, and the rounds read them where the boxes were (dead now)
+    // when they fit there, else from global memory
+    if (nc <= L.ccap) {
+      assoc_rounds(L, L.ck, L.cp, nc, D, n, g.phase + s * PH + 10);
+    } else {
+      for (int c = tid; c < L.ccap; c += NTA) {
+        ckey[c] = L.ck[c];
+        cflat[c] = L.cp[c];
       }
       __syncthreads();
-      assoc_rounds(L, lk, lp, nc, D, n, g.phase + s * PH + 10);
-    } else {
-      assoc_rounds(L, ckey, cflat, nc, D, n, g.phase + s * PH + 10);
+      const int cap = (int)(((size_t)T * 32 + (size_t)g.D * 32) / 12);
+      if (nc <= cap) {
+        unsigned long long* lk = (unsigned long long*)L.pb;
+        int* lp = (int*)(lk + nc);
+        for (int c = tid; c < nc; c += NTA) {
+          lk[c] = ckey[c];
+          lp[c] = cflat[c];
+        }
+        __syncthreads();
+        assoc_rounds(L, lk, lp, nc, D, n, g.phase + s * PH + 10);
+      } else {
+        assoc_rounds(L, ckey, cflat, nc, D, n, g.phase + s * PH + 10);
+      }
     }
   }
   if (tid == 0) g.phase[s * PH + 3] = wall_clock64();
@@ -2190,6 +2225,8 @@ int yk_tracker_create(yk_ctx* ctx, int n_streams, const yk_tracker_cfg* cfg, yk_
   }
   // enhanced policy: the two-launch step unless its LDS does not fit or YK_TRK_SINGLE=1
   t->lds_assoc = yk::trk::assoc_lds_bytes(cfg->max_tracks, cfg->max_dets);
+  if (t->lds_assoc <= yk::trk::LDS_CU)
+    t->lds_assoc = ((t->lds_assoc + 7) & ~(size_t)7) + (size_t)yk::trk::assoc_lds_cand(cfg->max_tracks, cfg->max_dets, g.C) * 12;
   const char* single = getenv("YK_TRK_SINGLE");
   t->split = cfg->policy == YK_POLICY_ENHANCED && t->lds_assoc <= 160 * 1024 && !(single && single[0] == '1');
   if (t->split) {

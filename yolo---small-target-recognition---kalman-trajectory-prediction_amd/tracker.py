@@ -235,6 +235,7 @@ class MultiStreamTracker:
             "k2_compute_us": float(t[9] - t[8]) / 100.0 if t[9] else 0.0,
             "k2_traj_us": float(t[6] - t[9]) / 100.0 if t[9] else 0.0,
             "k2_wave_cycles": [int(t[16 + k]) for k in range(4)],
+            "cand_sub_us": [float(t[b] - t[a]) / 100.0 for a, b in ((1, 20), (20, 21), (21, 22), (22, 2))] if t[22] else [],
             "assoc_clock_mhz": round(float(t[15]) / max(float(t[4] - t[0]) / 100.0, 1e-9), 1)}
 
     def snapshot(self, stream_index: int = 0) -> np.ndarray:
