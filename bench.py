@@ -364,6 +364,7 @@ def run_leg(a, P, cfg, dtype, frames, dev, local, rank, ws, headline):
     shard = P.shard
     local_c = shard.local_counters(frames_done, stats)
     local_c["live_min_start"] = float(live_start.min())
+    devices = shard.gather_devices(shard.device_identity(dev))  # raises unless one rank per GPU
     run, elapsed_max = shard.reduce_run(local_c, elapsed, dev)
     fps = run["frames"] / elapsed_max
     gflop = pipe.flops_per_frame() / 1e9
@@ -372,7 +373,7 @@ def run_leg(a, P, cfg, dtype, frames, dev, local, rank, ws, headline):
            "live_tracks_per_stream": round(run["current_active_tracks"] / (S * ws), 1),
            "live_tracks_per_stream_min_at_start": int(live_start.min()),
            "overflow": int(run["overflow"]), "tracks_created": int(run["total_tracks_created"]),
-           "conv_plan": plan_src, "window_monotonic_ns": [w0, w1]}
+           "conv_plan": plan_src, "window_monotonic_ns": [w0, w1], "rank_devices": devices}
     if overflow:
         log(f"tracker overflow on this rank: {overflow} detections/tracks dropped")
     if rank == 0 and not a.no_profile:
@@ -402,6 +403,15 @@ def run_leg(a, P, cfg, dtype, frames, dev, local, rank, ws, headline):
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
     return leg
+
+
+def cpu_baseline_seconds(a, rank, ws):
+    """Sample bound of the CPU baseline this rank runs, or 0: rank 0 only, after every rank's
+    timed region; at N > 1 a shorter sample (<= 10 s; the other ranks are idle by then), so a
+    scaling line carries the same baseline beside it.  None with --no-cpu-baseline or --gmd."""
+    if rank != 0 or a.no_cpu_baseline or a.gmd:
+        return 0
+    return a.cpu_seconds if ws == 1 else min(a.cpu_seconds, 10.0)
 
 
 def leg_argv(argv, dtype):
@@ -487,12 +497,13 @@ def main():
     # (tools/second_pipe.py: the second pipeline is as fast as the first on the first one's streams)
     legs = [run_leg_subprocess(d) for d in secondary]
     cpu = None
-    if rank == 0 and ws == 1 and not a.no_cpu_baseline and not a.gmd:
+    cpu_s = cpu_baseline_seconds(a, rank, ws)
+    if cpu_s:
         ncpu = os.cpu_count() or 2
         ref_threads = max(1, min(8, ncpu - 1))  # the reference's select_device for CPU
-        cpu = cpu_baseline(P, a.scale, S, cfg["targets"], (H, W), cfg["imgsz"], a.tracker, ref_threads, a.cpu_seconds)
+        cpu = cpu_baseline(P, a.scale, S, cfg["targets"], (H, W), cfg["imgsz"], a.tracker, ref_threads, cpu_s)
         n_all = _cpu_quota()
-        if n_all != ref_threads and a.cpu_all_seconds > 0:
+        if ws == 1 and n_all != ref_threads and a.cpu_all_seconds > 0:
             allc = cpu_baseline(P, a.scale, S, cfg["targets"], (H, W), cfg["imgsz"], a.tracker, n_all,
                                 a.cpu_all_seconds)
             cpu["all_cores"] = {k: allc[k] for k in ("value", "cores", "median_ms_per_frame", "p90_ms_per_frame",
@@ -517,6 +528,7 @@ def main():
                        "tracker_overflow": head["overflow"], "tracks_created": head["tracks_created"],
                        "conv_plan": head["conv_plan"], "graph": not a.no_graph, "tracker_overlapped": not a.no_pipeline,
                        "detector_inflight": a.inflight, "gflop_per_frame": head["gflop_per_frame"],
+                       "rank_devices": head["rank_devices"],
                        "global_motion": "optical_flow" if a.gmd else None},
             "network_mfma_frac": head["network_mfma_frac"],
             "pcie_inclusive_fps": head.get("pcie_inclusive_fps"),
@@ -530,6 +542,7 @@ def main():
     if ws > 1:
         import torch.distributed as dist
 
+        barrier(ws)  # rank 0's CPU baseline ran after the timed region
         dist.destroy_process_group()
     if bad:
         log("FAIL: the tracker dropped detections/tracks (stats.overflow != 0); results would diverge from the reference")

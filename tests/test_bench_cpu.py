@@ -31,3 +31,17 @@ def test_configs_name_baseline_workloads(cfg):
     assert c["dtype"] in B.PEAK and c["live_floor"] >= 16
     assert (c["H"], c["W"]) == ((1024, 1280) if cfg == 5 else (512, 640))
     assert c["S"] == (1 if cfg in (2, 4) else 8)
+
+
+def test_cpu_baseline_on_rank0_of_every_world_size():
+    """The CPU baseline rides on rank 0's line at N = 1 (full sample) and N > 1 (<= 10 s sample,
+    after every rank's timed region); other ranks and --no-cpu-baseline / --gmd runs skip it."""
+    import types
+
+    B = _bench()
+    a = types.SimpleNamespace(no_cpu_baseline=False, gmd=False, cpu_seconds=25.0)
+    assert B.cpu_baseline_seconds(a, 0, 1) == 25.0
+    assert B.cpu_baseline_seconds(a, 0, 8) == 10.0
+    assert B.cpu_baseline_seconds(a, 3, 8) == 0
+    a.no_cpu_baseline = True
+    assert B.cpu_baseline_seconds(a, 0, 1) == 0

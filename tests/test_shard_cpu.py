@@ -31,6 +31,15 @@ def _worker(rank, world, port, q, S=8):
         c = shard.local_counters(100 * S, stats)
         c["live_min_start"] = float(stats["current_active_tracks"].min())  # bench.py's extra key
         out, el = shard.reduce_run(c, 1.0 + rank)
+        devs = shard.gather_devices(shard.device_identity(None))
+        assert len(devs) == world and len(set(devs)) == world
+        # two ranks reporting one device: every rank raises, naming the pair
+        try:
+            shard.gather_devices("pci 0000:75:00 uuid same" if rank < 2 else f"pci 0000:{rank:02x}:00")
+            clash = None
+        except RuntimeError as e:
+            clash = str(e)
+        assert clash is not None and "ranks 0 and 1" in clash
         q.put((rank, ids, [shard.stream_seed(i, S) for i in ids], out, el))
     finally:
         dist.destroy_process_group()

@@ -109,24 +109,36 @@ def test_tracker_many_tracks_and_streams():
 
 @pytest.mark.parametrize("targets", [60, 100])
 def test_tracker_every_pair_candidates_beyond_lds(targets):
-    """iou_threshold 0 makes every (detection, track) pair a candidate: at 2048 x 512 the walk's
-    LDS area holds 2,005 of them, so 60 targets (~3.6k pairs) take the LDS head + global tail
-    path with the rounds on the dead box area, 100 targets (~10k) the rounds on global memory."""
+    """iou_threshold 0 makes every (detection, track) pair a candidate.  At 2048 tracks x 512
+    detections the walk's LDS area holds assoc_lds_cand = (163,840 - 133,632) / 12 = 2,517 of them
+    (reported by the kernel, phase word 23): 60 targets (~3.6k pairs) take the LDS head + global
+    tail path with the rounds on the dead box area (which holds (T*32 + D*32) / 12 = 6,826), 100
+    targets (~10k) the rounds on global memory.  The candidate count is the kernel's own (phase
+    word 12, counted on the pre-step tracks)."""
     yk = pkg()
     sc = yk.synth.Scene(seed=20 + targets, n_targets=targets, n_frames=12)
-    ms = yk.MultiStreamTracker(1, 150, 1, 0.0, max_tracks=2048, max_dets=512)
+    T, Dm = 2048, 512
+    ms = yk.MultiStreamTracker(1, 150, 1, 0.0, max_tracks=T, max_dets=Dm)
     ref = RefMultiTracker(150, 1, 0.0, stable_ties=True)
-    most = 0
+    most, cap = 0, None
     for t in range(12):
         dets = sc.detections(t)
         ms.step_host([dets])
         rows, counts, stats = ms.download()
-        most = max(most, len(dets) * int(stats[0]["current_active_tracks"]))
+        ph = ms.phase_us(0)
+        if ph["n_cand"]:
+            most = max(most, ph["n_cand"])
+            cap = ph["lds_cand_cap"]
         rb = ref.update(dets)
         ours = [yk.tracker._row_to_dict(r, yk.tracker.track_id_of(r["track_num"])) for r in rows[0, : counts[0]]]
         compare_frame(ours, rb, f"frame {t}")
         assert int(stats[0]["overflow"]) == 0
-    assert most > (2005 if targets == 60 else 6826)
+    assert cap == 2517, cap
+    dead_box_cap = (T * 32 + Dm * 32) // 12
+    if targets == 60:
+        assert cap < most <= dead_box_cap, (most, cap)
+    else:
+        assert most > dead_box_cap, most
 
 
 def test_standalone_track_object_ops():

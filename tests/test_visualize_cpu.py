@@ -210,9 +210,13 @@ def test_y4m_reader(tmp_path):
         f.write(f"YUV4MPEG2 W{w} H{h} F25:1 C420jpeg\n".encode())
         f.write(b"FRAME\n" + y.tobytes() + u2.tobytes() + np.full((h // 2, w // 2), 128, np.uint8).tobytes())
     ok, fr = FR.VideoReader(str(p2)).read()
-    # U - 128 = 32: B = Y + round(32 * 33292 / 2^14) = Y + 65, G = Y + round(32 * -6472 / 2^14) = Y - 13
-    assert ok and (fr[:, :, 0].astype(int) == np.minimum(y.astype(int) + 65, 255)).all()
-    assert (fr[:, :, 1].astype(int) == y.astype(int) - 13).all() and (fr[:, :, 2] == y).all()
+    # 4:2:0 = OpenCV's I420 path, BT.601 limited range: Y' = (Y - 16) * 1220542, U - 128 = 32:
+    # B = (Y' + 2^19 + 32 * 2116026) >> 20, G = (Y' + 2^19 + 32 * -409993) >> 20, R = (Y' + 2^19) >> 20
+    yy = (y.astype(np.int64) - 16) * 1220542 + (1 << 19)
+    assert ok and (fr[:, :, 0] == np.clip((yy + 32 * 2116026) >> 20, 0, 255)).all()
+    assert (fr[:, :, 1] == np.clip((yy - 32 * 409993) >> 20, 0, 255)).all()
+    assert (fr[:, :, 2] == np.clip(yy >> 20, 0, 255)).all()
+    assert int(fr[0, 0, 2]) == round((100 - 16) * 255 / 219)  # limited range: 84 -> 98 (rounded)
 
 
 def test_yolo_frames_accepts_paths(tmp_path):

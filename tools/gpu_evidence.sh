@@ -1,12 +1,12 @@
 #!/bin/bash
-# Round-2 final evidence for profiles/: default bench (config 3: fp32 headline + bf16 secondary,
+# Round-end evidence for profiles/: default bench (config 3: fp32 headline + bf16 secondary,
 # CPU baseline), rocprofv3 kernel trace (+ --stats) of the same workload cut to the bench's
 # windows, HBM PMC passes (fp32 and bf16 builds), config 2 / 4 / 5 lines -- all on the committed
 # conv plans (no autotune).
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
-O=gpurun_out/final
+O=gpurun_out/${EVIDENCE_DIR:-final}
 mkdir -p $O
 timeout -k 10 400 python -u bench.py --dump-ops $O/ops_c3.json > $O/bench_c3.json 2> $O/bench_c3.err || { echo "bench failed"; tail -20 $O/bench_c3.err; exit 1; }
 echo "bench ok"
@@ -26,9 +26,9 @@ timeout -k 10 300 python -u bench.py --config 4 --no-cpu-baseline > $O/bench_c4.
 timeout -k 10 300 python -u bench.py --config 2 --no-cpu-baseline > $O/bench_c2.json 2> $O/bench_c2.err || { echo "c2 failed"; tail -20 $O/bench_c2.err; exit 1; }
 timeout -k 10 400 python -u bench.py --config 5 --no-cpu-baseline --dump-ops $O/ops_c5.json > $O/bench_c5.json 2> $O/bench_c5.err || { echo "c5 failed"; tail -20 $O/bench_c5.err; exit 1; }
 python3 - <<'PY'
-import json
+import json, os
 for n in ("c3", "c4", "c2", "c5"):
-    d = json.load(open(f"gpurun_out/final/bench_{n}.json"))
+    d = json.load(open(f"gpurun_out/{os.environ.get('EVIDENCE_DIR', 'final')}/bench_{n}.json"))
     print(n, d["value"], d["dtype"], d["ms_per_step"], d["config"]["live_tracks_per_stream"], d["config"]["live_tracks_per_stream_min_at_start"],
           d["network_mfma_frac"], d["roofline"]["kernel"], d["roofline"]["frac"], d["roofline"]["traffic"], [(s["dtype"], s["value"]) for s in d["secondary"]])
 PY

@@ -1598,6 +1598,10 @@ __global__ void __launch_bounds__(NTA) assoc_kernel(Dev g, const DT* __restrict_
 
   const long long cyc0 = clock64();  // shader clock: phase[15] = cycles of this kernel (clock check)
   if (tid == 0) g.phase[s * PH + 0] = wall_clock64();
+  // candidate sub-phase stamps are written only when this step has both tracks and detections:
+  // clear them so phase_us never mixes a previous step's stamps in
+  if (tid == 0)
+    for (int k = 20; k < 23; ++k) g.phase[s * PH + k] = 0;
   int Draw = counts[s];
   if (Draw < 0) Draw = 0;
   const int D = Draw < g.D ? Draw : g.D;
@@ -1777,6 +1781,7 @@ __global__ void __launch_bounds__(NTA) assoc_kernel(Dev g, const DT* __restrict_
       g.phase[s * PH + 12] = L.misc[M_NCAND];
       g.phase[s * PH + 13] = (long long)(isfinite(wmax) ? wmax : -1.0);
       g.phase[s * PH + 14] = n - nfin;
+      g.phase[s * PH + 23] = L.ccap;  // candidates the walk's LDS area holds
     }
     nc = L.misc[M_NCAND];
     if (nc > g.C) {
@@ -1808,6 +1813,10 @@ __global__ void __launch_bounds__(NTA) assoc_kernel(Dev g, const DT* __restrict_
         assoc_rounds(L, ckey, cflat, nc, D, n, g.phase + s * PH + 10);
       }
     }
+  } else if (tid == 0) {  // no pairs: an empty candidate phase, no rounds
+    g.phase[s * PH + 2] = wall_clock64();
+    g.phase[s * PH + 10] = 0;
+    for (int k = 11; k < 15; ++k) g.phase[s * PH + k] = 0;
   }
   if (tid == 0) g.phase[s * PH + 3] = wall_clock64();
 

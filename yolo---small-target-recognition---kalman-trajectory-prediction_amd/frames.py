@@ -148,6 +148,23 @@ def _yuv2bgr(y, u, v):
     return np.clip(np.stack([b, g, r], axis=2), 0, 255).astype(np.uint8)
 
 
+def _yuv420_to_bgr(y, u, v):
+    """OpenCV COLOR_YUV2BGR_I420 (color_yuv.simd.hpp: BT.601 limited range, ITUR_BT_601_*
+    constants, 20-bit fixed point, Y - 16 clamped at 0) on chroma already upsampled by 2x2
+    replication, which is how that conversion shares one (u, v) pair per 2x2 block.  The
+    reference driver's cv2.VideoCapture decodes through FFmpeg's own converter, whose rounding
+    may differ in the last unit: parity with it is unpinned (no codec or cv2 in this image)."""
+    cy, cub, cug, cvg, cvr, sh = 1220542, 2116026, -409993, -852492, 1673527, 20
+    half = 1 << (sh - 1)
+    yy = np.maximum(y.astype(np.int64) - 16, 0) * cy
+    ui = u.astype(np.int64) - 128
+    vi = v.astype(np.int64) - 128
+    b = (yy + half + cub * ui) >> sh
+    g = (yy + half + cvg * vi + cug * ui) >> sh
+    r = (yy + half + cvr * vi) >> sh
+    return np.clip(np.stack([b, g, r], axis=2), 0, 255).astype(np.uint8)
+
+
 class VideoReader:
     """cv2.VideoCapture-like reader: ``read() -> (ok, frame)``, ``get(prop)``, ``isOpened()``."""
 
@@ -240,10 +257,11 @@ class VideoReader:
         y = np.frombuffer(f.read(w * h), np.uint8).reshape(h, w)
         u = np.frombuffer(f.read(ch * cw), np.uint8).reshape(ch, cw)
         v = np.frombuffer(f.read(ch * cw), np.uint8).reshape(ch, cw)
-        if (ch, cw) != (h, w):  # 4:2:0: nearest chroma upsampling (OpenCV's YUV420 -> BGR)
+        if (ch, cw) != (h, w):  # 4:2:0: OpenCV's I420 path (limited range), 2x2 chroma blocks
             u = np.repeat(np.repeat(u, 2, 0), 2, 1)[:h, :w]
             v = np.repeat(np.repeat(v, 2, 0), 2, 1)[:h, :w]
-        return True, _yuv2bgr(y, u, v)
+            return True, _yuv420_to_bgr(y, u, v)
+        return True, _yuv2bgr(y, u, v)  # 4:4:4
 
     def release(self):
         if self._y4m is not None:

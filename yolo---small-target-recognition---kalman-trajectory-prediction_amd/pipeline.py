@@ -41,7 +41,7 @@ from . import weights as Wt
 
 class StreamPipeline:
     def __init__(self, model_cfg: str = "yolov8s-small.yaml", n_streams: int = 8, frame_hw=(512, 640),
-                 dtype: str = "bf16", weights=None, seed: int = 0, conf: float = 0.25, iou: float = 0.7,
+                 dtype: str = "fp32", weights=None, seed: int = 0, conf: float = 0.25, iou: float = 0.7,
                  max_det: int = 300, max_lost_frames: int = 150, min_hits: int = 1, iou_threshold: float = 0.1,
                  max_tracks: int = 512, device: int = 0, pipelined: bool = False, imgsz=640, inflight: int = 1,
                  tracker_policy: int = 0, motion_method: str | None = None):

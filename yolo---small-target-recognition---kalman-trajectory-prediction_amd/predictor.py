@@ -119,11 +119,12 @@ class YOLO:
     DetectionModel without ultralytics and without executing the pickle, checkpoint.py).
     ``weights`` (YAML models only): None (seeded synthetic weights in the reference's shapes,
     SURVEY §8d), a state dict in the reference's naming, or a path to one saved with
-    torch.save (loaded with weights_only=True).  ``dtype``: 'fp32' (the reference's arithmetic,
-    exact-f32 MFMA), 'bf16' or 'fp8'."""
+    torch.save (loaded with weights_only=True).  ``dtype``: 'fp32' (the default: the reference's
+    arithmetic, so the unchanged driver gets the reference's decisions), or the explicit opt-ins
+    'bf16' / 'fp8' (faster, not parity-capable: their detections differ from the reference's)."""
 
     def __init__(self, model: str = "yolov8s-small.yaml", task=None, verbose: bool = False, *, weights=None,
-                 dtype: str = "bf16", device: int = 0, seed: int = 0, max_batch: int = 8):
+                 dtype: str = "fp32", device: int = 0, seed: int = 0, max_batch: int = 8):
         if task not in (None, "detect"):
             raise NotImplementedError(f"task {task!r}: only detection is on this path")
         self.ckpt_meta = None

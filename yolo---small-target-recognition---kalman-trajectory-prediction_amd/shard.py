@@ -39,6 +39,36 @@ def local_counters(frames_done: int, stats: np.ndarray) -> dict:
     return out
 
 
+def device_identity(device=None) -> str:
+    """This rank's physical device: the GPU's PCI address (domain:bus:device) and uuid, read
+    from the HIP device properties; ``cpu:<pid>`` for a CPU (gloo) rank."""
+    if device is None or torch.device(device).type != "cuda":
+        import os
+
+        return f"cpu:{os.getpid()}"
+    p = torch.cuda.get_device_properties(torch.device(device))
+    return f"pci {p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x} uuid {p.uuid}"
+
+
+def gather_devices(ident: str) -> list[str]:
+    """Every rank's device_identity(), in rank order, checked to be pairwise distinct (one
+    process per GPU: two ranks on one device would share its CUs and HBM, and a scaling line
+    measured that way is not an N-GPU number).  Raises RuntimeError naming the ranks that
+    collide.  [ident] when torch.distributed is not initialised."""
+    import torch.distributed as dist
+
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return [ident]
+    out = [None] * dist.get_world_size()
+    dist.all_gather_object(out, ident)
+    seen = {}
+    for r, d in enumerate(out):
+        if d in seen:
+            raise RuntimeError(f"ranks {seen[d]} and {r} run on the same device ({d}): launch one process per GPU")
+        seen[d] = r
+    return out
+
+
 def reduce_run(counters: dict, elapsed: float, device=None) -> tuple[dict, float]:
     """End-of-run exchange: SUM of the counters and MAX of the wall time over all ranks.
     Identity when torch.distributed is not initialised (single process)."""

@@ -230,7 +230,7 @@ class MultiStreamTracker:
         names = ["predict", "candidates", "rounds", "update", "create", "delete", "outputs"]
         return {n: float(t[k + 1] - t[k]) / 100.0 for k, n in enumerate(names)} | {
             "n_rounds": int(t[10]), "pairs_tested": int(t[11]), "n_cand": int(t[12]), "max_width": int(t[13]),
-            "n_nonfinite": int(t[14]),
+            "n_nonfinite": int(t[14]), "lds_cand_cap": int(t[23]),
             "k2_stage_us": float(t[8] - t[5]) / 100.0 if t[8] else 0.0,
             "k2_compute_us": float(t[9] - t[8]) / 100.0 if t[9] else 0.0,
             "k2_traj_us": float(t[6] - t[9]) / 100.0 if t[9] else 0.0,
