@@ -289,7 +289,17 @@ typedef struct yk_bt_cfg {
   int32_t fuse_score;        /* 1                                                      */
   int32_t max_tracks;        /* tracked + lost tracks per stream (<= 1024)             */
   int32_t max_dets;          /* detections per stream and frame (<= 1024)              */
+  int32_t assignment;        /* yk_bt_assignment: matching.linear_assignment's branch   */
+  int32_t reserved;          /* 0                                                      */
+  double match_thresh_f64;   /* match_thresh as the python float the YAML holds (the lap
+                                branch's cost_limit is float64); 0 = (double)match_thresh */
 } yk_bt_cfg;
+/* matching.linear_assignment (trackers/utils/matching.py:20-61): YK_BT_LAP = lap.lapjv(cost,
+ * extend_cost=True, cost_limit=thresh), the reference's default (use_lap=True; `lap` is a hard
+ * requirement, :9-17): the maximum-weight matching with weights thresh - cost over pairs with
+ * cost < thresh, unmatched lists ascending.  YK_BT_SCIPY = the scipy branch (:50-59): optimal
+ * assignment of the whole matrix, then cost <= thresh, unmatched lists in frozenset order. */
+enum yk_bt_assignment { YK_BT_LAP = 0, YK_BT_SCIPY = 1 };
 typedef struct yk_bt yk_bt;
 int yk_bt_create(yk_ctx* ctx, int n_streams, const yk_bt_cfg* cfg, yk_bt** out);
 int yk_bt_destroy(yk_bt* bt);

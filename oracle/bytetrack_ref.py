@@ -15,8 +15,12 @@ op a python float stays float32; lists mixing float32 scalars and python floats 
       needs cv2 -- absent here, so BOTSORT is stepped with img=None, as the reference skips GMC)
   * matching.iou_distance / fuse_score       trackers/utils/matching.py:64-157, with
       utils/metrics.py:23-52 bbox_ioa(iou=True) in float32
-  * matching.linear_assignment, the scipy branch (matching.py:50-59): `lap` is not installed,
-      so scipy.optimize.linear_sum_assignment, the threshold filter, and the unmatched lists in
+  * matching.linear_assignment (matching.py:20-61): by default the lap branch the reference
+      takes (use_lap=True; `lap>=0.5.12` is a hard requirement, matching.py:9-17): lapjv's
+      extended cost_limit problem (lapjv_extended; `lap` itself is not installed, so its
+      problem is restated and solved exactly by scipy -- unique optima agree, equal-cost ties
+      are unpinned), unmatched lists ascending.  use_lap=False keeps the scipy branch
+      (:50-59): linear_sum_assignment, the threshold filter, and the unmatched lists in
       CPython's frozenset iteration order (oracle/pyset_order.py restates that order for the
       device; here the real frozensets are used).
   * Track ids: BaseTrack._count is process-global (basetrack.py:67-92): one counter shared by
@@ -246,9 +250,42 @@ def fuse_score(cost, dets):
     return 1 - sim * sc
 
 
-def linear_assignment(cost, thresh):
+def lapjv_extended(cost, cost_limit):
+    """lap.lapjv(cost, extend_cost=True, cost_limit=cost_limit) (gatagat/lap 0.5.12, the `lap`
+    the reference requires, matching.py:9-17): the (n_rows + n_cols)-square float64 problem
+    whose top-left block is `cost`, every other entry cost_limit / 2 except the zero
+    bottom-right block; x / y map rows / columns to their partner, -1 for a dummy.  lap's
+    Jonker-Volgenant solver is replaced by scipy's exact solver on the same extended matrix:
+    both return an optimum, so they agree whenever the optimum is unique; among equal-cost
+    optima the choice is the solver's own (lap is not installed here: that tie rule is
+    unpinned)."""
+    n_rows, n_cols = cost.shape
+    n = n_rows + n_cols
+    ext = np.empty((n, n), dtype=np.double)
+    ext[:] = cost_limit / 2.0
+    ext[n_rows:, n_cols:] = 0
+    ext[:n_rows, :n_cols] = cost
+    r, c = scipy.optimize.linear_sum_assignment(ext)
+    x = np.full(n, -1, dtype=np.int64)
+    y = np.full(n, -1, dtype=np.int64)
+    x[r], y[c] = c, r
+    x, y = x[:n_rows], y[:n_cols]
+    x[x >= n_cols] = -1
+    y[y >= n_rows] = -1
+    return x, y
+
+
+def linear_assignment(cost, thresh, use_lap=True):
+    """matching.linear_assignment (matching.py:20-61).  use_lap=True (the reference's default):
+    lap.lapjv with extend_cost and cost_limit=thresh, matches in row order, unmatched lists
+    ascending (np.where).  use_lap=False: the scipy branch (optimal assignment of the whole
+    matrix, then the `cost <= thresh` filter, unmatched lists in frozenset order)."""
     if cost.size == 0:
         return np.empty((0, 2), dtype=int), tuple(range(cost.shape[0])), tuple(range(cost.shape[1]))
+    if use_lap:
+        x, y = lapjv_extended(cost, thresh)
+        matches = [[ix, mx] for ix, mx in enumerate(x) if mx >= 0]
+        return matches, np.where(x < 0)[0], np.where(y < 0)[0]
     x, y = scipy.optimize.linear_sum_assignment(cost)
     matches = np.asarray([[x[i], y[i]] for i in range(len(x)) if cost[x[i], y[i]] <= thresh])
     if len(matches) == 0:
@@ -293,8 +330,9 @@ class RefTracker:
     """BYTETracker (cfg tracker_type 'bytetrack', KalmanFilterXYAH) or BOTSORT without ReID /
     GMC (tracker_type 'botsort', KalmanFilterXYWH)."""
 
-    def __init__(self, cfg=None, frame_rate=30, ids: IdCounter | None = None):
+    def __init__(self, cfg=None, frame_rate=30, ids: IdCounter | None = None, use_lap: bool = True):
         cfg = dict(BYTETRACK_CFG if cfg is None else cfg)
+        self.use_lap = bool(use_lap)
         self.args = SimpleNamespace(**cfg)
         if self.args.tracker_type == "botsort" and self.args.with_reid:
             raise NotImplementedError("BoT-SORT ReID is not restated (with_reid: False)")
@@ -331,7 +369,7 @@ class RefTracker:
         tracked = [t for t in self.tracked if t.is_activated]
         pool = _joint(tracked, self.lost)
         multi_predict(pool, self.kind)
-        m, u_track, u_det = linear_assignment(self._dists(pool, dets), thresh=a.match_thresh)
+        m, u_track, u_det = linear_assignment(self._dists(pool, dets), thresh=a.match_thresh, use_lap=self.use_lap)
         for it, idt in m:
             t = pool[it]
             if t.state == TRACKED:
@@ -341,7 +379,7 @@ class RefTracker:
                 t.re_activate(dets[idt], self.frame_id)
                 refind.append(t)
         r_tracked = [pool[i] for i in u_track if pool[i].state == TRACKED]
-        m, u_track, _ = linear_assignment(iou_distance(r_tracked, dets2), thresh=0.5)
+        m, u_track, _ = linear_assignment(iou_distance(r_tracked, dets2), thresh=0.5, use_lap=self.use_lap)
         for it, idt in m:
             t = r_tracked[it]
             if t.state == TRACKED:
@@ -356,7 +394,7 @@ class RefTracker:
                 t.state = LOST
                 lost_new.append(t)
         dets = [dets[i] for i in u_det]
-        m, u_unc, u_det = linear_assignment(self._dists(unconfirmed, dets), thresh=0.7)
+        m, u_unc, u_det = linear_assignment(self._dists(unconfirmed, dets), thresh=0.7, use_lap=self.use_lap)
         for it, idt in m:
             unconfirmed[it].update(dets[idt], self.frame_id)
             activated.append(unconfirmed[it])

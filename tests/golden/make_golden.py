@@ -21,7 +21,8 @@ generators of synth.py / tests/cmc_sequences.py; only the expected outputs are s
                        with two whip pans (tests/gmd_helpers.py, 256x320): per-frame results,
                        stats, and every frame's corners / LK end points / status
   bytetrack.npz        BYTETracker and BOTSORT (no ReID / GMC) on a 40-frame detection sequence
-                       (tests/bt_helpers.py): every frame's output rows
+                       (tests/bt_helpers.py): every frame's output rows, with the
+                       lap branch of linear_assignment (the reference's) and the scipy branch
 """
 from __future__ import annotations
 
@@ -223,18 +224,21 @@ def bytetrack_inputs():
 
 
 def run_bytetrack_oracle():
+    """Rows of both linear_assignment branches: '<kind>_rows' = the lap branch the reference
+    takes (use_lap=True), '<kind>_scipy_rows' = the scipy branch (use_lap=False)."""
     from oracle import bytetrack_ref as R
 
     out = {}
     for kind, cfg in (("bytetrack", R.BYTETRACK_CFG), ("botsort", R.BOTSORT_CFG)):
-        ref = R.RefTracker(dict(cfg), ids=R.IdCounter())
-        rows, off = [], [0]
-        for x, c, k in bytetrack_inputs():
-            r = np.asarray(ref.update(R.Dets(x, c, k)), np.float32).reshape(-1, 8)
-            rows.append(r)
-            off.append(off[-1] + len(r))
-        out[f"{kind}_rows"] = np.concatenate(rows) if rows else np.zeros((0, 8), np.float32)
-        out[f"{kind}_off"] = np.array(off, np.int64)
+        for tag, use_lap in (("", True), ("_scipy", False)):
+            ref = R.RefTracker(dict(cfg), ids=R.IdCounter(), use_lap=use_lap)
+            rows, off = [], [0]
+            for x, c, k in bytetrack_inputs():
+                r = np.asarray(ref.update(R.Dets(x, c, k)), np.float32).reshape(-1, 8)
+                rows.append(r)
+                off.append(off[-1] + len(r))
+            out[f"{kind}{tag}_rows"] = np.concatenate(rows) if rows else np.zeros((0, 8), np.float32)
+            out[f"{kind}{tag}_off"] = np.array(off, np.int64)
     return out
 
 
@@ -256,9 +260,11 @@ def load(name):
         return {k: z[k] for k in z.files}
 
 
-def main():
+def main(names=None):
     torch.set_num_threads(min(8, os.cpu_count() or 1))
     for name, gen in GENERATORS.items():
+        if names and name not in names:
+            continue
         arrs = gen()
         np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **arrs)
         print(name, {k: v.shape for k, v in arrs.items() if not k.startswith(("cand", "keep"))},
@@ -266,4 +272,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    main(sys.argv[1:])  # no arguments: every fixture

@@ -71,3 +71,23 @@ def test_oracle_runs_both_trackers_with_shared_ids():
             seen.update(out[:, 4].astype(int).tolist() if out.size else [])
     assert len(seen) > 10 and ids.count >= max(seen)
 
+
+
+def test_lap_branch_known_answer_differs_from_scipy():
+    """matching.linear_assignment's default lap branch (lapjv, extend_cost, cost_limit = thresh)
+    against the scipy branch on the case where they part: rows A, B; columns d1, d2; costs
+    A-d1 0.4, A-d2 0.85, B-d1 0.5, B-d2 1 (no overlap); thresh 0.8.  scipy assigns A-d2 + B-d1
+    (1.35 < 1.4) and its filter keeps only B-d1; lapjv's extended problem keeps A-d1 (0.4 - 0.8
+    beats 0.5 - 0.8) and leaves B and d2 unmatched, the lists ascending."""
+    cost = np.array([[0.4, 0.85], [0.5, 1.0]], np.float32)
+    m, ua, ub = R.linear_assignment(cost, 0.8)
+    assert [list(p) for p in m] == [[0, 0]] and list(ua) == [1] and list(ub) == [1]
+    m, ua, ub = R.linear_assignment(cost, 0.8, use_lap=False)
+    assert [list(p) for p in m] == [[1, 0]] and list(ua) == [0] and list(ub) == [1]
+    # the matched set maximises the summed margins thresh - cost: A-d2 alone (0.6) beats A-d1 +
+    # B-d2 (0.3 + 0.1), and B-d1 (cost above thresh) is never kept; empty matrices give the
+    # tuple(range(...)) lists
+    x, y = R.lapjv_extended(np.array([[0.5, 0.2], [0.9, 0.7]]), 0.8)
+    assert list(x) == [1, -1] and list(y) == [-1, 0]
+    m, ua, ub = R.linear_assignment(np.zeros((0, 3), np.float32), 0.8)
+    assert len(m) == 0 and ua == () and ub == (0, 1, 2)

@@ -116,8 +116,9 @@ def test_global_motion_kernels_match_golden():
                                    int(st[0]["reset_triggers"])], want["stats"])
 
 
+@pytest.mark.parametrize("tag", ["", "_scipy"], ids=["lap", "scipy"])
 @pytest.mark.parametrize("kind", ["bytetrack", "botsort"])
-def test_bytetrack_kernel_matches_golden(kind):
+def test_bytetrack_kernel_matches_golden(kind, tag):
     """bytetrack.hip on the bytetrack fixture: every frame's rows in order, ids / score / cls / idx
     exact, boxes within 1e-3 px (the ByteTrack parity bar)."""
     import importlib
@@ -126,9 +127,9 @@ def test_bytetrack_kernel_matches_golden(kind):
 
     BT = importlib.import_module(pkg().__name__ + ".bytetrack")
     want = G.load("bytetrack")
-    rows, off = want[f"{kind}_rows"], want[f"{kind}_off"]
+    rows, off = want[f"{kind}{tag}_rows"], want[f"{kind}{tag}_off"]
     cfg = dict(R.BOTSORT_CFG if kind == "botsort" else R.BYTETRACK_CFG)
-    dev = BT.BatchedTracker(cfg, n_streams=1, max_tracks=256, max_dets=128)
+    dev = BT.BatchedTracker(cfg, n_streams=1, max_tracks=256, max_dets=128, use_lap=tag == "")
     for t, (x, c, k) in enumerate(G.bytetrack_inputs()):
         dev.step([np.c_[x, c, k]])
         got = dev.download()[0]

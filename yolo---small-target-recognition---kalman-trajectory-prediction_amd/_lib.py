@@ -41,10 +41,12 @@ class BtCfg(C.Structure):
     _fields_ = [("kind", C.c_int32), ("track_high_thresh", C.c_float), ("track_low_thresh", C.c_float),
                 ("new_track_thresh", C.c_float), ("match_thresh", C.c_float), ("track_buffer", C.c_int32),
                 ("frame_rate", C.c_int32), ("fuse_score", C.c_int32), ("max_tracks", C.c_int32),
-                ("max_dets", C.c_int32)]
+                ("max_dets", C.c_int32), ("assignment", C.c_int32), ("reserved", C.c_int32),
+                ("match_thresh_f64", C.c_double)]
 
 
 BT_BYTETRACK, BT_BOTSORT = 0, 1
+BT_LAP, BT_SCIPY = 0, 1  # yk_bt_assignment
 
 STATS_DTYPE = np.dtype([(k, np.int64) for k in (
     "frame_count", "next_track_id", "total_tracks_created", "total_tracks_terminated",

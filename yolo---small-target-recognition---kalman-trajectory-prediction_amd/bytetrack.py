@@ -10,6 +10,8 @@ Surfaces
   BatchedTracker(cfg, n_streams)  many streams per launch, detections resident on the device
       ([S, max_dets, 6] float32 x1 y1 x2 y2 conf cls + [S] int32 counts), as the detect-and-track
       pipeline hands them over.
+matching.linear_assignment follows its default lap branch (lap.lapjv with cost_limit, unmatched
+lists ascending); use_lap=False selects the scipy branch (matching.py:50-59).
 Track ids come from one counter shared by the streams of a BatchedTracker (the reference's
 BaseTrack._count is process-global); separate BYTETracker objects each own a counter, like
 separate processes.  BoT-SORT's ReID branch (with_reid) and its GMC (needs cv2 for every
@@ -59,7 +61,7 @@ class BatchedTracker:
     """n_streams independent BYTETracker / BOTSORT states stepped by one launch."""
 
     def __init__(self, cfg=None, n_streams: int = 1, frame_rate: int = 30, max_tracks: int = 512,
-                 max_dets: int = 512, device: int = 0):
+                 max_dets: int = 512, device: int = 0, use_lap: bool = True):
         a = load_tracker_cfg(cfg if cfg is not None else dict(BYTETRACK_DEFAULTS))
         if a.tracker_type == "botsort" and getattr(a, "with_reid", False):
             raise NotImplementedError("BoT-SORT ReID (with_reid: True) is not built on the device path")
@@ -69,7 +71,8 @@ class BatchedTracker:
                     track_high_thresh=float(a.track_high_thresh), track_low_thresh=float(a.track_low_thresh),
                     new_track_thresh=float(a.new_track_thresh), match_thresh=float(a.match_thresh),
                     track_buffer=int(a.track_buffer), frame_rate=int(frame_rate), fuse_score=int(bool(a.fuse_score)),
-                    max_tracks=self.max_tracks, max_dets=self.max_dets)
+                    max_tracks=self.max_tracks, max_dets=self.max_dets,
+                    assignment=L.BT_LAP if use_lap else L.BT_SCIPY, match_thresh_f64=float(a.match_thresh))
         h = C.c_void_p()
         L.check(L.lib().yk_bt_create(L.context(self.device), self.S, C.byref(c), C.byref(h)), "yk_bt_create")
         self._h = h
@@ -135,14 +138,15 @@ class BYTETracker:
 
     kind = "bytetrack"
 
-    def __init__(self, args=None, frame_rate: int = 30, max_tracks: int = 512, max_dets: int = 1024, device: int = 0):
+    def __init__(self, args=None, frame_rate: int = 30, max_tracks: int = 512, max_dets: int = 1024, device: int = 0,
+                 use_lap: bool = True):
         d = dict(vars(args)) if args is not None and not isinstance(args, (dict, str)) else args
         cfg = load_tracker_cfg(d if d is not None else dict(BOTSORT_DEFAULTS if self.kind == "botsort"
                                                              else BYTETRACK_DEFAULTS))
         if cfg.tracker_type != self.kind:
             cfg = SimpleNamespace(**{**vars(cfg), "tracker_type": self.kind})
         self.args = cfg
-        self._b = BatchedTracker(vars(cfg), 1, frame_rate, max_tracks, max_dets, device)
+        self._b = BatchedTracker(vars(cfg), 1, frame_rate, max_tracks, max_dets, device, use_lap)
         self.frame_id = 0
 
     def reset(self):

@@ -17,14 +17,19 @@
 // a predict batch whose means are all float32 computes its motion noise in float32.  IoU is
 // utils/metrics.py bbox_ioa(iou=True) in float32 (no FMA: -ffp-contract=off).
 //
-// Assignment (matching.py:20-61): `lap` is not installed here, so the checked behaviour is the
-// scipy branch: an optimal assignment of the full cost matrix, then the threshold filter.  A
-// pair whose boxes do not overlap costs exactly 1, so an optimal assignment's overlapping pairs
-// form a maximum-weight matching of the overlap graph with weights 1 - cost; every connected
-// component of that graph is solved on its own (Hungarian method, one thread per component).
-// Equal-cost alternatives (exact ties) are resolved by this solver, not by scipy's; the
-// unmatched lists follow CPython 3.10's frozenset iteration order (pyset_diff; restated and
-// checked in oracle/pyset_order.py), which decides e.g. the order of new-track activation.
+// Assignment (matching.py:20-61), both branches; the default is the one the reference takes.
+// lap (use_lap=True, `lap>=0.5.12` is a hard requirement, :9-17): lapjv(extend_cost=True,
+// cost_limit=thresh) solves the (n_rows + n_cols)-square problem padded with cost_limit / 2 and
+// a zero dummy block, i.e. it minimises sum over matched pairs of (cost - thresh): the
+// maximum-weight matching with weights thresh - cost over the pairs with cost < thresh; the
+// unmatched lists are ascending (np.where).  scipy (use_lap=False): an optimal assignment of the
+// full cost matrix, then the float32 threshold filter; a pair whose boxes do not overlap costs
+// exactly 1, so the overlapping pairs of an optimal assignment form a maximum-weight matching of
+// the overlap graph with weights 1 - cost; the unmatched lists follow CPython 3.10's frozenset
+// iteration order (pyset_diff; restated and checked in oracle/pyset_order.py), which decides
+// e.g. the order of new-track activation.  Either way every connected component of the edge
+// graph is solved on its own (Hungarian method, one thread per component); equal-cost
+// alternatives (exact ties) are this solver's choice, not lapjv's / scipy's.
 #include <climits>
 
 #include "yk_internal.h"
@@ -57,6 +62,8 @@ struct Hdr {
 struct Cfg {
   float th_high, th_low, th_new, th_match;
   int max_time_lost, fuse, xywh;  // xywh: BOTSORT (KalmanFilterXYWH / BOTrack)
+  int lap;                        // linear_assignment branch: 1 lap.lapjv (default), 0 scipy
+  double th_match_f64;            // match_thresh as the YAML's python float (lap's cost_limit)
 };
 
 struct Dev {
@@ -460,10 +467,19 @@ __device__ void hungarian(int n, int m, A a, double* w, int* col4row) {
     if (p[j]) col4row[p[j] - 1] = j - 1;
 }
 
-// linear_assignment (matching.py:20-61, scipy branch) of the nr x nc matrix in C (row-major,
-// global): mrow / mcol get the kept matches, urow / ucol the unmatched indices in the
-// reference's list order; misc[Q_A] / misc[Q_B] their counts.  All threads call it.
-__device__ void assign(const Dev& g, const Lds& L, float* C, int* E, double* hw, int nr, int nc, float thresh) {
+// linear_assignment (matching.py:20-61) of the nr x nc matrix in C (row-major, global): mrow /
+// mcol get the kept matches, urow / ucol the unmatched indices in the reference's list order;
+// misc[Q_A] / misc[Q_B] their counts.  All threads call it.
+//   lap branch (g.cfg.lap, the reference's default): lapjv on the extended problem (cost_limit /
+//   2 per dummy pairing, 0 dummy-dummy) minimises sum over matched pairs of (cost - thresh), so
+//   only pairs with cost < thresh (float64, the cost_limit's precision) are edges, a component
+//   of them is solved on min(cost - thresh, 0), every assigned edge is kept, and the unmatched
+//   lists are ascending (np.where).
+//   scipy branch: pairs that overlap (cost < 1) are the edges, a component is solved on the
+//   cost itself, the float32 `cost <= thresh` filter follows, frozenset-ordered unmatched lists.
+__device__ void assign(const Dev& g, const Lds& L, float* C, int* E, double* hw, int nr, int nc, float thresh,
+                       double thresh64) {
+  const bool lap = g.cfg.lap != 0;
   const int tid = threadIdx.x;
   int* wsum = L.misc + Q_WSUM;
   for (int r = tid; r < nr; r += NT) L.mrow[r] = -1;
@@ -488,7 +504,7 @@ __device__ void assign(const Dev& g, const Lds& L, float* C, int* E, double* hw,
   for (int v = tid; v < nn; v += NT) L.label[v] = v;
   __syncthreads();
   for (int e = tid; e < nr * nc; e += NT)
-    if (C[e] < 1.0f) E[atomicAdd(&L.misc[Q_E], 1)] = e;
+    if (lap ? (double)C[e] < thresh64 : C[e] < 1.0f) E[atomicAdd(&L.misc[Q_E], 1)] = e;
   __syncthreads();
   const int ne = L.misc[Q_E];
   for (int it = 0; it < nn + 2; ++it) {  // min-label propagation; converges within a component's diameter
@@ -550,20 +566,26 @@ __device__ void assign(const Dev& g, const Lds& L, float* C, int* E, double* hw,
     for (int c = 0; c < nc; ++c)
       if (L.label[nr + c] == root) cols[kc++] = c;
     int* res = cols + kc;  // [min(kr, kc)] (rows + cols + res <= 2 T + D ints per thread)
+    // lap: cost - thresh where negative (an edge), else 0 (no better than both unmatched)
+    auto cost = [&](int r, int c) {
+      const double v = (double)C[r * nc + c];
+      return lap ? fmin(v - thresh64, 0.0) : v;
+    };
+    auto keep = [&](int r, int c) { return lap ? (double)C[r * nc + c] < thresh64 : C[r * nc + c] <= thresh; };
     if (kr <= kc) {
-      hungarian(kr, kc, [&](int i, int j) { return (double)C[rows[i] * nc + cols[j]]; }, w, res);
+      hungarian(kr, kc, [&](int i, int j) { return cost(rows[i], cols[j]); }, w, res);
       for (int i = 0; i < kr; ++i) {
         const int r = rows[i], c = cols[res[i]];
-        if (C[r * nc + c] <= thresh) {
+        if (keep(r, c)) {
           L.mrow[r] = c;
           L.mcol[c] = r;
         }
       }
     } else {
-      hungarian(kc, kr, [&](int i, int j) { return (double)C[rows[j] * nc + cols[i]]; }, w, res);
+      hungarian(kc, kr, [&](int i, int j) { return cost(rows[j], cols[i]); }, w, res);
       for (int i = 0; i < kc; ++i) {
         const int c = cols[i], r = rows[res[i]];
-        if (C[r * nc + c] <= thresh) {
+        if (keep(r, c)) {
           L.mrow[r] = c;
           L.mcol[c] = r;
         }
@@ -571,7 +593,7 @@ __device__ void assign(const Dev& g, const Lds& L, float* C, int* E, double* hw,
     }
   }
   __syncthreads();
-  // unmatched lists: with no kept match, ascending (list(np.arange)); else frozenset order
+  // unmatched lists: lap branch or no kept match, ascending; else frozenset order
   int nm = 0;
   for (int base = 0; base < nr; base += NT) {
     const int r = base + tid;
@@ -583,11 +605,14 @@ __device__ void assign(const Dev& g, const Lds& L, float* C, int* E, double* hw,
   for (int c = tid; c < nc; c += NT) L.flag[nr + c] = L.mcol[c] >= 0 ? 1 : 0;
   __syncthreads();
   if (tid == 0) {
-    if (nm == 0) {
-      for (int r = 0; r < nr; ++r) L.urow[r] = r;
-      for (int c = 0; c < nc; ++c) L.ucol[c] = c;
-      L.misc[Q_A] = nr;
-      L.misc[Q_B] = nc;
+    if (nm == 0 || lap) {  // ascending: list(np.arange) / np.where(x < 0)
+      int a = 0, b = 0;
+      for (int r = 0; r < nr; ++r)
+        if (!L.flag[r]) L.urow[a++] = r;
+      for (int c = 0; c < nc; ++c)
+        if (!L.flag[nr + c]) L.ucol[b++] = c;
+      L.misc[Q_A] = a;
+      L.misc[Q_B] = b;
     } else {
       L.misc[Q_A] = pyset_diff(nr, L.flag, nm, L.ptab, L.urow);
       L.misc[Q_B] = pyset_diff(nc, L.flag + nr, nm, L.ptab, L.ucol);
@@ -723,7 +748,7 @@ __global__ void __launch_bounds__(NT) bt_step_kernel(Dev g, const float* __restr
     C[e] = pair_cost(&L.txy[4 * r], &L.dxy[4 * d], L.dsc[d], cf.fuse != 0);
   }
   __syncthreads();
-  assign(g, L, C, E, hw, npool, nh, cf.th_match);
+  assign(g, L, C, E, hw, npool, nh, cf.th_match, cf.th_match_f64);
   int nu1 = L.misc[Q_A], nud1 = L.misc[Q_B];
   // matches in row order (linear_sum_assignment returns rows ascending)
   for (int base = 0; base < npool; base += NT) {
@@ -763,7 +788,7 @@ __global__ void __launch_bounds__(NT) bt_step_kernel(Dev g, const float* __restr
     C[e] = pair_cost(&L.txy[4 * r], &L.dxy[4 * L.se[c]], 1.0f, false);
   }
   __syncthreads();
-  assign(g, L, C, E, hw, nrt, n2, 0.5f);
+  assign(g, L, C, E, hw, nrt, n2, 0.5f, 0.5);
   const int nu2 = L.misc[Q_A];
   for (int base = 0; base < nrt; base += NT) {
     const int r = base + tid;
@@ -803,7 +828,7 @@ __global__ void __launch_bounds__(NT) bt_step_kernel(Dev g, const float* __restr
     C[e] = pair_cost(&L.txy[4 * r], &L.dxy[4 * d], L.dsc[d], cf.fuse != 0);
   }
   __syncthreads();
-  assign(g, L, C, E, hw, nun, nud1, 0.7f);
+  assign(g, L, C, E, hw, nun, nud1, 0.7f, 0.7);
   const int nuu = L.misc[Q_A], nud3 = L.misc[Q_B];
   for (int base = 0; base < nun; base += NT) {
     const int r = base + tid;
@@ -1032,6 +1057,8 @@ int yk_bt_create(yk_ctx* ctx, int n_streams, const yk_bt_cfg* cfg, yk_bt** out) 
   g.cfg.max_time_lost = (int)((double)cfg->frame_rate / 30.0 * (double)cfg->track_buffer);
   g.cfg.fuse = cfg->fuse_score ? 1 : 0;
   g.cfg.xywh = cfg->kind == YK_BT_BOTSORT ? 1 : 0;
+  g.cfg.lap = cfg->assignment == YK_BT_SCIPY ? 0 : 1;
+  g.cfg.th_match_f64 = cfg->match_thresh_f64 != 0.0 ? cfg->match_thresh_f64 : (double)cfg->match_thresh;
   const size_t S = n_streams;
   hipError_t e = hipSuccess;
   auto A = [&](void** p, size_t bytes) {

@@ -23,6 +23,8 @@
 #include <climits>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
+#include <type_traits>
 #include <array>
 #include <map>
 #include <tuple>
@@ -66,12 +68,30 @@ struct BF16 {
   static constexpr int EPL = 8;  // k elements per lane per K-step (16x16x32: 4 groups x 8)
   static constexpr bool kExact = false;
   static constexpr bool kScaled = false;
+  static constexpr bool kSplit = false;
 };
 struct F32 {
   using T = float;
   static constexpr int EPL = 4;  // 16x16x4 issued 4x: 4 groups x 4
   static constexpr bool kExact = true;
   static constexpr bool kScaled = false;
+  static constexpr bool kSplit = false;
+};
+// fp32 activations (the F32 build's storage, K step and tables unchanged) multiplied on the BF16
+// matrix cores: every fp32 operand is split into three bf16 parts, x = x0 + x1 + x2 exactly
+// (round-to-nearest-even each time: |x1| <= 2^-8 |x|, |x2| <= 2^-16 |x|, and the last remainder
+// has <= 8 significant bits), and the six products whose magnitude reaches 2^-16 of w.x --
+// w0x0 + w0x1 + w1x0 + w1x1 + w0x2 + w2x0 -- are summed by three v_mfma_f32_16x16x32_bf16 (each
+// bf16 x bf16 product is exact in f32).  What is left out (w1x2, w2x1, w2x2) is <= 2^-24 |w.x|,
+// the size of one f32 rounding, so the result is fp32-grade; three 16-cycle bf16 MFMAs replace
+// four 32-cycle f32 ones per K step (2.7x the matrix rate).  Weights are split once at model
+// create (24-byte fragments, yk_model::wsplit); activations as they are loaded (split3).
+struct F32S {
+  using T = float;
+  static constexpr int EPL = 4;
+  static constexpr bool kExact = true;
+  static constexpr bool kScaled = false;
+  static constexpr bool kSplit = true;
 };
 // OCP e4m3 (gfx950 fp8; not MI300's fnuz) activations and weights.  A 16-byte fragment holds 16
 // K elements: one K step is 64 = two 16x16x32 fp8 MFMAs (bytes 0-7 and 8-15 of every lane; A and
@@ -83,7 +103,22 @@ struct FP8 {
   static constexpr int EPL = 16;
   static constexpr bool kExact = false;
   static constexpr bool kScaled = true;
+  static constexpr bool kSplit = false;
 };
+
+// Weight fragment of one lane and K step (A operand) and the prepared activation fragment (B
+// operand): 16 bytes as loaded for every trait but F32S, whose weight fragment is the three bf16
+// parts of the lane's 4 f32 weights (24 bytes: w0 | w1 in .a, w2 in .b) and whose activation
+// fragment is the three bf16 parts of its 4 f32 activations (split3).
+struct WF24 {
+  uint4 a;
+  uint2 b;
+};
+struct XS3 {
+  unsigned p0a, p0b, p1a, p1b, p2a, p2b;  // part k of elements (0, 1) / (2, 3), element 0 low
+};
+template <class Tr> struct Frag { using W = uint4; using X = uint4; static constexpr int WB = 16; };
+template <> struct Frag<F32S> { using W = WF24; using X = XS3; static constexpr int WB = 24; };
 
 template <class Tr>
 __device__ __forceinline__ f32x4 mma(const uint4& w, const uint4& x, f32x4 acc);
@@ -98,6 +133,14 @@ __device__ __forceinline__ f32x4 mma<FP8>(const uint4& w, const uint4& x, f32x4 
   const long x0 = (long)(((unsigned long long)x.y << 32) | x.x), x1 = (long)(((unsigned long long)x.w << 32) | x.z);
   acc = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(w0, x0, acc, 0, 0, 0);
   return __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(w1, x1, acc, 0, 0, 0);
+}
+typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ f32x4 mma_split(const WF24& w, const XS3& x, f32x4 acc) {
+  const u32x4v a1 = {w.a.x, w.a.y, w.a.x, w.a.y}, a2 = {w.a.z, w.a.w, w.a.z, w.a.w}, a3 = {w.a.x, w.a.y, w.b.x, w.b.y};
+  const u32x4v b1 = {x.p0a, x.p0b, x.p1a, x.p1b}, b3 = {x.p2a, x.p2b, x.p0a, x.p0b};
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a1), __builtin_bit_cast(bf16x8, b1), acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a2), __builtin_bit_cast(bf16x8, b1), acc, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a3), __builtin_bit_cast(bf16x8, b3), acc, 0, 0, 0);
 }
 template <>
 __device__ __forceinline__ f32x4 mma<F32>(const uint4& w, const uint4& x, f32x4 acc) {
@@ -150,6 +193,31 @@ __device__ __forceinline__ unsigned pack_bf16x2(float a, float b) {
   const bf16x2 h = {(__bf16)a, (__bf16)b};
   return __builtin_bit_cast(unsigned, h);
 }
+// x = x0 + x1 + x2 exactly, each part bf16 (RNE), packed two elements per dword (F32S above)
+__device__ __forceinline__ XS3 split3(const uint4& x) {
+  const float a0 = __uint_as_float(x.x), a1 = __uint_as_float(x.y), a2 = __uint_as_float(x.z), a3 = __uint_as_float(x.w);
+  XS3 o;
+  o.p0a = pack_bf16x2(a0, a1);
+  o.p0b = pack_bf16x2(a2, a3);
+  const float r0 = a0 - __uint_as_float(o.p0a << 16), r1 = a1 - __uint_as_float(o.p0a & 0xffff0000u);
+  const float r2 = a2 - __uint_as_float(o.p0b << 16), r3 = a3 - __uint_as_float(o.p0b & 0xffff0000u);
+  o.p1a = pack_bf16x2(r0, r1);
+  o.p1b = pack_bf16x2(r2, r3);
+  o.p2a = pack_bf16x2(r0 - __uint_as_float(o.p1a << 16), r1 - __uint_as_float(o.p1a & 0xffff0000u));
+  o.p2b = pack_bf16x2(r2 - __uint_as_float(o.p1b << 16), r3 - __uint_as_float(o.p1b & 0xffff0000u));
+  return o;
+}
+template <class Tr>
+__device__ __forceinline__ typename Frag<Tr>::X xprep(const uint4& x) {
+  if constexpr (Tr::kSplit) return split3(x);
+  else return x;
+}
+template <class Tr>
+__device__ __forceinline__ f32x4 mmaf(const typename Frag<Tr>::W& w, const typename Frag<Tr>::X& x, f32x4 acc) {
+  if constexpr (Tr::kSplit) return mma_split(w, x, acc);
+  else return mma<Tr>(w, x, acc);
+}
+
 __device__ __forceinline__ void store4(unsigned short* p, const float v[4]) {
   uint2 o;
   o.x = pack_bf16x2(v[0], v[1]);
@@ -789,6 +857,20 @@ __device__ __forceinline__ uint4 bload(__amdgpu_buffer_rsrc_t r, unsigned voff, 
   const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, soff, 0);
   return make_uint4(v.x, v.y, v.z, v.w);
 }
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+// weight fragment of step ks (Frag<Tr>::WB bytes per lane, 64 lanes per step)
+template <class Tr>
+__device__ __forceinline__ typename Frag<Tr>::W wload(__amdgpu_buffer_rsrc_t r, unsigned voff, int ks) {
+  if constexpr (Tr::kSplit) {
+    WF24 w;
+    w.a = bload(r, voff, ks * 64 * 24);
+    const u32x2 b = __builtin_amdgcn_raw_buffer_load_b64(r, (int)voff + 16, ks * 64 * 24, 0);
+    w.b = make_uint2(b.x, b.y);
+    return w;
+  } else {
+    return bload(r, voff, ks * 1024);
+  }
+}
 
 // floor(n / d) for 0 <= n < 2^22, d >= 1, with inv = 1/d rounded up to f32 by the host:
 // the f32 product is within one of the quotient, fixed by one compare.
@@ -869,12 +951,14 @@ __device__ __forceinline__ void conv_fast_body(const FastArgs& a, int2 blk, int 
     bb[i] = (nt0 + i < a.n_tiles && n0 < a.cout) ? *(const float4*)(a.bias + n0) : make_float4(0.f, 0.f, 0.f, 0.f);
     if constexpr (Tr::kScaled) sc[i] = dq4<Tr>(a.bias, a.n_tiles, n0 < a.cout ? n0 : 0);
     const int nt = nt0 + i < a.n_tiles ? nt0 + i : a.n_tiles - 1;
-    wo[i] = a.woff + (unsigned)(((size_t)nt * nk * 64 + lane) * 16);
+    wo[i] = a.woff + (unsigned)(((size_t)nt * nk * 64 + lane) * Frag<Tr>::WB);
   }
   __syncthreads();
-  auto issue = [&](int ks, int2 e, uint4* wf, uint4* xf) {
+  using WF = typename Frag<Tr>::W;
+  using XP = typename Frag<Tr>::X;
+  auto issue = [&](int ks, int2 e, WF* wf, uint4* xf) {
 #pragma unroll
-    for (int i = 0; i < NE; ++i) wf[i] = bload(wr, wo[i], ks * 1024);
+    for (int i = 0; i < NE; ++i) wf[i] = wload<Tr>(wr, wo[i], ks);
     const unsigned tap = (unsigned)e.y & 15u;
     const bool s1 = (e.y & 16) != 0, ev = (e.y & 32) != 0;
 #pragma unroll
@@ -884,14 +968,26 @@ __device__ __forceinline__ void conv_fast_body(const FastArgs& a, int2 blk, int 
       xf[t] = bload(xr, ok ? off : kOOB, 0);
     }
   };
-  auto load_step = [&](int ks, uint4* wf, uint4* xf) { issue(ks, tab[ks * 4 + kg], wf, xf); };
+  auto load_step = [&](int ks, WF* wf, uint4* xf) { issue(ks, tab[ks * 4 + kg], wf, xf); };
+  // one K step's MFMAs: the activation fragments are prepared once (F32S: split into bf16 parts)
+  // and used by every output-channel tile
+  auto step_mma = [&](const WF* wf, const uint4* xf) {
+    XP xp[NPT];
+#pragma unroll
+    for (int t = 0; t < NPT; ++t) xp[t] = xprep<Tr>(xf[t]);
+#pragma unroll
+    for (int i = 0; i < NE; ++i)
+#pragma unroll
+      for (int t = 0; t < NPT; ++t) acc[i][t] = mmaf<Tr>(wf[i], xp[t], acc[i][t]);
+  };
   int k0 = 0, k1 = nk;
   if (WS) {
     const int kq = (nk + 3) >> 2;
     k0 = wave * kq;
     k1 = k0 + kq < nk ? k0 + kq : nk;
   }
-  uint4 wb[SKD][NE], xb[SKD][NPT];
+  WF wb[SKD][NE];
+  uint4 xb[SKD][NPT];
   int ks = k0;
   if (k1 - k0 >= 2 * SKD) {
     // prologue and steady state issue the loads in the same pinned order (MFMAs of step d,
@@ -921,10 +1017,7 @@ __device__ __forceinline__ void conv_fast_body(const FastArgs& a, int2 blk, int 
         for (int d = 0; d < SKD; ++d) {
           __builtin_amdgcn_sched_barrier(0);
           const int2 e = tab[(ks + d + SKD) * 4 + kg];  // LDS read in flight over the MFMAs
-#pragma unroll
-          for (int i = 0; i < NE; ++i)
-#pragma unroll
-            for (int t = 0; t < NPT; ++t) acc[i][t] = mma<Tr>(wb[d][i], xb[d][t], acc[i][t]);
+          step_mma(wb[d], xb[d]);
           __builtin_amdgcn_sched_barrier(0);
           issue(ks + d + SKD, e, wb[d], xb[d]);
         }
@@ -940,12 +1033,7 @@ __device__ __forceinline__ void conv_fast_body(const FastArgs& a, int2 blk, int 
           for (int t = 0; t < NPT; ++t) acc[i][t] = mma2<Tr>(wb[d][i], wb[d + 1][i], xb[d][t], xb[d + 1][t], acc[i][t]);
     } else {
 #pragma unroll
-      for (int d = 0; d < SKD; ++d) {
-#pragma unroll
-        for (int i = 0; i < NE; ++i)
-#pragma unroll
-          for (int t = 0; t < NPT; ++t) acc[i][t] = mma<Tr>(wb[d][i], xb[d][t], acc[i][t]);
-      }
+      for (int d = 0; d < SKD; ++d) step_mma(wb[d], xb[d]);
     }
     ks += SKD;
   }
@@ -976,10 +1064,7 @@ __device__ __forceinline__ void conv_fast_body(const FastArgs& a, int2 blk, int 
 #pragma unroll
         for (int d = 0; d < SKD; ++d) {
           if (ks + d < k1) {
-#pragma unroll
-            for (int i = 0; i < NE; ++i)
-#pragma unroll
-              for (int t = 0; t < NPT; ++t) acc[i][t] = mma<Tr>(wb[d][i], xb[d][t], acc[i][t]);
+            step_mma(wb[d], xb[d]);
             if (ks + d + SKD < k1) load_step(ks + d + SKD, wb[d], xb[d]);
           }
         }
@@ -2633,6 +2718,13 @@ struct yk_model {
   char* arena = nullptr;      // every activation buffer (bufs[i] point into it)
   size_t arena_bytes = 0;
   size_t blob_bytes = 0;
+  // F32 build: every table-kernel conv's weights split into three bf16 parts (F32S, 24-byte
+  // fragments in the packed fragment order), for the split-MFMA variant (plan npt bit kSplitBit)
+  char* wsplit = nullptr;
+  size_t wsplit_bytes = 0;
+  std::vector<int64_t> ws_off;
+  bool split_default = false;  // YK_F32_SPLIT=1: the heuristic plan uses F32S where it can
+  bool autotune_split = true;  // YK_F32_SPLIT=0: autotune never picks F32S
 };
 
 namespace {
@@ -2837,7 +2929,7 @@ void set_fast_attr_n() {
   set_fast_attr<Tr, NNT, 1, WS>();
   set_fast_attr<Tr, NNT, 2, WS>();
   set_fast_attr<Tr, NNT, 4, WS>();
-  if constexpr (!WS) {
+  if constexpr (!WS && !Tr::kSplit) {
     set_fastw_attr<Tr, NNT, 1>();
     set_fastw_attr<Tr, NNT, 2>();
     set_fastw_attr<Tr, NNT, 4>();
@@ -2873,6 +2965,8 @@ void set_tile_attrs() {
   set_fast_attr_w<BF16, true>();
   set_fast_attr_w<F32, false>();
   set_fast_attr_w<F32, true>();
+  set_fast_attr_w<F32S, false>();
+  set_fast_attr_w<F32S, true>();
   set_wide_attr_n<FP8, 2>();
   set_wide_attr_n<FP8, 4>();
   set_fast_attr_w<FP8, false>();
@@ -2887,6 +2981,8 @@ void set_tile_attrs() {
 
 // Conv kernel choice for one op at batch B.
 enum { CK_DIRECT = 0, CK_TILE = 1, CK_SPLITK = 2, CK_FAST = 3, CK_WIDE = 4 };
+// CK_FAST plan npt bit: the F32 build's op runs the F32S split-MFMA body (modes 0 and 1 only)
+constexpr int kSplitBit = 64;
 // CK_WIDE plan: nnt in {2, 4} (output-channel tiles per workgroup), npt unused
 // CK_FAST plan: nnt in {1, 2, 3, 4}, npt = NPT | (WS << 4) with NPT in {1, 2, 4}
 struct ConvPlan {
@@ -3002,6 +3098,7 @@ ConvPlan conv_plan(const yk_model* m, const yk_op& op, int B) {
       p.kind = CK_FAST;
       p.nnt = t[1];
       p.npt = t[2];
+      if ((p.npt & kSplitBit) && !(m->wsplit && m->ws_off[idx] >= 0)) p.npt &= ~kSplitBit;
       return p;
     }
     if (t[0] == CK_TILE && m->ltab && m->ltab_off[idx] >= 0) {
@@ -3014,8 +3111,11 @@ ConvPlan conv_plan(const yk_model* m, const yk_op& op, int B) {
   }
   if (!m->tiled) return ConvPlan{};
   const size_t oi = (size_t)(&op - m->ops.data());
-  if (m->ktab && oi < m->ktab_off.size() && m->ktab_off[oi] >= 0 && (long)B * op.out_h * op.out_w < (1L << 22))
-    return fast_plan(op, B);  // (fdiv: pixel indices < 2^22)
+  if (m->ktab && oi < m->ktab_off.size() && m->ktab_off[oi] >= 0 && (long)B * op.out_h * op.out_w < (1L << 22)) {
+    ConvPlan p = fast_plan(op, B);  // (fdiv: pixel indices < 2^22)
+    if (m->split_default && m->wsplit && m->ws_off[oi] >= 0 && (p.npt >> 4) != 2) p.npt |= kSplitBit;
+    return p;
+  }
   if (op.out_h * op.out_w <= 1280) return splitk_plan(op, B);
   ConvPlan p;
   p.tp = tile_plan(op, esz, B);
@@ -3089,9 +3189,14 @@ void launch_fastw(const FastArgs& a, int nnt, int npt, hipStream_t st) {
 // 2 = per-wave pixels with the weight fragments shared through LDS (conv_fastw_kernel)
 template <class Tr>
 void launch_fast(const FastArgs& a, const ConvPlan& p, hipStream_t st) {
-  const int mode = p.npt >> 4;
-  if (mode == 2) launch_fastw<Tr>(a, p.nnt, p.npt & 15, st);
-  else if (mode == 1) launch_fast_w<Tr, true>(a, p.nnt, p.npt & 15, st);
+  const int mode = (p.npt >> 4) & 3;
+  if constexpr (!Tr::kSplit) {
+    if (mode == 2) {
+      launch_fastw<Tr>(a, p.nnt, p.npt & 15, st);
+      return;
+    }
+  }
+  if (mode == 1) launch_fast_w<Tr, true>(a, p.nnt, p.npt & 15, st);
   else launch_fast_w<Tr, false>(a, p.nnt, p.npt & 15, st);
 }
 
@@ -3277,6 +3382,15 @@ int launch_op(yk_model* m, const yk_op& op, const uint8_t* frames, int B, float 
           f.xcd = m->xcd;
           f.tstamp = (m->ts && (int)(&op - m->ops.data()) == m->ts_op) ? m->ts : nullptr;
           f.tstamp_cap = kTsCap;
+          if constexpr (std::is_same<Tr, F32>::value) {
+            if (cp.npt & kSplitBit) {  // split-MFMA body on the bf16-split weights
+              f.wblob = m->wsplit;
+              f.wbytes = (unsigned)m->wsplit_bytes;
+              f.woff = (unsigned)m->ws_off[(size_t)(&op - m->ops.data())];
+              launch_fast<F32S>(f, cp, st);
+              break;
+            }
+          }
           launch_fast<Tr>(f, cp, st);
         } else if constexpr (Tr::kScaled) {
           // FP8 runs only on the table-driven and wide kernels (16-channel K chunks)
@@ -3393,7 +3507,7 @@ int launch_any(yk_model* m, const yk_op& op, const uint8_t* frames, int B, float
 const char* op_kernel_name(const yk_model* m, const yk_op& op) {
   const int dt = m->desc.act_dtype;
   const bool f = dt == YK_ACT_F32;
-  const char* tn = tr_name(dt);
+  const char* tn = tr_name(dt);  // (F32S for a split-MFMA table conv below)
   static thread_local char buf[96];
   switch (op.kind) {
     case YK_K_CONV_INPUT:
@@ -3420,8 +3534,9 @@ const char* op_kernel_name(const yk_model* m, const yk_op& op) {
     return buf;
   }
   if (cp.kind == CK_FAST) {
-    const int npt = cp.npt & 15, mode = cp.npt >> 4;
+    const int npt = cp.npt & 15, mode = (cp.npt >> 4) & 3;
     const int skd = mode == 2 ? fastw_skd(cp.nnt, npt) : fast_skd(cp.nnt, npt);
+    if (cp.npt & kSplitBit) tn = "F32S";
     if (mode == 2)
       snprintf(buf, sizeof buf, "conv_fastw_kernel<yk::det::%s, %d, %d, %d>", tn, cp.nnt, npt, skd);
     else
@@ -3713,6 +3828,58 @@ hipError_t build_ktabs(yk_model* m, bool fast) {
   return e;
 }
 
+// host float -> bf16 bits, round-to-nearest-even (finite inputs)
+inline unsigned short h_f2bf(float f) {
+  unsigned u;
+  memcpy(&u, &f, 4);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (unsigned short)(u >> 16);
+}
+inline float h_bf2f(unsigned short h) {
+  const unsigned u = (unsigned)h << 16;
+  float f;
+  memcpy(&f, &u, 4);
+  return f;
+}
+
+// F32S weight fragments: the packed f32 A-operand fragments of every table-kernel conv ([n_tiles]
+// [k_steps][64 lanes][4 f32], model.py Program.pack) as [n_tiles][k_steps][64][24 B]: w0 of the
+// 4 elements, w1, w2 (bf16, element 0 in the low half of each dword), w = w0 + w1 + w2 exactly.
+hipError_t build_wsplit(yk_model* m, const char* host_blob, size_t blob_bytes) {
+  m->ws_off.assign(m->ops.size(), -1);
+  std::vector<unsigned short> out;
+  for (size_t i = 0; i < m->ops.size(); ++i) {
+    const yk_op& op = m->ops[i];
+    if (op.kind != YK_K_CONV || m->ktab_off.empty() || m->ktab_off[i] < 0) continue;
+    const size_t nfrag = (size_t)op.n_tiles * op.k_steps * 64;
+    if ((size_t)op.w_off + nfrag * 16 > blob_bytes) continue;
+    while ((out.size() * 2) % 256) out.push_back(0);  // 256-byte aligned per op
+    m->ws_off[i] = (int64_t)out.size() * 2;
+    const float* w = (const float*)(host_blob + op.w_off);
+    for (size_t f = 0; f < nfrag; ++f) {
+      unsigned short part[3][4];
+      for (int e = 0; e < 4; ++e) {
+        const float x = w[f * 4 + e];
+        part[0][e] = h_f2bf(x);
+        const float r1 = x - h_bf2f(part[0][e]);
+        part[1][e] = h_f2bf(r1);
+        part[2][e] = h_f2bf(r1 - h_bf2f(part[1][e]));
+      }
+      for (int k = 0; k < 3; ++k)
+        for (int e = 0; e < 4; ++e) out.push_back(part[k][e]);
+    }
+  }
+  if (out.empty()) return hipSuccess;
+  if (out.size() * 2 >= 0x7fff0000ull) {  // 32-bit buffer offsets
+    m->ws_off.assign(m->ops.size(), -1);
+    return hipSuccess;
+  }
+  m->wsplit_bytes = out.size() * 2;
+  hipError_t e = hipMalloc((void**)&m->wsplit, m->wsplit_bytes);
+  if (e == hipSuccess) e = hipMemcpy(m->wsplit, out.data(), m->wsplit_bytes, hipMemcpyHostToDevice);
+  return e;
+}
+
 hipError_t set_schedule(yk_model* m, int groups, int lanes) {
   for (auto& kv : m->graphs) (void)hipGraphExecDestroy(kv.second);
   m->graphs.clear();
@@ -3835,6 +4002,11 @@ int yk_model_create(yk_ctx* ctx, const yk_model_desc* desc, const void* host_blo
     if (e == hipSuccess) e = hipMemset(m->ts, 0, 3 * (size_t)kTsCap * sizeof(unsigned long long));
   }
   if (e == hipSuccess) e = build_ktabs(m, !(getenv("YK_CONV_FAST") && getenv("YK_CONV_FAST")[0] == '0'));
+  if (const char* env = getenv("YK_F32_SPLIT")) {
+    m->split_default = env[0] == '1';
+    m->autotune_split = env[0] != '0';
+  }
+  if (e == hipSuccess && desc->act_dtype == YK_ACT_F32) e = build_wsplit(m, (const char*)host_blob, (size_t)blob_bytes);
   if (e == hipSuccess && desc->act_dtype == YK_ACT_FP8)
     for (size_t i = 0; i < m->ops.size(); ++i)
       if (m->ops[i].kind == YK_K_CONV && (m->ktab_off[i] < 0 || m->ops[i].src_ch[0] % 16 ||
@@ -3887,7 +4059,7 @@ int yk_model_destroy(yk_model* m) {
   for (hipEvent_t v : m->ev) (void)hipEventDestroy(v);
   if (m->arena) (void)hipFree(m->arena);
   void* ptrs[] = {m->blob, m->cand, m->cand_count, m->slot_of, m->gkeys, m->gbox, m->gflag, m->dets, m->counts, m->ktab,
-                  m->ltab, m->lbox, m->ts};
+                  m->ltab, m->lbox, m->ts, m->wsplit};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   delete m;
@@ -3990,8 +4162,11 @@ int yk_model_set_plan(yk_model* m, int op_index, int batch, int kind, int nnt, i
   YK_CHECK_ARG(kind != CK_WIDE || ((nnt == 2 || nnt == 4) && (npt == 0 || npt == 4 || npt == 8)),
                "yk_model_set_plan: wide conv nnt must be 2 or 4, npt (waves) 0, 4 or 8");
   YK_CHECK_ARG(kind != CK_FAST || (nnt >= 1 && nnt <= 4 && ((npt & 15) == 1 || (npt & 15) == 2 || (npt & 15) == 4) &&
-                                   (npt >> 4) <= 2),
-               "yk_model_set_plan: table conv needs nnt in [1, 4], npt in {1, 2, 4} (+16: waves split K, +32: LDS-shared weights)");
+                                   ((npt >> 4) & 3) <= 2 && (npt & ~(kSplitBit | 63)) == 0),
+               "yk_model_set_plan: table conv needs nnt in [1, 4], npt in {1, 2, 4} (+16: waves split K, +32: LDS-shared "
+               "weights, +64: split-bf16 MFMA)");
+  YK_CHECK_ARG(kind != CK_FAST || !(npt & kSplitBit) || (m->wsplit && ((npt >> 4) & 3) != 2),
+               "yk_model_set_plan: the split-bf16 MFMA variant (+64) needs the fp32 build and modes 0 / 1");
   YK_CHECK_ARG(kind != CK_TILE || nnt == 0 || nnt == 1, "yk_model_set_plan: tiled conv nnt must be 0 or 1 (LDS-resident weights)");
   YK_CHECK_ARG(kind != CK_SPLITK || ((nnt == 1 || nnt == 2 || nnt == 4) && (npt == 1 || npt == 2 || npt == 4)),
                "yk_model_set_plan: split-K fragment tile must be nnt, npt in {1, 2, 4}");
@@ -4062,6 +4237,8 @@ int yk_model_autotune(yk_model* m, const uint8_t* frames, int batch, float conf,
             const long wgs = ((long)bt * op.out_h * op.out_w + px - 1) / px * ((op.n_tiles + nnt - 1) / nnt);
             if (wgs < 64) continue;
             cands.push_back({CK_FAST, nnt, npt | (mode << 4)});
+            if (mode < 2 && m->wsplit && m->ws_off[i] >= 0 && m->autotune_split)
+              cands.push_back({CK_FAST, nnt, npt | (mode << 4) | kSplitBit});
           }
     if (cands.empty()) continue;  // (FP8 without a table: yk_model_create refuses that)
     float best = 1e30f;
