@@ -413,6 +413,29 @@ int yk_model_outputs(yk_model* m, float** dev_dets, int32_t** dev_counts);
  * counts per image (parity harnesses compare them to the oracle's Detect output). */
 int yk_model_candidates(yk_model* m, float** dev_cand, int32_t** dev_counts);
 
+/* TorchNMS.nms + non_max_suppression's max_nms / max_det cut + scale_boxes / clip_boxes
+ * (ultralytics/utils/nms.py:13-167, 237-304 incl. the :291-296 early exit; utils/ops.py:105-184)
+ * on GIVEN boxes, through the same nms_kernel yk_detect runs after Detect.  dev_rows:
+ * [batch][max_rows][row_stride] float32 rows {x1, y1, x2, y2, score, ...} in network-input
+ * pixels, dev_counts: [batch] rows used.  Order among equal scores = input order (a stable sort).
+ * dets / counts as yk_detect (NULL = the model's own buffers); keep (optional, [batch][max_det]):
+ * the input row index of every output row.  max_rows <= n_anchors of the model.  Asynchronous. */
+int yk_nms(yk_model* m, const float* dev_rows, int row_stride, int max_rows, const int32_t* dev_counts, int batch,
+           float iou, int max_det, float* dets, int32_t* counts, int32_t* keep, void* stream);
+/* The NMS stage alone on the model's current candidate buffers (yk_model_candidates): keep
+ * gets each output row's candidate id (the anchor field). */
+int yk_nms_candidates(yk_model* m, int batch, float iou, int max_det, float* dets, int32_t* counts, int32_t* keep,
+                      void* stream);
+/* NMS counters since the last reset: out[0] = images whose greedy loop took the :291-296 early
+ * exit (no overlap with the kept box, every remaining box kept) with boxes left, out[1] = images
+ * processed.  Synchronises `stream`. */
+int yk_model_nms_stats(yk_model* m, int64_t* out, int reset, void* stream);
+/* Synchronise `stream`, then report a device-side error flagged by an earlier launch (NMS met a
+ * candidate row whose anchor index lies outside [0, n_anchors): that image's detections are
+ * dropped) as YK_ERR_STATE; yk_detect / yk_detect_graph / yk_nms report it on their next call
+ * without synchronising. */
+int yk_model_check(yk_model* m, void* stream);
+
 /* Per-op device time: launches every op of the program `reps` times back to back between two
  * hipEvents on `stream` and writes the average milliseconds per launch to host_ms[op]
  * (host_ms[n_ops] = the NMS kernel).  Outputs of the call are not meaningful. */

@@ -76,12 +76,18 @@ def _run_gpu(dtype, frames):
     fd = frames.cuda()
     pipe.frames.copy_(fd[0])
     pipe.capture(tune=False)
+    for m in pipe.models:
+        m.nms_stats(reset=True)  # count the timed frames' NMS only
     rec = StepRecorder(pipe, F)
     pipe.step_hook = rec
     for t in range(F):
         pipe.run(fd[t])
     pipe.sync()
     out = rec.host()
+    st = [m.nms_stats() for m in pipe.models]
+    _run_gpu.nms = {"early_exit_images": sum(e for e, _ in st), "images": sum(n for _, n in st)}
+    for m in pipe.models:
+        m.check()  # no device-side error flagged during the run
     del pipe
     torch.cuda.empty_cache()
     return out
@@ -128,8 +134,10 @@ def test_bench_pipeline_fp32_matches_oracle_chain_every_frame(chain):
                                              "live_tracks_end": live, "max_box_rel_dev": box_rel,
                                              "max_confidence_abs_dev": conf_dev,
                                              "oracle_tie_frames": chain["tie_frames"],
+                                             "nms_early_exit": _run_gpu.nms,
                                              "nms_score_ties": chain["nms_score_ties"],
                                              "terminated": chain["terminated"]}))
+    assert _run_gpu.nms["images"] == S * F  # every frame's NMS ran once on the device
     assert conf_dev <= 1e-2
     assert min(chain["live"]) >= 40, chain["live"]  # the bench's >= 64-track load (see bench.py CONFIGS)
     assert chain["terminated"] > 0  # the deletion path ran inside the chain

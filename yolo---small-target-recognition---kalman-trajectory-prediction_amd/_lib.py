@@ -24,7 +24,12 @@ TRAJ_OUT, VEL_HIST, TRAJ_HIST = 30, 50, 150
 
 
 class YKError(RuntimeError):
-    """A libyk.so call failed (message from yk_last_error())."""
+    """A libyk.so call failed (message from yk_last_error(); .status = the yk_status code, or
+    None when the error is raised on the Python side)."""
+
+    def __init__(self, msg, status=None):
+        super().__init__(msg)
+        self.status = status
 
 
 # ---------------------------------------------------------------- ABI structs
@@ -135,6 +140,10 @@ _SIGS = {
     "yk_gmd_download": ([_vp, _vp, _vp, _vp], C.c_int),
     "yk_gmd_points": ([_vp, C.c_int, _vp, _vp, _vp, C.POINTER(_i32), _vp], C.c_int),
     "yk_tracker_step_motion": ([_vp, _vp, C.c_int, C.c_int, _vp, _vp, _vp], C.c_int),
+    "yk_nms": ([_vp, _vp, C.c_int, C.c_int, _vp, C.c_int, C.c_float, C.c_int, _vp, _vp, _vp, _vp], C.c_int),
+    "yk_nms_candidates": ([_vp, C.c_int, C.c_float, C.c_int, _vp, _vp, _vp, _vp], C.c_int),
+    "yk_model_nms_stats": ([_vp, _vp, C.c_int, _vp], C.c_int),
+    "yk_model_check": ([_vp, _vp], C.c_int),
 }
 
 _lock = threading.Lock()
@@ -179,7 +188,7 @@ def lib() -> C.CDLL:
 def check(rc: int, what: str = "") -> None:
     if rc != YK_OK:
         msg = lib().yk_last_error().decode(errors="replace")
-        raise YKError(f"{what or 'yk call'} failed (status {rc}): {msg}")
+        raise YKError(f"{what or 'yk call'} failed (status {rc}): {msg}", rc)
 
 
 def ptr(a) -> C.c_void_p:

@@ -85,7 +85,14 @@ struct F32 {
 // bf16 x bf16 product is exact in f32).  What is left out (w1x2, w2x1, w2x2) is <= 2^-24 |w.x|,
 // the size of one f32 rounding, so the result is fp32-grade; three 16-cycle bf16 MFMAs replace
 // four 32-cycle f32 ones per K step (2.7x the matrix rate).  Weights are split once at model
-// create (24-byte fragments, yk_model::wsplit); activations as they are loaded (split3).
+// create (yk_model::wsplit), activations as they are loaded (split3).  Operand layout: an MFMA
+// operand is 4 VGPRs = one dword per element e of the lane's 4, and every dword pairs two parts
+// of ONE element: weights W01 = [w0(e) | w1(e)], W02 = [w0(e) | w2(e)] (32-byte fragments);
+// activations X00 = [x0 | x0], X11 = [x1 | x1], X20 = [x2 | x0] (each dword one v_cvt_pk_bf16_f32
+// of the element with itself or its remainder).  W01 x X00 = w0x0 + w1x0, W01 x X11 = w0x1 +
+// w1x1, W02 x X20 = w0x2 + w2x0: every operand is built in place by the instruction that produces
+// it, so no register copies are needed, and the three MFMA passes run over all NE x NPT
+// accumulators in turn (independent accumulators back to back).
 struct F32S {
   using T = float;
   static constexpr int EPL = 4;
@@ -110,15 +117,16 @@ struct FP8 {
 // operand): 16 bytes as loaded for every trait but F32S, whose weight fragment is the three bf16
 // parts of the lane's 4 f32 weights (24 bytes: w0 | w1 in .a, w2 in .b) and whose activation
 // fragment is the three bf16 parts of its 4 f32 activations (split3).
-struct WF24 {
-  uint4 a;
-  uint2 b;
+typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
+// F32S weight fragment (W01, W02) and activation fragment (X00, X11, X20), see F32S
+struct WS2 {
+  u32x4v w01, w02;
 };
 struct XS3 {
-  unsigned p0a, p0b, p1a, p1b, p2a, p2b;  // part k of elements (0, 1) / (2, 3), element 0 low
+  u32x4v x00, x11, x20;
 };
 template <class Tr> struct Frag { using W = uint4; using X = uint4; static constexpr int WB = 16; };
-template <> struct Frag<F32S> { using W = WF24; using X = XS3; static constexpr int WB = 24; };
+template <> struct Frag<F32S> { using W = WS2; using X = XS3; static constexpr int WB = 32; };
 
 template <class Tr>
 __device__ __forceinline__ f32x4 mma(const uint4& w, const uint4& x, f32x4 acc);
@@ -134,14 +142,13 @@ __device__ __forceinline__ f32x4 mma<FP8>(const uint4& w, const uint4& x, f32x4 
   acc = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(w0, x0, acc, 0, 0, 0);
   return __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(w1, x1, acc, 0, 0, 0);
 }
-typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ f32x4 mma_split(const WF24& w, const XS3& x, f32x4 acc) {
-  const u32x4v a1 = {w.a.x, w.a.y, w.a.x, w.a.y}, a2 = {w.a.z, w.a.w, w.a.z, w.a.w}, a3 = {w.a.x, w.a.y, w.b.x, w.b.y};
-  const u32x4v b1 = {x.p0a, x.p0b, x.p1a, x.p1b}, b3 = {x.p2a, x.p2b, x.p0a, x.p0b};
-  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a1), __builtin_bit_cast(bf16x8, b1), acc, 0, 0, 0);
-  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a2), __builtin_bit_cast(bf16x8, b1), acc, 0, 0, 0);
-  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a3), __builtin_bit_cast(bf16x8, b3), acc, 0, 0, 0);
+__device__ __forceinline__ f32x4 mfma_bf16(const u32x4v& a, const u32x4v& b, f32x4 acc) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), acc, 0, 0, 0);
 }
+// one split K step: per pixel fragment t (split just before its MFMAs, so one fragment's parts
+// are live at a time), pass p over the NE accumulators of t, then pass p + 1
+template <int NE, int NPT>
+__device__ __forceinline__ void mma_split_step(const WS2* w, const uint4* xf, f32x4 (*acc)[NPT]);
 template <>
 __device__ __forceinline__ f32x4 mma<F32>(const uint4& w, const uint4& x, f32x4 acc) {
   acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(w.x), __uint_as_float(x.x), acc, 0, 0, 0);
@@ -193,30 +200,38 @@ __device__ __forceinline__ unsigned pack_bf16x2(float a, float b) {
   const bf16x2 h = {(__bf16)a, (__bf16)b};
   return __builtin_bit_cast(unsigned, h);
 }
-// x = x0 + x1 + x2 exactly, each part bf16 (RNE), packed two elements per dword (F32S above)
+// x = x0 + x1 + x2 exactly per element, each part bf16 (RNE); the F32S activation operands
+// X00 = [x0 | x0], X11 = [x1 | x1], X20 = [x2 | x0] (one dword per element)
 __device__ __forceinline__ XS3 split3(const uint4& x) {
-  const float a0 = __uint_as_float(x.x), a1 = __uint_as_float(x.y), a2 = __uint_as_float(x.z), a3 = __uint_as_float(x.w);
+  const unsigned u[4] = {x.x, x.y, x.z, x.w};
   XS3 o;
-  o.p0a = pack_bf16x2(a0, a1);
-  o.p0b = pack_bf16x2(a2, a3);
-  const float r0 = a0 - __uint_as_float(o.p0a << 16), r1 = a1 - __uint_as_float(o.p0a & 0xffff0000u);
-  const float r2 = a2 - __uint_as_float(o.p0b << 16), r3 = a3 - __uint_as_float(o.p0b & 0xffff0000u);
-  o.p1a = pack_bf16x2(r0, r1);
-  o.p1b = pack_bf16x2(r2, r3);
-  o.p2a = pack_bf16x2(r0 - __uint_as_float(o.p1a << 16), r1 - __uint_as_float(o.p1a & 0xffff0000u));
-  o.p2b = pack_bf16x2(r2 - __uint_as_float(o.p1b << 16), r3 - __uint_as_float(o.p1b & 0xffff0000u));
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const float a = __uint_as_float(u[e]);
+    const unsigned d00 = pack_bf16x2(a, a);
+    const float r1 = a - __uint_as_float(d00 & 0xffff0000u);
+    const unsigned d11 = pack_bf16x2(r1, r1);
+    const float r2 = r1 - __uint_as_float(d11 & 0xffff0000u);
+    o.x00[e] = d00;
+    o.x11[e] = d11;
+    o.x20[e] = pack_bf16x2(r2, a);
+  }
   return o;
 }
-template <class Tr>
-__device__ __forceinline__ typename Frag<Tr>::X xprep(const uint4& x) {
-  if constexpr (Tr::kSplit) return split3(x);
-  else return x;
+template <int NE, int NPT>
+__device__ __forceinline__ void mma_split_step(const WS2* w, const uint4* xf, f32x4 (*acc)[NPT]) {
+#pragma unroll
+  for (int t = 0; t < NPT; ++t) {
+    const XS3 x = split3(xf[t]);
+#pragma unroll
+    for (int i = 0; i < NE; ++i) acc[i][t] = mfma_bf16(w[i].w01, x.x00, acc[i][t]);
+#pragma unroll
+    for (int i = 0; i < NE; ++i) acc[i][t] = mfma_bf16(w[i].w01, x.x11, acc[i][t]);
+#pragma unroll
+    for (int i = 0; i < NE; ++i) acc[i][t] = mfma_bf16(w[i].w02, x.x20, acc[i][t]);
+  }
 }
-template <class Tr>
-__device__ __forceinline__ f32x4 mmaf(const typename Frag<Tr>::W& w, const typename Frag<Tr>::X& x, f32x4 acc) {
-  if constexpr (Tr::kSplit) return mma_split(w, x, acc);
-  else return mma<Tr>(w, x, acc);
-}
+
 
 __device__ __forceinline__ void store4(unsigned short* p, const float v[4]) {
   uint2 o;
@@ -862,10 +877,9 @@ typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 template <class Tr>
 __device__ __forceinline__ typename Frag<Tr>::W wload(__amdgpu_buffer_rsrc_t r, unsigned voff, int ks) {
   if constexpr (Tr::kSplit) {
-    WF24 w;
-    w.a = bload(r, voff, ks * 64 * 24);
-    const u32x2 b = __builtin_amdgcn_raw_buffer_load_b64(r, (int)voff + 16, ks * 64 * 24, 0);
-    w.b = make_uint2(b.x, b.y);
+    WS2 w;
+    w.w01 = __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, ks * 64 * 32, 0);
+    w.w02 = __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff + 16, ks * 64 * 32, 0);
     return w;
   } else {
     return bload(r, voff, ks * 1024);
@@ -955,7 +969,6 @@ __device__ __forceinline__ void conv_fast_body(const FastArgs& a, int2 blk, int 
   }
   __syncthreads();
   using WF = typename Frag<Tr>::W;
-  using XP = typename Frag<Tr>::X;
   auto issue = [&](int ks, int2 e, WF* wf, uint4* xf) {
 #pragma unroll
     for (int i = 0; i < NE; ++i) wf[i] = wload<Tr>(wr, wo[i], ks);
@@ -972,13 +985,14 @@ __device__ __forceinline__ void conv_fast_body(const FastArgs& a, int2 blk, int 
   // one K step's MFMAs: the activation fragments are prepared once (F32S: split into bf16 parts)
   // and used by every output-channel tile
   auto step_mma = [&](const WF* wf, const uint4* xf) {
-    XP xp[NPT];
+    if constexpr (Tr::kSplit) {
+      mma_split_step<NE, NPT>(wf, xf, acc);
+    } else {
 #pragma unroll
-    for (int t = 0; t < NPT; ++t) xp[t] = xprep<Tr>(xf[t]);
+      for (int i = 0; i < NE; ++i)
 #pragma unroll
-    for (int i = 0; i < NE; ++i)
-#pragma unroll
-      for (int t = 0; t < NPT; ++t) acc[i][t] = mmaf<Tr>(wf[i], xp[t], acc[i][t]);
+        for (int t = 0; t < NPT; ++t) acc[i][t] = mma<Tr>(wf[i], xf[t], acc[i][t]);
+    }
   };
   int k0 = 0, k1 = nk;
   if (WS) {
@@ -2149,7 +2163,23 @@ struct NmsArgs {
   int* counts;
   float pad_x, pad_y, gain, clip_w, clip_h;
   int dbg;  // YK_NMS_DBG=1: phase times (us, s_memrealtime) in dets[b][max_det-1] (diagnostics only)
+  int* keep_out;  // [B][max_det] kept rows' candidate ids (the anchor field), or NULL
+  int* stat;      // [2] images that took the :291-296 early exit with boxes left, images processed
+  int* err;       // device view of a host-mapped word: bit 0 = a candidate row carried an anchor
+                  // outside [0, n_anchors) (the image's count is then 0); read by the host API
 };
+
+// Sort key of a candidate: ascending key = score descending (NaN first, as torch's sort puts it;
+// -0 == +0), then candidate id ascending -- the stable order of scores.sort(descending=True)
+__device__ __forceinline__ unsigned long long nms_key(float score, int id) {
+  unsigned u = __float_as_uint(score);
+  if (u == 0x80000000u) u = 0u;
+  const unsigned m = (u & 0x80000000u) ? ~u : (u | 0x80000000u);  // order-preserving float -> uint
+  return ((unsigned long long)(~m) << 32) | (unsigned)id;
+}
+__device__ __forceinline__ void nms_flag_error(int* err) {
+  __hip_atomic_fetch_or(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 
 __device__ __forceinline__ void bitonic_sort(unsigned long long* k, int n2) {
   for (int size = 2; size <= n2; size <<= 1) {
@@ -2202,7 +2232,7 @@ __device__ __forceinline__ unsigned long long after_mask(int w, int i) {
 // The greedy walk over precomputed masks (one wave).  Both mask rows of the picked box are read
 // together, so an iteration waits on one LDS round trip.
 __device__ int nms_walk(int n, int max_det, const unsigned long long* sup, const unsigned long long* ovl, int* keep,
-                        int* k_out) {
+                        int* k_out, int* early) {
   const int W = (n + 63) / 64;
   if (threadIdx.x < 64) {
     const int lane = threadIdx.x;
@@ -2245,6 +2275,7 @@ __device__ int nms_walk(int n, int max_det, const unsigned long long* sup, const
           ++r;
         }
         const int total = __shfl(incl, 63);
+        if (lane == 0 && total > 0) *early = 1;
         k = k + total < max_det ? k + total : max_det;
         break;
       }
@@ -2261,7 +2292,7 @@ __device__ int nms_walk(int n, int max_det, const unsigned long long* sup, const
 // walks the kept boxes: next kept = first candidate not yet removed; if it overlaps no remaining
 // box, every remaining box is kept (the :291-296 early exit) and the walk ends.
 __device__ int nms_bitmask(const float* box, int n, float thr, int max_det, unsigned long long* sup,
-                           unsigned long long* ovl, int* keep, int* k_out) {
+                           unsigned long long* ovl, int* keep, int* k_out, int* early) {
   const int W = (n + 63) / 64;
   for (int job = threadIdx.x; job < n * W; job += blockDim.x) {
     const int i = job / W, w = job - i * W;
@@ -2285,7 +2316,7 @@ __device__ int nms_bitmask(const float* box, int n, float thr, int max_det, unsi
     ovl[i * NMS_W + w] = om;
   }
   __syncthreads();
-  return nms_walk(n, max_det, sup, ovl, keep, k_out);
+  return nms_walk(n, max_det, sup, ovl, keep, k_out, early);
 }
 
 // TorchNMS.nms (utils/nms.py:237-304) on up to NMS_GW*64 sorted candidates by ONE wave, with no
@@ -2297,7 +2328,7 @@ __device__ int nms_bitmask(const float* box, int n, float thr, int max_det, unsi
 constexpr int NMS_GW = 4;
 template <int GW>
 __device__ int nms_greedy_wave(const float4* bx, const float* ar, int n, float thr, int max_det, int* keep,
-                               int* k_out) {
+                               int* k_out, int* early) {
   if (threadIdx.x < 64) {
     const int lane = threadIdx.x;
     const int W = (n + 63) / 64;
@@ -2360,6 +2391,7 @@ __device__ int nms_greedy_wave(const float4* bx, const float* ar, int n, float t
           if (al[w] && r < max_det) keep[r] = w * 64 + lane;
           base += __popcll(b);
         }
+        if (lane == 0 && base > k) *early = 1;
         k = base < max_det ? base : max_det;
         break;
       }
@@ -2404,6 +2436,8 @@ __device__ void nms_small(const NmsArgs& a, int b, int n, unsigned char* smem) {
   }
   int n2 = 1;
   while (n2 < n) n2 <<= 1;
+  if (tid < 16) misc[tid] = 0;  // [13] bad anchor, [14] early exit
+  __syncthreads();
   for (int i = tid; i < n2; i += NMS_NT) {
     unsigned long long k = ~0ull;
     if (i < n) {
@@ -2414,7 +2448,12 @@ __device__ void nms_small(const NmsArgs& a, int b, int n, unsigned char* smem) {
       stg[i * 5 + 2] = v23.x;
       stg[i * 5 + 3] = v23.y;
       stg[i * 5 + 4] = v45.x;
-      k = ((unsigned long long)(0xffffffffu - __float_as_uint(v45.x)) << 32) | (unsigned)__float_as_int(v45.y);
+      int anc = __float_as_int(v45.y);
+      if (anc < 0 || anc >= a.n_anchors) {  // not a row detect_kernel / nms_load_kernel wrote
+        misc[13] = 1;
+        anc = i;
+      }
+      k = nms_key(v45.x, anc);
     }
     keys[i] = k;
   }
@@ -2445,10 +2484,10 @@ __device__ void nms_small(const NmsArgs& a, int b, int n, unsigned char* smem) {
   if (n <= NMS_GW * 64) {
     if (a.dbg) t[3] = __builtin_amdgcn_s_memrealtime();
     // specialised on the live word count: the unrolled word loops carry no dead blocks
-    if (n <= 64) k = nms_greedy_wave<1>(bx, ar, n, a.iou, a.max_det, keep, misc + 15);
-    else if (n <= 128) k = nms_greedy_wave<2>(bx, ar, n, a.iou, a.max_det, keep, misc + 15);
-    else if (n <= 192) k = nms_greedy_wave<3>(bx, ar, n, a.iou, a.max_det, keep, misc + 15);
-    else k = nms_greedy_wave<NMS_GW>(bx, ar, n, a.iou, a.max_det, keep, misc + 15);
+    if (n <= 64) k = nms_greedy_wave<1>(bx, ar, n, a.iou, a.max_det, keep, misc + 15, misc + 14);
+    else if (n <= 128) k = nms_greedy_wave<2>(bx, ar, n, a.iou, a.max_det, keep, misc + 15, misc + 14);
+    else if (n <= 192) k = nms_greedy_wave<3>(bx, ar, n, a.iou, a.max_det, keep, misc + 15, misc + 14);
+    else k = nms_greedy_wave<NMS_GW>(bx, ar, n, a.iou, a.max_det, keep, misc + 15, misc + 14);
     if (a.dbg) t[4] = __builtin_amdgcn_s_memrealtime();
   } else {
   // sup / ovl words: each wave holds every column box in registers (lane = column within a
@@ -2503,11 +2542,13 @@ __device__ void nms_small(const NmsArgs& a, int b, int n, unsigned char* smem) {
   }
   __syncthreads();
   if (a.dbg) t[3] = __builtin_amdgcn_s_memrealtime();
-  k = nms_walk(n, a.max_det, sup, ovl, keep, misc + 15);
+  k = nms_walk(n, a.max_det, sup, ovl, keep, misc + 15, misc + 14);
   if (a.dbg) t[4] = __builtin_amdgcn_s_memrealtime();
   }
+  if (misc[13]) k = 0;  // corrupt candidate rows: no detections, error flagged below
   // outputs: x[i] rows, then scale_boxes (x - pad) / gain and clip (ops.py:105-184)
   for (int r = tid; r < k; r += NMS_NT) {
+    if (a.keep_out) a.keep_out[(size_t)b * a.max_det + r] = (int)(keys[pay[NMS_MASK_N + keep[r]]] & 0xffffffffu);
     const float* c = stg + pay[NMS_MASK_N + keep[r]] * 5;
     float* o = a.dets + ((size_t)b * a.max_det + r) * 6;
     const float x1 = (c[0] - a.pad_x) / a.gain, y1 = (c[1] - a.pad_y) / a.gain;
@@ -2519,7 +2560,14 @@ __device__ void nms_small(const NmsArgs& a, int b, int n, unsigned char* smem) {
     o[4] = c[4];
     o[5] = 0.f;
   }
-  if (tid == 0) a.counts[b] = k;
+  if (tid == 0) {
+    a.counts[b] = k;
+    if (misc[13]) nms_flag_error(a.err);
+    if (a.stat) {
+      atomicAdd(&a.stat[0], misc[14] && k > 0 ? 1 : 0);
+      atomicAdd(&a.stat[1], 1);
+    }
+  }
   if (a.dbg) {
     __syncthreads();
     t[5] = __builtin_amdgcn_s_memrealtime();
@@ -2551,19 +2599,31 @@ __global__ void __launch_bounds__(NMS_NT) nms_kernel(NmsArgs a) {
   int* misc = (int*)(smem + NMS_OFF_MISC);
   int* keep = (int*)(smem + NMS_OFF_KEEP);
   int* slot_of = a.slot_of + (size_t)b * a.n_anchors;
-  // keys: (~score_bits, anchor) -> ascending order = score desc, anchor asc (stable order)
+  if (tid < 16) misc[tid] = 0;  // [13] bad anchor, [14] early exit
+  __syncthreads();
+  // keys: (score desc, anchor asc) = the stable order (nms_key)
   for (int i = tid; i < n2; i += NMS_NT) {
     unsigned long long k = ~0ull;
     if (i < n) {
-      const unsigned sb = __float_as_uint(cand[i * 6 + 4]);
       int anc = __float_as_int(cand[i * 6 + 5]);
-      anc = (anc >= 0 && anc < a.n_anchors) ? anc : 0;  // rows are written by detect_kernel; never index outside
-      k = ((unsigned long long)(0xffffffffu - sb) << 32) | (unsigned)anc;
-      slot_of[anc] = i;
+      if (anc < 0 || anc >= a.n_anchors) {  // not a row detect_kernel / nms_load_kernel wrote:
+        misc[13] = 1;                        // never index outside slot_of; flag it
+        anc = 0;
+      } else {
+        slot_of[anc] = i;
+      }
+      k = nms_key(cand[i * 6 + 4], anc);
     }
     keys[i] = k;
   }
   __syncthreads();
+  if (misc[13]) {
+    if (tid == 0) {
+      a.counts[b] = 0;
+      nms_flag_error(a.err);
+    }
+    return;
+  }
   if (n > 1) bitonic_sort(keys, n2);
   if (n > a.max_nms) n = a.max_nms;  // nms.py:138-142
   for (int i = tid; i < n; i += NMS_NT) {
@@ -2582,7 +2642,7 @@ __global__ void __launch_bounds__(NMS_NT) nms_kernel(NmsArgs a) {
   const float thr = a.iou;
   if (n <= NMS_MASK_N) {
     unsigned long long* sup = (unsigned long long*)(smem + NMS_OFF_MASK);
-    k = nms_bitmask(box, n, thr, a.max_det, sup, sup + NMS_MASK_N * NMS_W, keep, misc + 15);
+    k = nms_bitmask(box, n, thr, a.max_det, sup, sup + NMS_MASK_N * NMS_W, keep, misc + 15, misc + 14);
   } else {
     for (int i = 0; i < n && k < a.max_det; ++i) {
       if (removed[i]) continue;
@@ -2600,6 +2660,7 @@ __global__ void __launch_bounds__(NMS_NT) nms_kernel(NmsArgs a) {
       any = __syncthreads_or(any);
       if (!any) {
         // inter.sum() == 0: keep every remaining box, in order, and stop (nms.py:291-296)
+        if (tid == 0 && i + 1 < n) misc[14] = 1;
         int base = k;
         for (int j0 = i + 1; j0 < n; j0 += NMS_NT) {
           const int j = j0 + tid;
@@ -2636,6 +2697,7 @@ __global__ void __launch_bounds__(NMS_NT) nms_kernel(NmsArgs a) {
   // outputs: x[i] rows, then scale_boxes (x - pad) / gain and clip (ops.py:105-184)
   for (int r = tid; r < k; r += NMS_NT) {
     const int i = keep[r];
+    if (a.keep_out) a.keep_out[(size_t)b * a.max_det + r] = (int)(keys[i] & 0xffffffffu);
     const int s = slot_of[(int)(keys[i] & 0xffffffffu)];
     const float* c = cand + (size_t)s * 6;
     float* o = a.dets + ((size_t)b * a.max_det + r) * 6;
@@ -2648,7 +2710,34 @@ __global__ void __launch_bounds__(NMS_NT) nms_kernel(NmsArgs a) {
     o[4] = c[4];
     o[5] = 0.f;
   }
-  if (tid == 0) a.counts[b] = k;
+  if (tid == 0) {
+    a.counts[b] = k;
+    if (a.stat) {
+      atomicAdd(&a.stat[0], misc[14] && k > 0 ? 1 : 0);
+      atomicAdd(&a.stat[1], 1);
+    }
+  }
+}
+
+// yk_nms: given boxes -> the candidate list the Detect ops would write (candidate id = row index,
+// so the stable order is score desc, then input order -- torch_nms's stable sort)
+__global__ void __launch_bounds__(256) nms_load_kernel(const float* rows, int row_stride, int max_rows,
+                                                      const int* counts, float* cand, int* cand_count, int cap) {
+  const int b = blockIdx.y;
+  int n = counts[b];
+  n = n < 0 ? 0 : n > max_rows ? max_rows : n;
+  n = n > cap ? cap : n;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i == 0) cand_count[b] = n;
+  if (i >= n) return;
+  const float* r = rows + ((size_t)b * max_rows + i) * row_stride;
+  float* c = cand + ((size_t)b * cap + i) * 6;
+  c[0] = r[0];
+  c[1] = r[1];
+  c[2] = r[2];
+  c[3] = r[3];
+  c[4] = r[4];
+  c[5] = __int_as_float(i);
 }
 
 #pragma clang fp contract(fast)
@@ -2681,6 +2770,9 @@ struct yk_model {
   int key_cap = 0;
   float* dets = nullptr;
   int* counts = nullptr;
+  int* nms_stat = nullptr;          // [2] device: NMS early exits, images (yk_model_nms_stats)
+  volatile int* err_host = nullptr;  // host-mapped error word the kernels flag (nms_flag_error)
+  int* err_dev = nullptr;
   std::map<std::tuple<int, float, float, int, const void*, void*, void*>, hipGraphExec_t> graphs;
   int plan_batch = 1;  // batch the kernel names of yk_model_op_kernel are reported for
   bool tiled = true;  // LDS-tiled conv kernel where its tile fits (YK_CONV_DIRECT=1 forces the direct kernel)
@@ -3559,7 +3651,8 @@ const char* op_kernel_name(const yk_model* m, const yk_op& op) {
   return buf;
 }
 
-int launch_nms(yk_model* m, int B, float iou, int max_det, float* dets, int32_t* counts, hipStream_t st);
+int launch_nms(yk_model* m, int B, float iou, int max_det, float* dets, int32_t* counts, hipStream_t st,
+               int32_t* keep = nullptr);
 
 // Buffers an op reads and writes.  The candidate list (virtual buffer n_bufs) is appended to
 // with atomics by every Detect op, so Detect ops do not order against each other.
@@ -3731,7 +3824,8 @@ int detect_impl(yk_model* m, const uint8_t* frames, int B, float conf, float iou
   return launch_nms(m, B, iou, max_det, dets, counts, st);
 }
 
-int launch_nms(yk_model* m, int B, float iou, int max_det, float* dets, int32_t* counts, hipStream_t st) {
+int launch_nms(yk_model* m, int B, float iou, int max_det, float* dets, int32_t* counts, hipStream_t st,
+               int32_t* keep) {
   const yk_model_desc& D = m->desc;
   NmsArgs a;
   a.cand = m->cand;
@@ -3754,6 +3848,9 @@ int launch_nms(yk_model* m, int B, float iou, int max_det, float* dets, int32_t*
   a.clip_w = (float)D.frame_w;
   a.clip_h = (float)D.frame_h;
   a.dbg = m->nms_dbg;
+  a.keep_out = keep;
+  a.stat = m->nms_stat;
+  a.err = m->err_dev;
   hipLaunchKernelGGL(nms_kernel, dim3(B), dim3(NMS_NT), nms_lds_bytes(), st, a);
   YK_HIP(hipGetLastError());
   return YK_OK;
@@ -3843,8 +3940,9 @@ inline float h_bf2f(unsigned short h) {
 }
 
 // F32S weight fragments: the packed f32 A-operand fragments of every table-kernel conv ([n_tiles]
-// [k_steps][64 lanes][4 f32], model.py Program.pack) as [n_tiles][k_steps][64][24 B]: w0 of the
-// 4 elements, w1, w2 (bf16, element 0 in the low half of each dword), w = w0 + w1 + w2 exactly.
+// [k_steps][64 lanes][4 f32], model.py Program.pack) as [n_tiles][k_steps][64][32 B]: W01 =
+// [w0(e) | w1(e)] for the lane's 4 elements e, then W02 = [w0(e) | w2(e)] (bf16, low half first),
+// w = w0 + w1 + w2 exactly.
 hipError_t build_wsplit(yk_model* m, const char* host_blob, size_t blob_bytes) {
   m->ws_off.assign(m->ops.size(), -1);
   std::vector<unsigned short> out;
@@ -3865,8 +3963,11 @@ hipError_t build_wsplit(yk_model* m, const char* host_blob, size_t blob_bytes) {
         part[1][e] = h_f2bf(r1);
         part[2][e] = h_f2bf(r1 - h_bf2f(part[1][e]));
       }
-      for (int k = 0; k < 3; ++k)
-        for (int e = 0; e < 4; ++e) out.push_back(part[k][e]);
+      for (int k : {1, 2})
+        for (int e = 0; e < 4; ++e) {
+          out.push_back(part[0][e]);
+          out.push_back(part[k][e]);
+        }
     }
   }
   if (out.empty()) return hipSuccess;
@@ -3878,6 +3979,16 @@ hipError_t build_wsplit(yk_model* m, const char* host_blob, size_t blob_bytes) {
   hipError_t e = hipMalloc((void**)&m->wsplit, m->wsplit_bytes);
   if (e == hipSuccess) e = hipMemcpy(m->wsplit, out.data(), m->wsplit_bytes, hipMemcpyHostToDevice);
   return e;
+}
+
+// The kernels' host-mapped error word (nms_flag_error): a flagged launch made its images'
+// detections empty; the next call on the model reports it (and clears it) as YK_ERR_STATE.
+int take_device_error(yk_model* m) {
+  if (!m->err_host || !m->err_host[0]) return YK_OK;
+  m->err_host[0] = 0;
+  yk::set_error("yk_detect: an earlier launch met candidate rows whose anchor index lies outside [0, n_anchors) "
+                "(stale or corrupt candidate buffers); those images' detections were dropped");
+  return YK_ERR_STATE;
 }
 
 hipError_t set_schedule(yk_model* m, int groups, int lanes) {
@@ -3986,7 +4097,18 @@ int yk_model_create(yk_ctx* ctx, const yk_model_desc* desc, const void* host_blo
   alloc((void**)&m->gflag, B * A);
   alloc((void**)&m->dets, B * desc->max_det * 6 * sizeof(float));
   alloc((void**)&m->counts, B * sizeof(int));
+  alloc((void**)&m->nms_stat, 2 * sizeof(int));
   if (e == hipSuccess) e = hipMemset(m->counts, 0, B * sizeof(int));
+  if (e == hipSuccess) e = hipMemset(m->nms_stat, 0, 2 * sizeof(int));
+  if (e == hipSuccess) {
+    void* h = nullptr;
+    e = hipHostMalloc(&h, 64, hipHostMallocMapped | hipHostMallocCoherent);
+    if (e == hipSuccess) {
+      m->err_host = (volatile int*)h;
+      m->err_host[0] = 0;
+      e = hipHostGetDevicePointer((void**)&m->err_dev, h, 0);
+    }
+  }
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)nms_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)nms_lds_bytes());
   set_tile_attrs();
@@ -4059,9 +4181,10 @@ int yk_model_destroy(yk_model* m) {
   for (hipEvent_t v : m->ev) (void)hipEventDestroy(v);
   if (m->arena) (void)hipFree(m->arena);
   void* ptrs[] = {m->blob, m->cand, m->cand_count, m->slot_of, m->gkeys, m->gbox, m->gflag, m->dets, m->counts, m->ktab,
-                  m->ltab, m->lbox, m->ts, m->wsplit};
+                  m->ltab, m->lbox, m->ts, m->wsplit, m->nms_stat};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
+  if (m->err_host) (void)hipHostFree((void*)m->err_host);
   delete m;
   return YK_OK;
 }
@@ -4069,6 +4192,7 @@ int yk_model_destroy(yk_model* m) {
 int yk_detect(yk_model* m, const uint8_t* frames, int batch, float conf, float iou, int max_det, float* dets,
               int32_t* counts, void* stream) {
   YK_CHECK_ARG(m, "yk_detect: NULL model");
+  if (const int rc = take_device_error(m)) return rc;
   yk::DeviceGuard guard(m->ctx->device);
   return detect_impl(m, frames, batch, conf, iou, max_det, dets, counts, (hipStream_t)stream);
 }
@@ -4076,6 +4200,7 @@ int yk_detect(yk_model* m, const uint8_t* frames, int batch, float conf, float i
 int yk_detect_graph(yk_model* m, const uint8_t* frames, int batch, float conf, float iou, int max_det, float* dets,
                     int32_t* counts, void* stream) {
   YK_CHECK_ARG(m, "yk_detect_graph: NULL model");
+  if (const int rc = take_device_error(m)) return rc;
   yk::DeviceGuard guard(m->ctx->device);
   hipStream_t st = (hipStream_t)stream;
   auto key = std::make_tuple(batch, conf, iou, max_det, (const void*)frames, (void*)dets, (void*)counts);
@@ -4265,6 +4390,54 @@ int yk_model_autotune(yk_model* m, const uint8_t* frames, int batch, float conf,
   (void)hipEventDestroy(e0);
   (void)hipEventDestroy(e1);
   return YK_OK;
+}
+
+int yk_nms_candidates(yk_model* m, int batch, float iou, int max_det, float* dets, int32_t* counts, int32_t* keep,
+                      void* stream) {
+  YK_CHECK_ARG(m, "yk_nms_candidates: NULL model");
+  YK_CHECK_ARG(batch >= 1 && batch <= m->desc.max_batch, "yk_nms_candidates: batch out of range [1, max_batch]");
+  YK_CHECK_ARG(iou >= 0.f && iou <= 1.f, "Invalid IoU, valid values are between 0.0 and 1.0");
+  YK_CHECK_ARG(max_det >= 0 && max_det <= m->desc.max_det, "yk_nms_candidates: max_det exceeds the model's capacity");
+  if (const int rc = take_device_error(m)) return rc;
+  yk::DeviceGuard guard(m->ctx->device);
+  return launch_nms(m, batch, iou, max_det, dets ? dets : m->dets, counts ? counts : m->counts, (hipStream_t)stream,
+                    keep);
+}
+
+int yk_nms(yk_model* m, const float* dev_rows, int row_stride, int max_rows, const int32_t* dev_counts, int batch,
+           float iou, int max_det, float* dets, int32_t* counts, int32_t* keep, void* stream) {
+  YK_CHECK_ARG(m && dev_rows && dev_counts, "yk_nms: NULL argument");
+  YK_CHECK_ARG(row_stride >= 5, "yk_nms: rows need x1 y1 x2 y2 score (row_stride >= 5)");
+  YK_CHECK_ARG(max_rows >= 0 && max_rows <= m->desc.n_anchors, "yk_nms: max_rows exceeds the model's candidate capacity");
+  YK_CHECK_ARG(batch >= 1 && batch <= m->desc.max_batch, "yk_nms: batch out of range [1, max_batch]");
+  yk::DeviceGuard guard(m->ctx->device);
+  hipStream_t st = (hipStream_t)stream;
+  if (max_rows > 0)
+    hipLaunchKernelGGL(nms_load_kernel, dim3((max_rows + 255) / 256, batch), dim3(256), 0, st, dev_rows, row_stride,
+                       max_rows, dev_counts, m->cand, m->cand_count, m->desc.n_anchors);
+  else
+    hipLaunchKernelGGL(zero_i32_kernel, dim3(1), dim3(64), 0, st, m->cand_count, batch);
+  YK_HIP(hipGetLastError());
+  return yk_nms_candidates(m, batch, iou, max_det, dets, counts, keep, stream);
+}
+
+int yk_model_nms_stats(yk_model* m, int64_t* out, int reset, void* stream) {
+  YK_CHECK_ARG(m && out, "yk_model_nms_stats: NULL argument");
+  yk::DeviceGuard guard(m->ctx->device);
+  int h[2] = {0, 0};
+  YK_HIP(hipStreamSynchronize((hipStream_t)stream));
+  YK_HIP(hipMemcpy(h, m->nms_stat, sizeof h, hipMemcpyDeviceToHost));
+  out[0] = h[0];
+  out[1] = h[1];
+  if (reset) YK_HIP(hipMemset(m->nms_stat, 0, sizeof h));
+  return YK_OK;
+}
+
+int yk_model_check(yk_model* m, void* stream) {
+  YK_CHECK_ARG(m, "yk_model_check: NULL model");
+  yk::DeviceGuard guard(m->ctx->device);
+  YK_HIP(hipStreamSynchronize((hipStream_t)stream));
+  return take_device_error(m);
 }
 
 int yk_model_op_kernel(yk_model* m, int op_index, char* buf, int len) {

@@ -535,6 +535,46 @@ class DeviceModel:
                    L.ptr(counts), st), "yk_detect")
         return dets, counts
 
+    def nms(self, rows: torch.Tensor, counts: torch.Tensor, iou=0.7, max_det=300, stream=None):
+        """yk_nms: TorchNMS.nms (+ max_nms / max_det / scale / clip) of the model's nms_kernel on
+        given boxes.  rows: float32 device [B, R, >=5] (x1 y1 x2 y2 score, network-input pixels),
+        counts: int32 device [B].  Returns (dets [B, max_det, 6], counts [B], keep [B, max_det]:
+        input row of every output row)."""
+        if rows.dtype != torch.float32 or rows.dim() != 3 or rows.shape[2] < 5 or not rows.is_contiguous():
+            raise ValueError("rows must be a contiguous float32 tensor [B, R, >=5]")
+        if counts.dtype != torch.int32 or counts.shape != (rows.shape[0],):
+            raise ValueError("counts must be an int32 tensor [B]")
+        B, R, S = rows.shape
+        dev = rows.device
+        dets = torch.zeros((B, max_det, 6), dtype=torch.float32, device=dev)
+        cnt = torch.zeros(B, dtype=torch.int32, device=dev)
+        keep = torch.full((B, max_det), -1, dtype=torch.int32, device=dev)
+        st = L.current_stream(self.device) if stream is None else C.c_void_p(stream)
+        L.check(L.lib().yk_nms(self._h, L.ptr(rows), int(S), int(R), L.ptr(counts), int(B), C.c_float(iou),
+                               int(max_det), L.ptr(dets), L.ptr(cnt), L.ptr(keep), st), "yk_nms")
+        return dets, cnt, keep
+
+    def nms_candidates(self, B: int, iou=0.7, max_det=300):
+        """yk_nms_candidates: the NMS stage alone on the model's current candidate buffers."""
+        dev = torch.device("cuda", self.device)
+        dets = torch.zeros((B, max_det, 6), dtype=torch.float32, device=dev)
+        cnt = torch.zeros(B, dtype=torch.int32, device=dev)
+        keep = torch.full((B, max_det), -1, dtype=torch.int32, device=dev)
+        L.check(L.lib().yk_nms_candidates(self._h, int(B), C.c_float(iou), int(max_det), L.ptr(dets), L.ptr(cnt),
+                                          L.ptr(keep), L.current_stream(self.device)), "yk_nms_candidates")
+        return dets, cnt, keep
+
+    def nms_stats(self, reset: bool = False):
+        """(images that took TorchNMS's :291-296 early exit with boxes left, images processed)."""
+        out = np.zeros(2, np.int64)
+        L.check(L.lib().yk_model_nms_stats(self._h, L.ptr(out), int(bool(reset)), L.current_stream(self.device)),
+                "yk_model_nms_stats")
+        return int(out[0]), int(out[1])
+
+    def check(self):
+        """Synchronise and raise YKError if a device-side error was flagged (yk_model_check)."""
+        L.check(L.lib().yk_model_check(self._h, L.current_stream(self.device)), "yk_model_check")
+
     def set_lanes(self, lanes: int):
         """Streams the op DAG is scheduled onto (1 = strictly sequential, the reference's order)."""
         L.check(L.lib().yk_model_set_lanes(self._h, int(lanes)), "yk_model_set_lanes")
