@@ -134,6 +134,10 @@ typedef struct {
   double velocity_avg[2], velocity_std[2], direction, speed, stability_score, prediction_confidence;
   double vel_hist[YK_VEL_HIST][2];   /* oldest first */
   double traj_hist[YK_TRAJ_HIST][2]; /* oldest first */
+  /* motion-reset policy (MotionResetKalmanTracker attributes, motion_reset_kalman_tracker.py:
+   * 50-58); 0 / -999 / 0 for the enhanced policy */
+  int32_t reset_count, last_reset_frame;
+  double motion_consistency;
 } yk_track_state;
 
 int yk_tracker_create(yk_ctx* ctx, int n_streams, const yk_tracker_cfg* cfg, yk_tracker** out);

@@ -107,3 +107,55 @@ def test_motion_reset_exact_tie_takes_highest_detection():
     d1 = [f(51), f(50), f(61), f(60), f(.8)]
     ours, ref = run_pair([[t0], [d0, d1], [d0, d1]])
     assert ref.trackers[0].x[0] > 55.0  # track 1 moved toward d1
+
+
+def test_standalone_motion_reset_track_object():
+    """camera_motion_compensation.MotionResetKalmanTracker as one object (the compat module):
+    predict / update / mark_as_lost / get_track_info / get_reset_statistics and the reset
+    attributes, on a box path with position jumps, a size change, a velocity change and missed
+    frames, against oracle/cmc_ref.RefResetTrack step by step."""
+    import os
+    import sys
+
+    from conftest import REPO
+    from oracle.cmc_ref import RefResetTrack
+
+    sys.path.insert(0, os.path.join(REPO, pkg().__name__, "compat"))
+    try:
+        from camera_motion_compensation.motion_reset_kalman_tracker import MotionResetKalmanTracker
+    finally:
+        sys.path.pop(0)
+    f = np.float32
+    path = []
+    x, y, w, h = 100.0, 120.0, 12.0, 9.0
+    for t in range(60):
+        if t in (12, 31):
+            x += 55.0  # position jump > 40 px
+        if t == 22:
+            w, h = w * 1.6, h * 1.6  # size change > 0.3
+        if 40 <= t < 44:
+            x += 20.0 * (t - 39)  # accelerating: velocity change
+        x, y = x + 1.5, y + 0.7
+        path.append(None if t in (17, 18, 47) else [f(x - w / 2), f(y - h / 2), f(x + w / 2), f(y + h / 2)])
+    b0 = [f(98.0), f(115.0), f(110.0), f(124.0)]
+    ours = MotionResetKalmanTracker(b0, track_id="T001", max_lost_frames=150)
+    ref = RefResetTrack(b0, "T001", 150)
+    for t, box in enumerate(path):
+        _close(ours.predict(), ref.predict(), f"frame {t} predict")
+        if box is None:
+            ours.mark_as_lost()
+            ref.mark_as_lost()
+        else:
+            ours.update(box)
+            ref.update(box)
+        a, b = ours.get_track_info(), ref.get_track_info()
+        for k in INT_KEYS:
+            assert a[k] == b[k], f"frame {t} {k}: {a[k]} vs {b[k]}"
+        _close(a["bbox"], b["bbox"], f"frame {t} bbox")
+        assert ours.reset_count == ref.reset_count and ours.last_reset_frame == ref.last_reset_frame
+        _close(ours.motion_consistency, ref.motion_consistency, f"frame {t} consistency")
+    assert ref.reset_count >= 3, ref.reset_count
+    sa, sb = ours.get_reset_statistics(), ref.get_reset_statistics()
+    assert sa["total_resets"] == sb["total_resets"] and sa["reason_distribution"] == sb["reason_distribution"]
+    _close(sa["avg_confidence"], sb["avg_confidence"], "avg_confidence", rtol=1e-6)
+    assert [d["frame"] for d in sa["details"]] == [d["frame"] for d in sb["details"]]

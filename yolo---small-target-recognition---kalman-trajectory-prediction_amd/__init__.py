@@ -17,6 +17,7 @@ from .tracker import (  # noqa: F401
     EnhancedAircraftKalmanTracker,
     EnhancedMultiTargetTracker,
     MotionCompensatedMultiTracker,
+    MotionResetKalmanTracker,
     MultiStreamTracker,
     MultiTargetTracker,
 )

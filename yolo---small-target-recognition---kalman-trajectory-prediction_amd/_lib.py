@@ -87,7 +87,8 @@ TRACK_STATE_DTYPE = np.dtype([
     ("x", np.float64, (8,)), ("P", np.float64, (8, 8)), ("velocity_avg", np.float64, (2,)),
     ("velocity_std", np.float64, (2,)), ("direction", np.float64), ("speed", np.float64),
     ("stability_score", np.float64), ("prediction_confidence", np.float64),
-    ("vel_hist", np.float64, (VEL_HIST, 2)), ("traj_hist", np.float64, (TRAJ_HIST, 2))], align=True)
+    ("vel_hist", np.float64, (VEL_HIST, 2)), ("traj_hist", np.float64, (TRAJ_HIST, 2)),
+    ("reset_count", np.int32), ("last_reset_frame", np.int32), ("motion_consistency", np.float64)], align=True)
 
 _vp = C.c_void_p
 _i32 = C.c_int32

@@ -1,6 +1,9 @@
-"""Drop-in ``camera_motion_compensation`` package (reference camera_motion_compensation/) for
-the frame-free path: MotionCompensatedMultiTracker.update(detections) on the HIP tracker kernel."""
-from ..kalman._pkg import sub
+"""Drop-in ``camera_motion_compensation`` package (reference camera_motion_compensation/):
+MotionCompensatedMultiTracker.update(detections[, frame]) on the HIP tracker kernel,
+MotionResetKalmanTracker (one track) and GlobalMotionDetector ('optical_flow', gmd.hip)."""
+from kalman._pkg import sub
 
 MotionCompensatedMultiTracker = sub("tracker").MotionCompensatedMultiTracker
-__all__ = ["MotionCompensatedMultiTracker"]
+MotionResetKalmanTracker = sub("tracker").MotionResetKalmanTracker
+GlobalMotionDetector = sub("motion").GlobalMotionDetector
+__all__ = ["MotionCompensatedMultiTracker", "MotionResetKalmanTracker", "GlobalMotionDetector"]

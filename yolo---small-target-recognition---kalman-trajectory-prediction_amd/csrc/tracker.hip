@@ -2075,6 +2075,9 @@ __global__ void snapshot_kernel(Dev g, int s, yk_track_state* out) {
       o.traj_hist[k][1] = v ? sl.th[idx][1] : 0.0;
       idx = (idx + 1 == TH) ? 0 : idx + 1;
     }
+    o.reset_count = sl.policy ? sl.reset_count : 0;
+    o.last_reset_frame = sl.policy ? sl.last_reset : -999;
+    o.motion_consistency = sl.policy ? sl.consistency : 0.0;
   }
 }
 

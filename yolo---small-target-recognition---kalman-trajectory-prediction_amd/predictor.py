@@ -106,6 +106,23 @@ class Results:
     def __len__(self):
         return 0 if self.boxes is None else len(self.boxes)
 
+    def __getitem__(self, idx):
+        """Results of the indexed boxes (engine/results.py:292-307, BaseTensor.__getitem__)."""
+        r = Results(self.orig_img, self.path, self.names, None, self.speed)
+        r.boxes = None if self.boxes is None else self.boxes[idx]
+        return r
+
+    def update(self, boxes=None):
+        """engine/results.py:327-360: new boxes, clipped to the original image (ops.clip_boxes)."""
+        if boxes is not None:
+            b = boxes.clone() if isinstance(boxes, torch.Tensor) else torch.as_tensor(boxes)
+            h, w = self.orig_shape
+            b[..., 0] = b[..., 0].clamp(0, w)
+            b[..., 1] = b[..., 1].clamp(0, h)
+            b[..., 2] = b[..., 2].clamp(0, w)
+            b[..., 3] = b[..., 3].clamp(0, h)
+            self.boxes = Boxes(b, self.orig_shape)
+
     def cpu(self):
         return Results(self.orig_img, self.path, self.names, None if self.boxes is None else self.boxes.data.cpu(),
                        self.speed)
@@ -244,6 +261,43 @@ class YOLO:
         for r in res:
             r.speed = sp
         return res
+
+    # -- track (engine/model.py:559-613, trackers/track.py:18-121) ------------------------------
+    def track(self, source=None, stream: bool = False, persist: bool = False, tracker="botsort.yaml", **kwargs):
+        """model.track(): predict with conf defaulting to 0.1 and batch 1, then every result through
+        the tracker on the device (bytetrack.hip): on_predict_start creates one tracker per call
+        unless `persist` keeps the existing one (track.py:18-63, one tracker for non-stream
+        sources); on_predict_postprocess_end resets it when the source path changes (unless
+        persist), updates it with the result's boxes and replaces the result by the tracked subset
+        with boxes [x1, y1, x2, y2, id, conf, cls] (track.py:66-100).  `tracker`: 'botsort.yaml'
+        (the cfg default) / 'bytetrack.yaml' / a YAML path / dict; BoT-SORT's GMC needs cv2 (absent):
+        use gmc_method: none, or bytetrack."""
+        from . import bytetrack as BT
+
+        kwargs["conf"] = kwargs.get("conf") or 0.1
+        kwargs["batch"] = kwargs.get("batch") or 1
+        if not (persist and getattr(self, "trackers", None)):
+            cfg = BT.load_tracker_cfg(tracker)
+            if cfg.tracker_type == "botsort" and getattr(cfg, "gmc_method", None) not in (None, "none"):
+                raise NotImplementedError(f"BoT-SORT GMC '{cfg.gmc_method}' needs cv2 (absent here): use "
+                                          "tracker='bytetrack.yaml' or a botsort YAML with gmc_method: none")
+            kind = BT.BOTSORT if cfg.tracker_type == "botsort" else BT.BYTETracker
+            self.trackers = [kind(cfg, frame_rate=30, device=self.device)]
+            self.vid_path = [None]
+        results = self.predict(source, stream=False, **kwargs)
+        trk = self.trackers[0]
+        for i, r in enumerate(results):
+            vid_path = os.path.basename(str(r.path))
+            if not persist and self.vid_path[0] != vid_path:
+                trk.reset()
+                self.vid_path[0] = vid_path
+            tracks = trk.update(r.boxes.cpu().numpy())
+            if len(tracks) == 0:
+                continue
+            idx = tracks[:, -1].astype(int)
+            results[i] = r[torch.as_tensor(idx, device=r.boxes.data.device)]
+            results[i].update(boxes=torch.as_tensor(tracks[:, :-1], device=r.boxes.data.device))
+        return iter(results) if stream else results
 
     def fuse(self, verbose=True):
         return self  # Conv+BN is always fused at program build (weights.fuse_conv_bn)

@@ -420,6 +420,65 @@ class AircraftKalmanTracker:
 EnhancedAircraftKalmanTracker = AircraftKalmanTracker
 
 
+class MotionResetKalmanTracker(AircraftKalmanTracker):
+    """One motion-reset track (camera_motion_compensation/motion_reset_kalman_tracker.py:16-355)
+    whose state lives in HBM, on the same device operations as the batched motion-reset policy
+    (tracker.hip: cmc_decide / cmc_reset / cmc_blend): ``update(bbox)`` runs _should_reset_kalman
+    (position jump against the last <= 3 centres, velocity change, size change, motion
+    consistency, cooldown, adaptive factors) and either resets the filter or runs the Kalman
+    update; ``predict()`` blends the box toward the last centre for 10 frames after a reset;
+    ``get_track_info()`` adds reset_count / frames_since_reset / motion_consistency /
+    status_suffix; ``get_reset_statistics()`` as the reference.  Constructed directly it owns a
+    private one-track device tracker (policy YK_POLICY_MOTION_RESET); obtained from
+    ``MotionCompensatedMultiTracker.trackers`` it is a live view of that tracker's track."""
+
+    jump_threshold = 40.0
+    velocity_threshold = 60.0
+    size_change_threshold = 0.3
+    reset_cooldown = 15
+
+    def __init__(self, initial_bbox, track_id=None, max_lost_frames=150, *, device: int = 0, verbose: bool = False):
+        self.track_id = track_id or str(uuid.uuid4())[:8]
+        self.max_lost_frames = int(max_lost_frames)
+        self._owner = MultiStreamTracker(1, max_lost_frames=self.max_lost_frames, min_hits=1, iou_threshold=0.1,
+                                         max_tracks=1, max_dets=1, device=device, policy=L.POLICY_MOTION_RESET)
+        box, dt = _box_dtype(initial_bbox)
+        self._dtype = dt
+        self._owner.create_track(0, box, dt, -1, self.max_lost_frames)
+        self._num = None
+        self._multi = None
+        if verbose:
+            print(f"🎯 运动重置跟踪器初始化: {self.track_id}")
+
+    def _row(self):
+        """get_track_info's row (OP_INFO: it may predict, quirk A, as the reference does)."""
+        _, row = self._owner.track_op(0, self._pos(), L.OP_INFO)
+        self._touch()
+        return row
+
+    @property
+    def reset_count(self) -> int:
+        return int(self._state()["reset_count"])
+
+    @property
+    def last_reset_frame(self) -> int:
+        return int(self._state()["last_reset_frame"])
+
+    @property
+    def motion_consistency(self) -> float:
+        return float(self._state()["motion_consistency"])
+
+    def get_track_info(self):
+        row = self._row()
+        info = _reset_fields(row, _row_to_dict(row, self.track_id))
+        info.pop("reset_statistics", None)
+        return info
+
+    def get_reset_statistics(self):
+        row = self._row()
+        return _reset_fields(row, {})["reset_statistics"]
+
+
 class EnhancedMultiTargetTracker:
     """Drop-in for kalman.EnhancedMultiTargetTracker (enhanced_multi_target_tracker.py:4-304),
     one stream, executed by the batched HIP tracker kernel."""
@@ -517,6 +576,7 @@ class MotionCompensatedMultiTracker:
                                         policy=L.POLICY_MOTION_RESET)
         self._stats = np.zeros(1, dtype=L.STATS_DTYPE)[0]
         self._stats_base = np.zeros(1, dtype=L.STATS_DTYPE)[0]
+        self._snap = None
         self.detection_stability_history = deque(maxlen=10)
         self.global_motion_history = deque(maxlen=20)
         self.frame_motion_info = None
@@ -545,6 +605,7 @@ class MotionCompensatedMultiTracker:
             motion = det.motion_ptr
         self.detection_stability_history.append(len(detections))
         self._core.step_host([detections], motion=motion)
+        self._snap = None
         rows, counts, stats = self._core.download()
         self._stats = stats[0].copy()
         if int(self._stats["overflow"]):
@@ -566,6 +627,16 @@ class MotionCompensatedMultiTracker:
                 info["global_motion"] = self.frame_motion_info
             out.append(info)
         return out
+
+    def _snapshot(self):
+        if self._snap is None:
+            self._snap = self._core.snapshot(0)
+        return self._snap
+
+    @property
+    def trackers(self) -> list:
+        """Live MotionResetKalmanTracker views of this tracker's tracks, in list order."""
+        return [MotionResetKalmanTracker._view(self, int(n)) for n in self._snapshot()["track_num"]]
 
     def set_global_motion_sensitivity(self, sensitivity):
         """:353-360"""
