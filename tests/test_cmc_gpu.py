@@ -154,7 +154,7 @@ def test_standalone_motion_reset_track_object():
         _close(a["bbox"], b["bbox"], f"frame {t} bbox")
         assert ours.reset_count == ref.reset_count and ours.last_reset_frame == ref.last_reset_frame
         _close(ours.motion_consistency, ref.motion_consistency, f"frame {t} consistency")
-    assert ref.reset_count >= 3, ref.reset_count
+    assert ref.reset_count >= 2, ref.reset_count  # the jumps at frames 12 and 31 (cooldown 15)
     sa, sb = ours.get_reset_statistics(), ref.get_reset_statistics()
     assert sa["total_resets"] == sb["total_resets"] and sa["reason_distribution"] == sb["reason_distribution"]
     _close(sa["avg_confidence"], sb["avg_confidence"], "avg_confidence", rtol=1e-6)
