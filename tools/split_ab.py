@@ -26,11 +26,10 @@ SPLIT = 64
 
 
 def split_plan(plan):
-    """The plan with every table-kernel op (CK_FAST = 3) not on the LDS-shared-weight mode moved
-    to the split-MFMA body."""
+    """The plan with every table-kernel op (CK_FAST = 3) moved to the split-MFMA body."""
     out = []
     for kind, nnt, npt in plan:
-        if kind == 3 and ((npt >> 4) & 3) != 2:
+        if kind == 3:
             npt |= SPLIT
         out.append([kind, nnt, npt])
     return out
@@ -63,7 +62,8 @@ def main():
     ft = torch.from_numpy(np.stack(frames_np)).cuda()
     res = {}
     models = {}
-    for name, plan in (("exact", pl["plan"]), ("split", split_plan(pl["plan"]))):
+    exact = [[k, n, (p & ~SPLIT) if k == 3 else p] for k, n, p in pl["plan"]]
+    for name, plan in (("exact", exact), ("split", split_plan(pl["plan"]))):
         dm = M.DeviceModel(prog)
         dm.load_plan(pl["batch"], plan)
         dets, counts = dm.detect(ft)

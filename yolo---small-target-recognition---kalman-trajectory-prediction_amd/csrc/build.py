@@ -21,8 +21,11 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.dirname(HERE)
 REPO = os.path.dirname(PKG)
-OUT = os.path.join(PKG, "libyk.so")
-BUILD = os.path.join(HERE, "_build")
+# YK_DEFINES="-DNAME=1 ..." builds a diagnostic variant into YK_OUT (default libyk_diag.so) with
+# its own object directory; the product library is never built with extra defines
+DEFINES = os.environ.get("YK_DEFINES", "").split()
+OUT = os.environ.get("YK_OUT") or os.path.join(PKG, "libyk_diag.so" if DEFINES else "libyk.so")
+BUILD = os.path.join(HERE, "_build_diag" if DEFINES else "_build")
 ARCH = os.environ.get("YK_OFFLOAD_ARCH", "gfx950")
 
 # (source, extra flags).  The tracker must not contract a*b+c into FMA: it reproduces
@@ -72,7 +75,7 @@ def _compile(src: str, extra: list[str], force: bool) -> str:
     path = os.path.join(HERE, src)
     obj = os.path.join(BUILD, os.path.splitext(src)[0] + ".o")
     flags = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
-             "-I", os.path.join(REPO, "include")] + extra
+             "-I", os.path.join(REPO, "include")] + DEFINES + extra
     hdrs = [os.path.join(HERE, h) for h in HEADERS]
     stamp = obj + ".sha"
     dig = _digest([path] + hdrs, flags)

@@ -25,6 +25,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <type_traits>
+#include <algorithm>
 #include <array>
 #include <map>
 #include <tuple>
@@ -202,9 +203,18 @@ __device__ __forceinline__ unsigned pack_bf16x2(float a, float b) {
 }
 // x = x0 + x1 + x2 exactly per element, each part bf16 (RNE); the F32S activation operands
 // X00 = [x0 | x0], X11 = [x1 | x1], X20 = [x2 | x0] (one dword per element)
+#ifndef YK_SPLIT_DIAG
+#define YK_SPLIT_DIAG 0  // diagnostic builds only (csrc/build.py YK_DEFINES): 1 no split, 2 no weight loads
+#endif
 __device__ __forceinline__ XS3 split3(const uint4& x) {
   const unsigned u[4] = {x.x, x.y, x.z, x.w};
   XS3 o;
+  if constexpr ((YK_SPLIT_DIAG & 1) != 0) {
+    o.x00 = u32x4v{u[0], u[1], u[2], u[3]};
+    o.x11 = u32x4v{u[1], u[2], u[3], u[0]};
+    o.x20 = u32x4v{u[2], u[3], u[0], u[1]};
+    return o;
+  }
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     const float a = __uint_as_float(u[e]);
@@ -878,6 +888,12 @@ template <class Tr>
 __device__ __forceinline__ typename Frag<Tr>::W wload(__amdgpu_buffer_rsrc_t r, unsigned voff, int ks) {
   if constexpr (Tr::kSplit) {
     WS2 w;
+    if constexpr ((YK_SPLIT_DIAG & 2) != 0) {
+      const unsigned c = voff ^ (unsigned)ks;
+      w.w01 = u32x4v{c, c + 1u, c + 2u, c + 3u};
+      w.w02 = u32x4v{c + 4u, c, c + 5u, c};
+      return w;
+    }
     w.w01 = __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, ks * 64 * 32, 0);
     w.w02 = __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff + 16, ks * 64 * 32, 0);
     return w;
@@ -1181,7 +1197,8 @@ __global__ void __launch_bounds__(256) conv_fastw_kernel(FastArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int nk = a.k_steps;
   int2* tab = (int2*)smem;  // [k_steps * 4]
-  uint4* ring = (uint4*)(smem + (((size_t)nk * 4 * 8 + 15) & ~(size_t)15));  // [2][4][NNT][64]
+  using WF = typename Frag<Tr>::W;
+  WF* ring = (WF*)(smem + (((size_t)nk * 4 * 8 + 15) & ~(size_t)15));  // [2][4][NNT][64]
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int kg = lane >> 4, col = lane & 15;
@@ -1227,15 +1244,16 @@ __global__ void __launch_bounds__(256) conv_fastw_kernel(FastArgs a) {
     if constexpr (Tr::kScaled) sc[i] = dq4<Tr>(a.bias, a.n_tiles, n0 < a.cout ? n0 : 0);
   }
   // weight staging: fragment f = wave + 4 j (j < NNT) of a chunk = (step d = f & 3, tile i = f >> 2)
-  uint4 wst[NNT];
+  // (F32S: the 32-byte split fragment, two loads and two ring stores)
+  WF wst[NNT];
   auto stage_load = [&](int c) {
 #pragma unroll
     for (int j = 0; j < NNT; ++j) {
       const int f = wave + 4 * j, d = f & 3, i = f >> 2;
       const int ks = 4 * c + d;
       const int nt = nt0 + i < a.n_tiles ? nt0 + i : a.n_tiles - 1;
-      const unsigned off = a.woff + (unsigned)((((size_t)nt * nk + (ks < nk ? ks : 0)) * 64 + lane) * 16);
-      wst[j] = bload(wr, off, 0);
+      const unsigned off = a.woff + (unsigned)((((size_t)nt * nk + (ks < nk ? ks : 0)) * 64 + lane) * Frag<Tr>::WB);
+      wst[j] = wload<Tr>(wr, off, 0);
     }
   };
   auto stage_store = [&](int buf) {
@@ -1267,7 +1285,7 @@ __global__ void __launch_bounds__(256) conv_fastw_kernel(FastArgs a) {
   for (int c = 0; c < nch; ++c) {
     const bool more = c + 1 < nch;
     if (more) stage_load(c + 1);  // in flight over this chunk's MFMAs
-    const uint4* wb = ring + (size_t)(c & 1) * 4 * NNT * 64;
+    const WF* wb = ring + (size_t)(c & 1) * 4 * NNT * 64;
     if constexpr (Tr::kScaled) {
       // FP8: steps (d, d + 1) of the chunk on one block-scaled K=128 MFMA (odd tail: zeros)
       const uint4 z = make_uint4(0u, 0u, 0u, 0u);
@@ -1297,16 +1315,20 @@ __global__ void __launch_bounds__(256) conv_fastw_kernel(FastArgs a) {
       for (int d = 0; d < 4; ++d) {
         const int ks = 4 * c + d;
         if (ks < nk) {
-          uint4 wf[NNT];
+          WF wf[NNT];
 #pragma unroll
           for (int i = 0; i < NNT; ++i) wf[i] = wb[(d * NNT + i) * 64 + lane];
           // step ks's activations sit in slot ks % SKD = d % SKD (SKD divides 4): a compile-time
           // index, so the slots stay registers
           uint4* xf = xb[d % SKD];
+          if constexpr (Tr::kSplit) {
+            mma_split_step<NNT, NPT>(wf, xf, acc);
+          } else {
 #pragma unroll
-          for (int i = 0; i < NNT; ++i)
+            for (int i = 0; i < NNT; ++i)
 #pragma unroll
-            for (int t = 0; t < NPT; ++t) acc[i][t] = mma<Tr>(wf[i], xf[t], acc[i][t]);
+              for (int t = 0; t < NPT; ++t) acc[i][t] = mma<Tr>(wf[i], xf[t], acc[i][t]);
+          }
           if (ks + SKD < nk) act_load(ks + SKD, xf);
         }
       }
@@ -1352,8 +1374,8 @@ __global__ void __launch_bounds__(256) conv_fastw_kernel(FastArgs a) {
   if (a.tstamp && tid == 0 && wg_lin < a.tstamp_cap) a.tstamp[3 * wg_lin + 2] = wall_clock64();
 }
 
-inline size_t fastw_lds(int k_steps, int nnt) {
-  return (((size_t)k_steps * 4 * 8 + 15) & ~(size_t)15) + (size_t)2 * 4 * nnt * 64 * 16;
+inline size_t fastw_lds(int k_steps, int nnt, int wb) {
+  return (((size_t)k_steps * 4 * 8 + 15) & ~(size_t)15) + (size_t)2 * 4 * nnt * 64 * wb;
 }
 
 // ---------------------------------------------------------------- persistent LDS-tiled conv (wide layers)
@@ -1585,6 +1607,231 @@ __global__ void __launch_bounds__(64 * NW) conv_wide_kernel(WideArgs a) {
     commit((T*)((unsigned char*)xt0 + ((it + 1) & 1) * tbytes));
     __syncthreads();
     t = tn;
+  }
+}
+
+// ---------------------------------------------------------------- halo-tile split conv (F32 build)
+// The F32S body of conv_fast splits every activation fragment into its bf16 parts as it loads
+// it -- once per tap and per output-channel group, so a 3x3 conv splits each element 9 times
+// per group -- and that VALU work, not the matrix cores, bounds it (r03 PMC + ISA: ~4 VALU per
+// v_mfma_f32_16x16x32_bf16, whose issue shadow holds 2).  Here a workgroup stages its output
+// tile's input window (tile + halo) into LDS ALREADY SPLIT, 16 channels at a time, and every
+// tap reads its B operands straight from there: the split runs once per staged element.
+// Operand layout ("K-slot", weights built by build_wkslot): lane group kg's 8 bf16 K slots hold
+// its 4 channels twice, XA = [x0(e0..3) | x1(e0..3)] and XB = [x0(e0..3) | x2(e0..3)], against
+// weight fragments A1 = [w0 | w0], A2 = [w1 | w1], A3 = [w2 | w0]: A1.XA + A2.XA + A3.XB = the six
+// products of F32S (w0x0 + w0x1 + w1x0 + w1x1 + w2x0 + w0x2), three MFMAs per fragment pair.
+// K order: chunk of 16 channels major, tap minor (step s = chunk * k*k + tap).
+// LDS: two chunk buffers x 8 planes (XA / XB x kg) x kHaloPx pixels x 16 B.  Plane bases are
+// multiples of 256 B, so the 16 consecutive pixels of a fragment row fall on 16 different
+// 4-bank groups (ds_read_b128 conflict-free).  One barrier per chunk: chunk c + 1's global loads
+// are in flight over chunk c's MFMAs, then split and written to the other buffer.
+// Wave layout: WM = 0, the four waves split the tile's pixels (NPT fragments each) and share
+// NE output-channel tiles; WM = 1, they share all NPT fragments and own NE tiles each.
+struct HaloArgs {
+  const void* arena;
+  unsigned arena_bytes;
+  unsigned soff0, soff1;  // byte offsets of the two source views (image b0, channel coff)
+  int h0, w0, cs0, up0, h1, w1, cs1, up1;
+  int c0, cin, n_chunks;
+  int stride, pad, in_h, in_w, out_h, out_w;
+  int tr, tc, twin, npx, tiles_x, tiles_y;  // output tile rows x cols, input window width, pixels
+  const void* wblob;  // K-slot weights: byte offset woff, [n_tiles][n_chunks * k * k][64][48 B]
+  unsigned wbytes, woff;
+  const float* bias;
+  int n_tiles;
+  void* dst;
+  int d_cstride, d_coff, cout;
+  const void* res;
+  int r_cstride, r_coff;
+  int act;
+  int xcd;
+};
+constexpr int kHaloPx = 256;                                 // pixels per LDS plane
+constexpr int kHaloPlaneB = kHaloPx * 16;                    // bytes per plane
+constexpr size_t kHaloLds = (size_t)2 * 8 * kHaloPlaneB;     // 64 KiB: two workgroups per CU
+
+struct WK3 {
+  u32x4v a1, a2, a3;
+};
+
+// x = x0 + x1 + x2 per element (bf16 RNE parts, as split3), in the K-slot layout
+__device__ __forceinline__ void split_kslot(const uint4& x, u32x4v& xa, u32x4v& xb) {
+  const float a0 = __uint_as_float(x.x), a1 = __uint_as_float(x.y), a2 = __uint_as_float(x.z),
+              a3 = __uint_as_float(x.w);
+  const unsigned p0 = pack_bf16x2(a0, a1), p1 = pack_bf16x2(a2, a3);
+  const float r0 = a0 - __uint_as_float(p0 << 16), r1 = a1 - __uint_as_float(p0 & 0xffff0000u);
+  const float r2 = a2 - __uint_as_float(p1 << 16), r3 = a3 - __uint_as_float(p1 & 0xffff0000u);
+  const unsigned q0 = pack_bf16x2(r0, r1), q1 = pack_bf16x2(r2, r3);
+  const float s0 = r0 - __uint_as_float(q0 << 16), s1 = r1 - __uint_as_float(q0 & 0xffff0000u);
+  const float s2 = r2 - __uint_as_float(q1 << 16), s3 = r3 - __uint_as_float(q1 & 0xffff0000u);
+  xa = u32x4v{p0, p1, q0, q1};
+  xb = u32x4v{p0, p1, pack_bf16x2(s0, s1), pack_bf16x2(s2, s3)};
+}
+
+template <int NE, int NPT, int WM, int KS>
+__global__ void __launch_bounds__(256) conv_halo_kernel(HaloArgs a) {
+  constexpr int T = KS * KS;
+  constexpr int UPT = kHaloPx * 4 / 256;  // staging units (pixel, channel group) per thread
+  constexpr int BUF = 8 * kHaloPlaneB;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int kg = lane >> 4, col = lane & 15;
+  const int2 blk = xcd_block(a.xcd);
+  const int tpi = a.tiles_x * a.tiles_y;
+  const int b = blk.x / tpi, rr = blk.x - b * tpi;
+  const int tyi = rr / a.tiles_x, txi = rr - tyi * a.tiles_x;
+  const int oy0 = tyi * a.tr, ox0 = txi * a.tc;
+  const int iy0 = oy0 * a.stride - a.pad, ix0 = ox0 * a.stride - a.pad;
+  const int nt0 = (blk.y * (WM ? 4 : 1) + (WM ? wave : 0)) * NE;
+  const __amdgpu_buffer_rsrc_t xr = make_srd(a.arena, a.arena_bytes);
+  const __amdgpu_buffer_rsrc_t wr = make_srd(a.wblob, a.wbytes);
+  // the lane's pixel of each fragment: LDS byte offset of its window origin in plane XA(kg)
+  unsigned lb[NPT];
+  int opx[NPT];  // output pixel index, -1 outside the image / tile
+#pragma unroll
+  for (int t = 0; t < NPT; ++t) {
+    const int f = WM ? t : wave * NPT + t;
+    const int q = f * 16 + col;
+    const int ty = q / a.tc, tx = q - ty * a.tc;
+    const bool v = q < a.tr * a.tc && oy0 + ty < a.out_h && ox0 + tx < a.out_w;
+    lb[t] = (unsigned)(kg * kHaloPlaneB + (v ? (ty * a.stride * a.twin + tx * a.stride) * 16 : 0));
+    opx[t] = v ? (b * a.out_h + oy0 + ty) * a.out_w + ox0 + tx : -1;
+  }
+  // staging units: pixel px = (tid & 15) + 16 (tid >> 6) + 64 j of the window, channel group
+  // kgu = (tid >> 4) & 3 -- eight lanes of a ds_write_b128 group write 8 consecutive pixels of
+  // one plane (conflict-free)
+  const int kgu = (tid >> 4) & 3;
+  unsigned sv0[UPT], sv1[UPT];
+  int sl[UPT];
+#pragma unroll
+  for (int j = 0; j < UPT; ++j) {
+    const int px = (tid & 15) + 16 * (tid >> 6) + 64 * j;
+    sl[j] = -1;
+    sv0[j] = sv1[j] = kOOB;
+    if (px < a.npx) {
+      const int py = px / a.twin, pxx = px - py * a.twin;
+      const int iy = iy0 + py, ix = ix0 + pxx;
+      sl[j] = kgu * kHaloPlaneB + px * 16;
+      if (iy >= 0 && iy < a.in_h && ix >= 0 && ix < a.in_w) {
+        sv0[j] = a.soff0 + (unsigned)(((b * a.h0 + (iy >> a.up0)) * a.w0 + (ix >> a.up0)) * a.cs0 * 4);
+        sv1[j] = a.soff1 + (unsigned)(((b * a.h1 + (iy >> a.up1)) * a.w1 + (ix >> a.up1)) * a.cs1 * 4);
+      }
+    }
+  }
+  uint4 st[UPT];
+  auto fetch = [&](int c) {
+    const int ch = c * 16 + kgu * 4;
+    const bool s1 = ch >= a.c0, cv = ch < a.cin;
+    const unsigned co = (unsigned)((s1 ? ch - a.c0 : ch) * 4);
+#pragma unroll
+    for (int j = 0; j < UPT; ++j) {
+      const unsigned o = s1 ? sv1[j] : sv0[j];
+      st[j] = bload(xr, cv && o != kOOB ? o + co : kOOB, 0);
+    }
+  };
+  auto commit = [&](int buf) {
+    unsigned char* base = smem + buf * BUF;
+#pragma unroll
+    for (int j = 0; j < UPT; ++j)
+      if (sl[j] >= 0) {
+        u32x4v xa, xb;
+        split_kslot(st[j], xa, xb);
+        *(u32x4v*)(base + sl[j]) = xa;
+        *(u32x4v*)(base + 4 * kHaloPlaneB + sl[j]) = xb;
+      }
+  };
+  const int nsteps = a.n_chunks * T;
+  unsigned wo[NE];
+#pragma unroll
+  for (int i = 0; i < NE; ++i) {
+    const int nt = nt0 + i < a.n_tiles ? nt0 + i : a.n_tiles - 1;
+    wo[i] = a.woff + (unsigned)(((size_t)nt * nsteps * 64 + lane) * 48);
+  }
+  auto wload3 = [&](int s, WK3* w) {
+#pragma unroll
+    for (int i = 0; i < NE; ++i) {
+      w[i].a1 = __builtin_amdgcn_raw_buffer_load_b128(wr, (int)wo[i], s * 64 * 48, 0);
+      w[i].a2 = __builtin_amdgcn_raw_buffer_load_b128(wr, (int)wo[i] + 16, s * 64 * 48, 0);
+      w[i].a3 = __builtin_amdgcn_raw_buffer_load_b128(wr, (int)wo[i] + 32, s * 64 * 48, 0);
+    }
+  };
+  f32x4 acc[NE][NPT];
+#pragma unroll
+  for (int i = 0; i < NE; ++i)
+#pragma unroll
+    for (int t = 0; t < NPT; ++t) acc[i][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  WK3 wb[2][NE];
+  fetch(0);
+  wload3(0, wb[0]);
+  commit(0);
+  __syncthreads();
+  // step s = c * T + t uses weight slot s & 1 = (t + P) & 1 with P = the parity of c * T (a
+  // compile-time index: chunks run in pairs); step s + 1's weights load over step s's MFMAs
+  auto chunk = [&](int c, auto par) {
+    constexpr int P = decltype(par)::value;
+    const bool more = c + 1 < a.n_chunks;
+    if (more) fetch(c + 1);
+    const unsigned char* xs = smem + (c & 1) * BUF;
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+      const int s = c * T + t;
+      if (s + 1 < nsteps) wload3(s + 1, wb[(t + P + 1) & 1]);
+      const int dy = t / KS, dx = t - dy * KS;
+      const unsigned toff = (unsigned)((dy * a.twin + dx) * 16);
+      u32x4v xa[NPT], xb[NPT];
+#pragma unroll
+      for (int f = 0; f < NPT; ++f) {
+        xa[f] = *(const u32x4v*)(xs + lb[f] + toff);
+        xb[f] = *(const u32x4v*)(xs + 4 * kHaloPlaneB + lb[f] + toff);
+      }
+      const WK3* w = wb[(t + P) & 1];
+#pragma unroll
+      for (int f = 0; f < NPT; ++f)
+#pragma unroll
+        for (int i = 0; i < NE; ++i) acc[i][f] = mfma_bf16(w[i].a1, xa[f], acc[i][f]);
+#pragma unroll
+      for (int f = 0; f < NPT; ++f)
+#pragma unroll
+        for (int i = 0; i < NE; ++i) acc[i][f] = mfma_bf16(w[i].a2, xa[f], acc[i][f]);
+#pragma unroll
+      for (int f = 0; f < NPT; ++f)
+#pragma unroll
+        for (int i = 0; i < NE; ++i) acc[i][f] = mfma_bf16(w[i].a3, xb[f], acc[i][f]);
+    }
+    if (more) commit((c + 1) & 1);
+    __syncthreads();
+  };
+  int c = 0;
+  for (; c + 2 <= a.n_chunks; c += 2) {
+    chunk(c, std::integral_constant<int, 0>{});
+    chunk(c + 1, std::integral_constant<int, (T & 1)>{});
+  }
+  if (c < a.n_chunks) chunk(c, std::integral_constant<int, 0>{});
+#pragma unroll
+  for (int i = 0; i < NE; ++i) {
+    const int nt = nt0 + i;
+    const int n0 = nt * 16 + kg * 4;
+    if (nt >= a.n_tiles || n0 >= a.cout) continue;
+    const float4 bb = *(const float4*)(a.bias + n0);
+#pragma unroll
+    for (int f = 0; f < NPT; ++f) {
+      const int p = opx[f];
+      if (p < 0) continue;
+      float v[4] = {acc[i][f][0] + bb.x, acc[i][f][1] + bb.y, acc[i][f][2] + bb.z, acc[i][f][3] + bb.w};
+      if (a.act) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = silu<true>(v[j]);
+      }
+      if (a.res) {
+        float r[4];
+        load4((const float*)a.res + (size_t)p * a.r_cstride + a.r_coff + n0, r);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = r[j] + v[j];
+      }
+      store4((float*)a.dst + (size_t)p * a.d_cstride + a.d_coff + n0, v);
+    }
   }
 }
 
@@ -2815,6 +3062,10 @@ struct yk_model {
   char* wsplit = nullptr;
   size_t wsplit_bytes = 0;
   std::vector<int64_t> ws_off;
+  // F32 build: the same weights in conv_halo_kernel's K-slot layout (build_wkslot)
+  char* wkslot = nullptr;
+  size_t wkslot_bytes = 0;
+  std::vector<int64_t> wk_off;
   bool split_default = false;  // YK_F32_SPLIT=1: the heuristic plan uses F32S where it can
   bool autotune_split = true;  // YK_F32_SPLIT=0: autotune never picks F32S
 };
@@ -3021,7 +3272,7 @@ void set_fast_attr_n() {
   set_fast_attr<Tr, NNT, 1, WS>();
   set_fast_attr<Tr, NNT, 2, WS>();
   set_fast_attr<Tr, NNT, 4, WS>();
-  if constexpr (!WS && !Tr::kSplit) {
+  if constexpr (!WS) {
     set_fastw_attr<Tr, NNT, 1>();
     set_fastw_attr<Tr, NNT, 2>();
     set_fastw_attr<Tr, NNT, 4>();
@@ -3046,7 +3297,23 @@ void set_wide_attr_n() {
   set_wide_attr_w<Tr, NNT, 4>();
   set_wide_attr_w<Tr, NNT, 8>();
 }
+template <int NE, int NPT>
+void set_halo_attr_p() {
+  (void)hipFuncSetAttribute((const void*)conv_halo_kernel<NE, NPT, 0, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kHaloLds);
+  (void)hipFuncSetAttribute((const void*)conv_halo_kernel<NE, NPT, 0, 3>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kHaloLds);
+  (void)hipFuncSetAttribute((const void*)conv_halo_kernel<NE, NPT, 1, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kHaloLds);
+  (void)hipFuncSetAttribute((const void*)conv_halo_kernel<NE, NPT, 1, 3>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kHaloLds);
+}
+template <int NE>
+void set_halo_attr_n() {
+  set_halo_attr_p<NE, 1>();
+  set_halo_attr_p<NE, 2>();
+  set_halo_attr_p<NE, 4>();
+}
 void set_tile_attrs() {
+  set_halo_attr_n<1>();
+  set_halo_attr_n<2>();
+  set_halo_attr_n<4>();
   set_tile_attrs_t<BF16>();
   set_tile_attrs_t<F32>();
   set_wide_attr_n<BF16, 2>();
@@ -3072,10 +3339,11 @@ void set_tile_attrs() {
 }
 
 // Conv kernel choice for one op at batch B.
-enum { CK_DIRECT = 0, CK_TILE = 1, CK_SPLITK = 2, CK_FAST = 3, CK_WIDE = 4 };
-// CK_FAST plan npt bit: the F32 build's op runs the F32S split-MFMA body (modes 0 and 1 only)
+enum { CK_DIRECT = 0, CK_TILE = 1, CK_SPLITK = 2, CK_FAST = 3, CK_WIDE = 4, CK_HALO = 5 };
+// CK_FAST plan npt bit: the F32 build's op runs the F32S split-MFMA body (every mode)
 constexpr int kSplitBit = 64;
 // CK_WIDE plan: nnt in {2, 4} (output-channel tiles per workgroup), npt unused
+// CK_HALO plan (F32 build): nnt = NE in {1, 2, 4}, npt = NPT | WM << 4 with NPT in {1, 2, 4}
 // CK_FAST plan: nnt in {1, 2, 3, 4}, npt = NPT | (WS << 4) with NPT in {1, 2, 4}
 struct ConvPlan {
   int kind = CK_DIRECT, nnt = 0, npt = 0;
@@ -3139,6 +3407,40 @@ WidePlan wide_plan(const yk_op& op, int esz, int nnt, int nw = 4) {
   return w;
 }
 
+// conv_halo_kernel tile: the output tile (tr x tc, its 16 * NF pixels row-major) whose input
+// window fits a plane (kHaloPx pixels) at the least cost ~ MFMA work incl. the tile's padding
+// (pixels x taps) + staging (window pixels).  Sources: 4-channel groups never straddle the two.
+struct HaloPlan {
+  bool ok = false;
+  int tr = 0, tc = 0, twin = 0, npx = 0, tiles_x = 0, tiles_y = 0;
+};
+HaloPlan halo_plan(const yk_op& op, int npt, int wm) {
+  HaloPlan h;
+  const int k = op.ksize, s = op.stride;
+  const int c0 = op.src_ch[0], cin = op.src_ch[0] + (op.n_src > 1 ? op.src_ch[1] : 0);
+  if ((k != 1 && k != 3) || cin % 4 || c0 % 4 || op.out_h < 1 || op.out_w < 1) return h;
+  const int px = 16 * (wm ? npt : 4 * npt);
+  long best = -1;
+  for (int tc = 1; tc <= op.out_w && tc <= px; ++tc) {
+    const int tr = std::min(px / tc, op.out_h);
+    const int twin = (tc - 1) * s + k, thin = (tr - 1) * s + k;
+    if (twin * thin > kHaloPx) continue;
+    const long tiles = (long)((op.out_h + tr - 1) / tr) * ((op.out_w + tc - 1) / tc);
+    const long cost = tiles * (4L * k * k * px + twin * thin);
+    if (best < 0 || cost < best) {
+      best = cost;
+      h.tr = tr;
+      h.tc = tc;
+      h.twin = twin;
+      h.npx = twin * thin;
+      h.tiles_x = (op.out_w + tc - 1) / tc;
+      h.tiles_y = (op.out_h + tr - 1) / tr;
+    }
+  }
+  h.ok = best >= 0;
+  return h;
+}
+
 // conv_fast_kernel geometry: the largest fragment tile (NNT x NPT) that still gives >= 1024
 // workgroups (>= 4 waves per CU) and wastes < 25% of the n-tiles; the four waves split K (WS)
 // when the per-wave-pixel layout would give too few workgroups.
@@ -3193,6 +3495,13 @@ ConvPlan conv_plan(const yk_model* m, const yk_op& op, int B) {
       if ((p.npt & kSplitBit) && !(m->wsplit && m->ws_off[idx] >= 0)) p.npt &= ~kSplitBit;
       return p;
     }
+    if (t[0] == CK_HALO && m->wkslot && m->wk_off[idx] >= 0 && halo_plan(op, t[2] & 15, (t[2] >> 4) & 1).ok) {
+      ConvPlan p;
+      p.kind = CK_HALO;
+      p.nnt = t[1];
+      p.npt = t[2];
+      return p;
+    }
     if (t[0] == CK_TILE && m->ltab && m->ltab_off[idx] >= 0) {
       ConvPlan p;
       p.kind = CK_TILE;
@@ -3205,7 +3514,7 @@ ConvPlan conv_plan(const yk_model* m, const yk_op& op, int B) {
   const size_t oi = (size_t)(&op - m->ops.data());
   if (m->ktab && oi < m->ktab_off.size() && m->ktab_off[oi] >= 0 && (long)B * op.out_h * op.out_w < (1L << 22)) {
     ConvPlan p = fast_plan(op, B);  // (fdiv: pixel indices < 2^22)
-    if (m->split_default && m->wsplit && m->ws_off[oi] >= 0 && (p.npt >> 4) != 2) p.npt |= kSplitBit;
+    if (m->split_default && m->wsplit && m->ws_off[oi] >= 0) p.npt |= kSplitBit;
     return p;
   }
   if (op.out_h * op.out_w <= 1280) return splitk_plan(op, B);
@@ -3260,7 +3569,8 @@ template <class Tr, int NNT, int NPT>
 void launch_fastw_t(const FastArgs& a, hipStream_t st) {
   constexpr int SKD = fastw_skd(NNT, NPT);
   dim3 grid((a.M + 64 * NPT - 1) / (64 * NPT), (a.n_tiles + NNT - 1) / NNT);
-  hipLaunchKernelGGL((conv_fastw_kernel<Tr, NNT, NPT, SKD>), grid, dim3(256), fastw_lds(a.k_steps, NNT), st, a);
+  hipLaunchKernelGGL((conv_fastw_kernel<Tr, NNT, NPT, SKD>), grid, dim3(256), fastw_lds(a.k_steps, NNT, Frag<Tr>::WB), st,
+                     a);
 }
 template <class Tr, int NNT>
 void launch_fastw_n(const FastArgs& a, int npt, hipStream_t st) {
@@ -3282,14 +3592,41 @@ void launch_fastw(const FastArgs& a, int nnt, int npt, hipStream_t st) {
 template <class Tr>
 void launch_fast(const FastArgs& a, const ConvPlan& p, hipStream_t st) {
   const int mode = (p.npt >> 4) & 3;
-  if constexpr (!Tr::kSplit) {
-    if (mode == 2) {
-      launch_fastw<Tr>(a, p.nnt, p.npt & 15, st);
-      return;
-    }
+  if (mode == 2) {
+    launch_fastw<Tr>(a, p.nnt, p.npt & 15, st);
+    return;
   }
   if (mode == 1) launch_fast_w<Tr, true>(a, p.nnt, p.npt & 15, st);
   else launch_fast_w<Tr, false>(a, p.nnt, p.npt & 15, st);
+}
+
+template <int NE, int NPT, int WM, int KS>
+void launch_halo_t(const HaloArgs& a, int B, hipStream_t st) {
+  const int per = NE * (WM ? 4 : 1);
+  dim3 grid(B * a.tiles_x * a.tiles_y, (a.n_tiles + per - 1) / per);
+  hipLaunchKernelGGL((conv_halo_kernel<NE, NPT, WM, KS>), grid, dim3(256), kHaloLds, st, a);
+}
+template <int NE, int NPT, int WM>
+void launch_halo_k(const HaloArgs& a, int B, int ks, hipStream_t st) {
+  if (ks == 3) launch_halo_t<NE, NPT, WM, 3>(a, B, st);
+  else launch_halo_t<NE, NPT, WM, 1>(a, B, st);
+}
+template <int NE, int NPT>
+void launch_halo_w(const HaloArgs& a, int B, int wm, int ks, hipStream_t st) {
+  if (wm) launch_halo_k<NE, NPT, 1>(a, B, ks, st);
+  else launch_halo_k<NE, NPT, 0>(a, B, ks, st);
+}
+template <int NE>
+void launch_halo_p(const HaloArgs& a, int B, int npt, int wm, int ks, hipStream_t st) {
+  if (npt == 4) launch_halo_w<NE, 4>(a, B, wm, ks, st);
+  else if (npt == 2) launch_halo_w<NE, 2>(a, B, wm, ks, st);
+  else launch_halo_w<NE, 1>(a, B, wm, ks, st);
+}
+void launch_halo(const HaloArgs& a, int B, const ConvPlan& p, int ks, hipStream_t st) {
+  const int npt = p.npt & 15, wm = (p.npt >> 4) & 1;
+  if (p.nnt == 4) launch_halo_p<4>(a, B, npt, wm, ks, st);
+  else if (p.nnt == 2) launch_halo_p<2>(a, B, npt, wm, ks, st);
+  else launch_halo_p<1>(a, B, npt, wm, ks, st);
 }
 
 template <class Tr, int NNT, int UPT, int NW>
@@ -3431,6 +3768,54 @@ int launch_op(yk_model* m, const yk_op& op, const uint8_t* frames, int B, float 
           } else {
             if (nw == 8) launch_wide_n<Tr, 4, 8>(w, wp.upt, wp.lds, st);
             else launch_wide_n<Tr, 4, 4>(w, wp.upt, wp.lds, st);
+          }
+        } else if (cp.kind == CK_HALO) {
+          if constexpr (std::is_same<Tr, F32>::value) {
+            const size_t oi = (size_t)(&op - m->ops.data());
+            const HaloPlan hp = halo_plan(op, cp.npt & 15, (cp.npt >> 4) & 1);
+            HaloArgs h;
+            h.arena = m->arena;
+            h.arena_bytes = (unsigned)m->arena_bytes;
+            h.soff0 = (unsigned)(((const char*)a.src[0].p - (const char*)m->arena) + (size_t)a.src[0].coff * 4);
+            h.soff1 = (unsigned)(((const char*)a.src[1].p - (const char*)m->arena) + (size_t)a.src[1].coff * 4);
+            h.h0 = a.src[0].h;
+            h.w0 = a.src[0].w;
+            h.cs0 = a.src[0].cstride;
+            h.up0 = a.src[0].up;
+            h.h1 = a.src[1].h;
+            h.w1 = a.src[1].w;
+            h.cs1 = a.src[1].cstride;
+            h.up1 = a.src[1].up;
+            h.c0 = a.c0;
+            h.cin = a.cin;
+            h.n_chunks = (a.cin + 15) / 16;
+            h.stride = a.stride;
+            h.pad = a.pad;
+            h.in_h = a.in_h;
+            h.in_w = a.in_w;
+            h.out_h = a.out_h;
+            h.out_w = a.out_w;
+            h.tr = hp.tr;
+            h.tc = hp.tc;
+            h.twin = hp.twin;
+            h.npx = hp.npx;
+            h.tiles_x = hp.tiles_x;
+            h.tiles_y = hp.tiles_y;
+            h.wblob = m->wkslot;
+            h.wbytes = (unsigned)m->wkslot_bytes;
+            h.woff = (unsigned)m->wk_off[oi];
+            h.bias = a.bias;
+            h.n_tiles = a.n_tiles;
+            h.dst = a.dst;
+            h.d_cstride = a.d_cstride;
+            h.d_coff = a.d_coff;
+            h.cout = a.cout;
+            h.res = a.res;
+            h.r_cstride = a.r_cstride;
+            h.r_coff = a.r_coff;
+            h.act = a.act;
+            h.xcd = m->xcd;
+            launch_halo(h, B, cp, op.ksize, st);
           }
         } else if (cp.kind == CK_FAST) {
           FastArgs f;
@@ -3623,6 +4008,10 @@ const char* op_kernel_name(const yk_model* m, const yk_op& op) {
     const WidePlan wp = wide_plan(op, esz_of(dt), cp.nnt, cp.npt);
     const int upt = wp.upt <= 4 ? 4 : wp.upt <= 8 ? 8 : wp.upt <= 12 ? 12 : 16;
     snprintf(buf, sizeof buf, "conv_wide_kernel<yk::det::%s, %d, %d, %d>", tn, cp.nnt, upt, cp.npt);
+    return buf;
+  }
+  if (cp.kind == CK_HALO) {
+    snprintf(buf, sizeof buf, "conv_halo_kernel<%d, %d, %d, %d>", cp.nnt, cp.npt & 15, (cp.npt >> 4) & 1, op.ksize);
     return buf;
   }
   if (cp.kind == CK_FAST) {
@@ -3981,6 +4370,62 @@ hipError_t build_wsplit(yk_model* m, const char* host_blob, size_t blob_bytes) {
   return e;
 }
 
+// conv_halo_kernel weights (K-slot layout, see conv_halo_kernel): per conv op with a table (its
+// packed f32 fragments [n_tiles][k_steps][64 lanes][4 f32] hold W[co][tap * cin + ch] at step
+// kappa / 16, lane (kappa % 16 / 4) * 16 + co % 16, element kappa % 4), the fragments of step
+// s = chunk * k*k + tap as [n_tiles][steps][64][A1 | A2 | A3] (48 B): channel ch = 16 chunk +
+// 4 kg + e (zero past cin), A1 = [w0(e) x4 | w0(e) x4], A2 = [w1 | w1], A3 = [w2 | w0].
+hipError_t build_wkslot(yk_model* m, const char* host_blob, size_t blob_bytes) {
+  m->wk_off.assign(m->ops.size(), -1);
+  std::vector<unsigned short> out;
+  for (size_t i = 0; i < m->ops.size(); ++i) {
+    const yk_op& op = m->ops[i];
+    if (op.kind != YK_K_CONV || m->ktab_off.empty() || m->ktab_off[i] < 0) continue;
+    const int k = op.ksize, cin = op.src_ch[0] + (op.n_src > 1 ? op.src_ch[1] : 0);
+    if ((k != 1 && k != 3) || cin % 4 || op.src_ch[0] % 4) continue;
+    if ((size_t)op.w_off + (size_t)op.n_tiles * op.k_steps * 64 * 16 > blob_bytes) continue;
+    const int T = k * k, nch = (cin + 15) / 16, nsteps = nch * T;
+    while ((out.size() * 2) % 256) out.push_back(0);
+    m->wk_off[i] = (int64_t)out.size() * 2;
+    const float* w = (const float*)(host_blob + op.w_off);
+    for (int nt = 0; nt < op.n_tiles; ++nt)
+      for (int s = 0; s < nsteps; ++s) {
+        const int c = s / T, tap = s - c * T;
+        for (int lane = 0; lane < 64; ++lane) {
+          const int kg = lane >> 4, col = lane & 15;
+          unsigned short part[3][4];
+          for (int e = 0; e < 4; ++e) {
+            const int ch = 16 * c + 4 * kg + e;
+            float x = 0.f;
+            if (ch < cin) {
+              const int kap = tap * cin + ch, ks = kap >> 4, r = kap & 15;
+              x = w[(((size_t)nt * op.k_steps + ks) * 64 + (r >> 2) * 16 + col) * 4 + (r & 3)];
+            }
+            part[0][e] = h_f2bf(x);
+            const float r1 = x - h_bf2f(part[0][e]);
+            part[1][e] = h_f2bf(r1);
+            part[2][e] = h_f2bf(r1 - h_bf2f(part[1][e]));
+          }
+          for (int e = 0; e < 4; ++e) out.push_back(part[0][e]);  // A1
+          for (int e = 0; e < 4; ++e) out.push_back(part[0][e]);
+          for (int e = 0; e < 4; ++e) out.push_back(part[1][e]);  // A2
+          for (int e = 0; e < 4; ++e) out.push_back(part[1][e]);
+          for (int e = 0; e < 4; ++e) out.push_back(part[2][e]);  // A3
+          for (int e = 0; e < 4; ++e) out.push_back(part[0][e]);
+        }
+      }
+  }
+  if (out.empty()) return hipSuccess;
+  if (out.size() * 2 >= 0x7fff0000ull) {  // 32-bit buffer offsets
+    m->wk_off.assign(m->ops.size(), -1);
+    return hipSuccess;
+  }
+  m->wkslot_bytes = out.size() * 2;
+  hipError_t e = hipMalloc((void**)&m->wkslot, m->wkslot_bytes);
+  if (e == hipSuccess) e = hipMemcpy(m->wkslot, out.data(), m->wkslot_bytes, hipMemcpyHostToDevice);
+  return e;
+}
+
 // The kernels' host-mapped error word (nms_flag_error): a flagged launch made its images'
 // detections empty; the next call on the model reports it (and clears it) as YK_ERR_STATE.
 int take_device_error(yk_model* m) {
@@ -4129,6 +4574,7 @@ int yk_model_create(yk_ctx* ctx, const yk_model_desc* desc, const void* host_blo
     m->autotune_split = env[0] != '0';
   }
   if (e == hipSuccess && desc->act_dtype == YK_ACT_F32) e = build_wsplit(m, (const char*)host_blob, (size_t)blob_bytes);
+  if (e == hipSuccess && desc->act_dtype == YK_ACT_F32) e = build_wkslot(m, (const char*)host_blob, (size_t)blob_bytes);
   if (e == hipSuccess && desc->act_dtype == YK_ACT_FP8)
     for (size_t i = 0; i < m->ops.size(); ++i)
       if (m->ops[i].kind == YK_K_CONV && (m->ktab_off[i] < 0 || m->ops[i].src_ch[0] % 16 ||
@@ -4181,7 +4627,7 @@ int yk_model_destroy(yk_model* m) {
   for (hipEvent_t v : m->ev) (void)hipEventDestroy(v);
   if (m->arena) (void)hipFree(m->arena);
   void* ptrs[] = {m->blob, m->cand, m->cand_count, m->slot_of, m->gkeys, m->gbox, m->gflag, m->dets, m->counts, m->ktab,
-                  m->ltab, m->lbox, m->ts, m->wsplit, m->nms_stat};
+                  m->ltab, m->lbox, m->ts, m->wsplit, m->wkslot, m->nms_stat};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (m->err_host) (void)hipHostFree((void*)m->err_host);
@@ -4283,15 +4729,19 @@ int yk_model_profile(yk_model* m, const uint8_t* frames, int batch, float conf, 
 
 int yk_model_set_plan(yk_model* m, int op_index, int batch, int kind, int nnt, int npt) {
   YK_CHECK_ARG(m && op_index >= -1 && op_index < (int)m->ops.size(), "yk_model_set_plan: bad op index");
-  YK_CHECK_ARG(kind >= -1 && kind <= CK_WIDE, "yk_model_set_plan: kind must be -1 (heuristic), 0, 1, 2, 3 or 4");
+  YK_CHECK_ARG(kind >= -1 && kind <= CK_HALO, "yk_model_set_plan: kind must be -1 (heuristic), 0, 1, 2, 3, 4 or 5");
+  YK_CHECK_ARG(kind != CK_HALO || (m->wkslot && (nnt == 1 || nnt == 2 || nnt == 4) &&
+                                   ((npt & 15) == 1 || (npt & 15) == 2 || (npt & 15) == 4) && (npt & ~31) == 0),
+               "yk_model_set_plan: halo conv (kind 5) needs the fp32 build, nnt in {1, 2, 4}, npt in {1, 2, 4} (+16: "
+               "waves split output channels)");
   YK_CHECK_ARG(kind != CK_WIDE || ((nnt == 2 || nnt == 4) && (npt == 0 || npt == 4 || npt == 8)),
                "yk_model_set_plan: wide conv nnt must be 2 or 4, npt (waves) 0, 4 or 8");
   YK_CHECK_ARG(kind != CK_FAST || (nnt >= 1 && nnt <= 4 && ((npt & 15) == 1 || (npt & 15) == 2 || (npt & 15) == 4) &&
                                    ((npt >> 4) & 3) <= 2 && (npt & ~(kSplitBit | 63)) == 0),
                "yk_model_set_plan: table conv needs nnt in [1, 4], npt in {1, 2, 4} (+16: waves split K, +32: LDS-shared "
                "weights, +64: split-bf16 MFMA)");
-  YK_CHECK_ARG(kind != CK_FAST || !(npt & kSplitBit) || (m->wsplit && ((npt >> 4) & 3) != 2),
-               "yk_model_set_plan: the split-bf16 MFMA variant (+64) needs the fp32 build and modes 0 / 1");
+  YK_CHECK_ARG(kind != CK_FAST || !(npt & kSplitBit) || m->wsplit,
+               "yk_model_set_plan: the split-bf16 MFMA variant (+64) needs the fp32 build");
   YK_CHECK_ARG(kind != CK_TILE || nnt == 0 || nnt == 1, "yk_model_set_plan: tiled conv nnt must be 0 or 1 (LDS-resident weights)");
   YK_CHECK_ARG(kind != CK_SPLITK || ((nnt == 1 || nnt == 2 || nnt == 4) && (npt == 1 || npt == 2 || npt == 4)),
                "yk_model_set_plan: split-K fragment tile must be nnt, npt in {1, 2, 4}");
@@ -4362,8 +4812,18 @@ int yk_model_autotune(yk_model* m, const uint8_t* frames, int batch, float conf,
             const long wgs = ((long)bt * op.out_h * op.out_w + px - 1) / px * ((op.n_tiles + nnt - 1) / nnt);
             if (wgs < 64) continue;
             cands.push_back({CK_FAST, nnt, npt | (mode << 4)});
-            if (mode < 2 && m->wsplit && m->ws_off[i] >= 0 && m->autotune_split)
+            if (m->wsplit && m->ws_off[i] >= 0 && m->autotune_split)
               cands.push_back({CK_FAST, nnt, npt | (mode << 4) | kSplitBit});
+          }
+    if (m->wkslot && m->wk_off[i] >= 0 && m->autotune_split)
+      for (int wm = 0; wm < 2; ++wm)
+        for (int ne : {1, 2, 4})
+          for (int npt : {1, 2, 4}) {
+            const int per = ne * (wm ? 4 : 1), groups = (op.n_tiles + per - 1) / per;
+            if (per > 1 && 4 * op.n_tiles < 3 * groups * per) continue;
+            const HaloPlan hp = halo_plan(op, npt, wm);
+            if (!hp.ok || (long)bt * hp.tiles_x * hp.tiles_y * groups < 64) continue;
+            cands.push_back({CK_HALO, ne, npt | (wm << 4)});
           }
     if (cands.empty()) continue;  // (FP8 without a table: yk_model_create refuses that)
     float best = 1e30f;
