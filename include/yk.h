@@ -398,6 +398,35 @@ int yk_model_destroy(yk_model* m);
  * plan[n_plan][4] = {op, kind, nnt, npt} applied with yk_model_set_plan at plan_batch. */
 int yk_model_load(yk_ctx* ctx, const char* path, yk_model** out);
 
+/* The detector program built by the library itself from a raw fp32 state dict: what
+ * DetectionModel(yaml) + load_state_dict + fuse() do before predict (nn/tasks.py:1524-1700
+ * parse_model channel / repeat rules of the yolov8-small P2 topology at `scale`, Conv+BN fold
+ * with eps 1e-3, utils/torch_utils.py:255-286), then the lowering and weight packing of
+ * model.py Program -- byte-identical to it -- for one frame size, imgsz, dtype and max_batch.
+ * Host-only (no device call).  A tensor is named as in the state dict
+ * ("model.2.m.0.cv1.conv.weight", "model.25.cv3.0.2.bias", ...), fp32, C-contiguous; nc is read
+ * from model.25.cv3.0.2.weight.  yk_program_get's pointers stay valid until
+ * yk_program_destroy. */
+typedef struct {
+  const char* name;
+  int32_t ndim;
+  int64_t shape[4];
+  const float* data;
+} yk_tensor;
+typedef struct {
+  int32_t n;
+  const yk_tensor* tensors;
+} yk_weights;
+typedef struct yk_program yk_program;
+int yk_program_build(const yk_weights* weights, char scale, int act_dtype, int frame_h, int frame_w, int imgsz,
+                     int max_batch, int max_det, yk_program** out);
+int yk_program_get(const yk_program* p, const yk_model_desc** desc, const void** blob, int64_t* blob_bytes);
+int yk_program_destroy(yk_program* p);
+/* yk_program_build (max_det 300, predict's default) + yk_model_create: the self-contained C-ABI
+ * model load; examples/c_host.c shows it from a raw state-dict file. */
+int yk_model_load_weights(yk_ctx* ctx, const yk_weights* weights, char scale, int act_dtype, int frame_h, int frame_w,
+                          int imgsz, int max_batch, yk_model** out);
+
 /* One predict() over `batch` frames resident in HBM (dev_frames: batch x frame_h x frame_w x 3
  * uint8 BGR).  Writes dev_dets[batch][max_det][6] = x1,y1,x2,y2,conf,cls (original-image pixels,
  * like Results.boxes.data) and dev_counts[batch].  NULL outputs use the model's own buffers

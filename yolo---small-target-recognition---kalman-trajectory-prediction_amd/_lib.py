@@ -92,6 +92,41 @@ TRACK_STATE_DTYPE = np.dtype([
 
 _vp = C.c_void_p
 _i32 = C.c_int32
+class Tensor(C.Structure):
+    """yk_tensor: one named fp32 state-dict tensor (host memory)."""
+    _fields_ = [("name", C.c_char_p), ("ndim", C.c_int32), ("shape", C.c_int64 * 4), ("data", C.c_void_p)]
+
+
+class Weights(C.Structure):
+    _fields_ = [("n", C.c_int32), ("tensors", C.POINTER(Tensor))]
+
+
+def weights_struct(sd: dict):
+    """(yk_weights, keep-alive list) for a state dict of torch tensors / numpy arrays: every
+    floating tensor as contiguous fp32 (what the checkpoint loader's .float() gives)."""
+    import numpy as np
+
+    keep, items = [], []
+    for k, v in sd.items():
+        a = v.detach().cpu().float().numpy() if hasattr(v, "detach") else np.asarray(v)
+        if a.dtype.kind != "f" or a.ndim > 4:
+            continue
+        a = np.ascontiguousarray(a, dtype=np.float32)
+        name = k.encode()
+        keep += [a, name]
+        t = Tensor()
+        t.name = name
+        t.ndim = a.ndim
+        for d in range(a.ndim):
+            t.shape[d] = a.shape[d]
+        t.data = a.ctypes.data
+        items.append(t)
+    arr = (Tensor * len(items))(*items)
+    keep.append(arr)
+    w = Weights(len(items), arr)
+    return w, keep
+
+
 _SIGS = {
     "yk_abi_version": ([], C.c_int),
     "yk_last_error": ([], C.c_char_p),
@@ -125,6 +160,12 @@ _SIGS = {
     "yk_model_get_schedule": ([_vp, _vp, _vp], C.c_int),
     "yk_model_get_plan": ([_vp, _vp, _vp], C.c_int),
     "yk_model_load": ([_vp, C.c_char_p, C.POINTER(_vp)], C.c_int),
+    "yk_program_build": ([C.POINTER(Weights), C.c_char, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                          C.POINTER(_vp)], C.c_int),
+    "yk_program_get": ([_vp, C.POINTER(_vp), C.POINTER(_vp), C.POINTER(C.c_int64)], C.c_int),
+    "yk_program_destroy": ([_vp], C.c_int),
+    "yk_model_load_weights": ([_vp, C.POINTER(Weights), C.c_char, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                               C.POINTER(_vp)], C.c_int),
     "yk_bt_create": ([_vp, C.c_int, C.POINTER(BtCfg), C.POINTER(_vp)], C.c_int),
     "yk_bt_destroy": ([_vp], C.c_int),
     "yk_bt_reset": ([_vp, _vp], C.c_int),

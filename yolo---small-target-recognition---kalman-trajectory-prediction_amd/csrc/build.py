@@ -25,13 +25,15 @@ REPO = os.path.dirname(PKG)
 # its own object directory; the product library is never built with extra defines
 DEFINES = os.environ.get("YK_DEFINES", "").split()
 OUT = os.environ.get("YK_OUT") or os.path.join(PKG, "libyk_diag.so" if DEFINES else "libyk.so")
-BUILD = os.path.join(HERE, "_build_diag" if DEFINES else "_build")
+BUILD = os.path.join(HERE, ("_build_diag_" + hashlib.sha1(" ".join(DEFINES).encode()).hexdigest()[:8]) if DEFINES
+                     else "_build")
 ARCH = os.environ.get("YK_OFFLOAD_ARCH", "gfx950")
 
 # (source, extra flags).  The tracker must not contract a*b+c into FMA: it reproduces
 # numpy's separately rounded float64 arithmetic (see tracker.hip header).
 SOURCES = [
     ("yk_capi.cpp", []),
+    ("program.cpp", []),
     ("tracker.hip", ["-ffp-contract=off"]),
     ("detector.hip", []),
     ("bytetrack.hip", ["-ffp-contract=off"]),

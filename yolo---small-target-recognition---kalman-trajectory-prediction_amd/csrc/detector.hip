@@ -1621,11 +1621,14 @@ __global__ void __launch_bounds__(64 * NW) conv_wide_kernel(WideArgs a) {
 // its 4 channels twice, XA = [x0(e0..3) | x1(e0..3)] and XB = [x0(e0..3) | x2(e0..3)], against
 // weight fragments A1 = [w0 | w0], A2 = [w1 | w1], A3 = [w2 | w0]: A1.XA + A2.XA + A3.XB = the six
 // products of F32S (w0x0 + w0x1 + w1x0 + w1x1 + w2x0 + w0x2), three MFMAs per fragment pair.
-// K order: chunk of 16 channels major, tap minor (step s = chunk * k*k + tap).
-// LDS: two chunk buffers x 8 planes (XA / XB x kg) x kHaloPx pixels x 16 B.  Plane bases are
-// multiples of 256 B, so the 16 consecutive pixels of a fragment row fall on 16 different
-// 4-bank groups (ds_read_b128 conflict-free).  One barrier per chunk: chunk c + 1's global loads
-// are in flight over chunk c's MFMAs, then split and written to the other buffer.
+// K order: 16-channel group major, tap minor (step s = group * k*k + tap).
+// LDS: two chunk buffers of 32 KiB; a chunk is one 16-channel group of the window (3x3: 8 planes
+// XA / XB x kg of kHaloPx pixels x 16 B) or four of them (1x1, no halo: 32 planes of kHaloPx / 4
+// pixels).  Plane bases are multiples of 256 B, so the 16 consecutive pixels of a fragment row
+// fall on 16 different 4-bank groups (ds_read_b128 conflict-free).  One barrier per chunk: chunk
+// c + 1's global loads are in flight over chunk c's MFMAs, then split and written to the other
+// buffer.  Within a chunk each step's B operands are read one step ahead and the weight
+// fragments D steps ahead (a ring of D register slots).
 // Wave layout: WM = 0, the four waves split the tile's pixels (NPT fragments each) and share
 // NE output-channel tiles; WM = 1, they share all NPT fragments and own NE tiles each.
 struct HaloArgs {
@@ -1633,9 +1636,14 @@ struct HaloArgs {
   unsigned arena_bytes;
   unsigned soff0, soff1;  // byte offsets of the two source views (image b0, channel coff)
   int h0, w0, cs0, up0, h1, w1, cs1, up1;
-  int c0, cin, n_chunks;
+  int c0, cin;
   int stride, pad, in_h, in_w, out_h, out_w;
   int tr, tc, twin, npx, tiles_x, tiles_y;  // output tile rows x cols, input window width, pixels
+  int rp;  // LDS row pitch of the window (pixels): rp = tc (mod 16) (stride 1) or 2 rp = tc (mod 16)
+           // (stride 2), so a fragment's 16 pixels fall on 16 consecutive 4-bank groups wherever
+           // its rows break
+  int hw;  // stride 2: the window's even columns are stored first (hw of them), then the odd
+           // ones, so the pixels one tap reads are consecutive in LDS
   const void* wblob;  // K-slot weights: byte offset woff, [n_tiles][n_chunks * k * k][64][48 B]
   unsigned wbytes, woff;
   const float* bias;
@@ -1647,6 +1655,9 @@ struct HaloArgs {
   int act;
   int xcd;
 };
+#ifndef YK_HALO_DIAG
+#define YK_HALO_DIAG 0  // diagnostic builds only (csrc/build.py YK_DEFINES): 1 no weight loads, 2 no staging, 4 no LDS reads
+#endif
 constexpr int kHaloPx = 256;                                 // pixels per LDS plane
 constexpr int kHaloPlaneB = kHaloPx * 16;                    // bytes per plane
 constexpr size_t kHaloLds = (size_t)2 * 8 * kHaloPlaneB;     // 64 KiB: two workgroups per CU
@@ -1672,8 +1683,14 @@ __device__ __forceinline__ void split_kslot(const uint4& x, u32x4v& xa, u32x4v& 
 template <int NE, int NPT, int WM, int KS>
 __global__ void __launch_bounds__(256) conv_halo_kernel(HaloArgs a) {
   constexpr int T = KS * KS;
-  constexpr int UPT = kHaloPx * 4 / 256;  // staging units (pixel, channel group) per thread
-  constexpr int BUF = 8 * kHaloPlaneB;
+  constexpr int CC = KS == 1 ? 4 : 1;   // 16-channel groups staged per chunk (1x1: no halo, 4 groups)
+  constexpr int PXC = kHaloPx / CC;     // pixels per plane
+  constexpr int PLB = PXC * 16;         // bytes per plane
+  constexpr int S = CC * T;             // K steps per chunk
+  constexpr int D = KS == 3 ? 3 : 2;    // weight-fragment ring: step s + D loads over step s
+  constexpr int BUF = 8 * CC * PLB;     // one chunk buffer (kHaloLds / 2)
+  constexpr int UPT = 4;                // staging units per thread: 1024 = 4 kg x kHaloPx per chunk
+  static_assert(S % D == 0, "the ring slot of a chunk's first step is 0");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1685,9 +1702,11 @@ __global__ void __launch_bounds__(256) conv_halo_kernel(HaloArgs a) {
   const int oy0 = tyi * a.tr, ox0 = txi * a.tc;
   const int iy0 = oy0 * a.stride - a.pad, ix0 = ox0 * a.stride - a.pad;
   const int nt0 = (blk.y * (WM ? 4 : 1) + (WM ? wave : 0)) * NE;
+  const int n_groups = (a.cin + 15) >> 4, nsteps = n_groups * T;
+  const int n_chunks = (n_groups + CC - 1) / CC;
   const __amdgpu_buffer_rsrc_t xr = make_srd(a.arena, a.arena_bytes);
   const __amdgpu_buffer_rsrc_t wr = make_srd(a.wblob, a.wbytes);
-  // the lane's pixel of each fragment: LDS byte offset of its window origin in plane XA(kg)
+  // the lane's pixel of each fragment: LDS byte offset of its window origin in plane XA(g 0, kg)
   unsigned lb[NPT];
   int opx[NPT];  // output pixel index, -1 outside the image / tile
 #pragma unroll
@@ -1696,24 +1715,26 @@ __global__ void __launch_bounds__(256) conv_halo_kernel(HaloArgs a) {
     const int q = f * 16 + col;
     const int ty = q / a.tc, tx = q - ty * a.tc;
     const bool v = q < a.tr * a.tc && oy0 + ty < a.out_h && ox0 + tx < a.out_w;
-    lb[t] = (unsigned)(kg * kHaloPlaneB + (v ? (ty * a.stride * a.twin + tx * a.stride) * 16 : 0));
+    lb[t] = (unsigned)(kg * PLB + (v ? (ty * a.stride * a.rp + tx) * 16 : 0));
     opx[t] = v ? (b * a.out_h + oy0 + ty) * a.out_w + ox0 + tx : -1;
   }
-  // staging units: pixel px = (tid & 15) + 16 (tid >> 6) + 64 j of the window, channel group
-  // kgu = (tid >> 4) & 3 -- eight lanes of a ds_write_b128 group write 8 consecutive pixels of
-  // one plane (conflict-free)
+  // staging unit j of a thread: channel group kgu = (tid >> 4) & 3, window pixel px = (tid & 15)
+  // + 16 (tid >> 6) (+ 64 j with one 16-channel group per chunk; with four, group j) -- the eight
+  // lanes of a ds_write_b128 group write 8 consecutive pixels of one plane (conflict-free)
   const int kgu = (tid >> 4) & 3;
   unsigned sv0[UPT], sv1[UPT];
   int sl[UPT];
 #pragma unroll
   for (int j = 0; j < UPT; ++j) {
-    const int px = (tid & 15) + 16 * (tid >> 6) + 64 * j;
+    const int px = (tid & 15) + 16 * (tid >> 6) + (CC == 1 ? 64 * j : 0);
+    const int g = CC == 1 ? 0 : j;
     sl[j] = -1;
     sv0[j] = sv1[j] = kOOB;
     if (px < a.npx) {
       const int py = px / a.twin, pxx = px - py * a.twin;
       const int iy = iy0 + py, ix = ix0 + pxx;
-      sl[j] = kgu * kHaloPlaneB + px * 16;
+      const int cx = a.hw ? ((pxx & 1) ? a.hw + (pxx >> 1) : (pxx >> 1)) : pxx;
+      sl[j] = (g * 8 + kgu) * PLB + (py * a.rp + cx) * 16;
       if (iy >= 0 && iy < a.in_h && ix >= 0 && ix < a.in_w) {
         sv0[j] = a.soff0 + (unsigned)(((b * a.h0 + (iy >> a.up0)) * a.w0 + (ix >> a.up0)) * a.cs0 * 4);
         sv1[j] = a.soff1 + (unsigned)(((b * a.h1 + (iy >> a.up1)) * a.w1 + (ix >> a.up1)) * a.cs1 * 4);
@@ -1722,16 +1743,17 @@ __global__ void __launch_bounds__(256) conv_halo_kernel(HaloArgs a) {
   }
   uint4 st[UPT];
   auto fetch = [&](int c) {
-    const int ch = c * 16 + kgu * 4;
-    const bool s1 = ch >= a.c0, cv = ch < a.cin;
-    const unsigned co = (unsigned)((s1 ? ch - a.c0 : ch) * 4);
+    if constexpr ((YK_HALO_DIAG & 2) != 0) return;  // diagnostic: no staging
 #pragma unroll
     for (int j = 0; j < UPT; ++j) {
+      const int ch = (c * CC + (CC == 1 ? 0 : j)) * 16 + kgu * 4;
+      const bool s1 = ch >= a.c0, cv = ch < a.cin;
       const unsigned o = s1 ? sv1[j] : sv0[j];
-      st[j] = bload(xr, cv && o != kOOB ? o + co : kOOB, 0);
+      st[j] = bload(xr, cv && o != kOOB ? o + (unsigned)((s1 ? ch - a.c0 : ch) * 4) : kOOB, 0);
     }
   };
   auto commit = [&](int buf) {
+    if constexpr ((YK_HALO_DIAG & 2) != 0) return;
     unsigned char* base = smem + buf * BUF;
 #pragma unroll
     for (int j = 0; j < UPT; ++j)
@@ -1739,10 +1761,9 @@ __global__ void __launch_bounds__(256) conv_halo_kernel(HaloArgs a) {
         u32x4v xa, xb;
         split_kslot(st[j], xa, xb);
         *(u32x4v*)(base + sl[j]) = xa;
-        *(u32x4v*)(base + 4 * kHaloPlaneB + sl[j]) = xb;
+        *(u32x4v*)(base + 4 * PLB + sl[j]) = xb;
       }
   };
-  const int nsteps = a.n_chunks * T;
   unsigned wo[NE];
 #pragma unroll
   for (int i = 0; i < NE; ++i) {
@@ -1752,9 +1773,29 @@ __global__ void __launch_bounds__(256) conv_halo_kernel(HaloArgs a) {
   auto wload3 = [&](int s, WK3* w) {
 #pragma unroll
     for (int i = 0; i < NE; ++i) {
+      if constexpr ((YK_HALO_DIAG & 1) != 0) {  // diagnostic: no weight loads
+        const unsigned v = wo[i] ^ (unsigned)s;
+        w[i].a1 = u32x4v{v, v + 1u, v + 2u, v + 3u};
+        w[i].a2 = u32x4v{v + 4u, v, v + 5u, v};
+        w[i].a3 = u32x4v{v, v + 7u, v, v + 9u};
+        continue;
+      }
       w[i].a1 = __builtin_amdgcn_raw_buffer_load_b128(wr, (int)wo[i], s * 64 * 48, 0);
       w[i].a2 = __builtin_amdgcn_raw_buffer_load_b128(wr, (int)wo[i] + 16, s * 64 * 48, 0);
       w[i].a3 = __builtin_amdgcn_raw_buffer_load_b128(wr, (int)wo[i] + 32, s * 64 * 48, 0);
+    }
+  };
+  // B operands of step k of a chunk (group k / T, tap k % T) from buffer xs
+  auto read_ops = [&](const unsigned char* xs, int k, u32x4v* xa, u32x4v* xb) {
+    const int g = k / T, t = k - g * T;
+    const int dy = t / KS, dx = t - dy * KS;
+    const int cdx = a.hw ? ((dx & 1) ? a.hw + (dx >> 1) : (dx >> 1)) : dx;
+    const unsigned toff = (unsigned)((dy * a.rp + cdx) * 16);
+#pragma unroll
+    for (int f = 0; f < NPT; ++f) {
+      const unsigned char* p = xs + g * 8 * PLB + lb[f] + toff;
+      xa[f] = *(const u32x4v*)p;
+      xb[f] = *(const u32x4v*)(p + 4 * PLB);
     }
   };
   f32x4 acc[NE][NPT];
@@ -1762,53 +1803,46 @@ __global__ void __launch_bounds__(256) conv_halo_kernel(HaloArgs a) {
   for (int i = 0; i < NE; ++i)
 #pragma unroll
     for (int t = 0; t < NPT; ++t) acc[i][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  WK3 wb[2][NE];
+  WK3 wb[D][NE];
+  u32x4v xa[2][NPT], xb[2][NPT];
   fetch(0);
-  wload3(0, wb[0]);
+#pragma unroll
+  for (int d = 0; d < D; ++d)
+    if (d < nsteps) wload3(d, wb[d]);
   commit(0);
   __syncthreads();
-  // step s = c * T + t uses weight slot s & 1 = (t + P) & 1 with P = the parity of c * T (a
-  // compile-time index: chunks run in pairs); step s + 1's weights load over step s's MFMAs
-  auto chunk = [&](int c, auto par) {
-    constexpr int P = decltype(par)::value;
-    const bool more = c + 1 < a.n_chunks;
-    if (more) fetch(c + 1);
+  for (int c = 0; c < n_chunks; ++c) {
+    const bool more = c + 1 < n_chunks;
+    if (more) fetch(c + 1);  // in flight over this chunk's MFMAs
     const unsigned char* xs = smem + (c & 1) * BUF;
+    const int s0 = c * S;
+    read_ops(xs, 0, xa[0], xb[0]);
 #pragma unroll
-    for (int t = 0; t < T; ++t) {
-      const int s = c * T + t;
-      if (s + 1 < nsteps) wload3(s + 1, wb[(t + P + 1) & 1]);
-      const int dy = t / KS, dx = t - dy * KS;
-      const unsigned toff = (unsigned)((dy * a.twin + dx) * 16);
-      u32x4v xa[NPT], xb[NPT];
+    for (int k = 0; k < S; ++k) {
+      const int s = s0 + k;
+      if (s < nsteps) {  // (a 1x1 conv's last chunk may hold fewer than CC groups)
+        if (k + 1 < S && s + 1 < nsteps) read_ops(xs, k + 1, xa[(k + 1) & 1], xb[(k + 1) & 1]);
+        const WK3* w = wb[k % D];
+        const u32x4v* ca = xa[k & 1];
+        const u32x4v* cb = xb[k & 1];
 #pragma unroll
-      for (int f = 0; f < NPT; ++f) {
-        xa[f] = *(const u32x4v*)(xs + lb[f] + toff);
-        xb[f] = *(const u32x4v*)(xs + 4 * kHaloPlaneB + lb[f] + toff);
+        for (int f = 0; f < NPT; ++f)
+#pragma unroll
+          for (int i = 0; i < NE; ++i) acc[i][f] = mfma_bf16(w[i].a1, ca[f], acc[i][f]);
+#pragma unroll
+        for (int f = 0; f < NPT; ++f)
+#pragma unroll
+          for (int i = 0; i < NE; ++i) acc[i][f] = mfma_bf16(w[i].a2, ca[f], acc[i][f]);
+#pragma unroll
+        for (int f = 0; f < NPT; ++f)
+#pragma unroll
+          for (int i = 0; i < NE; ++i) acc[i][f] = mfma_bf16(w[i].a3, cb[f], acc[i][f]);
+        if (s + D < nsteps) wload3(s + D, wb[k % D]);
       }
-      const WK3* w = wb[(t + P) & 1];
-#pragma unroll
-      for (int f = 0; f < NPT; ++f)
-#pragma unroll
-        for (int i = 0; i < NE; ++i) acc[i][f] = mfma_bf16(w[i].a1, xa[f], acc[i][f]);
-#pragma unroll
-      for (int f = 0; f < NPT; ++f)
-#pragma unroll
-        for (int i = 0; i < NE; ++i) acc[i][f] = mfma_bf16(w[i].a2, xa[f], acc[i][f]);
-#pragma unroll
-      for (int f = 0; f < NPT; ++f)
-#pragma unroll
-        for (int i = 0; i < NE; ++i) acc[i][f] = mfma_bf16(w[i].a3, xb[f], acc[i][f]);
     }
     if (more) commit((c + 1) & 1);
     __syncthreads();
-  };
-  int c = 0;
-  for (; c + 2 <= a.n_chunks; c += 2) {
-    chunk(c, std::integral_constant<int, 0>{});
-    chunk(c + 1, std::integral_constant<int, (T & 1)>{});
   }
-  if (c < a.n_chunks) chunk(c, std::integral_constant<int, 0>{});
 #pragma unroll
   for (int i = 0; i < NE; ++i) {
     const int nt = nt0 + i;
@@ -3313,7 +3347,6 @@ void set_halo_attr_n() {
 void set_tile_attrs() {
   set_halo_attr_n<1>();
   set_halo_attr_n<2>();
-  set_halo_attr_n<4>();
   set_tile_attrs_t<BF16>();
   set_tile_attrs_t<F32>();
   set_wide_attr_n<BF16, 2>();
@@ -3343,7 +3376,7 @@ enum { CK_DIRECT = 0, CK_TILE = 1, CK_SPLITK = 2, CK_FAST = 3, CK_WIDE = 4, CK_H
 // CK_FAST plan npt bit: the F32 build's op runs the F32S split-MFMA body (every mode)
 constexpr int kSplitBit = 64;
 // CK_WIDE plan: nnt in {2, 4} (output-channel tiles per workgroup), npt unused
-// CK_HALO plan (F32 build): nnt = NE in {1, 2, 4}, npt = NPT | WM << 4 with NPT in {1, 2, 4}
+// CK_HALO plan (F32 build): nnt = NE in {1, 2}, npt = NPT | WM << 4 with NPT in {1, 2, 4}
 // CK_FAST plan: nnt in {1, 2, 3, 4}, npt = NPT | (WS << 4) with NPT in {1, 2, 4}
 struct ConvPlan {
   int kind = CK_DIRECT, nnt = 0, npt = 0;
@@ -3412,7 +3445,7 @@ WidePlan wide_plan(const yk_op& op, int esz, int nnt, int nw = 4) {
 // (pixels x taps) + staging (window pixels).  Sources: 4-channel groups never straddle the two.
 struct HaloPlan {
   bool ok = false;
-  int tr = 0, tc = 0, twin = 0, npx = 0, tiles_x = 0, tiles_y = 0;
+  int tr = 0, tc = 0, twin = 0, npx = 0, tiles_x = 0, tiles_y = 0, rp = 0, hw = 0;
 };
 HaloPlan halo_plan(const yk_op& op, int npt, int wm) {
   HaloPlan h;
@@ -3424,7 +3457,10 @@ HaloPlan halo_plan(const yk_op& op, int npt, int wm) {
   for (int tc = 1; tc <= op.out_w && tc <= px; ++tc) {
     const int tr = std::min(px / tc, op.out_h);
     const int twin = (tc - 1) * s + k, thin = (tr - 1) * s + k;
-    if (twin * thin > kHaloPx) continue;
+    int rp = twin;  // stride 1: rp = tc (mod 16); stride 2 (even tc): 2 rp = tc (mod 16)
+    if (s == 1) rp = twin + (((tc - twin) % 16) + 16) % 16;
+    else if (s == 2 && tc % 2 == 0) rp = twin + (((tc / 2 - twin) % 8) + 8) % 8;
+    if (rp * thin > kHaloPx / (k == 1 ? 4 : 1)) continue;  // a plane (1x1: four 16-channel groups per chunk)
     const long tiles = (long)((op.out_h + tr - 1) / tr) * ((op.out_w + tc - 1) / tc);
     const long cost = tiles * (4L * k * k * px + twin * thin);
     if (best < 0 || cost < best) {
@@ -3433,6 +3469,8 @@ HaloPlan halo_plan(const yk_op& op, int npt, int wm) {
       h.tc = tc;
       h.twin = twin;
       h.npx = twin * thin;
+      h.rp = rp;
+      h.hw = s == 2 ? (twin + 1) / 2 : 0;
       h.tiles_x = (op.out_w + tc - 1) / tc;
       h.tiles_y = (op.out_h + tr - 1) / tr;
     }
@@ -3624,8 +3662,7 @@ void launch_halo_p(const HaloArgs& a, int B, int npt, int wm, int ks, hipStream_
 }
 void launch_halo(const HaloArgs& a, int B, const ConvPlan& p, int ks, hipStream_t st) {
   const int npt = p.npt & 15, wm = (p.npt >> 4) & 1;
-  if (p.nnt == 4) launch_halo_p<4>(a, B, npt, wm, ks, st);
-  else if (p.nnt == 2) launch_halo_p<2>(a, B, npt, wm, ks, st);
+  if (p.nnt == 2) launch_halo_p<2>(a, B, npt, wm, ks, st);
   else launch_halo_p<1>(a, B, npt, wm, ks, st);
 }
 
@@ -3788,7 +3825,6 @@ int launch_op(yk_model* m, const yk_op& op, const uint8_t* frames, int B, float 
             h.up1 = a.src[1].up;
             h.c0 = a.c0;
             h.cin = a.cin;
-            h.n_chunks = (a.cin + 15) / 16;
             h.stride = a.stride;
             h.pad = a.pad;
             h.in_h = a.in_h;
@@ -3799,6 +3835,8 @@ int launch_op(yk_model* m, const yk_op& op, const uint8_t* frames, int B, float 
             h.tc = hp.tc;
             h.twin = hp.twin;
             h.npx = hp.npx;
+            h.rp = hp.rp;
+            h.hw = hp.hw;
             h.tiles_x = hp.tiles_x;
             h.tiles_y = hp.tiles_y;
             h.wblob = m->wkslot;
@@ -4730,9 +4768,9 @@ int yk_model_profile(yk_model* m, const uint8_t* frames, int batch, float conf, 
 int yk_model_set_plan(yk_model* m, int op_index, int batch, int kind, int nnt, int npt) {
   YK_CHECK_ARG(m && op_index >= -1 && op_index < (int)m->ops.size(), "yk_model_set_plan: bad op index");
   YK_CHECK_ARG(kind >= -1 && kind <= CK_HALO, "yk_model_set_plan: kind must be -1 (heuristic), 0, 1, 2, 3, 4 or 5");
-  YK_CHECK_ARG(kind != CK_HALO || (m->wkslot && (nnt == 1 || nnt == 2 || nnt == 4) &&
+  YK_CHECK_ARG(kind != CK_HALO || (m->wkslot && (nnt == 1 || nnt == 2) &&
                                    ((npt & 15) == 1 || (npt & 15) == 2 || (npt & 15) == 4) && (npt & ~31) == 0),
-               "yk_model_set_plan: halo conv (kind 5) needs the fp32 build, nnt in {1, 2, 4}, npt in {1, 2, 4} (+16: "
+               "yk_model_set_plan: halo conv (kind 5) needs the fp32 build, nnt in {1, 2}, npt in {1, 2, 4} (+16: "
                "waves split output channels)");
   YK_CHECK_ARG(kind != CK_WIDE || ((nnt == 2 || nnt == 4) && (npt == 0 || npt == 4 || npt == 8)),
                "yk_model_set_plan: wide conv nnt must be 2 or 4, npt (waves) 0, 4 or 8");
@@ -4817,7 +4855,7 @@ int yk_model_autotune(yk_model* m, const uint8_t* frames, int batch, float conf,
           }
     if (m->wkslot && m->wk_off[i] >= 0 && m->autotune_split)
       for (int wm = 0; wm < 2; ++wm)
-        for (int ne : {1, 2, 4})
+        for (int ne : {1, 2})
           for (int npt : {1, 2, 4}) {
             const int per = ne * (wm ? 4 : 1), groups = (op.n_tiles + per - 1) / per;
             if (per > 1 && 4 * op.n_tiles < 3 * groups * per) continue;

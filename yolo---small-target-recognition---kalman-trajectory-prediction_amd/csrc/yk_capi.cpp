@@ -42,6 +42,7 @@ int64_t yk_struct_size(int which) {
     case 7: return (int64_t)sizeof(yk_bt_cfg);
     case 8: return (int64_t)sizeof(yk_motion);
     case 9: return (int64_t)sizeof(yk_gmd_stats);
+    case 10: return (int64_t)sizeof(yk_tensor);
     default: return -1;
   }
 }

@@ -463,11 +463,27 @@ class EngineModel:
     """A model created from an engine file by the library itself (yk_model_load): no Program on
     the Python side; frame size and batch come from the file."""
 
-    def __init__(self, path: str, device: int = 0):
+    def __init__(self, path: str | None, device: int = 0, _handle=None):
         self.device = int(device)
+        if _handle is not None:
+            self._h = _handle
+            return
         h = C.c_void_p()
         L.check(L.lib().yk_model_load(L.context(self.device), str(path).encode(), C.byref(h)), "yk_model_load")
         self._h = h
+
+    @classmethod
+    def from_state_dict(cls, sd: dict, scale: str, dtype: str, frame_h: int, frame_w: int, imgsz: int = 640,
+                        max_batch: int = 8, device: int = 0):
+        """The detector built by the library from a raw fp32 state dict (yk_model_load_weights:
+        parse_model rules, BN fold and packing in C++, csrc/program.cpp) -- no Program."""
+        w, keep = L.weights_struct(sd)
+        h = C.c_void_p()
+        L.check(L.lib().yk_model_load_weights(L.context(int(device)), C.byref(w), str(scale)[:1].encode(), ACT[dtype],
+                                              int(frame_h), int(frame_w), int(imgsz), int(max_batch), C.byref(h)),
+                "yk_model_load_weights")
+        del keep
+        return cls(None, device, _handle=h)
 
     def __del__(self):
         h = getattr(self, "_h", None)

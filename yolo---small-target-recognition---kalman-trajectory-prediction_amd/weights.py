@@ -118,12 +118,23 @@ def _plant(sd, ar, box_bins, gain, thr, dog):
         sd[f"model.{d}.cv2.{lvl}.2.bias"][:] = logit.repeat(4)
 
 
+def _sqrt_f32(x: torch.Tensor) -> torch.Tensor:
+    """IEEE (correctly rounded) float32 square root.  torch.sqrt on the CPU goes through MKL's
+    vector math here, which misrounds ~0.6% of float32 inputs by one ulp; the C-ABI builder
+    (csrc/program.cpp) uses sqrtf, so both hosts fold identical weights."""
+    import numpy as np
+
+    return torch.from_numpy(np.sqrt(x.detach().cpu().numpy().astype(np.float32)))
+
+
 def fuse_conv_bn(w: torch.Tensor, gamma, beta, mean, var, eps: float = BN_EPS):
     """fuse_conv_and_bn (torch_utils.py:255-286) in float32: W' = diag(g/sqrt(eps+var)) W,
-    b' = beta - g*mean/sqrt(var+eps) (the conv has no bias)."""
-    scale = gamma.div(torch.sqrt(eps + var))
+    b' = beta - g*mean/sqrt(var+eps) (the conv has no bias).  Every step is one correctly rounded
+    float32 operation (the sqrt included, see _sqrt_f32)."""
+    sq = _sqrt_f32(var + eps)
+    scale = gamma.div(sq)
     wf = (w.reshape(w.shape[0], -1) * scale[:, None]).reshape(w.shape)
-    bf = beta - gamma.mul(mean).div(torch.sqrt(var + eps))
+    bf = beta - gamma.mul(mean).div(sq)
     return wf, bf
 
 
@@ -138,3 +149,25 @@ def fused_convs(sd: dict, ar: A.Arch) -> dict:
             w, b = sd[f"{p}.weight"].float(), sd[f"{p}.bias"].float()
         out[p] = (w.contiguous(), b.contiguous(), k, s, bn)
     return out
+
+
+def save_raw(path: str, sd: dict) -> None:
+    """The state dict as a raw fp32 file for the C-ABI builder (yk_model_load_weights via
+    examples/c_host.c): b"YKWTS\\0\\0\\0", int32 version 1, int32 n, then per floating tensor int32
+    name length, name, int32 ndim, int64 shape[ndim], float32 data (C order), little-endian."""
+    import struct
+
+    import numpy as np
+
+    items = []
+    for k, v in sd.items():
+        a = v.detach().cpu().float().numpy() if hasattr(v, "detach") else np.asarray(v)
+        if a.dtype.kind == "f" and a.ndim <= 4:
+            items.append((k, np.ascontiguousarray(a, dtype="<f4")))
+    with open(path, "wb") as f:
+        f.write(b"YKWTS\0\0\0" + struct.pack("<ii", 1, len(items)))
+        for k, a in items:
+            name = k.encode()
+            f.write(struct.pack("<i", len(name)) + name + struct.pack("<i", a.ndim))
+            f.write(struct.pack(f"<{a.ndim}q", *a.shape))
+            f.write(a.tobytes())
