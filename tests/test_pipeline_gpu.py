@@ -226,3 +226,72 @@ def test_pipeline_with_global_motion_matches_serial():
         assert m0.tobytes() == m1.tobytes() and ms0.tobytes() == ms1.tobytes()
         for s in range(S):
             assert r0[s][: c0[s]].tobytes() == r1[s][: c1[s]].tobytes()
+
+
+def _pan_scene(seed, F, K=10):
+    """A camera pan (tests/gmd_helpers.py, texture at 0.6 contrast) over K bright 18-px targets
+    that move with the world plus their own drift: the planted detector sees ~2 boxes per
+    target and nothing on the texture, the 50+ px/frame pans trigger the global reset branch,
+    and the targets' screen jumps the per-track motion resets."""
+    from gmd_helpers import camera_sequence
+
+    frames, off = camera_sequence(seed, F, h=512, w=640, whip_at=(8, 16), n_targets=0)
+    rng = np.random.default_rng(seed)
+    pos, vel = rng.uniform([60, 60], [452, 580], (K, 2)), rng.normal(0, 1.5, (K, 2))
+    out = (frames.astype(np.float32) * 0.6 + 20).astype(np.uint8)
+    for f in range(F):
+        for y, x in pos + vel * f - (off[f] - off[0]):
+            y, x = int(y) % 480, int(x) % 600
+            out[f, y:y + 18, x:x + 18] = 240
+    return out
+
+
+@pytest.mark.timeout(600)
+def test_stream_pipeline_global_motion_fp32_matches_oracle_chain():
+    """StreamPipeline(tracker_policy=1, motion_method='optical_flow') at fp32 -- device detector,
+    device GlobalMotionDetector and the motion-reset tracker on the two-launch step -- against the
+    oracle chain per stream and frame.  The detections of every step equal the torch-CPU
+    detector's (oracle/detector_ref.py; counts identical, boxes / scores within 1e-4); the oracle
+    tracker RefCMCMultiTracker(150, 1, 0.1).update(dets, frame) with its own
+    RefGlobalMotionDetector (oracle/cmc_ref.py + oracle/gmd_ref.py) is fed the step's device
+    detections (so a near-tie between two boxes of one target cannot move an association), and
+    every tracker row is held to the motion-reset tests' bars (test_cmc_gpu.compare: decisions
+    and counters identical, floats within 1e-9); global_resets / individual_resets /
+    tracking_recoveries identical, global resets reached."""
+    from oracle.cmc_ref import RefCMCMultiTracker
+    from test_cmc_gpu import compare
+
+    P = pkg()
+    pipeline = importlib.import_module(P.__name__ + ".pipeline")
+    TR = P.tracker
+    S, F = 2, 24
+    seqs = [_pan_scene(90 + s, F) for s in range(S)]
+    pipe = pipeline.StreamPipeline("yolov8s-small.yaml", S, (512, 640), "fp32", seed=0, max_tracks=256,
+                                   tracker_policy=1, motion_method="optical_flow")
+    ar = pipe.prog.ar
+    ref = D.RefDetector(_layers(ar), pipe.prog.sd, P.arch.detect_strides(ar))
+    refs = [RefCMCMultiTracker(150, 1, 0.1) for _ in range(S)]
+    torch.set_num_threads(8)
+    n_rows = 0
+    for t in range(F):
+        fr = [seqs[s][t] for s in range(S)]
+        pipe.run(torch.from_numpy(np.stack(fr)).cuda())
+        pipe.sync()
+        rows, counts, stats = pipe.tracker.download()
+        dd, dc = pipe.dets.cpu().numpy(), pipe.counts.cpu().numpy()
+        want, _ = D.predict(ref, fr)
+        for s in range(S):
+            where = f"frame {t} stream {s}"
+            w = want[s].numpy()
+            assert int(dc[s]) == len(w), where
+            np.testing.assert_allclose(dd[s, : dc[s], :4], w[:, :4], rtol=1e-4, atol=1e-3, err_msg=where)
+            np.testing.assert_allclose(dd[s, : dc[s], 4], w[:, 4], rtol=1e-4, atol=1e-6, err_msg=where)
+            dets = [[b[0], b[1], b[2], b[3], b[4]] for b in dd[s, : dc[s], :5]]
+            rb = refs[s].update(dets, fr[s])
+            ours = [TR._reset_fields(r, TR._row_to_dict(r, TR.track_id_of(r["track_num"]))) for r in rows[s, : counts[s]]]
+            compare(ours, rb, where)
+            for k in ("global_motion_events", "global_resets", "individual_resets", "tracking_recoveries"):
+                assert int(stats[s][k]) == refs[s].stats[k], f"{where} {k}: {int(stats[s][k])} vs {refs[s].stats[k]}"
+            n_rows += len(rb)
+    assert n_rows > 200
+    assert sum(r.stats["global_resets"] for r in refs) >= 2

@@ -635,9 +635,10 @@ __device__ void cmc_after_update(Slot& s, const DT* b) {
 }
 
 // predict() (:287-312): for 10 frames after a reset the returned box's centre is blended from
-// the last history position toward the prediction (the state itself is not changed)
-__device__ void cmc_blend(const Slot& s, double* box) {
-  const int since = s.age - s.last_reset;
+// the last history position toward the prediction (the state itself is not changed).  age: the
+// track's age after that predict (assoc_kernel blends without running it: s.age + 1)
+__device__ void cmc_blend(const Slot& s, double* box, int age) {
+  const int since = age - s.last_reset;
   if (since >= 10 || s.ph_len == 0) return;
   const int li = ring_at<8>(s.ph_head, s.ph_len - 1);
   double w = (double)since / 10.0;
@@ -741,7 +742,7 @@ __device__ void long_term_predict(S& s, int k, double* box, double& conf) {
     kf_predict(s);
     state_to_bbox(s.x, box);
     if constexpr (S::kPol) {
-      if (s.policy) cmc_blend(s, box);  // the subclass's predict()
+      if (s.policy) cmc_blend(s, box, s.age);  // the subclass's predict()
     }
     conf = 1.0;
     return;
@@ -1070,7 +1071,7 @@ __global__ void __launch_bounds__(NT) step_kernel(Dev g, const DT* __restrict__ 
     Slot& sl = slots[order[i]];
     kf_predict(sl);
     state_to_bbox(sl.x, &L.pb[4 * i]);
-    if (POL && sl.policy) cmc_blend(sl, &L.pb[4 * i]);
+    if (POL && sl.policy) cmc_blend(sl, &L.pb[4 * i], sl.age);
   }
   __syncthreads();
   if (tid == 0) g.phase[s * PH + 1] = wall_clock64();
@@ -1469,7 +1470,7 @@ __host__ __device__ inline int assoc_lds_cand(int T, int D, int C) {
   const size_t k = b < LDS_CU ? (LDS_CU - b) / 12 : 0;
   return (int)(k < (size_t)C ? k : (size_t)C);
 }
-__host__ __device__ inline size_t tracks_lds_bytes() { return (size_t)IPB * STAGE_D * 8 + (size_t)IPB * 36 + 16; }
+__host__ __device__ inline size_t tracks_lds_bytes() { return (size_t)IPB * STAGE_D * 8 + (size_t)IPB * 36 + 16 + 16; }
 
 __device__ LdsA carve_a(char* base, int T, int D, int C) {
   LdsA L;
@@ -1533,8 +1534,10 @@ __device__ __forceinline__ int xbin(double x, double x0, double ibw, int nb) {
 
 // Greedy association (multi:134-178) as locally-dominant rounds (header comment) over nc
 // candidates {IoU bits, (d << 16) | t}; inlined once with LDS and once with global operands.
+// rev: among equal IoUs the highest (d, t) first (the motion-reset tracker's reversed sort of
+// (iou, d, t) tuples, motion_compensated_multi_tracker.py:262-270), else the lowest
 __device__ __forceinline__ void assoc_rounds(const LdsA& L, const unsigned long long* ckey, const int* cpid, int nc,
-                                             int D, int n, long long* round_out) {
+                                             int D, int n, long long* round_out, bool rev) {
   const int tid = threadIdx.x;
   for (int round = 0; round <= D + 1; ++round) {
     for (int d = tid; d < D; d += NTA) {
@@ -1567,14 +1570,16 @@ __device__ __forceinline__ void assoc_rounds(const LdsA& L, const unsigned long 
       const int f = cpid[c], d = f >> 16, t = f & 0xffff;
       if (L.det_match[d] < 0 && L.trk_match[t] < 0) {
         const unsigned long long k = ckey[c];
-        if (k == L.row_max[d]) atomicMin(&L.row_arg[d], f);
-        if (k == L.col_max[t]) atomicMin(&L.col_arg[t], f);
+        const int rk = rev ? INT_MAX - f : f;
+        if (k == L.row_max[d]) atomicMin(&L.row_arg[d], rk);
+        if (k == L.col_max[t]) atomicMin(&L.col_arg[t], rk);
       }
     }
     __syncthreads();
     for (int c = tid; c < nc; c += NTA) {
       const int f = cpid[c], d = f >> 16, t = f & 0xffff;
-      if (L.row_arg[d] == f && L.col_arg[t] == f) {
+      const int rk = rev ? INT_MAX - f : f;
+      if (L.row_arg[d] == rk && L.col_arg[t] == rk) {
         L.det_match[d] = t;
         L.trk_match[t] = d;
       }
@@ -1583,9 +1588,10 @@ __device__ __forceinline__ void assoc_rounds(const LdsA& L, const unsigned long 
   }
 }
 
-template <typename DT>
+template <typename DT, int POL>
 __global__ void __launch_bounds__(NTA) assoc_kernel(Dev g, const DT* __restrict__ dets, int row_stride,
-                                                   const int* __restrict__ counts) {
+                                                   const int* __restrict__ counts,
+                                                   const yk_motion* __restrict__ motion) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int s = blockIdx.x, tid = threadIdx.x;
   const int T = g.T;
@@ -1605,8 +1611,22 @@ __global__ void __launch_bounds__(NTA) assoc_kernel(Dev g, const DT* __restrict_
   int Draw = counts[s];
   if (Draw < 0) Draw = 0;
   const int D = Draw < g.D ? Draw : g.D;
-  const int n = H.n_tracks;
+  const int n_old = H.n_tracks;
+  int nfree_base = H.n_free;
+  int greset = 0;
+  if (POL && tid == 0) greset = global_branch(H, motion, s, Draw) ? 1 : 0;
   if (tid < 16) L.misc[tid] = 0;  // counters ([16, 32): wave sums)
+  if (POL) {
+    __syncthreads();
+    if (tid == 0) L.misc[M_GRESET] = greset;
+    __syncthreads();
+    greset = L.misc[M_GRESET];
+    if (greset) {  // _perform_global_reset (:150-169): trackers.clear(), slots back to the stack
+      for (int i = tid; i < n_old; i += NTA) fstack[nfree_base + i] = order[i];
+      nfree_base += n_old;
+    }
+  }
+  const int n = greset ? 0 : n_old;
   for (int i = tid; i < D * 4; i += NTA) {
     const int d = i >> 2, k = i & 3;
     L.det[i] = (double)dets[((size_t)s * g.D + d) * row_stride + k];
@@ -1624,6 +1644,7 @@ __global__ void __launch_bounds__(NTA) assoc_kernel(Dev g, const DT* __restrict_
     for (int c = 0; c < 4; ++c) xp[c] = sl.x[c] + sl.x[c + 4];
     double* b = &L.pb[4 * i];
     state_to_bbox(xp, b);
+    if (POL && sl.policy) cmc_blend(sl, b, sl.age + 1);  // the subclass's predict() box
     const double w = b[2] - b[0];
     if (isfinite(b[0]) && isfinite(b[2]) && isfinite(w)) {
       lx0 = fmin(lx0, b[0]);
@@ -1759,7 +1780,8 @@ __global__ void __launch_bounds__(NTA) assoc_kernel(Dev g, const DT* __restrict_
           const int kk = o < len ? k0 + o : nfin + (o - len);
           const int t = index ? tsorted[kk] : kk;
           const double v = iou_mixed<DT>(db, &L.pb[4 * t]);
-          if (v >= g.thr) {  // enhanced: iou >= thr (multi:245)
+          // enhanced: iou >= thr (multi:245); motion-reset: iou > thr (motion_compensated_multi_tracker.py:260)
+          if (POL ? v > g.thr : v >= g.thr) {
             const int c = atomicAdd(&L.misc[M_NCAND], 1);
             const unsigned long long key = (unsigned long long)__double_as_longlong(v);
             const int f = (d << 16) | t;  // orders like the row-major pair index d * n + t
@@ -1792,7 +1814,7 @@ __global__ void __launch_bounds__(NTA) assoc_kernel(Dev g, const DT* __restrict_
     // LDS head joins the global tail, and the rounds read them where the boxes were (dead now)
     // when they fit there, else from global memory
     if (nc <= L.ccap) {
-      assoc_rounds(L, L.ck, L.cp, nc, D, n, g.phase + s * PH + 10);
+      assoc_rounds(L, L.ck, L.cp, nc, D, n, g.phase + s * PH + 10, POL != 0);
     } else {
       for (int c = tid; c < L.ccap; c += NTA) {
         ckey[c] = L.ck[c];
@@ -1808,9 +1830,9 @@ __global__ void __launch_bounds__(NTA) assoc_kernel(Dev g, const DT* __restrict_
           lp[c] = cflat[c];
         }
         __syncthreads();
-        assoc_rounds(L, lk, lp, nc, D, n, g.phase + s * PH + 10);
+        assoc_rounds(L, lk, lp, nc, D, n, g.phase + s * PH + 10, POL != 0);
       } else {
-        assoc_rounds(L, ckey, cflat, nc, D, n, g.phase + s * PH + 10);
+        assoc_rounds(L, ckey, cflat, nc, D, n, g.phase + s * PH + 10, POL != 0);
       }
     }
   } else if (tid == 0) {  // no pairs: an empty candidate phase, no rounds
@@ -1826,24 +1848,33 @@ __global__ void __launch_bounds__(NTA) assoc_kernel(Dev g, const DT* __restrict_
   // status 1 and time_since_update > 30 (long_term_predictions).
   int* flags = (int*)L.col_max;
   int* newdet = (int*)L.row_max;
+  // A motion-reset update that resets the filter leaves the same counters as the plain update
+  // (cmc_reset: hits + 1, hit_streak + 1, tsu 0), so the decisions hold for both policies; that
+  // tracker reports every live track and counts a deleted tracker that had been reset.
   const int fc = (int)H.st.frame_count + 1;
-  int recov = 0;
+  int recov = 0, trecov = 0;
   int2* items_vh = g.items_vh + (size_t)s * T;
   for (int i = tid; i < n; i += NTA) {
     const Slot& sl = slots[L.order_tmp[i]];
     const bool m = L.trk_match[i] >= 0;
     items_vh[i] = make_int2(sl.vh_len, sl.vh_head);
     const int age = sl.age + 1, tsu = m ? 0 : sl.tsu + 1, hs = m ? sl.hit_streak + 1 : 0;
-    recov += (m && sl.is_lost) ? 1 : 0;
     const bool del = tsu > g.max_lost || (age < 5 && hs == 0 && tsu > 15) || (age < 10 && hs <= 1 && tsu > 30);
-    const bool q = hs >= g.min_hits || fc <= g.min_hits || !m;
-    flags[i] = (del ? 0 : 1) | (q ? 2 : 0) | (tsu > 30 ? 4 : 0);
+    if (POL && sl.policy) {
+      trecov += (del && sl.reset_count > 0) ? 1 : 0;
+      flags[i] = del ? 0 : 3;
+    } else {
+      recov += (m && sl.is_lost) ? 1 : 0;
+      const bool q = hs >= g.min_hits || fc <= g.min_hits || !m;
+      flags[i] = (del ? 0 : 1) | (q ? 2 : 0) | (tsu > 30 ? 4 : 0);
+    }
   }
   if (recov) atomicAdd(&L.misc[M_RECOVER], recov);
+  if (trecov) atomicAdd(&L.misc[M_TRECOV], trecov);
   // new tracks for unmatched detections, ascending detection order (multi:92-101)
   int n_new_total = 0;
   const int next_num = (int)H.st.next_track_id;
-  const int nfree0 = H.n_free;
+  const int nfree0 = nfree_base;
   for (int base = 0; base < D; base += NTA) {
     const int d = base + tid;
     const int flag = (d < D && L.det_match[d] < 0) ? 1 : 0;
@@ -1855,7 +1886,7 @@ __global__ void __launch_bounds__(NTA) assoc_kernel(Dev g, const DT* __restrict_
         L.order_tmp[pos] = fstack[nfree0 - 1 - r];
         newdet[r] = d;
         // a new track: age 0, hit_streak 1, tsu 0, not lost (kf.py:32-101)
-        flags[pos] = 1 | ((1 >= g.min_hits || fc <= g.min_hits) ? 2 : 0);
+        flags[pos] = 1 | ((POL || 1 >= g.min_hits || fc <= g.min_hits) ? 2 : 0);
       } else {
         atomicAdd(&L.misc[M_OVERFLOW], 1);
       }
@@ -1902,17 +1933,19 @@ __global__ void __launch_bounds__(NTA) assoc_kernel(Dev g, const DT* __restrict_
     H.st.frame_count = fc;
     H.st.next_track_id += n_new;
     H.st.total_tracks_created += n_new;
-    H.st.total_tracks_terminated += pushed;
+    H.st.total_tracks_terminated += pushed + (greset ? n_old : 0);
+    H.st.global_resets += greset;
     H.st.current_active_tracks = kept;
     H.st.long_term_predictions += L.misc[M_LONGTERM];
     H.st.successful_recoveries += L.misc[M_RECOVER];
+    H.st.tracking_recoveries += L.misc[M_TRECOV];
     H.st.overflow += L.misc[M_OVERFLOW] + (Draw - D);
     g.counts[s] = nout;
-    g.stats[s] = H.st;
+    g.stats[s] = H.st;  // tracks_kernel adds the step's individual resets to both
   }
 }
 
-template <typename DT>
+template <typename DT, int POL>
 __global__ void __launch_bounds__(NT) tracks_kernel(Dev g, const DT* __restrict__ dets, int row_stride) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int s = blockIdx.y, tid = threadIdx.x;
@@ -1924,14 +1957,14 @@ __global__ void __launch_bounds__(NT) tracks_kernel(Dev g, const DT* __restrict_
   int4* it = (int4*)(smem + (size_t)IPB * STAGE_D * 8);    // [IPB]
   int2* ivh = (int2*)(it + IPB);  // [IPB] {vh_len, vh_head} before the step, then {th_len, th_head} after it
   int* lst = (int*)(ivh + IPB);   // [3][IPB] the block's items by path: update, lost, new
-  int* lcnt = lst + 3 * IPB;      // [3]
+  int* lcnt = lst + 3 * IPB;      // [3] path counts, then [3] the step's motion-reset filter resets
   Slot* slots = g.slots + (size_t)s * g.T;
   if (blockIdx.x == 0 && tid == 0) g.phase[s * PH + 5] = wall_clock64();
   if (tid < m) {
     it[tid] = g.items[(size_t)s * g.T + base + tid];
     ivh[tid] = g.items_vh[(size_t)s * g.T + base + tid];
   }
-  if (tid < 3) lcnt[tid] = 0;
+  if (tid < 4) lcnt[tid] = 0;
   __syncthreads();
   // one path per wave (a wave runs every path its lanes take, one after the other)
   if (tid < m) {
@@ -1960,7 +1993,42 @@ __global__ void __launch_bounds__(NT) tracks_kernel(Dev g, const DT* __restrict_
   if (blockIdx.x == 0 && tid == 0) g.phase[s * PH + 8] = wall_clock64();
   const int wv = tid >> 6, ln = tid & 63;
   const long long cw0 = clock64();
-  if (wv < 3 && ln < lcnt[wv]) {
+  if (POL && wv < 3 && ln < lcnt[wv]) {
+    // the motion-reset tracker on the slot itself (its histories are part of the update)
+    const int j = lst[wv * IPB + ln];
+    const int4 w = it[j];
+    Slot& sl = slots[w.x];
+    DT db[4] = {DT(0), DT(0), DT(0), DT(0)};
+    if (w.y >= 0) {  // (a lost track has no detection)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) db[k] = dets[((size_t)s * g.D + w.y) * row_stride + k];
+    }
+    if (w.z < 0) {
+      kf_predict(sl);  // the subclass's predict() blends only the returned box
+      if (w.y >= 0) {  // MotionResetKalmanTracker.update (:261-285)
+        double val[3] = {0.0, 0.0, 0.0};
+        int why = 0;
+        Num conf{0.0, KPY};
+        if (sl.policy && cmc_decide<DT>(sl, db, val, why, conf)) {
+          cmc_reset<DT>(sl, db, val, why, conf);
+          atomicAdd(&lcnt[3], 1);
+        } else {
+          kf_update<DT>(sl, db, stage + (size_t)j * STAGE_D);
+          if (sl.policy) ph_push(sl, sl.x[0], sl.x[1], false);  // the base update's position_history append
+        }
+        if (sl.policy) cmc_after_update<DT>(sl, db);
+      } else {
+        mark_lost(sl);
+      }
+    } else {
+      double z[4];
+      bbox_to_state<DT>(db, z);
+      slot_init(sl, z, w.z, g.max_lost);
+      cmc_init<DT>(sl, db);
+    }
+    if (w.w >= 0) track_info(sl, g.rows[(size_t)s * g.T + w.w], false);
+    ivh[j] = make_int2(sl.th_len, sl.th_head);
+  } else if (!POL && wv < 3 && ln < lcnt[wv]) {
     const int j = lst[wv * IPB + ln];
     const int4 w = it[j];
     Slot& gs = slots[w.x];
@@ -1991,6 +2059,10 @@ __global__ void __launch_bounds__(NT) tracks_kernel(Dev g, const DT* __restrict_
   }
   if (blockIdx.x == 0 && ln == 0 && wv < 3) g.phase[s * PH + 16 + wv] = clock64() - cw0;
   __syncthreads();
+  if (POL && tid == 0 && lcnt[3]) {  // stats['individual_resets'] of this step
+    atomicAdd((unsigned long long*)&g.hdr[s].st.individual_resets, (unsigned long long)lcnt[3]);
+    atomicAdd((unsigned long long*)&g.stats[s].individual_resets, (unsigned long long)lcnt[3]);
+  }
   if (blockIdx.x == 0 && tid == 0) g.phase[s * PH + 9] = wall_clock64();
   for (int u = tid; u < m * TOUT; u += NT) {
     const int j = u / TOUT, k = u - j * TOUT;
@@ -2092,7 +2164,7 @@ __global__ void track_op_kernel(Dev g, int s, int pos, int op, int arg, const do
     case YK_OP_PREDICT:
       kf_predict(sl);
       state_to_bbox(sl.x, out5);
-      if (sl.policy) cmc_blend(sl, out5);
+      if (sl.policy) cmc_blend(sl, out5, sl.age);
       break;
     case YK_OP_UPDATE: {
       DT b[4];
@@ -2161,7 +2233,7 @@ struct yk_tracker {
   Dev dev;
   size_t lds;
   size_t lds_assoc;
-  bool split;  // enhanced policy on assoc_kernel + tracks_kernel (else one workgroup per stream)
+  bool split;  // assoc_kernel + tracks_kernel (else one workgroup per stream: YK_TRK_SINGLE=1 / LDS)
   yk_track_state* d_snap;
   yk_track_out* d_row1;
   double* d_box;  // [8]: in[4], out[4]
@@ -2240,18 +2312,17 @@ int yk_tracker_create(yk_ctx* ctx, int n_streams, const yk_tracker_cfg* cfg, yk_
   if (t->lds_assoc <= yk::trk::LDS_CU)
     t->lds_assoc = ((t->lds_assoc + 7) & ~(size_t)7) + (size_t)yk::trk::assoc_lds_cand(cfg->max_tracks, cfg->max_dets, g.C) * 12;
   const char* single = getenv("YK_TRK_SINGLE");
-  t->split = cfg->policy == YK_POLICY_ENHANCED && t->lds_assoc <= 160 * 1024 && !(single && single[0] == '1');
+  t->split = t->lds_assoc <= 160 * 1024 && !(single && single[0] == '1');
   if (t->split) {
     const int la = (int)t->lds_assoc, lt = (int)yk::trk::tracks_lds_bytes();
-    if (hipFuncSetAttribute((const void*)yk::trk::assoc_kernel<float>, hipFuncAttributeMaxDynamicSharedMemorySize, la) !=
-            hipSuccess ||
-        hipFuncSetAttribute((const void*)yk::trk::assoc_kernel<double>, hipFuncAttributeMaxDynamicSharedMemorySize, la) !=
-            hipSuccess ||
-        hipFuncSetAttribute((const void*)yk::trk::tracks_kernel<float>, hipFuncAttributeMaxDynamicSharedMemorySize, lt) !=
-            hipSuccess ||
-        hipFuncSetAttribute((const void*)yk::trk::tracks_kernel<double>, hipFuncAttributeMaxDynamicSharedMemorySize, lt) !=
-            hipSuccess)
-      (void)hipGetLastError();
+    const void* ka[] = {(const void*)yk::trk::assoc_kernel<float, 0>, (const void*)yk::trk::assoc_kernel<double, 0>,
+                        (const void*)yk::trk::assoc_kernel<float, 1>, (const void*)yk::trk::assoc_kernel<double, 1>};
+    const void* kt[] = {(const void*)yk::trk::tracks_kernel<float, 0>, (const void*)yk::trk::tracks_kernel<double, 0>,
+                        (const void*)yk::trk::tracks_kernel<float, 1>, (const void*)yk::trk::tracks_kernel<double, 1>};
+    for (int i = 0; i < 4; ++i)
+      if (hipFuncSetAttribute(ka[i], hipFuncAttributeMaxDynamicSharedMemorySize, la) != hipSuccess ||
+          hipFuncSetAttribute(kt[i], hipFuncAttributeMaxDynamicSharedMemorySize, lt) != hipSuccess)
+        (void)hipGetLastError();
   }
   int rc = yk_tracker_reset(t, nullptr);
   if (rc != YK_OK) {
@@ -2301,16 +2372,29 @@ int yk_tracker_step_motion(yk_tracker* t, const void* dets, int dtype, int row_s
     const dim3 g2((t->dev.T + yk::trk::IPB - 1) / yk::trk::IPB, t->S);
     const size_t l2 = yk::trk::tracks_lds_bytes();
     hipStream_t st = (hipStream_t)stream;
+    const yk::trk::Dev& g = t->dev;
     if (dtype == YK_F32) {
-      hipLaunchKernelGGL((yk::trk::assoc_kernel<float>), dim3(t->S), dim3(yk::trk::NTA), t->lds_assoc, st, t->dev,
-                         (const float*)dets, row_stride, counts);
-      hipLaunchKernelGGL((yk::trk::tracks_kernel<float>), g2, dim3(yk::trk::NT), l2, st, t->dev, (const float*)dets,
-                         row_stride);
+      const float* d = (const float*)dets;
+      if (mr) {
+        hipLaunchKernelGGL((yk::trk::assoc_kernel<float, 1>), dim3(t->S), dim3(yk::trk::NTA), t->lds_assoc, st, g, d,
+                           row_stride, counts, motion);
+        hipLaunchKernelGGL((yk::trk::tracks_kernel<float, 1>), g2, dim3(yk::trk::NT), l2, st, g, d, row_stride);
+      } else {
+        hipLaunchKernelGGL((yk::trk::assoc_kernel<float, 0>), dim3(t->S), dim3(yk::trk::NTA), t->lds_assoc, st, g, d,
+                           row_stride, counts, motion);
+        hipLaunchKernelGGL((yk::trk::tracks_kernel<float, 0>), g2, dim3(yk::trk::NT), l2, st, g, d, row_stride);
+      }
     } else {
-      hipLaunchKernelGGL((yk::trk::assoc_kernel<double>), dim3(t->S), dim3(yk::trk::NTA), t->lds_assoc, st, t->dev,
-                         (const double*)dets, row_stride, counts);
-      hipLaunchKernelGGL((yk::trk::tracks_kernel<double>), g2, dim3(yk::trk::NT), l2, st, t->dev, (const double*)dets,
-                         row_stride);
+      const double* d = (const double*)dets;
+      if (mr) {
+        hipLaunchKernelGGL((yk::trk::assoc_kernel<double, 1>), dim3(t->S), dim3(yk::trk::NTA), t->lds_assoc, st, g, d,
+                           row_stride, counts, motion);
+        hipLaunchKernelGGL((yk::trk::tracks_kernel<double, 1>), g2, dim3(yk::trk::NT), l2, st, g, d, row_stride);
+      } else {
+        hipLaunchKernelGGL((yk::trk::assoc_kernel<double, 0>), dim3(t->S), dim3(yk::trk::NTA), t->lds_assoc, st, g, d,
+                           row_stride, counts, motion);
+        hipLaunchKernelGGL((yk::trk::tracks_kernel<double, 0>), g2, dim3(yk::trk::NT), l2, st, g, d, row_stride);
+      }
     }
     YK_HIP(hipGetLastError());
     return YK_OK;
