@@ -47,7 +47,7 @@ int detect_and_track(const char* engine, const unsigned char* frames_dev, int B,
   return 0;
 }
 
-/* Raw state-dict file (weights.save_raw / tools/export_weights.py): "YKWTS\0\0\0", int32
+/* Raw state-dict file (weights.save_raw): "YKWTS\0\0\0", int32
  * version 1, int32 n; per tensor: int32 name length, the name (no NUL), int32 ndim, int64
  * shape[ndim], float32 data (C order).  Little-endian. */
 typedef struct {

@@ -94,6 +94,18 @@ def build_module_tree(ar, sd):
 
 
 def write_checkpoint(path, ar, yaml_dict, sd, half=True):
+    """The stand-in ultralytics modules live in sys.modules only while the file is written, so a
+    later ``from ultralytics import YOLO`` (the compat package) is not shadowed by them."""
+    before = set(sys.modules)
+    try:
+        return _write_checkpoint(path, ar, yaml_dict, sd, half)
+    finally:
+        for k in set(sys.modules) - before:
+            if k == "ultralytics" or k.startswith("ultralytics."):
+                del sys.modules[k]
+
+
+def _write_checkpoint(path, ar, yaml_dict, sd, half):
     C = _fake_classes()
     model = build_module_tree(ar, sd)
     if half:

@@ -1,0 +1,53 @@
+#!/bin/bash
+# Round-3 GPU driver.  STEPS (space separated) picks what runs, in order:
+#   pytest   the whole -m gpu suite
+#   bench    the default bench line (committed plan) with --dump-ops
+#   tune     concurrent autotune of the fp32 plan (all kernel kinds incl. split / halo) -> plan_tuned.json
+#   btuned   bench on plan_tuned.json
+#   trace    rocprofv3 kernel trace + stats of the default bench, cut to the timed window
+#   pmc      FETCH_SIZE / WRITE_SIZE passes of the fp32 build
+#   cmc      the camera-motion-compensation bench line (motion-reset tracker + global motion)
+#   diag     tools/cmc_pipe_diag.py
+# Every GPU step has its own time limit; the first failure ends the script.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+export TMPDIR=/tmp
+O=gpurun_out/${OUT_DIR:-r3}
+mkdir -p $O
+PLAN=${PLAN:-}
+BARGS=${BARGS:-}
+for s in ${STEPS:-pytest bench}; do
+  case $s in
+    pytest)
+      timeout -k 10 900 python -u -m pytest tests -m gpu -v --maxfail=3 --timeout 200 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} > $O/pytest_gpu.log 2>&1 || { echo "pytest failed"; grep -E "FAILED|ERROR|passed|failed" $O/pytest_gpu.log | tail -20; exit 1; }
+      tail -2 $O/pytest_gpu.log ;;
+    bench)
+      timeout -k 10 400 python -u bench.py ${PLAN:+--plan-in $PLAN} $BARGS --dump-ops $O/ops.json > $O/bench.json 2> $O/bench.err || { echo "bench failed"; tail -30 $O/bench.err; exit 1; }
+      cat $O/bench.json ;;
+    tune)
+      timeout -k 10 600 python -u tools/tune_concurrent.py --dtype fp32 --out $O/plan_tuned.json > $O/tune.log 2>&1 || { echo "tune failed"; tail -20 $O/tune.log; exit 1; }
+      tail -1 $O/tune.log ;;
+    btuned)
+      timeout -k 10 300 python -u bench.py --steps 100 --secondary none --no-cpu-baseline --plan-in $O/plan_tuned.json --dump-ops $O/ops_tuned.json > $O/bench_tuned.json 2> $O/bench_tuned.err || { echo "bench tuned failed"; tail -20 $O/bench_tuned.err; exit 1; }
+      python3 -c "import json; d=json.load(open('$O/bench_tuned.json')); print('tuned', d['value'], d['ms_per_step'], d['roofline']['kernel'], d['roofline']['frac'])" ;;
+    trace)
+      timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- python3 -u bench.py ${PLAN:+--plan-in $PLAN} --steps 50 --secondary none --no-cpu-baseline > $O/trace_bench.json 2> $O/trace_bench.err || { echo "trace failed"; tail -20 $O/trace_bench.err; exit 1; }
+      python3 tools/rocprof_window.py $O/trace/run_kernel_trace.csv $O/trace_bench.json > $O/trace_window.json || exit 1
+      rm -f $O/trace/run_kernel_trace.csv
+      echo "trace ok" ;;
+    pmc)
+      B="bench.py ${PLAN:+--plan-in $PLAN} --steps 5 --warmup 2 --preroll 4 --secondary none --no-cpu-baseline --no-profile"
+      timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch -o run -- python3 -u $B > /dev/null 2> $O/pmc_fetch.err || { echo "pmc fetch failed"; tail -5 $O/pmc_fetch.err; exit 1; }
+      timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write -o run -- python3 -u $B > /dev/null 2> $O/pmc_write.err || { echo "pmc write failed"; tail -5 $O/pmc_write.err; exit 1; }
+      python3 tools/pmc_summary.py $O/pmc_fetch/run_counter_collection.csv $O/pmc_write/run_counter_collection.csv $O/pmc_traffic.json
+      rm -f $O/pmc_fetch/run_counter_collection.csv $O/pmc_write/run_counter_collection.csv
+      echo "pmc ok" ;;
+    cmc)
+      timeout -k 10 300 python -u bench.py --tracker motion_reset --gmd --secondary none --no-cpu-baseline > $O/bench_cmc.json 2> $O/bench_cmc.err || { echo "bench cmc failed"; tail -20 $O/bench_cmc.err; exit 1; }
+      cat $O/bench_cmc.json ;;
+    diag)
+      timeout -k 10 300 python -u tools/cmc_pipe_diag.py 3 > $O/cmc_diag.txt 2> $O/cmc_diag.err || { echo "diag failed"; tail -20 $O/cmc_diag.err; exit 1; }
+      grep -v "^   oracle tracks" $O/cmc_diag.txt | head -60 ;;
+    *) echo "unknown step $s"; exit 1 ;;
+  esac
+done
