@@ -5,7 +5,13 @@ them (aircraft_detection_tracking.py:99-106)."""
 import numpy as np
 
 
-def jumpy_sequence(seed: int, K: int = 12, T: int = 160, W: int = 640, H: int = 512, events: bool = True):
+def jumpy_sequence(seed: int, K: int = 12, T: int = 160, W: int = 640, H: int = 512, events: bool = True,
+                   dup: float = 0.0, shuffle: bool = True):
+    """dup: probability that a visible target also yields a second box shifted by 2-8 px (the
+    planted detector's two-boxes-per-target clutter): the association rounds then hold chains
+    of overlapping candidates, and pairs of already matched rows and columns stay candidates
+    in later rounds.  shuffle=False lists the targets in index order (a duplicate right after its
+    box), so detection 0 and the oldest track (list position 0) overlap on most frames."""
     rng = np.random.default_rng(seed)
     pos = rng.uniform([40, 40], [W - 40, H - 40], (K, 2))
     vel = rng.uniform(-2.0, 2.0, (K, 2))
@@ -32,7 +38,7 @@ def jumpy_sequence(seed: int, K: int = 12, T: int = 160, W: int = 640, H: int = 
                 elif u < 0.05:     # occlusion burst
                     hidden[k] = int(rng.integers(1, 25))
         dets = []
-        order = rng.permutation(K)
+        order = rng.permutation(K) if shuffle else np.arange(K)
         for k in order:
             if hidden[k] > 0:
                 hidden[k] -= 1
@@ -41,5 +47,8 @@ def jumpy_sequence(seed: int, K: int = 12, T: int = 160, W: int = 640, H: int = 
             w, h = size[k] * rng.uniform(0.95, 1.05, 2)
             b = np.array([c[0] - w / 2, c[1] - h / 2, c[0] + w / 2, c[1] + h / 2], np.float32)
             dets.append([b[0], b[1], b[2], b[3], np.float32(rng.uniform(0.3, 0.95))])
+            if dup and rng.uniform() < dup:
+                o = (rng.choice([-1, 1], 2) * rng.uniform(2, 8, 2)).astype(np.float32)
+                dets.append([b[0] + o[0], b[1] + o[1], b[2] + o[0], b[3] + o[1], np.float32(rng.uniform(0.3, 0.95))])
         frames.append(dets)
     return frames

@@ -12,6 +12,7 @@ relative (atol 1e-3 px).  The bf16 leg is measured against the same fp32 oracle 
 fraction of (stream, frame) decisions that agree is reported, not asserted bit-identical.
 """
 import json
+import os
 
 import numpy as np
 import pytest
@@ -25,6 +26,7 @@ from oracle.tracker_ref import RefMultiTracker
 pytestmark = pytest.mark.gpu
 
 S, F, TARGETS = 8, 160, 40  # bench.py config 3's streams and targets
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _layers(ar):
@@ -73,6 +75,12 @@ def _run_gpu(dtype, frames):
     pipe = pipeline.StreamPipeline("yolov8s-small.yaml", S, (512, 640), dtype, seed=0, max_tracks=512,
                                    pipelined=True, inflight=4)
     pipe.set_schedule(1, 1)  # bench.py's schedule with 3 forwards in flight
+    # the committed conv plan bench.py loads for this workload (so the kernels under test are the
+    # bench's own: split-bf16 / halo-tile variants included)
+    with open(os.path.join(REPO, "plans", f"s_640x512_i640_b{S}_{dtype}.json")) as f:
+        pl = json.load(f)
+    assert len(pl["plan"]) == len(pipe.prog.ops)
+    pipe.model.load_plan(pl["batch"], pl["plan"])
     fd = frames.cuda()
     pipe.frames.copy_(fd[0])
     pipe.capture(tune=False)

@@ -73,6 +73,17 @@ def test_motion_reset_matches_oracle(seed):
     assert ref.stats["individual_resets"] > 5  # the sequence exercises the reset path
 
 
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_motion_reset_cluttered_detections(seed):
+    """Two overlapping boxes for most targets (the planted detector's clutter): the association
+    rounds run long chains, and a pair whose detection and track were both matched in earlier
+    rounds -- detection 0 with the track at list position 0 among them -- stays a candidate while
+    later rounds still run (the reversed-rank round bookkeeping must not re-match it)."""
+    # seed 1 (101): three frames where the old bookkeeping re-matched pair (0, 0) (checked on the
+    # CPU by simulating the rounds against cmc_greedy)
+    run_pair(jumpy_sequence(100 + seed, K=12, T=90, dup=1.0, shuffle=False))
+
+
 def test_motion_reset_float64_detections_and_deletions():
     frames = [[[float(v) for v in d] for d in f] for f in jumpy_sequence(7, K=8, T=120)]
     run_pair(frames, max_lost=20)

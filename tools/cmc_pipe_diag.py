@@ -50,6 +50,21 @@ def main(F=3, S=2):
         for s in range(S):
             dets = [[b[0], b[1], b[2], b[3], b[4]] for b in dd[s, : dc[s], :5]]
             snap_before = [(trk.track_id, np.asarray(getattr(trk, 'x', [0]))[:4].ravel().tolist()) for trk in refs[s].trackers]
+            if s == 0:  # T001's state on both sides before this update, its predict() box and IoUs
+                import copy
+                from oracle.tracker_ref import ref_iou
+                for trk in refs[s].trackers[:1]:
+                    c = copy.deepcopy(trk)
+                    pb = c.predict()
+                    print(f"   [{t}] oracle T{trk.track_id:03d} age {trk.age} last_reset {trk.last_reset_frame} "
+                          f"x {np.asarray(trk.x).ravel().tolist()} ph {[list(map(float, v)) for v in trk.position_history]} "
+                          f"pred {list(map(float, pb))}")
+                    ious = [(d, float(ref_iou(dt[:4], pb))) for d, dt in enumerate(dets)]
+                    print(f"   [{t}] oracle IoU>0 {[(d, round(v, 6)) for d, v in ious if v > 0]}")
+                snap = pipe.tracker.snapshot(0)
+                for r in snap[:1]:
+                    print(f"   [{t}] device T{int(r['track_num']):03d} (after step) age {int(r['age'])} "
+                          f"last_reset {int(r['last_reset_frame'])} resets {int(r['reset_count'])} x {r['x'].tolist()}")
             rb = refs[s].update(dets, fr[s])
             mi = refs[s].frame_motion_info
             print(f"== frame {t} stream {s}: dets {int(dc[s])}, device motion {motion[s]}, oracle motion {mi}")

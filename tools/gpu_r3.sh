@@ -8,6 +8,7 @@
 #   pmc      FETCH_SIZE / WRITE_SIZE passes of the fp32 build
 #   cmc      the camera-motion-compensation bench line (motion-reset tracker + global motion)
 #   diag     tools/cmc_pipe_diag.py
+#   ab       tools/split_ab.py: committed (split / halo) plan vs the round-2 exact-f32 plan, accuracy vs the oracle
 # Every GPU step has its own time limit; the first failure ends the script.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
@@ -48,6 +49,9 @@ for s in ${STEPS:-pytest bench}; do
     diag)
       timeout -k 10 300 python -u tools/cmc_pipe_diag.py 3 > $O/cmc_diag.txt 2> $O/cmc_diag.err || { echo "diag failed"; tail -20 $O/cmc_diag.err; exit 1; }
       grep -v "^   oracle tracks" $O/cmc_diag.txt | head -60 ;;
+    ab)
+      timeout -k 10 300 python -u tools/split_ab.py --plan plans/s_640x512_i640_b8_fp32.json --plan-exact plans/exp/s_640x512_i640_b8_fp32_exact_r2.json > $O/split_ab.json 2> $O/split_ab.err || { echo "ab failed"; tail -20 $O/split_ab.err; exit 1; }
+      python3 -c "import json; d=json.load(open('$O/split_ab.json')); print({k: d[k] for k in ('exact_total_us','split_total_us')}, json.dumps(d['accuracy']), d['split_vs_exact'])" ;;
     *) echo "unknown step $s"; exit 1 ;;
   esac
 done

@@ -46,6 +46,7 @@ def main():
     ap.add_argument("--batch", type=int, default=8)
     ap.add_argument("--oracle-batch", type=int, default=2)
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--plan-exact", default="", help="plan of the exact leg (default: --plan with the split bit cleared)")
     a = ap.parse_args()
     P = importlib.import_module(PKG)
     M = importlib.import_module(PKG + ".model")
@@ -63,7 +64,12 @@ def main():
     res = {}
     models = {}
     exact = [[k, n, (p & ~SPLIT) if k == 3 else p] for k, n, p in pl["plan"]]
-    for name, plan in (("exact", exact), ("split", split_plan(pl["plan"]))):
+    split = split_plan(pl["plan"])
+    if a.plan_exact:  # two committed plans side by side (the split one as it is)
+        with open(a.plan_exact) as f:
+            exact = json.load(f)["plan"]
+        split = pl["plan"]
+    for name, plan in (("exact", exact), ("split", split)):
         dm = M.DeviceModel(prog)
         dm.load_plan(pl["batch"], plan)
         dets, counts = dm.detect(ft)

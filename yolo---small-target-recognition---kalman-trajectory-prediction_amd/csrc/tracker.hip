@@ -1570,7 +1570,7 @@ __device__ __forceinline__ void assoc_rounds(const LdsA& L, const unsigned long 
       const int f = cpid[c], d = f >> 16, t = f & 0xffff;
       if (L.det_match[d] < 0 && L.trk_match[t] < 0) {
         const unsigned long long k = ckey[c];
-        const int rk = rev ? INT_MAX - f : f;
+        const int rk = rev ? (INT_MAX - 1) - f : f;  // never the INT_MAX "no candidate" sentinel
         if (k == L.row_max[d]) atomicMin(&L.row_arg[d], rk);
         if (k == L.col_max[t]) atomicMin(&L.col_arg[t], rk);
       }
@@ -1578,8 +1578,10 @@ __device__ __forceinline__ void assoc_rounds(const LdsA& L, const unsigned long 
     __syncthreads();
     for (int c = tid; c < nc; c += NTA) {
       const int f = cpid[c], d = f >> 16, t = f & 0xffff;
-      const int rk = rev ? INT_MAX - f : f;
-      if (L.row_arg[d] == rk && L.col_arg[t] == rk) {
+      const int rk = rev ? (INT_MAX - 1) - f : f;
+      // (a detection or track matched in an earlier round keeps the sentinel in its arg slot:
+      // only still-unmatched pairs may take this round's match)
+      if (L.row_arg[d] == rk && L.col_arg[t] == rk && L.det_match[d] < 0 && L.trk_match[t] < 0) {
         L.det_match[d] = t;
         L.trk_match[t] = d;
       }
