@@ -77,6 +77,35 @@ def decisions(tracks):
     return [(d["track_id"], d["status"], d["age"], d["hits"], d["time_since_update"]) for d in tracks]
 
 
+def near_tie_boxes(pred: torch.Tensor, hw, conf: float = 0.25, iou: float = 0.7, rel: float = 1e-5):
+    """NMS near-ties of one image's Detect output [5, A]: candidates (score > conf) that overlap
+    another candidate at IoU > iou (so NMS keeps exactly one of the two) with scores within `rel`
+    of each other.  Two fp32 convolution implementations that differ only in summation order
+    (activations within ~3e-6 of each other, max-normalised) may keep either member of such a
+    pair; returns every member's box clipped to the frame (xyxy, float32 [N, 4])."""
+    s = pred[4]
+    idx = torch.nonzero(s > conf).flatten()
+    if idx.numel() < 2:
+        return np.zeros((0, 4), np.float32)
+    b = pred[:4, idx].T
+    xy = torch.cat((b[:, :2] - b[:, 2:] / 2, b[:, :2] + b[:, 2:] / 2), 1)
+    lt = torch.maximum(xy[:, None, :2], xy[None, :, :2])
+    rb = torch.minimum(xy[:, None, 2:], xy[None, :, 2:])
+    wh = (rb - lt).clamp(min=0)
+    inter = wh[..., 0] * wh[..., 1]
+    area = (xy[:, 2] - xy[:, 0]) * (xy[:, 3] - xy[:, 1])
+    ov = inter / (area[:, None] + area[None] - inter) > iou
+    sc = s[idx]
+    close = (sc[:, None] - sc[None]).abs() <= rel * torch.maximum(sc[:, None], sc[None])
+    m = ov & close
+    m.fill_diagonal_(False)
+    xy = xy[m.any(1)]
+    H, W = hw
+    xy[:, 0::2] = xy[:, 0::2].clamp(0, W)
+    xy[:, 1::2] = xy[:, 1::2].clamp(0, H)
+    return xy.numpy().astype(np.float32)
+
+
 def score_ties(pred: torch.Tensor, conf: float = 0.25) -> int:
     """Exact duplicate scores among the NMS candidates (score > conf) of one image's Detect
     output [5, A]: non_max_suppression's scores.sort (utils/nms.py:264) is unstable on them."""

@@ -45,3 +45,14 @@ def test_cpu_baseline_on_rank0_of_every_world_size():
     assert B.cpu_baseline_seconds(a, 3, 8) == 0
     a.no_cpu_baseline = True
     assert B.cpu_baseline_seconds(a, 0, 1) == 0
+
+
+def test_kernel_peak_prices_split_kernels_on_bf16_rate():
+    """fp32 convs that run on the bf16 matrix cores (F32S bodies, halo-tile kernel) are held to
+    the peak of that instruction mix (dense bf16 / 6), the exact-f32 MFMA kernels to 157.3."""
+    B = _bench()
+    pk, basis = B.kernel_peak("conv_fast_kernel<yk::det::F32S, 3, 4, true, 2>", "fp32")
+    assert abs(pk - 2500.0 / 6) < 1e-9 and "bf16" in basis
+    assert B.kernel_peak("conv_halo_kernel<1, 4, 1, 3>", "fp32")[0] == pk
+    assert B.kernel_peak("conv_fast_kernel<yk::det::F32, 4, 2, false, 2>", "fp32")[0] == 157.3
+    assert B.kernel_peak("conv_fastw_kernel<yk::det::BF16, 4, 2, 2>", "bf16")[0] == 2500.0

@@ -19,13 +19,19 @@ import pytest
 import torch
 
 from conftest import pkg
-from gpu_helpers import StepRecorder, decisions, score_ties, track_dicts
+from gpu_helpers import StepRecorder, decisions, near_tie_boxes, score_ties, track_dicts
 from oracle import detector_ref as D
 from oracle.tracker_ref import RefMultiTracker
 
 pytestmark = pytest.mark.gpu
 
 S, F, TARGETS = 8, 160, 40  # bench.py config 3's streams and targets
+# NMS near-tie: two overlapping candidates (IoU > 0.7) whose scores differ by less than this
+# (relative) -- below the resolution of fp32 convolutions that differ only in summation order
+# (layer activations ~3e-6 apart, max-normalised; tools/split_ab.py)
+TIE_REL = 1e-5
+PLANS = {"exact_r2": "plans/exp/s_640x512_i640_b8_fp32_exact_r2.json",  # round-2 exact-f32 MFMA plan
+         "committed": "plans/s_640x512_i640_b8_fp32.json"}              # bench.py's plan (split-bf16 / halo)
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
@@ -53,21 +59,22 @@ def chain():
     ref = D.RefDetector(_layers(ar), sd, P.arch.detect_strides(ar))
     torch.set_num_threads(_threads())
     trks = [RefMultiTracker(150, 1, 0.1, stable_ties=True, fast_iou=True) for _ in range(S)]
-    dets, tracks, ties = [], [], 0
+    dets, tracks, ties, near = [], [], 0, []
     for t in range(F):
         fr = list(frames[t].numpy())
         want, y = D.predict(ref, fr)
         ties += sum(score_ties(y[s]) for s in range(S))
+        near.append([near_tie_boxes(y[s], fr[s].shape[:2], rel=TIE_REL) for s in range(S)])
         dets.append([w.numpy() for w in want])
         tracks.append([trks[s].update([[b[0], b[1], b[2], b[3], b[4]] for b in want[s][:, :5].numpy()])
                        for s in range(S)])
-    return {"frames": frames, "dets": dets, "tracks": tracks, "nms_score_ties": ties,
+    return {"frames": frames, "dets": dets, "tracks": tracks, "nms_score_ties": ties, "near": near,
             "tie_frames": sum(tr.tie_frames for tr in trks),
             "terminated": sum(tr.stats["total_tracks_terminated"] for tr in trks),
             "live": [len(tr.trackers) for tr in trks]}
 
 
-def _run_gpu(dtype, frames):
+def _run_gpu(dtype, frames, plan=None):
     P = pkg()
     import importlib
 
@@ -77,7 +84,7 @@ def _run_gpu(dtype, frames):
     pipe.set_schedule(1, 1)  # bench.py's schedule with 3 forwards in flight
     # the committed conv plan bench.py loads for this workload (so the kernels under test are the
     # bench's own: split-bf16 / halo-tile variants included)
-    with open(os.path.join(REPO, "plans", f"s_640x512_i640_b{S}_{dtype}.json")) as f:
+    with open(os.path.join(REPO, plan or f"plans/s_640x512_i640_b{S}_{dtype}.json")) as f:
         pl = json.load(f)
     assert len(pl["plan"]) == len(pipe.prog.ops)
     pipe.model.load_plan(pl["batch"], pl["plan"])
@@ -101,50 +108,77 @@ def _run_gpu(dtype, frames):
     return out
 
 
+def _in_boxes(rows, boxes):
+    """every row's box is one of `boxes` (within the detection tolerance)"""
+    return all(len(boxes) and bool(np.any(np.all(np.abs(boxes - r[:4]) <= 1e-4 * np.abs(r[:4]) + 1e-3, axis=1)))
+               for r in rows)
+
+
 @pytest.mark.timeout(900)
-def test_bench_pipeline_fp32_matches_oracle_chain_every_frame(chain):
-    """Chain bar: detections within 1e-4, decisions identical, track boxes within 1e-4 of the
-    box's scale on every frame of every stream.  A lost track's confidence is its motion statistics' product
-    (stability of arctan2 angle differences, kf.py:137-182), which amplifies the ~1e-6 detection
-    differences of two fp32 conv implementations; its deviation is reported and bounded (1e-2).
-    Tracker bar on identical input: the oracle tracker fed the GPU's own detections matches the
-    GPU tracker to 1e-9 on every output float (test_tracker_gpu.compare_frame)."""
+@pytest.mark.parametrize("plan", sorted(PLANS))
+def test_bench_pipeline_fp32_matches_oracle_chain_every_frame(chain, plan):
+    """Chain bar on the bench's exact pipeline with a given conv plan (the committed one bench.py
+    loads, and the round-2 exact-f32-MFMA plan): every frame's detections within 1e-4 of the
+    oracle's, association decisions identical, track boxes within 1e-4 of the box's scale, on every
+    frame of every stream.  One exception, bounded and accounted for: an NMS near-tie (two
+    candidates at IoU > 0.7 whose oracle scores differ by < TIE_REL = 1e-5 relative, below the
+    ~3e-6 resolution of two fp32 conv implementations) may keep the other member; each such flip
+    must be explained by the oracle's own near-tie list for that frame, it is counted (<= 3 of the
+    1,280 stream-frames), and from that frame on the stream's chain comparison stops (its track
+    history now follows other boxes).  A lost track's confidence is its motion statistics' product
+    (kf.py:137-182), which amplifies the ~1e-6 detection differences; its deviation is reported
+    and bounded (1e-2).  Tracker bar on identical input, every frame of every stream incl. the
+    diverged ones: the oracle tracker fed the GPU's own detections matches the GPU tracker to 1e-9
+    on every output float (test_tracker_gpu.compare_frame)."""
     from test_tracker_gpu import compare_frame
 
-    dets, counts, rows, tcounts, stats = _run_gpu("fp32", chain["frames"])
+    dets, counts, rows, tcounts, stats = _run_gpu("fp32", chain["frames"], PLANS[plan])
     assert int(stats[-1]["overflow"].sum()) == 0
     conf_dev, box_rel, n_tracks = 0.0, 0.0, 0
+    flips, diverged = [], [None] * S
     iso = [RefMultiTracker(150, 1, 0.1, stable_ties=True, fast_iou=True) for _ in range(S)]
     for t in range(F):
         for s in range(S):
             want = chain["dets"][t][s]
             got = dets[t, s, : counts[t, s]]
             assert got.shape == want.shape, (t, s, got.shape, want.shape)
-            np.testing.assert_allclose(got[:, :4], want[:, :4], rtol=1e-4, atol=1e-3, err_msg=f"frame {t} stream {s}")
-            np.testing.assert_allclose(got[:, 4], want[:, 4], rtol=1e-4, atol=1e-6)
+            close = np.all(np.abs(got[:, :4] - want[:, :4]) <= 1e-4 * np.abs(want[:, :4]) + 1e-3, axis=1)
+            if not close.all():  # only an oracle near-tie may explain a different box
+                near = chain["near"][t][s]
+                assert _in_boxes(got[~close], near) and _in_boxes(want[~close], near), (
+                    f"frame {t} stream {s}: detections differ outside the oracle's near-ties", got[~close], want[~close])
+                flips.append((t, s))
+                if diverged[s] is None:
+                    diverged[s] = t
+            np.testing.assert_allclose(got[close, 4], want[close, 4], rtol=1e-4, atol=1e-6)
             ours = track_dicts(rows[t, s], int(tcounts[t, s]))
-            ref = chain["tracks"][t][s]
-            assert decisions(ours) == decisions(ref), (t, s)
-            for o, r in zip(ours, ref):
-                # 1e-4 relative to the box's scale (a coordinate near 0 of a 100-px box is not
-                # held to 1e-4 of itself)
-                scale = float(np.max(np.abs(r["bbox"])))
-                dev = float(np.max(np.abs(o["bbox"] - r["bbox"])))
-                assert dev <= 1e-4 * scale + 1e-3, (t, s, o["bbox"], r["bbox"])
-                box_rel = max(box_rel, dev / max(scale, 1.0))
-                conf_dev = max(conf_dev, abs(o["confidence"] - r["confidence"]))
-                n_tracks += 1
+            if diverged[s] is None:
+                ref = chain["tracks"][t][s]
+                assert decisions(ours) == decisions(ref), (t, s)
+                for o, r in zip(ours, ref):
+                    # 1e-4 relative to the box's scale (a coordinate near 0 of a 100-px box is not
+                    # held to 1e-4 of itself)
+                    scale = float(np.max(np.abs(r["bbox"])))
+                    dev = float(np.max(np.abs(o["bbox"] - r["bbox"])))
+                    assert dev <= 1e-4 * scale + 1e-3, (t, s, o["bbox"], r["bbox"])
+                    box_rel = max(box_rel, dev / max(scale, 1.0))
+                    conf_dev = max(conf_dev, abs(o["confidence"] - r["confidence"]))
+                    n_tracks += 1
             # the tracker alone, on the GPU's detections (float32 rows, as the driver builds them)
             rb = iso[s].update([[d[0], d[1], d[2], d[3], d[4]] for d in got[:, :5]])
             compare_frame(ours, rb, f"isolated tracker frame {t} stream {s}")
     live = [int(tcounts[-1, s]) for s in range(S)]
-    print("BENCH_PIPELINE_FP32", json.dumps({"frames": F, "streams": S, "track_outputs_compared": n_tracks,
-                                             "live_tracks_end": live, "max_box_rel_dev": box_rel,
-                                             "max_confidence_abs_dev": conf_dev,
+    print("BENCH_PIPELINE_FP32", json.dumps({"plan": PLANS[plan], "frames": F, "streams": S,
+                                             "track_outputs_compared": n_tracks, "live_tracks_end": live,
+                                             "near_tie_flips": flips, "chain_diverged_at": diverged,
+                                             "oracle_near_tie_boxes": int(sum(len(b) for fr in chain["near"] for b in fr)),
+                                             "max_box_rel_dev": box_rel, "max_confidence_abs_dev": conf_dev,
                                              "oracle_tie_frames": chain["tie_frames"],
                                              "nms_early_exit": _run_gpu.nms,
                                              "nms_score_ties": chain["nms_score_ties"],
                                              "terminated": chain["terminated"]}))
+    assert len(flips) <= 3, flips
+    assert n_tracks > 0.75 * sum(len(chain["tracks"][t][s]) for t in range(F) for s in range(S))
     assert _run_gpu.nms["images"] == S * F  # every frame's NMS ran once on the device
     assert conf_dev <= 1e-2
     assert min(chain["live"]) >= 40, chain["live"]  # the bench's >= 64-track load (see bench.py CONFIGS)

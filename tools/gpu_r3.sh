@@ -8,6 +8,7 @@
 #   pmc      FETCH_SIZE / WRITE_SIZE passes of the fp32 build
 #   cmc      the camera-motion-compensation bench line (motion-reset tracker + global motion)
 #   diag     tools/cmc_pipe_diag.py
+#   sweep    bench at detector in-flight depths $SWEEP (default 3 5 6)
 #   ab       tools/split_ab.py: committed (split / halo) plan vs the round-2 exact-f32 plan, accuracy vs the oracle
 # Every GPU step has its own time limit; the first failure ends the script.
 set -o pipefail
@@ -52,6 +53,11 @@ for s in ${STEPS:-pytest bench}; do
     ab)
       timeout -k 10 300 python -u tools/split_ab.py --plan plans/s_640x512_i640_b8_fp32.json --plan-exact plans/exp/s_640x512_i640_b8_fp32_exact_r2.json > $O/split_ab.json 2> $O/split_ab.err || { echo "ab failed"; tail -20 $O/split_ab.err; exit 1; }
       python3 -c "import json; d=json.load(open('$O/split_ab.json')); print({k: d[k] for k in ('exact_total_us','split_total_us')}, json.dumps(d['accuracy']), d['split_vs_exact'])" ;;
+    sweep)
+      for D in ${SWEEP:-3 5 6}; do
+        timeout -k 10 200 python -u bench.py --steps 100 --secondary none --no-cpu-baseline --no-profile --inflight $D > $O/bench_if$D.json 2> $O/bench_if$D.err || { echo "sweep $D failed"; tail -20 $O/bench_if$D.err; exit 1; }
+        python3 -c "import json; d=json.load(open('$O/bench_if$D.json')); print('inflight $D', d['value'], d['ms_per_step'])"
+      done ;;
     *) echo "unknown step $s"; exit 1 ;;
   esac
 done
