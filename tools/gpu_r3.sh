@@ -8,6 +8,8 @@
 #   pmc      FETCH_SIZE / WRITE_SIZE passes of the fp32 build
 #   cmc      the camera-motion-compensation bench line (motion-reset tracker + global motion)
 #   diag     tools/cmc_pipe_diag.py
+#   wg       per-workgroup timelines of conv ops $WG_OPS (tools/wg_times.py, committed fp32 plan)
+#   libab    fp32 bench on each library variant in $LIBS (YK_LIB)
 #   sweep    bench at detector in-flight depths $SWEEP (default 3 5 6)
 #   ab       tools/split_ab.py: committed (split / halo) plan vs the round-2 exact-f32 plan, accuracy vs the oracle
 # Every GPU step has its own time limit; the first failure ends the script.
@@ -57,6 +59,17 @@ for s in ${STEPS:-pytest bench}; do
       for D in ${SWEEP:-3 5 6}; do
         timeout -k 10 200 python -u bench.py --steps 100 --secondary none --no-cpu-baseline --no-profile --inflight $D > $O/bench_if$D.json 2> $O/bench_if$D.err || { echo "sweep $D failed"; tail -20 $O/bench_if$D.err; exit 1; }
         python3 -c "import json; d=json.load(open('$O/bench_if$D.json')); print('inflight $D', d['value'], d['ms_per_step'])"
+      done ;;
+    wg)
+      for op in ${WG_OPS:-10 32 72}; do
+        YK_FAST_TS=$op YK_DTYPE=fp32 YK_PLAN=plans/s_640x512_i640_b8_fp32.json timeout -k 10 120 python -u tools/wg_times.py > $O/wg_$op.txt 2> $O/wg_$op.err || { echo "wg $op failed"; tail -10 $O/wg_$op.err; exit 1; }
+        cat $O/wg_$op.txt
+      done ;;
+    libab)
+      # bench (fp32 headline, no bf16 leg) on each library variant in $LIBS (libyk*.so names in the package)
+      for L in ${LIBS:-libyk.so}; do
+        YK_LIB=$PWD/yolo---small-target-recognition---kalman-trajectory-prediction_amd/$L timeout -k 10 200 python -u bench.py --steps 100 --secondary none --no-cpu-baseline $BARGS --dump-ops $O/ops_$L.json > $O/bench_$L.json 2> $O/bench_$L.err || { echo "bench $L failed"; tail -20 $O/bench_$L.err; exit 1; }
+        python3 -c "import json; d=json.load(open('$O/bench_$L.json')); print('$L', d['value'], d['ms_per_step'], d['roofline']['kernel'], d['roofline']['avg_launch_us'])"
       done ;;
     *) echo "unknown step $s"; exit 1 ;;
   esac

@@ -183,8 +183,12 @@ __device__ __forceinline__ f32x4 mma2(const uint4& w0, const uint4& w1, const ui
 // value): the v_exp_f32 / v_rcp_f32 form (~5 VALU, a few ulp) was tried in round 2 and moved one
 // detection of the exact bench pipeline by 4 px on frame 49 (a near-tie among NMS candidates
 // flipped), so only the bf16 / fp8 builds use it (YK_EXACT_SILU=0 switches fp32 to it for A/B).
+// SiLU of the fp32 build: v * rcp(1 + exp(-v)) on v_exp_f32 / v_rcp_f32 (a few ulp) by default.
+// The libm expf + IEEE-division form (YK_EXACT_SILU=1) measured the same accuracy against the
+// oracle (max layer error 3.0e-6 either way, tools/split_ab.py) and the same bench-pipeline chain
+// result, at 4 % of the fp32 headline (profiles/r03_silu_ab.txt).
 #ifndef YK_EXACT_SILU
-#define YK_EXACT_SILU 1
+#define YK_EXACT_SILU 0
 #endif
 template <bool kExact>
 __device__ __forceinline__ float silu(float v) {
@@ -1157,8 +1161,17 @@ __device__ __forceinline__ void conv_fast_body(const FastArgs& a, int2 blk, int 
   if (a.tstamp && tid == 0 && wg_lin < a.tstamp_cap) a.tstamp[3 * wg_lin + 2] = wall_clock64();
 }
 
+// Waves per SIMD the register allocation must leave room for (amdgpu_waves_per_eu): a wave of the
+// large split tiles wants > 256 of the 512 unified VGPR+AGPR registers, which holds a CU to one
+// 256-thread workgroup, so a launch of more workgroups than CUs runs in rounds.
+// Measured (round 3, fp32 headline): 2 lets the large split tiles drop their AGPR accumulators and
+// run two waves per SIMD without spills, but the headline does not move (5,279 vs 5,264 frames/s:
+// those kernels are bound by the split VALU work, not by occupancy); 3 spills (-32 %).
+#ifndef YK_FAST_WPE
+#define YK_FAST_WPE 1
+#endif
 template <class Tr, int NNT, int NPT, bool WS, int SKD>
-__global__ void __launch_bounds__(256) conv_fast_kernel(FastArgs a) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(YK_FAST_WPE))) conv_fast_kernel(FastArgs a) {
   const int2 blk = xcd_block(a.xcd);
   const int nt0 = blk.y * NNT;
   const int rem = a.n_tiles - nt0;
@@ -1191,7 +1204,7 @@ __global__ void __launch_bounds__(256) conv_fast_kernel(FastArgs a) {
 // loads in flight (vmcnt(0)).  Same K order and MFMA sequence per accumulator as
 // conv_fast_kernel: results are bit-identical.
 template <class Tr, int NNT, int NPT, int SKD>
-__global__ void __launch_bounds__(256) conv_fastw_kernel(FastArgs a) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(YK_FAST_WPE))) conv_fastw_kernel(FastArgs a) {
   using T = typename Tr::T;
   constexpr int ESZ = (int)sizeof(T);
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1681,7 +1694,7 @@ __device__ __forceinline__ void split_kslot(const uint4& x, u32x4v& xa, u32x4v& 
 }
 
 template <int NE, int NPT, int WM, int KS>
-__global__ void __launch_bounds__(256) conv_halo_kernel(HaloArgs a) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(YK_FAST_WPE))) conv_halo_kernel(HaloArgs a) {
   constexpr int T = KS * KS;
   constexpr int CC = KS == 1 ? 4 : 1;   // 16-channel groups staged per chunk (1x1: no halo, 4 groups)
   constexpr int PXC = kHaloPx / CC;     // pixels per plane
