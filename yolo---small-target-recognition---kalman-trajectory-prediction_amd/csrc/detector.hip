@@ -200,6 +200,7 @@ __device__ __forceinline__ float silu(float v) {
 
 // store / load 4 consecutive channels
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2v __attribute__((ext_vector_type(2)));
 // f32 -> bf16 round-to-nearest-even with the hardware v_cvt_pk_bf16_f32 (NaN stays NaN)
 __device__ __forceinline__ unsigned pack_bf16x2(float a, float b) {
   const bf16x2 h = {(__bf16)a, (__bf16)b};
@@ -219,16 +220,39 @@ __device__ __forceinline__ XS3 split3(const uint4& x) {
     o.x20 = u32x4v{u[2], u[3], u[0], u[1]};
     return o;
   }
+#ifndef YK_SPLIT_PK
+#define YK_SPLIT_PK 1  // 0: the scalar remainders (A/B builds only)
+#endif
+  if constexpr (!YK_SPLIT_PK) {
 #pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    const float a = __uint_as_float(u[e]);
-    const unsigned d00 = pack_bf16x2(a, a);
-    const float r1 = a - __uint_as_float(d00 & 0xffff0000u);
-    const unsigned d11 = pack_bf16x2(r1, r1);
-    const float r2 = r1 - __uint_as_float(d11 & 0xffff0000u);
-    o.x00[e] = d00;
-    o.x11[e] = d11;
-    o.x20[e] = pack_bf16x2(r2, a);
+    for (int e = 0; e < 4; ++e) {
+      const float a = __uint_as_float(u[e]);
+      const unsigned d00 = pack_bf16x2(a, a);
+      const float r1 = a - __uint_as_float(d00 & 0xffff0000u);
+      const unsigned d11 = pack_bf16x2(r1, r1);
+      const float r2 = r1 - __uint_as_float(d11 & 0xffff0000u);
+      o.x00[e] = d00;
+      o.x11[e] = d11;
+      o.x20[e] = pack_bf16x2(r2, a);
+    }
+    return o;
+  }
+  // element pairs: the two remainders of a pair are one v_pk_add_f32 each (6 VALU per element)
+#pragma unroll
+  for (int e = 0; e < 4; e += 2) {
+    const f32x2v a = {__uint_as_float(u[e]), __uint_as_float(u[e + 1])};
+    const unsigned d00a = pack_bf16x2(a[0], a[0]), d00b = pack_bf16x2(a[1], a[1]);
+    const f32x2v h0 = {__uint_as_float(d00a & 0xffff0000u), __uint_as_float(d00b & 0xffff0000u)};
+    const f32x2v r1 = a - h0;
+    const unsigned d11a = pack_bf16x2(r1[0], r1[0]), d11b = pack_bf16x2(r1[1], r1[1]);
+    const f32x2v h1 = {__uint_as_float(d11a & 0xffff0000u), __uint_as_float(d11b & 0xffff0000u)};
+    const f32x2v r2 = r1 - h1;
+    o.x00[e] = d00a;
+    o.x00[e + 1] = d00b;
+    o.x11[e] = d11a;
+    o.x11[e + 1] = d11b;
+    o.x20[e] = pack_bf16x2(r2[0], a[0]);
+    o.x20[e + 1] = pack_bf16x2(r2[1], a[1]);
   }
   return o;
 }
@@ -1684,11 +1708,14 @@ __device__ __forceinline__ void split_kslot(const uint4& x, u32x4v& xa, u32x4v& 
   const float a0 = __uint_as_float(x.x), a1 = __uint_as_float(x.y), a2 = __uint_as_float(x.z),
               a3 = __uint_as_float(x.w);
   const unsigned p0 = pack_bf16x2(a0, a1), p1 = pack_bf16x2(a2, a3);
-  const float r0 = a0 - __uint_as_float(p0 << 16), r1 = a1 - __uint_as_float(p0 & 0xffff0000u);
-  const float r2 = a2 - __uint_as_float(p1 << 16), r3 = a3 - __uint_as_float(p1 & 0xffff0000u);
+  // the remainders of an element pair in one v_pk_add_f32
+  const f32x2v ra = f32x2v{a0, a1} - f32x2v{__uint_as_float(p0 << 16), __uint_as_float(p0 & 0xffff0000u)};
+  const f32x2v rb = f32x2v{a2, a3} - f32x2v{__uint_as_float(p1 << 16), __uint_as_float(p1 & 0xffff0000u)};
+  const float r0 = ra[0], r1 = ra[1], r2 = rb[0], r3 = rb[1];
   const unsigned q0 = pack_bf16x2(r0, r1), q1 = pack_bf16x2(r2, r3);
-  const float s0 = r0 - __uint_as_float(q0 << 16), s1 = r1 - __uint_as_float(q0 & 0xffff0000u);
-  const float s2 = r2 - __uint_as_float(q1 << 16), s3 = r3 - __uint_as_float(q1 & 0xffff0000u);
+  const f32x2v sa = ra - f32x2v{__uint_as_float(q0 << 16), __uint_as_float(q0 & 0xffff0000u)};
+  const f32x2v sb = rb - f32x2v{__uint_as_float(q1 << 16), __uint_as_float(q1 & 0xffff0000u)};
+  const float s0 = sa[0], s1 = sa[1], s2 = sb[0], s3 = sb[1];
   xa = u32x4v{p0, p1, q0, q1};
   xb = u32x4v{p0, p1, pack_bf16x2(s0, s1), pack_bf16x2(s2, s3)};
 }
