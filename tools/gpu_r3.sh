@@ -23,13 +23,13 @@ BARGS=${BARGS:-}
 for s in ${STEPS:-pytest bench}; do
   case $s in
     pytest)
-      timeout -k 10 900 python -u -m pytest tests -m gpu -v --maxfail=3 --timeout 200 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} > $O/pytest_gpu.log 2>&1 || { echo "pytest failed"; grep -E "FAILED|ERROR|passed|failed" $O/pytest_gpu.log | tail -20; exit 1; }
+      timeout -k 10 900 python -u -m pytest tests -m gpu -v -rP --maxfail=3 --timeout 200 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} > $O/pytest_gpu.log 2>&1 || { echo "pytest failed"; grep -E "FAILED|ERROR|passed|failed" $O/pytest_gpu.log | tail -20; exit 1; }
       tail -2 $O/pytest_gpu.log ;;
     bench)
       timeout -k 10 400 python -u bench.py ${PLAN:+--plan-in $PLAN} $BARGS --dump-ops $O/ops.json > $O/bench.json 2> $O/bench.err || { echo "bench failed"; tail -30 $O/bench.err; exit 1; }
       cat $O/bench.json ;;
     tune)
-      timeout -k 10 600 python -u tools/tune_concurrent.py --dtype fp32 --out $O/plan_tuned.json > $O/tune.log 2>&1 || { echo "tune failed"; tail -20 $O/tune.log; exit 1; }
+      timeout -k 10 600 python -u tools/tune_concurrent.py --dtype fp32 --tune-batch ${TUNE_BATCH:-16} --out $O/plan_tuned.json > $O/tune.log 2>&1 || { echo "tune failed"; tail -20 $O/tune.log; exit 1; }
       tail -1 $O/tune.log ;;
     btuned)
       timeout -k 10 300 python -u bench.py --steps 100 --secondary none --no-cpu-baseline --plan-in $O/plan_tuned.json --dump-ops $O/ops_tuned.json > $O/bench_tuned.json 2> $O/bench_tuned.err || { echo "bench tuned failed"; tail -20 $O/bench_tuned.err; exit 1; }
