@@ -10,6 +10,8 @@
 #   diag     tools/cmc_pipe_diag.py
 #   wg       per-workgroup timelines of conv ops $WG_OPS (tools/wg_times.py, committed fp32 plan)
 #   libab    fp32 bench on each library variant in $LIBS (YK_LIB)
+#   c4plan   config-4 bench with its run-time autotuned plan written to plan_c4.json
+#   smoke    __graft_entry__.smoke()
 #   sweep    bench at detector in-flight depths $SWEEP (default 3 5 6)
 #   ab       tools/split_ab.py: committed (split / halo) plan vs the round-2 exact-f32 plan, accuracy vs the oracle
 # Every GPU step has its own time limit; the first failure ends the script.
@@ -71,6 +73,12 @@ for s in ${STEPS:-pytest bench}; do
         YK_LIB=$PWD/yolo---small-target-recognition---kalman-trajectory-prediction_amd/$L timeout -k 10 200 python -u bench.py --steps 100 --secondary none --no-cpu-baseline $BARGS --dump-ops $O/ops_$L.json > $O/bench_$L.json 2> $O/bench_$L.err || { echo "bench $L failed"; tail -20 $O/bench_$L.err; exit 1; }
         python3 -c "import json; d=json.load(open('$O/bench_$L.json')); print('$L', d['value'], d['ms_per_step'], d['roofline']['kernel'], d['roofline']['avg_launch_us'])"
       done ;;
+    smoke)
+      timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1 || { echo "smoke failed"; tail -20 $O/smoke.txt; exit 1; }
+      tail -3 $O/smoke.txt ;;
+    c4plan)
+      timeout -k 10 300 python -u bench.py --config 4 --no-cpu-baseline --steps 100 --plan-out $O/plan_c4.json > $O/bench_c4.json 2> $O/bench_c4.err || { echo "c4 failed"; tail -20 $O/bench_c4.err; exit 1; }
+      python3 -c "import json; d=json.load(open('$O/bench_c4.json')); print('c4', d['value'], d['config']['conv_plan'])" ;;
     *) echo "unknown step $s"; exit 1 ;;
   esac
 done
