@@ -106,6 +106,49 @@ def near_tie_boxes(pred: torch.Tensor, hw, conf: float = 0.25, iou: float = 0.7,
     return xy.numpy().astype(np.float32)
 
 
+def dets_match(got, want, near=None, rel: float = 1e-5):
+    """Detections [N, >=5] of the GPU against the oracle's for one image, under the fp32 bars.
+    Returns "same" (row by row within 1e-4 / atol 1e-3 px, scores 1e-4), "tie" (equal only up to
+    near-ties: a row out of place sits among oracle rows whose scores are within `rel` of its own
+    -- the score order is unresolved at fp32 resolution -- or a differing box is a member of an
+    oracle NMS near-tie pair in `near`, see near_tie_boxes), or None.  After a call,
+    dets_match.perm[j] is the oracle row GPU row j matched and dets_match.flip says whether an NMS
+    near-tie kept the other member of a pair (otherwise the rows differ only in order)."""
+    def close(a, b):
+        return bool(np.all(np.abs(a[:4] - b[:4]) <= 1e-4 * np.abs(b[:4]) + 1e-3)) and \
+            abs(float(a[4]) - float(b[4])) <= 1e-4 * abs(float(b[4])) + 1e-6
+
+    def member(box):
+        return near is not None and len(near) > 0 and \
+            bool(np.any(np.all(np.abs(near - box[:4]) <= 1e-4 * np.abs(box[:4]) + 1e-3, axis=1)))
+
+    n = len(want)
+    dets_match.perm, dets_match.flip = np.arange(n), False
+    if len(got) != n:
+        return None
+    if all(close(g, w) for g, w in zip(got, want)):
+        return "same"
+    for i in range(n):  # every differing position is explained by a near-tie
+        if not close(got[i], want[i]):
+            peers = np.abs(want[:, 4] - want[i, 4]) <= rel * abs(float(want[i, 4]))
+            if peers.sum() < 2 and not (member(want[i]) and member(got[i])):
+                return None
+    used = np.zeros(n, bool)  # and the two sets agree (an NMS near-tie may swap a pair's member)
+    perm, flip = np.zeros(n, int), False
+    for i in range(n):
+        j = next((j for j in range(n) if not used[j] and close(got[j], want[i])), None)
+        if j is None:
+            j = next((j for j in range(n) if not used[j] and member(got[j]) and member(want[i])
+                      and abs(float(got[j, 4]) - float(want[i, 4])) <= rel * abs(float(want[i, 4]))), None)
+            flip = True
+        if j is None:
+            return None
+        used[j] = True
+        perm[j] = i
+    dets_match.perm, dets_match.flip = perm, flip  # GPU row j is oracle row perm[j]
+    return "tie"
+
+
 def score_ties(pred: torch.Tensor, conf: float = 0.25) -> int:
     """Exact duplicate scores among the NMS candidates (score > conf) of one image's Detect
     output [5, A]: non_max_suppression's scores.sort (utils/nms.py:264) is unstable on them."""
