@@ -11,6 +11,7 @@
 #   wg       per-workgroup timelines of conv ops $WG_OPS (tools/wg_times.py, committed fp32 plan)
 #   libab    fp32 bench on each library variant in $LIBS (YK_LIB)
 #   c4plan   config-4 bench with its run-time autotuned plan written to plan_c4.json
+#   c4tune   config-4 plan tuned over every kernel kind vs the committed one
 #   smoke    __graft_entry__.smoke()
 #   sweep    bench at detector in-flight depths $SWEEP (default 3 5 6)
 #   ab       tools/split_ab.py: committed (split / halo) plan vs the round-2 exact-f32 plan, accuracy vs the oracle
@@ -79,6 +80,14 @@ for s in ${STEPS:-pytest bench}; do
     c4plan)
       timeout -k 10 300 python -u bench.py --config 4 --no-cpu-baseline --steps 100 --plan-out $O/plan_c4.json > $O/bench_c4.json 2> $O/bench_c4.err || { echo "c4 failed"; tail -20 $O/bench_c4.err; exit 1; }
       python3 -c "import json; d=json.load(open('$O/bench_c4.json')); print('c4', d['value'], d['config']['conv_plan'])" ;;
+    c4tune)
+      # config 4 (one stream per GPU): concurrent autotune at batch $TUNE_BATCH (default 4 = four forwards of
+      # batch 1 in flight) over every kernel kind, then config-4 benches on the committed and the tuned plan
+      timeout -k 10 600 python -u tools/tune_concurrent.py --dtype fp32 --streams 1 --tune-batch ${TUNE_BATCH:-4} --out $O/plan_c4_tuned.json > $O/tune_c4.log 2>&1 || { echo "tune c4 failed"; tail -20 $O/tune_c4.log; exit 1; }
+      for P in plans/s_640x512_i640_b1_fp32.json $O/plan_c4_tuned.json; do
+        timeout -k 10 300 python -u bench.py --config 4 --no-cpu-baseline --steps 200 --plan-in $P > $O/bench_c4_$(basename $P) 2> $O/bench_c4.err || { echo "c4 bench failed"; tail -20 $O/bench_c4.err; exit 1; }
+        python3 -c "import json; d=json.load(open('$O/bench_c4_$(basename $P)')); print('c4', '$P', d['value'], d['ms_per_step'], d['roofline']['kernel'])"
+      done ;;
     *) echo "unknown step $s"; exit 1 ;;
   esac
 done
