@@ -325,7 +325,7 @@ def run_leg(a, P, cfg, dtype, frames, dev, local, rank, ws, headline):
                                    motion_method="optical_flow" if a.gmd else None)
     pipe.set_schedule(a.groups, lanes)
     pipe.frames.copy_(frames[0])
-    plan_src = "heuristic"
+    plan_src, parity = "heuristic", None
     pth = (a.plan_in if (headline and a.plan_in) else plan_path(a, dtype, (S + a.groups - 1) // a.groups, W, H, imgsz))
     tune = a.autotune
     if not tune and os.path.exists(pth):
@@ -337,6 +337,9 @@ def run_leg(a, P, cfg, dtype, frames, dev, local, rank, ws, headline):
         for m in pipe.models:
             m.load_plan(pl["batch"], pl["plan"])
         plan_src = os.path.relpath(pth, REPO)
+        # the plan's chain-parity record: near-tie flips / order ties of this plan over the
+        # 1,280-stream-frame oracle chain, asserted by tests/test_bench_pipeline_gpu.py
+        parity = pl.get("parity")
     elif not tune:
         log(f"no committed conv plan at {pth}: autotuning")
         tune = True
@@ -385,7 +388,8 @@ def run_leg(a, P, cfg, dtype, frames, dev, local, rank, ws, headline):
            "live_tracks_per_stream": round(run["current_active_tracks"] / (S * ws), 1),
            "live_tracks_per_stream_min_at_start": int(live_start.min()),
            "overflow": int(run["overflow"]), "tracks_created": int(run["total_tracks_created"]),
-           "conv_plan": plan_src, "window_monotonic_ns": [w0, w1], "rank_devices": devices}
+           "conv_plan": plan_src, "conv_plan_parity": parity, "window_monotonic_ns": [w0, w1],
+           "rank_devices": devices}
     if overflow:
         log(f"tracker overflow on this rank: {overflow} detections/tracks dropped")
     if rank == 0 and not a.no_profile:
@@ -538,7 +542,8 @@ def main():
                        "live_tracks_per_stream_min_at_start": head["live_tracks_per_stream_min_at_start"],
                        "live_tracks_floor": cfg["live_floor"], "live_tracks_floor_met": ok_floor,
                        "tracker_overflow": head["overflow"], "tracks_created": head["tracks_created"],
-                       "conv_plan": head["conv_plan"], "graph": not a.no_graph, "tracker_overlapped": not a.no_pipeline,
+                       "conv_plan": head["conv_plan"], "conv_plan_parity": head["conv_plan_parity"],
+                       "graph": not a.no_graph, "tracker_overlapped": not a.no_pipeline,
                        "detector_inflight": a.inflight, "gflop_per_frame": head["gflop_per_frame"],
                        "rank_devices": head["rank_devices"],
                        "global_motion": "optical_flow" if a.gmd else None},

@@ -29,6 +29,7 @@ int detect_and_track(const char* engine, const unsigned char* frames_dev, int B,
   yk_ctx* ctx = NULL;
   yk_model* model = NULL;
   yk_tracker* trk = NULL;
+  CHECK(yk_abi_check()); /* this file's struct layouts == the loaded libyk.so's (YK_ABI_VERSION) */
   CHECK(yk_ctx_create(0, &ctx));
   CHECK(yk_model_load(ctx, engine, &model));
   yk_tracker_cfg cfg = {150, 1, 0.1, 512, 300, YK_POLICY_ENHANCED};
@@ -120,7 +121,8 @@ int detect_from_weights(const char* weights_path, char scale, int act_dtype, int
   }
   yk_ctx* ctx = NULL;
   yk_model* model = NULL;
-  int rc = yk_ctx_create(0, &ctx);
+  int rc = yk_abi_check();
+  if (!rc) rc = yk_ctx_create(0, &ctx);
   if (!rc) rc = yk_model_load_weights(ctx, &rw.w, scale, act_dtype, frame_h, frame_w, imgsz, B, &model);
   free_raw_weights(&rw);
   if (!rc) rc = yk_detect(model, frames_dev, B, 0.25f, 0.7f, 300, dets_dev, counts_dev, NULL);

@@ -29,7 +29,9 @@
 extern "C" {
 #endif
 
-#define YK_ABI_VERSION 2
+/* 3: yk_bt_cfg gained assignment / match_thresh_f64, yk_track_state the motion-reset fields
+ * (round 3).  A host built against another layout must not call in: see yk_abi_check(). */
+#define YK_ABI_VERSION 3
 
 enum yk_status {
   YK_OK = 0,
@@ -203,7 +205,8 @@ int yk_track_op(yk_tracker* trk, int stream_index, int pos, int op, int arg, con
 
 /* sizeof() of the ABI structs, for bindings that mirror them (0: yk_tracker_cfg,
  * 1: yk_tracker_stats, 2: yk_track_out, 3: yk_track_state, 4: yk_view, 5: yk_op,
- * 6: yk_model_desc, 7: yk_bt_cfg, 8: yk_motion, 9: yk_gmd_stats); -1 for an unknown id. */
+ * 6: yk_model_desc, 7: yk_bt_cfg, 8: yk_motion, 9: yk_gmd_stats, 10: yk_tensor); -1 for an
+ * unknown id. */
 int64_t yk_struct_size(int which);
 
 /* Append a new track created from a box (AircraftKalmanTracker.__init__, :23-101) to the
@@ -513,6 +516,21 @@ int yk_model_buffer(yk_model* m, int buf, void** dev_ptr);
 
 /* Synchronous device -> host copy (bindings without their own HIP runtime access). */
 int yk_memcpy_d2h(void* host_dst, const void* dev_src, int64_t bytes);
+
+/* Host-side layout check, compiled into the caller with the caller's view of the structs: 0 when
+ * the loaded library has this header's ABI version and every struct size, else YK_ERR_STATE.
+ * Call it once before any other entry point. */
+static inline int yk_abi_check(void) {
+  const int64_t want[11] = {(int64_t)sizeof(yk_tracker_cfg), (int64_t)sizeof(yk_tracker_stats),
+                            (int64_t)sizeof(yk_track_out), (int64_t)sizeof(yk_track_state),
+                            (int64_t)sizeof(yk_view), (int64_t)sizeof(yk_op), (int64_t)sizeof(yk_model_desc),
+                            (int64_t)sizeof(yk_bt_cfg), (int64_t)sizeof(yk_motion), (int64_t)sizeof(yk_gmd_stats),
+                            (int64_t)sizeof(yk_tensor)};
+  if (yk_abi_version() != YK_ABI_VERSION) return YK_ERR_STATE;
+  for (int i = 0; i < 11; ++i)
+    if (yk_struct_size(i) != want[i]) return YK_ERR_STATE;
+  return YK_OK;
+}
 
 #ifdef __cplusplus
 }

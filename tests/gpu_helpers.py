@@ -149,6 +149,22 @@ def dets_match(got, want, near=None, rel: float = 1e-5):
     return "tie"
 
 
+def resync_rows(got, want, perm):
+    """The oracle chain's input after a near-tie frame (dets_match == "tie"): the oracle's rows in
+    the GPU's order, except that a row the GPU kept instead of the oracle's pair member (an NMS
+    near-tie flip) is the GPU's own row -- so the oracle chain continues on the boxes the GPU
+    chain follows and every later frame's decisions can still be compared.  Also returns the
+    flips as (oracle row, GPU row) pairs."""
+    rows, flips = [], []
+    for j in range(len(got)):
+        w = want[perm[j]]
+        same = bool(np.all(np.abs(got[j, :4] - w[:4]) <= 1e-4 * np.abs(w[:4]) + 1e-3))
+        rows.append(w if same else got[j])
+        if not same:
+            flips.append((w, got[j]))
+    return np.asarray(rows, np.float32).reshape(-1, want.shape[1]), flips
+
+
 def score_ties(pred: torch.Tensor, conf: float = 0.25) -> int:
     """Exact duplicate scores among the NMS candidates (score > conf) of one image's Detect
     output [5, A]: non_max_suppression's scores.sort (utils/nms.py:264) is unstable on them."""

@@ -58,3 +58,33 @@ def test_no_gpu_means_loud_failure():
         pytest.skip("GPU present")
     with pytest.raises(pkg().YKError):
         pkg().EnhancedMultiTargetTracker(150, 1, 0.1)
+
+
+def test_c_host_abi_check_passes_against_this_library(tmp_path):
+    """The header-inline yk_abi_check() (version + every struct size, compiled with the host's
+    view of the structs) returns YK_OK against the built libyk.so; a host compiled with a
+    different YK_ABI_VERSION gets YK_ERR_STATE.  Only yk_abi_version / yk_struct_size are called
+    (no GPU)."""
+    import shutil
+    import subprocess
+
+    if shutil.which("gcc") is None:
+        pytest.skip("gcc missing")
+    lib_dir = os.path.dirname(pkg()._lib.LIB_PATH)
+    src = tmp_path / "abi.c"
+    src.write_text('#include <stdio.h>\n#include "yk.h"\nint main(void) { printf("%d\\n", yk_abi_check()); return 0; }\n')
+    out = {}
+    for tag, extra in (("same", []), ("other", ["-DYK_ABI_OVERRIDE"])):
+        exe = tmp_path / f"abi_{tag}"
+        cflags = ["-I", os.path.join(REPO, "include")]
+        if extra:  # a host built against another header version
+            hdr = tmp_path / "old" / "yk.h"
+            hdr.parent.mkdir()
+            hdr.write_text(open(HEADER).read().replace("#define YK_ABI_VERSION 3", "#define YK_ABI_VERSION 2"))
+            cflags = ["-I", str(hdr.parent)]
+        subprocess.run(["gcc", "-std=c11", *cflags, str(src), "-L", lib_dir, "-l:libyk.so",
+                        f"-Wl,-rpath,{lib_dir}", "-o", str(exe)], check=True, capture_output=True)
+        r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=60)
+        assert r.returncode == 0, r.stderr
+        out[tag] = int(r.stdout.strip())
+    assert out == {"same": 0, "other": 4}, out

@@ -89,13 +89,16 @@ def _edge_set(n, seed):
         b[6] = [x0 + 1, y0 + 1, x0 + 1, y0 + 9]  # zero width, inside box 0's cluster
         b[7] = b[6]
         s[6] = s[7] = np.float32(0.3)  # late in the order: a zero-area kept box overlaps nothing (early exit)
+    if n >= 16:
+        s.view(np.uint32)[9] = 0xFFC00000  # a NaN with the sign bit set: torch still sorts it first
     return b, s
 
 
 @pytest.mark.parametrize("n", [1, 8, 40, 200, 400, 1500, 3000])
 @pytest.mark.parametrize("max_det,thr", [(300, 0.7), (1024, 0.7), (1024, 0.3)])
 def test_nms_kernel_edge_cases_every_path(n, max_det, thr):
-    """Ties (stable: input order), NaN score (sorted first, as torch's sort puts NaN), NaN corner
+    """Ties (stable: input order), NaN scores of either sign (sorted first, as torch's sort puts
+    every NaN), NaN corner
     (its IoU is NaN: suppressed by `iou <= thr` being false, never counted as no-overlap), degenerate
     boxes (0/0 IoU), and the max_det cut -- against torch_nms + [:max_det] on every size path."""
     boxes, scores = _edge_set(n, seed=n)

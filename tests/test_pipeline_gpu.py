@@ -70,11 +70,11 @@ def test_reference_driver_loop_through_compat_packages(tmp_path):
     ``YOLO(model_path)`` with no dtype argument (so the drop-in default), frames read through the
     VideoCapture-like reader (a .npy frame stack, since no codec is in the image), the per-frame
     body of :88-131, the visualizer and the VideoWriter-like sink -- held to the oracle under the
-    bench-pipeline bars: every frame's detections equal the torch-CPU fp32 detector's (up to
-    accounted near-ties), the track dicts equal the oracle chain (detector -> numpy
-    RefMultiTracker(150, 1, 0.1)) up to the first near-tie -- decisions (id, status, age, hits,
-    tsu) identical, boxes within 1e-4 of the box's scale -- and equal the oracle tracker fed the
-    GPU's detections on every frame.  160 frames so the 150-miss deletion happens inside the loop."""
+    strict chain bar: every frame's detections equal the torch-CPU fp32 detector's row for row,
+    the track dicts equal the oracle chain (detector -> numpy RefMultiTracker(150, 1, 0.1)) on
+    every frame -- decisions (id, status, age, hits, tsu) identical, boxes within 1e-4 of the
+    box's scale -- and equal the oracle tracker fed the GPU's detections.  No near-tie
+    allowance.  160 frames so the 150-miss deletion happens inside the loop."""
     sys.path.insert(0, os.path.join(REPO, pkg().__name__, "compat"))
     try:
         from kalman.enhanced_multi_target_tracker import EnhancedMultiTargetTracker
@@ -138,50 +138,41 @@ def test_reference_driver_loop_through_compat_packages(tmp_path):
     assert frame_count == F and tracker.frame_count == F
     assert results[0].boxes.xyxy.is_cuda and results[0].orig_shape == (512, 640)
     # --- the oracle chain on the same frames -----------------------------------------------------
-    # Chain bar as in test_bench_pipeline_gpu: per frame, the detections equal the oracle's (or
-    # differ only by a near-tie: equal oracle scores / a score gap < 1e-5 whose order fp32 cannot
-    # resolve -- the chain then takes the oracle's rows in the GPU's order -- or an NMS near-tie
-    # pair, after which the chain stops); the track dicts equal the oracle chain's (oracle detector
-    # -> oracle tracker); on every frame they also equal the oracle tracker fed the GPU's own
-    # detections (1e-9, test_tracker_gpu.compare_frame).
-    from gpu_helpers import dets_match, near_tie_boxes
+    # Strict chain bar, no near-tie allowance: per frame, the detections equal the oracle's row for
+    # row (1e-4 relative, 1e-3 px; scores 1e-4); the track dicts equal the oracle chain's (oracle
+    # detector -> oracle tracker): decisions identical, boxes within 1e-4 of the box's scale; and on
+    # every frame they also equal the oracle tracker fed the GPU's own detections (1e-9,
+    # test_tracker_gpu.compare_frame).
+    from gpu_helpers import dets_match
     from test_tracker_gpu import compare_frame
 
     ref = D.RefDetector(_layers(model.arch), model.state_dict, P.arch.detect_strides(model.arch))
     trk = RefMultiTracker(150, 1, 0.1, stable_ties=True, fast_iou=True)
     iso = RefMultiTracker(150, 1, 0.1, stable_ties=True, fast_iou=True)
     torch.set_num_threads(max(1, min(16, len(os.sched_getaffinity(0)))))
-    n_tracks, box_rel, ties, chain_until = 0, 0.0, [], F
+    n_tracks, box_rel = 0, 0.0
     for t in range(F):
-        want, y = D.predict(ref, [frames[t]])
+        want, _ = D.predict(ref, [frames[t]])
         wd = want[0][:, :5].numpy()
         got_d, ours = per_frame[t]
-        m = dets_match(got_d, wd, near_tie_boxes(y[0], frames[t].shape[:2]))
-        assert m is not None, (f"frame {t}: detections differ outside near-ties", got_d, wd)
-        if m == "tie":
-            ties.append(t)
-            if dets_match.flip:  # another box kept: the chain's histories part here
-                chain_until = min(chain_until, t)
-            else:  # only the order of equal-score rows differs: the chain takes the oracle's rows in the GPU's order
-                wd = wd[dets_match.perm]
+        assert dets_match(got_d, wd) == "same", (f"frame {t}: detections differ from the oracle's", got_d, wd)
         rb = trk.update([[b[0], b[1], b[2], b[3], b[4]] for b in wd])
-        if t < chain_until:
-            assert decisions(ours) == decisions(rb), t
-            for o, r in zip(ours, rb):
-                scale = float(np.max(np.abs(r["bbox"])))
-                dev = float(np.max(np.abs(np.asarray(o["bbox"]) - r["bbox"])))
-                assert dev <= 1e-4 * scale + 1e-3, (t, o["track_id"], o["bbox"], r["bbox"])
-                box_rel = max(box_rel, dev / max(scale, 1.0))
-                n_tracks += 1
+        assert decisions(ours) == decisions(rb), t
+        for o, r in zip(ours, rb):
+            scale = float(np.max(np.abs(r["bbox"])))
+            dev = float(np.max(np.abs(np.asarray(o["bbox"]) - r["bbox"])))
+            assert dev <= 1e-4 * scale + 1e-3, (t, o["track_id"], o["bbox"], r["bbox"])
+            box_rel = max(box_rel, dev / max(scale, 1.0))
+            n_tracks += 1
         compare_frame(ours, iso.update([[b[0], b[1], b[2], b[3], b[4]] for b in got_d]), f"isolated tracker frame {t}")
-    assert len(ties) <= 3, ties
-    assert n_tracks > 0.75 * sum(len(per_frame[t][1]) for t in range(F))  # the chain ran
+    assert n_tracks == sum(len(per_frame[t][1]) for t in range(F))  # every output of every frame compared
     st = iso.stats
     assert st["total_tracks_terminated"] >= 1 and st["successful_recoveries"] > 0, st  # deletion + recovery ran
     assert tracker.get_statistics()["total_tracks_terminated"] == st["total_tracks_terminated"]
+    assert trk.stats == st  # the oracle chain and the isolated oracle tracker agree too
     assert detection_frames > 0 and prediction_frames > 0 and state_changes > 0
-    print("DRIVER_LOOP", {"frames": F, "chain_track_outputs_compared": n_tracks, "near_tie_frames": ties,
-                          "max_box_rel_dev": box_rel, "stats": dict(st), "state_changes": state_changes})
+    print("DRIVER_LOOP", {"frames": F, "chain_track_outputs_compared": n_tracks, "max_box_rel_dev": box_rel,
+                          "stats": dict(st), "state_changes": state_changes})
 
 
 def test_pipelined_tracker_stream_matches_serial():

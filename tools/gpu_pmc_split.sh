@@ -1,6 +1,6 @@
 #!/bin/bash
 # PMC passes over the F32S (split) conv kernels of the fp32 headline, on the product library and
-# on the YK_SPLIT_DIAG=3 build (no split VALU, no weight loads): where the split kernel's time goes
+# on the YK_DIAG=3 build (csrc/build.py YK_DEFINES=-DYK_DIAG=3 YK_OUT=...libyk_diag3.so: no split VALU, no weight loads): where the split kernel's time goes
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp

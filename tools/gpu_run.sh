@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-3 GPU driver.  STEPS (space separated) picks what runs, in order:
+# GPU driver (one gpurun call runs a list of steps).  STEPS (space separated) picks what runs, in order:
 #   pytest   the whole -m gpu suite
 #   bench    the default bench line (committed plan) with --dump-ops
 #   tune     concurrent autotune of the fp32 plan (all kernel kinds incl. split / halo) -> plan_tuned.json
@@ -19,7 +19,7 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
-O=gpurun_out/${OUT_DIR:-r3}
+O=gpurun_out/${OUT_DIR:-r4}
 mkdir -p $O
 PLAN=${PLAN:-}
 BARGS=${BARGS:-}

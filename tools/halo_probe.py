@@ -2,7 +2,7 @@
 """Per-op device time of every halo-tile split conv variant (plan kind 5: NE x NPT x WM) against
 the op's entry in a base plan, on the fp32 bench workload (batch-8 forward, YOLOv8s+P2).  One
 JSON line: {op: {"base": [kind, nnt, npt, us], "halo": [[ne, npt, wm, us], ...]}}.  With YK_LIB
-pointing at a YK_HALO_DIAG build the same sweep shows what bounds the kernel.
+pointing at a YK_DIAG=4|8 build (detector.hip, "Diagnostic builds") the same sweep shows what bounds the kernel.
 
 usage: halo_probe.py [--plan gpurun_out/.../plan.json] [--ops 72,73,76] [--reps 10]
 """

@@ -192,6 +192,9 @@ _lock = threading.Lock()
 _lib = None
 
 
+ABI_VERSION = 3  # include/yk.h YK_ABI_VERSION
+
+
 def exported_symbols() -> list[str]:
     return sorted(_SIGS)
 
@@ -215,11 +218,11 @@ def lib() -> C.CDLL:
             fn = getattr(L, name)
             fn.argtypes = args
             fn.restype = res
-        if L.yk_abi_version() != 2:
-            raise YKError("libyk.so ABI version mismatch")
+        if L.yk_abi_version() != ABI_VERSION:
+            raise YKError(f"libyk.so ABI version {L.yk_abi_version()}, this package expects {ABI_VERSION}")
         sizes = {0: C.sizeof(TrackerCfg), 1: STATS_DTYPE.itemsize, 2: TRACK_OUT_DTYPE.itemsize,
                  3: TRACK_STATE_DTYPE.itemsize, 7: C.sizeof(BtCfg), 8: MOTION_DTYPE.itemsize,
-                 9: GMD_STATS_DTYPE.itemsize}
+                 9: GMD_STATS_DTYPE.itemsize, 10: C.sizeof(Tensor)}
         for k, v in sizes.items():
             if L.yk_struct_size(k) != v:
                 raise YKError(f"ABI struct {k} size mismatch: C {L.yk_struct_size(k)} vs python {v}")

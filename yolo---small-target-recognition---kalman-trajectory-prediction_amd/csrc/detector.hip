@@ -33,6 +33,22 @@
 
 #include "yk_internal.h"
 
+// Diagnostic builds.  csrc/build.py YK_DEFINES="-DYK_DIAG=<mask>" builds libyk_diag.so with its
+// own objects; the product library is always built with YK_DIAG = 0, where every bit below is off
+// and the diagnostic branches are discarded at compile time.
+//     1  F32S: operands used unsplit (no split VALU)      2  F32S: no weight loads
+//     4  halo kernel: no weight loads                     8  halo kernel: no input staging
+//    32  F32S split with scalar remainders               64  fp32 SiLU on v_exp_f32 / v_rcp_f32
+//   128  two waves per SIMD for the table / halo kernels (amdgpu_waves_per_eu(2))
+#ifndef YK_DIAG
+#define YK_DIAG 0
+#endif
+#define YK_SPLIT_DIAG (YK_DIAG & 3)
+#define YK_HALO_DIAG ((YK_DIAG >> 2) & 3)
+#define YK_SPLIT_PK ((YK_DIAG & 32) == 0)
+#define YK_EXACT_SILU ((YK_DIAG & 64) == 0)
+#define YK_FAST_WPE ((YK_DIAG & 128) ? 2 : 1)
+
 namespace yk {
 namespace det {
 
@@ -179,17 +195,13 @@ __device__ __forceinline__ f32x4 mma2(const uint4& w0, const uint4& w1, const ui
   }
 }
 
-// SiLU in the conv epilogues.  The fp32 build keeps libm expf + an IEEE division (~36 VALU per
-// value): the v_exp_f32 / v_rcp_f32 form (~5 VALU, a few ulp) was tried in round 2 and moved one
-// detection of the exact bench pipeline by 4 px on frame 49 (a near-tie among NMS candidates
-// flipped), so only the bf16 / fp8 builds use it (YK_EXACT_SILU=0 switches fp32 to it for A/B).
-// SiLU of the fp32 build: v * rcp(1 + exp(-v)) on v_exp_f32 / v_rcp_f32 (a few ulp) by default.
-// The libm expf + IEEE-division form (YK_EXACT_SILU=1) measured the same accuracy against the
-// oracle (max layer error 3.0e-6 either way, tools/split_ab.py) and the same bench-pipeline chain
-// result, at 4 % of the fp32 headline (profiles/r03_silu_ab.txt).
-#ifndef YK_EXACT_SILU
-#define YK_EXACT_SILU 0
-#endif
+// SiLU in the conv epilogues.  The fp32 build (kExact: F32 / F32S) evaluates the reference's
+// expression x / (1 + exp(-x)) with libm expf and an IEEE division (~36 VALU per value); the
+// bf16 / fp8 builds use v * rcp(1 + exp(-v)) on v_exp_f32 / v_rcp_f32 (~5 VALU, a few ulp).  The
+// fast form was the fp32 default for part of round 3 (+4 % on the fp32 headline,
+// profiles/r03_silu_ab.txt) and reordered two equal-score detections in frame 0 of the drop-in
+// driver loop (tests/test_pipeline_gpu.py), so the fp32 build keeps the exact form (YK_DIAG bit
+// 64 switches fp32 to the fast form for A/B runs).
 template <bool kExact>
 __device__ __forceinline__ float silu(float v) {
 #if YK_EXACT_SILU
@@ -208,9 +220,6 @@ __device__ __forceinline__ unsigned pack_bf16x2(float a, float b) {
 }
 // x = x0 + x1 + x2 exactly per element, each part bf16 (RNE); the F32S activation operands
 // X00 = [x0 | x0], X11 = [x1 | x1], X20 = [x2 | x0] (one dword per element)
-#ifndef YK_SPLIT_DIAG
-#define YK_SPLIT_DIAG 0  // diagnostic builds only (csrc/build.py YK_DEFINES): 1 no split, 2 no weight loads
-#endif
 __device__ __forceinline__ XS3 split3(const uint4& x) {
   const unsigned u[4] = {x.x, x.y, x.z, x.w};
   XS3 o;
@@ -220,9 +229,6 @@ __device__ __forceinline__ XS3 split3(const uint4& x) {
     o.x20 = u32x4v{u[2], u[3], u[0], u[1]};
     return o;
   }
-#ifndef YK_SPLIT_PK
-#define YK_SPLIT_PK 1  // 0: the scalar remainders (A/B builds only)
-#endif
   if constexpr (!YK_SPLIT_PK) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -1191,9 +1197,6 @@ __device__ __forceinline__ void conv_fast_body(const FastArgs& a, int2 blk, int 
 // Measured (round 3, fp32 headline): 2 lets the large split tiles drop their AGPR accumulators and
 // run two waves per SIMD without spills, but the headline does not move (5,279 vs 5,264 frames/s:
 // those kernels are bound by the split VALU work, not by occupancy); 3 spills (-32 %).
-#ifndef YK_FAST_WPE
-#define YK_FAST_WPE 1
-#endif
 template <class Tr, int NNT, int NPT, bool WS, int SKD>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(YK_FAST_WPE))) conv_fast_kernel(FastArgs a) {
   const int2 blk = xcd_block(a.xcd);
@@ -1692,9 +1695,6 @@ struct HaloArgs {
   int act;
   int xcd;
 };
-#ifndef YK_HALO_DIAG
-#define YK_HALO_DIAG 0  // diagnostic builds only (csrc/build.py YK_DEFINES): 1 no weight loads, 2 no staging, 4 no LDS reads
-#endif
 constexpr int kHaloPx = 256;                                 // pixels per LDS plane
 constexpr int kHaloPlaneB = kHaloPx * 16;                    // bytes per plane
 constexpr size_t kHaloLds = (size_t)2 * 8 * kHaloPlaneB;     // 64 KiB: two workgroups per CU
@@ -2490,11 +2490,13 @@ struct NmsArgs {
                   // outside [0, n_anchors) (the image's count is then 0); read by the host API
 };
 
-// Sort key of a candidate: ascending key = score descending (NaN first, as torch's sort puts it;
-// -0 == +0), then candidate id ascending -- the stable order of scores.sort(descending=True)
+// Sort key of a candidate: ascending key = score descending (every NaN first whatever its sign
+// bit, as torch's sort puts them; -0 == +0), then candidate id ascending -- the stable order of
+// scores.sort(descending=True)
 __device__ __forceinline__ unsigned long long nms_key(float score, int id) {
   unsigned u = __float_as_uint(score);
   if (u == 0x80000000u) u = 0u;
+  if (score != score) u = 0x7fc00000u;  // canonical positive NaN: above +inf in the key order
   const unsigned m = (u & 0x80000000u) ? ~u : (u | 0x80000000u);  // order-preserving float -> uint
   return ((unsigned long long)(~m) << 32) | (unsigned)id;
 }
@@ -4948,6 +4950,11 @@ int yk_nms(yk_model* m, const float* dev_rows, int row_stride, int max_rows, con
   YK_CHECK_ARG(row_stride >= 5, "yk_nms: rows need x1 y1 x2 y2 score (row_stride >= 5)");
   YK_CHECK_ARG(max_rows >= 0 && max_rows <= m->desc.n_anchors, "yk_nms: max_rows exceeds the model's candidate capacity");
   YK_CHECK_ARG(batch >= 1 && batch <= m->desc.max_batch, "yk_nms: batch out of range [1, max_batch]");
+  // every argument check and a pending device error come before nms_load_kernel overwrites the
+  // model's candidate lists (which yk_model_candidates / yk_nms_candidates users may still read)
+  YK_CHECK_ARG(iou >= 0.f && iou <= 1.f, "Invalid IoU, valid values are between 0.0 and 1.0");
+  YK_CHECK_ARG(max_det >= 0 && max_det <= m->desc.max_det, "yk_nms: max_det exceeds the model's capacity");
+  if (const int rc = take_device_error(m)) return rc;
   yk::DeviceGuard guard(m->ctx->device);
   hipStream_t st = (hipStream_t)stream;
   if (max_rows > 0)

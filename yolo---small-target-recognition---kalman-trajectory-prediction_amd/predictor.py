@@ -136,8 +136,9 @@ class YOLO:
     DetectionModel without ultralytics and without executing the pickle, checkpoint.py).
     ``weights`` (YAML models only): None (seeded synthetic weights in the reference's shapes,
     SURVEY §8d), a state dict in the reference's naming, or a path to one saved with
-    torch.save (loaded with weights_only=True).  ``dtype``: 'fp32' (the default: the reference's
-    arithmetic, so the unchanged driver gets the reference's decisions), or the explicit opt-ins
+    torch.save (loaded with weights_only=True).  ``dtype``: 'fp32' (the default: fp32-grade
+    arithmetic with the reference's exact SiLU, so the unchanged driver gets the reference's
+    decisions up to fp32 near-ties), or the explicit opt-ins
     'bf16' / 'fp8' (faster, not parity-capable: their detections differ from the reference's)."""
 
     def __init__(self, model: str = "yolov8s-small.yaml", task=None, verbose: bool = False, *, weights=None,
