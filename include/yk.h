@@ -178,6 +178,33 @@ int yk_tracker_download(yk_tracker* trk, yk_track_out* host_rows, int32_t* host_
  * [16]-[19] shader cycles of the per-track waves (update / lost / new paths). */
 int yk_tracker_phase_ticks(yk_tracker* trk, int stream_index, int64_t* host_ticks, void* stream);
 
+/* Per-step event log of the enhanced policy: what the reference prints inside update()
+ * (enhanced_multi_target_tracker.py:79,89,101,109; enhanced_aircraft_kalman_tracker.py:271,313).
+ * One record per work item of the step: the tracks in list order at the start of the step
+ * (list_pos 0..n-1), then the tracks created this step (list_pos n..). */
+enum yk_track_event_kind { YK_EV_NONE = 0, YK_EV_RECOVERED = 1, YK_EV_LOST = 2, YK_EV_CREATED = 3 };
+typedef struct {
+  int32_t kind;        /* yk_track_event_kind: matched while lost / newly unmatched / new track  */
+  int32_t track_num;
+  int32_t list_pos;    /* position in the step's list (existing tracks first, then new ones)     */
+  int32_t det;         /* matched or source detection, -1 for an unmatched track                 */
+  int32_t lost_frames; /* YK_EV_RECOVERED: lost_frames before the update ("lost for N frames")    */
+  int32_t deleted_tsu; /* >= 0: removed at the end of the step with this time_since_update, else -1 */
+  double iou;          /* YK_EV_RECOVERED: IoU of the matched pair (the greedy match order key)  */
+  double x, y, vx, vy; /* YK_EV_LOST: state after predict (lost_start_state[:2], [4:6])         */
+  double confidence;   /* YK_EV_LOST: motion_analysis['prediction_confidence']                  */
+} yk_track_event;
+
+/* Turn the event log on (1) or off (0, the default: the step writes nothing extra).  Enhanced
+ * policy on the two-launch step only (YK_ERR_STATE otherwise). */
+int yk_tracker_set_events(yk_tracker* trk, int enable);
+
+/* The last step's events of one stream (synchronises `stream`): host_events must hold max_tracks
+ * records; *n_out receives the number of work items (every record up to it is valid, kind
+ * YK_EV_NONE for a track with no event). */
+int yk_tracker_events(yk_tracker* trk, int stream_index, yk_track_event* host_events, int32_t* n_out,
+                      void* stream);
+
 /* Snapshot the live tracks of one stream in list order (EnhancedMultiTargetTracker.trackers).
  * host_states must hold max_tracks entries; *n_out receives the number written. */
 int yk_tracker_snapshot(yk_tracker* trk, int stream_index, yk_track_state* host_states,
@@ -205,8 +232,8 @@ int yk_track_op(yk_tracker* trk, int stream_index, int pos, int op, int arg, con
 
 /* sizeof() of the ABI structs, for bindings that mirror them (0: yk_tracker_cfg,
  * 1: yk_tracker_stats, 2: yk_track_out, 3: yk_track_state, 4: yk_view, 5: yk_op,
- * 6: yk_model_desc, 7: yk_bt_cfg, 8: yk_motion, 9: yk_gmd_stats, 10: yk_tensor); -1 for an
- * unknown id. */
+ * 6: yk_model_desc, 7: yk_bt_cfg, 8: yk_motion, 9: yk_gmd_stats, 10: yk_tensor,
+ * 11: yk_track_event); -1 for an unknown id. */
 int64_t yk_struct_size(int which);
 
 /* Append a new track created from a box (AircraftKalmanTracker.__init__, :23-101) to the
@@ -521,13 +548,13 @@ int yk_memcpy_d2h(void* host_dst, const void* dev_src, int64_t bytes);
  * the loaded library has this header's ABI version and every struct size, else YK_ERR_STATE.
  * Call it once before any other entry point. */
 static inline int yk_abi_check(void) {
-  const int64_t want[11] = {(int64_t)sizeof(yk_tracker_cfg), (int64_t)sizeof(yk_tracker_stats),
+  const int64_t want[12] = {(int64_t)sizeof(yk_tracker_cfg), (int64_t)sizeof(yk_tracker_stats),
                             (int64_t)sizeof(yk_track_out), (int64_t)sizeof(yk_track_state),
                             (int64_t)sizeof(yk_view), (int64_t)sizeof(yk_op), (int64_t)sizeof(yk_model_desc),
                             (int64_t)sizeof(yk_bt_cfg), (int64_t)sizeof(yk_motion), (int64_t)sizeof(yk_gmd_stats),
-                            (int64_t)sizeof(yk_tensor)};
+                            (int64_t)sizeof(yk_tensor), (int64_t)sizeof(yk_track_event)};
   if (yk_abi_version() != YK_ABI_VERSION) return YK_ERR_STATE;
-  for (int i = 0; i < 11; ++i)
+  for (int i = 0; i < 12; ++i)
     if (yk_struct_size(i) != want[i]) return YK_ERR_STATE;
   return YK_OK;
 }

@@ -296,6 +296,8 @@ class RefMultiTracker:
         # diagnostics for parity harnesses: exact IoU ties among candidate pairs
         self.last_iou = None
         self.tie_frames = 0
+        if verbose:  # enhanced_multi_target_tracker.py:40
+            print(f"增强版多目标跟踪器初始化完成 - 最大丢失容忍: {max_lost_frames}帧 ({max_lost_frames/30:.1f}秒)")
 
     def _associate(self, dets, boxes):
         if self.fast_iou and all(isinstance(v, np.float32) for det in dets for v in det[:4]):
@@ -370,8 +372,22 @@ class RefMultiTracker:
                 if info["status"] == "predicted" and info["lost_frames"] > 30:
                     self.stats["long_term_predictions"] += 1
         if self.verbose and self.frame_count % 100 == 0:
-            print(f"\n=== 跟踪统计 (帧 {self.frame_count}) ===")
+            self._print_statistics()
         return out
+
+    def _print_statistics(self):
+        # enhanced_multi_target_tracker.py:272-287
+        print(f"\n=== 跟踪统计 (帧 {self.frame_count}) ===")
+        print(f"当前活跃轨迹: {self.stats['current_active_tracks']}")
+        print(f"总创建轨迹: {self.stats['total_tracks_created']}")
+        print(f"总终止轨迹: {self.stats['total_tracks_terminated']}")
+        print(f"成功恢复次数: {self.stats['successful_recoveries']}")
+        print(f"长期预测次数: {self.stats['long_term_predictions']}")
+        for t in self.trackers:
+            status = "丢失" if t.is_lost else "正常"
+            confidence = t.motion_analysis.get("prediction_confidence", 0.0)
+            print(f"  {t.track_id}: {status}, 年龄:{t.age}, "
+                  f"命中:{t.hits}, 丢失:{t.lost_frames}, 置信度:{confidence:.2f}")
 
     def get_statistics(self):
         return {**self.stats, "frame_count": self.frame_count,

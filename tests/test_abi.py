@@ -48,6 +48,7 @@ def test_struct_sizes_match_python_mirrors():
     assert lib.yk_struct_size(8) == L.MOTION_DTYPE.itemsize
     assert lib.yk_struct_size(9) == L.GMD_STATS_DTYPE.itemsize
     assert lib.yk_struct_size(10) == ctypes.sizeof(L.Tensor)
+    assert lib.yk_struct_size(11) == L.TRACK_EVENT_DTYPE.itemsize
     assert lib.yk_struct_size(99) == -1
 
 

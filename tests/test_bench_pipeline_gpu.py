@@ -47,12 +47,12 @@ def _threads():
     return max(1, min(16, n))
 
 
-@pytest.fixture(scope="module")
-def chain():
+def build_chain(seeds, n_frames, targets):
     """Frames (rendered once on the CPU, the same arrays for both sides) and the oracle chain's
-    per-frame detections and track dicts for every stream."""
+    per-frame detections and track dicts for every stream (scene seed per stream)."""
     P = pkg()
-    scenes = [P.synth.Scene(seed=P.shard.stream_seed(s, S), n_targets=TARGETS, n_frames=F + 1) for s in range(S)]
+    S, F = len(seeds), n_frames
+    scenes = [P.synth.Scene(seed=sd, n_targets=targets, n_frames=F + 1) for sd in seeds]
     frames = torch.stack([sc.frames_torch(0, F, "cpu") for sc in scenes], 1)  # [F, S, H, W, 3]
     ar = P.arch.parse_arch(P.arch.load_model_dict("yolov8s-small.yaml"))
     sd = P.weights.synthetic_state_dict(ar, 0)
@@ -71,7 +71,14 @@ def chain():
     return {"frames": frames, "dets": dets, "tracks": tracks, "nms_score_ties": ties, "near": near,
             "tie_frames": sum(tr.tie_frames for tr in trks),
             "terminated": sum(tr.stats["total_tracks_terminated"] for tr in trks),
-            "live": [len(tr.trackers) for tr in trks]}
+            "live": [len(tr.trackers) for tr in trks], "S": S, "F": F}
+
+
+@pytest.fixture(scope="module")
+def chain():
+    """bench.py config 3's streams: seeds shard.stream_seed(s, 8), 40 targets each."""
+    P = pkg()
+    return build_chain([P.shard.stream_seed(s, S) for s in range(S)], F, TARGETS)
 
 
 def _run_gpu(dtype, frames, plan=None):
@@ -79,6 +86,7 @@ def _run_gpu(dtype, frames, plan=None):
     import importlib
 
     pipeline = importlib.import_module(P.__name__ + ".pipeline")
+    F, S = frames.shape[:2]
     pipe = pipeline.StreamPipeline("yolov8s-small.yaml", S, (512, 640), dtype, seed=0, max_tracks=512,
                                    pipelined=True, inflight=4)
     pipe.set_schedule(1, 1)  # bench.py's schedule with 3 forwards in flight
@@ -128,10 +136,20 @@ def test_bench_pipeline_fp32_matches_oracle_chain_every_frame(chain, plan):
     deviation is reported and bounded (1e-2).  Tracker bar on identical input: the oracle tracker
     fed the GPU's own detections matches the GPU tracker to 1e-9 on every output float
     (test_tracker_gpu.compare_frame)."""
+    out = check_chain(chain, PLANS[plan], parity_record=plan == "committed")
+    assert min(chain["live"]) >= 40, chain["live"]  # the bench's >= 64-track load (see bench.py CONFIGS)
+    assert chain["terminated"] > 0  # the deletion path ran inside the chain
+    assert out["near_tie_flips"] + out["order_ties"] <= 3
+
+
+def check_chain(chain, plan_path, parity_record=False):
+    """The resynced chain comparison of test_bench_pipeline_fp32_matches_oracle_chain_every_frame
+    for any stream count (chain from build_chain); returns the summary it prints."""
     from gpu_helpers import resync_rows
     from test_tracker_gpu import compare_frame
 
-    dets, counts, rows, tcounts, stats = _run_gpu("fp32", chain["frames"], PLANS[plan])
+    S, F = chain["S"], chain["F"]
+    dets, counts, rows, tcounts, stats = _run_gpu("fp32", chain["frames"], plan_path)
     assert int(stats[-1]["overflow"].sum()) == 0
     conf_dev, box_rel, n_tracks, n_outputs = 0.0, 0.0, 0, 0
     flips, flip_scores, order_ties = [], [], []
@@ -172,26 +190,36 @@ def test_bench_pipeline_fp32_matches_oracle_chain_every_frame(chain, plan):
     live = [int(tcounts[-1, s]) for s in range(S)]
     for fs in flip_scores:
         print("NEAR_TIE_FLIP", json.dumps(fs))
-    print("BENCH_PIPELINE_FP32", json.dumps({"plan": PLANS[plan], "frames": F, "streams": S,
-                                             "stream_frames_compared": F * S, "track_outputs_compared": n_tracks,
-                                             "live_tracks_end": live, "near_tie_flips": flips,
-                                             "order_ties": order_ties,
-                                             "oracle_near_tie_boxes": int(sum(len(b) for fr in chain["near"] for b in fr)),
-                                             "max_box_rel_dev": box_rel, "max_confidence_abs_dev": conf_dev,
-                                             "oracle_tie_frames": chain["tie_frames"],
-                                             "nms_early_exit": _run_gpu.nms,
-                                             "nms_score_ties": chain["nms_score_ties"],
-                                             "terminated": chain["terminated"]}))
+    summary = {"plan": plan_path, "frames": F, "streams": S, "stream_frames_compared": F * S,
+               "track_outputs_compared": n_tracks, "live_tracks_end": live, "near_tie_flips": len(flips),
+               "near_tie_flip_frames": flips, "order_ties": len(order_ties), "order_tie_frames": order_ties,
+               "oracle_near_tie_boxes": int(sum(len(b) for fr in chain["near"] for b in fr)),
+               "max_box_rel_dev": box_rel, "max_confidence_abs_dev": conf_dev,
+               "oracle_tie_frames": chain["tie_frames"], "nms_early_exit": _run_gpu.nms,
+               "nms_score_ties": chain["nms_score_ties"], "terminated": chain["terminated"]}
+    print("BENCH_PIPELINE_FP32", json.dumps(summary))
     assert n_tracks == n_outputs  # every track output of every stream-frame compared
-    assert len(flips) + len(order_ties) <= 3, (flips, order_ties)
-    if plan == "committed":  # the count bench.py's line reports for its plan
-        with open(os.path.join(REPO, PLANS[plan])) as f:
+    if parity_record:  # the count bench.py's line reports for this plan
+        with open(os.path.join(REPO, plan_path)) as f:
             rec = json.load(f).get("parity", {})
-        assert rec.get("near_tie_flips") == len(flips) and rec.get("order_ties") == len(order_ties), (rec, flips, order_ties)
+        assert rec.get("near_tie_flips") == len(flips) and rec.get("order_ties") == len(order_ties), \
+            (rec, flips, order_ties)
     assert _run_gpu.nms["images"] == S * F  # every frame's NMS ran once on the device
     assert conf_dev <= 1e-2
-    assert min(chain["live"]) >= 40, chain["live"]  # the bench's >= 64-track load (see bench.py CONFIGS)
-    assert chain["terminated"] > 0  # the deletion path ran inside the chain
+    return summary
+
+
+@pytest.mark.timeout(900)
+def test_config4_rank_leg_b1_fp32_plan_matches_oracle_chain():
+    """BASELINE config 4's per-rank leg (one stream per GPU, bench.py --config 4): the committed
+    batch-1 fp32 plan (plans/s_640x512_i640_b1_fp32.json) under the same resynced chain bar as
+    config 3, on rank 5's stream (scene seed shard.stream_seed(5, 1) = 5000, 40 targets), 160
+    frames with >= 64 live tracks at the end."""
+    P = pkg()
+    ch = build_chain([P.shard.stream_seed(5, 1)], F, TARGETS)
+    out = check_chain(ch, "plans/s_640x512_i640_b1_fp32.json", parity_record=True)
+    assert min(out["live_tracks_end"]) >= 64, out["live_tracks_end"]
+    assert ch["terminated"] > 0
 
 
 @pytest.mark.timeout(900)
@@ -230,3 +258,49 @@ def _iou(a, b):
     inter = ix * iy
     area = lambda z: (z[..., 2] - z[..., 0]) * (z[..., 3] - z[..., 1])  # noqa: E731
     return inter / (area(a) + area(b) - inter)
+
+
+@pytest.mark.timeout(900)
+def test_config2_b1_bf16_plan_properties_and_tracker():
+    """BASELINE config 2 (batch 1, bf16, 16 tracks; bench.py --config 2) on its committed plan
+    (plans/s_640x512_i640_b1_bf16.json).  bf16 is not parity-capable, so the detections are held
+    by property against the fp32 oracle on every frame -- count within 15 % (or 2), recall and
+    precision at IoU > 0.5 >= 0.9 over the run, scores descending and > conf, boxes inside the
+    frame, no two kept boxes above the NMS IoU threshold (0.7) -- and the device tracker on those
+    detections is held bit for bit (1e-9 floats) to RefMultiTracker fed the same rows."""
+    from test_tracker_gpu import compare_frame
+
+    P = pkg()
+    Fc = 100
+    ch = build_chain([P.shard.stream_seed(0, 1)], Fc, 12)
+    dets, counts, rows, tcounts, stats = _run_gpu("bf16", ch["frames"], "plans/s_640x512_i640_b1_bf16.json")
+    assert int(stats[-1]["overflow"].sum()) == 0
+    iso = RefMultiTracker(150, 1, 0.1, stable_ties=True, fast_iou=True)
+    tp_r = n_ref = tp_p = n_got = 0
+    for t in range(Fc):
+        want = ch["dets"][t][0]
+        got = dets[t, 0, : counts[t, 0]]
+        assert abs(len(got) - len(want)) <= max(2, int(0.15 * len(want))), (t, len(got), len(want))
+        if len(got):
+            sc = got[:, 4]
+            assert np.all(np.diff(sc) <= 0) and np.all(sc > 0.25), t
+            assert np.all(got[:, [0, 2]] >= 0) and np.all(got[:, [0, 2]] <= 640), t
+            assert np.all(got[:, [1, 3]] >= 0) and np.all(got[:, [1, 3]] <= 512), t
+            io = _iou(got[:, :4], got[:, :4])
+            np.fill_diagonal(io, 0)
+            assert float(io.max()) <= 0.7 + 1e-6, t  # NMS left no pair above its threshold
+        if len(got) and len(want):
+            io = _iou(want[:, :4], got[:, :4])
+            tp_r += int((io.max(1) > 0.5).sum())
+            tp_p += int((io.max(0) > 0.5).sum())
+        n_ref += len(want)
+        n_got += len(got)
+        ours = track_dicts(rows[t, 0], int(tcounts[t, 0]))
+        compare_frame(ours, iso.update([[d[0], d[1], d[2], d[3], d[4]] for d in got[:, :5]]), f"config 2 frame {t}")
+    recall, precision = tp_r / max(n_ref, 1), tp_p / max(n_got, 1)
+    live = int(tcounts[-1, 0])
+    print("CONFIG2_B1_BF16", json.dumps({"frames": Fc, "recall_iou50": round(recall, 4),
+                                         "precision_iou50": round(precision, 4), "live_tracks_end": live,
+                                         "detections": n_got, "oracle_detections": n_ref}))
+    assert recall >= 0.9 and precision >= 0.9
+    assert live >= 16

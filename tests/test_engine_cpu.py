@@ -50,3 +50,31 @@ def test_c_host_example_compiles_and_links(tmp_path):
     r = subprocess.run([gcc, "-shared", str(obj), "-L", pkgdir, "-l:libyk.so",
                         "-Wl,--unresolved-symbols=ignore-in-shared-libs", "-o", str(so)], capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
+
+
+def test_event_lines_order_and_format():
+    """tracker.event_lines on hand-made event records: recoveries by IoU descending then detection,
+    losses / creations / deletions by list position; the reference's strings and number formats
+    (enhanced_multi_target_tracker.py:79,89,101,109; enhanced_aircraft_kalman_tracker.py:271,313)."""
+    import numpy as np
+
+    from conftest import pkg
+
+    P = pkg()
+    L = P._lib
+    ev = np.zeros(6, dtype=L.TRACK_EVENT_DTYPE)
+    ev["deleted_tsu"] = -1
+    ev[0] = (L.EV_RECOVERED, 3, 0, 2, 4, -1, 0.5, 0, 0, 0, 0, 0)
+    ev[1] = (L.EV_LOST, 5, 1, -1, 0, 0, 0.0, 12.345, -0.04, 1.005, -2.0, 0.125)
+    ev[2] = (L.EV_RECOVERED, 1, 2, 0, 1, -1, 0.75, 0, 0, 0, 0, 0)
+    ev[3] = (L.EV_NONE, 7, 3, -1, 0, 151, 0.0, 0, 0, 0, 0, 0)
+    ev[4] = (L.EV_CREATED, 12, 4, 1, 0, -1, 0.0, 0, 0, 0, 0, 0)
+    ev[5] = (L.EV_RECOVERED, 9, 5, 1, 2, -1, 0.5, 0, 0, 0, 0, 0)
+    assert P.tracker.event_lines(ev) == [
+        "目标 T001 重新检测到，丢失了 1 帧", "跟踪器 T001 重新检测到，切换回检测模式",
+        "目标 T009 重新检测到，丢失了 2 帧", "跟踪器 T009 重新检测到，切换回检测模式",
+        "目标 T003 重新检测到，丢失了 4 帧", "跟踪器 T003 重新检测到，切换回检测模式",
+        f"目标 T005 丢失 - 位置: [{12.345:.1f}, {-0.04:.1f}], 速度: [{1.005:.2f}, {-2.0:.2f}], 运动置信度: {0.125:.2f}",
+        "跟踪器 T005 丢失检测，切换到预测模式",
+        "创建新跟踪器: T012",
+        "删除跟踪器 T005 - 丢失时间: 0帧", "删除跟踪器 T007 - 丢失时间: 151帧"]

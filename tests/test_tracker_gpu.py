@@ -216,3 +216,39 @@ def test_config5_tracker_leg_256_tracks_150_frame_bursts():
                                              "live_end": [len(r.trackers) for r in refs],
                                              "terminated": [r.stats["total_tracks_terminated"] for r in refs],
                                              "tie_frames": [r.tie_frames for r in refs]}))
+
+
+@pytest.mark.parametrize("max_lost,min_hits,thr,frames_n", [(30, 1, 0.1, 220), (450, 3, 0.3, 110), (0, 1, 0.1, 40)])
+def test_tracker_event_messages_match_oracle(capsys, max_lost, min_hits, thr, frames_n):
+    """verbose=True: the device event log (yk_tracker_set_events / yk_tracker_events) replayed by
+    tracker.event_lines prints exactly the reference's lines, frame by frame -- init (:40),
+    recoveries (kf.py:271 + multi:79, greedy match order), losses (kf.py:313 + multi:89, list
+    order), creations (multi:101), deletions (multi:109), and the 100-frame statistics block with
+    its per-tracker lines (multi:272-287) -- against RefMultiTracker(verbose=True).  max_lost 0
+    removes a track on the step it is lost (a loss and a deletion in one step)."""
+    yk = pkg()
+    sc = yk.synth.Scene(seed=11, n_targets=24, n_frames=frames_n)
+    ours = yk.EnhancedMultiTargetTracker(max_lost, min_hits, thr, verbose=True)
+    a0 = capsys.readouterr().out
+    ref = RefMultiTracker(max_lost, min_hits, thr, verbose=True, stable_ties=True)
+    b0 = capsys.readouterr().out
+    assert a0 == b0 and a0.startswith("增强版多目标跟踪器初始化完成")
+    kinds = {"recover": 0, "lost": 0, "create": 0, "delete": 0, "stats": 0}
+    for t in range(sc.T):
+        dets = sc.detections(t)
+        ours.update(dets)
+        a = capsys.readouterr().out
+        ref.update(dets)
+        b = capsys.readouterr().out
+        assert a == b, f"frame {t}:\n--- device\n{a}\n--- oracle\n{b}"
+        kinds["recover"] += b.count("切换回检测模式")
+        kinds["lost"] += b.count("切换到预测模式")
+        kinds["create"] += b.count("创建新跟踪器")
+        kinds["delete"] += b.count("删除跟踪器")
+        kinds["stats"] += b.count("=== 跟踪统计")
+    print("EVENT_MESSAGES", max_lost, min_hits, thr, kinds)
+    assert kinds["lost"] > 0 and kinds["create"] > 0 and kinds["recover"] > 0
+    if max_lost != 450:
+        assert kinds["delete"] > 0
+    if frames_n >= 100:
+        assert kinds["stats"] >= 1

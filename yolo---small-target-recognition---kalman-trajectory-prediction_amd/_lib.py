@@ -60,6 +60,13 @@ STATS_DTYPE = np.dtype([(k, np.int64) for k in (
 
 GMD_OPTICAL_FLOW, GMD_FEATURE_MATCHING, GMD_HYBRID = 0, 1, 2
 GMD_METHODS = {"optical_flow": GMD_OPTICAL_FLOW, "feature_matching": GMD_FEATURE_MATCHING, "hybrid": GMD_HYBRID}
+# yk_track_event (include/yk.h): one record per work item of a step
+TRACK_EVENT_DTYPE = np.dtype([("kind", np.int32), ("track_num", np.int32), ("list_pos", np.int32), ("det", np.int32),
+                              ("lost_frames", np.int32), ("deleted_tsu", np.int32), ("iou", np.float64),
+                              ("x", np.float64), ("y", np.float64), ("vx", np.float64), ("vy", np.float64),
+                              ("confidence", np.float64)])
+EV_NONE, EV_RECOVERED, EV_LOST, EV_CREATED = 0, 1, 2, 3
+
 MOTION_DTYPE = np.dtype([("valid", np.int32), ("is_motion", np.int32), ("should_reset", np.int32),
                          ("magnitude_kind", np.int32), ("magnitude", np.float32), ("vector", np.float32, (2,)),
                          ("consistency", np.float32), ("n_corners", np.int32), ("n_tracked", np.int32),
@@ -153,6 +160,8 @@ _SIGS = {
     "yk_model_profile": ([_vp, _vp, C.c_int, C.c_float, C.c_float, C.c_int, C.c_int, _vp, _vp], C.c_int),
     "yk_model_op_kernel": ([_vp, C.c_int, C.c_char_p, C.c_int], C.c_int),
     "yk_tracker_phase_ticks": ([_vp, C.c_int, _vp, _vp], C.c_int),
+    "yk_tracker_set_events": ([_vp, C.c_int], C.c_int),
+    "yk_tracker_events": ([_vp, C.c_int, _vp, _vp, _vp], C.c_int),
     "yk_model_set_lanes": ([_vp, C.c_int], C.c_int),
     "yk_model_set_schedule": ([_vp, C.c_int, C.c_int], C.c_int),
     "yk_model_set_plan": ([_vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int], C.c_int),
@@ -222,7 +231,7 @@ def lib() -> C.CDLL:
             raise YKError(f"libyk.so ABI version {L.yk_abi_version()}, this package expects {ABI_VERSION}")
         sizes = {0: C.sizeof(TrackerCfg), 1: STATS_DTYPE.itemsize, 2: TRACK_OUT_DTYPE.itemsize,
                  3: TRACK_STATE_DTYPE.itemsize, 7: C.sizeof(BtCfg), 8: MOTION_DTYPE.itemsize,
-                 9: GMD_STATS_DTYPE.itemsize, 10: C.sizeof(Tensor)}
+                 9: GMD_STATS_DTYPE.itemsize, 10: C.sizeof(Tensor), 11: TRACK_EVENT_DTYPE.itemsize}
         for k, v in sizes.items():
             if L.yk_struct_size(k) != v:
                 raise YKError(f"ABI struct {k} size mismatch: C {L.yk_struct_size(k)} vs python {v}")

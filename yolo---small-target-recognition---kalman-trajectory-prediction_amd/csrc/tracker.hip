@@ -119,6 +119,7 @@ struct Dev {
   int4* items;              // [S][T] enhanced two-kernel step: {slot, det, track_num, out_row} per work item
   int2* items_vh;           // [S][T] {vh_len, vh_head} of the item's slot before the step
   int* n_items;             // [S]
+  yk_track_event* events;   // [S][T] per-work-item event log (yk_tracker_set_events), or NULL
   int T, D, C;
   int max_lost, min_hits;
   double thr;
@@ -1537,7 +1538,8 @@ __device__ __forceinline__ int xbin(double x, double x0, double ibw, int nb) {
 // rev: among equal IoUs the highest (d, t) first (the motion-reset tracker's reversed sort of
 // (iou, d, t) tuples, motion_compensated_multi_tracker.py:262-270), else the lowest
 __device__ __forceinline__ void assoc_rounds(const LdsA& L, const unsigned long long* ckey, const int* cpid, int nc,
-                                             int D, int n, long long* round_out, bool rev) {
+                                             int D, int n, long long* round_out, bool rev,
+                                             yk_track_event* ev = nullptr) {
   const int tid = threadIdx.x;
   for (int round = 0; round <= D + 1; ++round) {
     for (int d = tid; d < D; d += NTA) {
@@ -1584,6 +1586,7 @@ __device__ __forceinline__ void assoc_rounds(const LdsA& L, const unsigned long 
       if (L.row_arg[d] == rk && L.col_arg[t] == rk && L.det_match[d] < 0 && L.trk_match[t] < 0) {
         L.det_match[d] = t;
         L.trk_match[t] = d;
+        if (ev) ev[t].iou = __longlong_as_double((long long)ckey[c]);  // the event log's match order key
       }
     }
     __syncthreads();
@@ -1603,6 +1606,8 @@ __global__ void __launch_bounds__(NTA) assoc_kernel(Dev g, const DT* __restrict_
   int* order = g.order + (size_t)s * T;
   int* fstack = g.free_stack + (size_t)s * T;
   int* wsum = L.misc + MA_WSUM;
+  // event log (enhanced policy only): written only when the host enabled it
+  yk_track_event* evs = (!POL && g.events) ? g.events + (size_t)s * T : nullptr;
 
   const long long cyc0 = clock64();  // shader clock: phase[15] = cycles of this kernel (clock check)
   if (tid == 0) g.phase[s * PH + 0] = wall_clock64();
@@ -1816,7 +1821,7 @@ __global__ void __launch_bounds__(NTA) assoc_kernel(Dev g, const DT* __restrict_
     // LDS head joins the global tail, and the rounds read them where the boxes were (dead now)
     // when they fit there, else from global memory
     if (nc <= L.ccap) {
-      assoc_rounds(L, L.ck, L.cp, nc, D, n, g.phase + s * PH + 10, POL != 0);
+      assoc_rounds(L, L.ck, L.cp, nc, D, n, g.phase + s * PH + 10, POL != 0, evs);
     } else {
       for (int c = tid; c < L.ccap; c += NTA) {
         ckey[c] = L.ck[c];
@@ -1832,9 +1837,9 @@ __global__ void __launch_bounds__(NTA) assoc_kernel(Dev g, const DT* __restrict_
           lp[c] = cflat[c];
         }
         __syncthreads();
-        assoc_rounds(L, lk, lp, nc, D, n, g.phase + s * PH + 10, POL != 0);
+        assoc_rounds(L, lk, lp, nc, D, n, g.phase + s * PH + 10, POL != 0, evs);
       } else {
-        assoc_rounds(L, ckey, cflat, nc, D, n, g.phase + s * PH + 10, POL != 0);
+        assoc_rounds(L, ckey, cflat, nc, D, n, g.phase + s * PH + 10, POL != 0, evs);
       }
     }
   } else if (tid == 0) {  // no pairs: an empty candidate phase, no rounds
@@ -1869,6 +1874,11 @@ __global__ void __launch_bounds__(NTA) assoc_kernel(Dev g, const DT* __restrict_
       recov += (m && sl.is_lost) ? 1 : 0;
       const bool q = hs >= g.min_hits || fc <= g.min_hits || !m;
       flags[i] = (del ? 0 : 1) | (q ? 2 : 0) | (tsu > 30 ? 4 : 0);
+      if (evs) {  // multi:104-110: removed with this time_since_update
+        evs[i].list_pos = i;
+        evs[i].det = L.trk_match[i];
+        evs[i].deleted_tsu = del ? tsu : -1;
+      }
     }
   }
   if (recov) atomicAdd(&L.misc[M_RECOVER], recov);
@@ -1887,6 +1897,11 @@ __global__ void __launch_bounds__(NTA) assoc_kernel(Dev g, const DT* __restrict_
       if (pos < T && r < nfree0) {
         L.order_tmp[pos] = fstack[nfree0 - 1 - r];
         newdet[r] = d;
+        if (evs) {
+          evs[pos].list_pos = pos;
+          evs[pos].det = d;
+          evs[pos].deleted_tsu = -1;
+        }
         // a new track: age 0, hit_streak 1, tsu 0, not lost (kf.py:32-101)
         flags[pos] = 1 | ((POL || 1 >= g.min_hits || fc <= g.min_hits) ? 2 : 0);
       } else {
@@ -2035,18 +2050,37 @@ __global__ void __launch_bounds__(NT) tracks_kernel(Dev g, const DT* __restrict_
     const int4 w = it[j];
     Slot& gs = slots[w.x];
     LSlot sl;
+    yk_track_event* ev = g.events ? g.events + (size_t)s * g.T + base + j : nullptr;
     if (w.z < 0) {
       lslot_load(sl, gs);
+      const int was_lost = sl.is_lost, lost_before = sl.lost_frames;
       kf_predict(sl);  // multi:55-58
       if (w.y >= 0) {  // multi:71-80
         DT db[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) db[k] = dets[((size_t)s * g.D + w.y) * row_stride + k];
         kf_update<DT>(sl, db, stage + (size_t)j * STAGE_D);
+        if (ev) {  // kf.py:264-271, multi:76-79
+          ev->kind = was_lost ? YK_EV_RECOVERED : YK_EV_NONE;
+          ev->lost_frames = lost_before;
+        }
       } else {
+        if (ev) {  // kf.py:305-314 (state after predict), multi:86-89
+          ev->kind = was_lost ? YK_EV_NONE : YK_EV_LOST;
+          ev->x = sl.x[0];
+          ev->y = sl.x[1];
+          ev->vx = sl.x[4];
+          ev->vy = sl.x[5];
+          ev->confidence = sl.pconf;
+        }
         mark_lost(sl);  // multi:83-89
       }
+      if (ev) ev->track_num = sl.track_num;
     } else {  // multi:92-101
+      if (ev) {
+        ev->kind = YK_EV_CREATED;
+        ev->track_num = w.z;
+      }
       DT db[4];
 #pragma unroll
       for (int k = 0; k < 4; ++k) db[k] = dets[((size_t)s * g.D + w.y) * row_stride + k];
@@ -2237,6 +2271,7 @@ struct yk_tracker {
   size_t lds_assoc;
   bool split;  // assoc_kernel + tracks_kernel (else one workgroup per stream: YK_TRK_SINGLE=1 / LDS)
   yk_track_state* d_snap;
+  yk_track_event* d_events;  // allocated by the first yk_tracker_set_events(1)
   yk_track_out* d_row1;
   double* d_box;  // [8]: in[4], out[4]
   int* d_status;
@@ -2341,7 +2376,8 @@ int yk_tracker_destroy(yk_tracker* t) {
   yk::DeviceGuard guard(t->ctx->device);
   Dev& g = t->dev;
   void* ptrs[] = {g.slots, g.hdr, g.order, g.free_stack, g.cand_key, g.cand_flat, g.rows,
-                  g.counts, g.stats, g.items, g.items_vh, g.n_items, g.phase, t->d_snap, t->d_row1, t->d_box, t->d_status};
+                  g.counts, g.stats, g.items, g.items_vh, g.n_items, g.phase, t->d_events, t->d_snap, t->d_row1,
+                  t->d_box, t->d_status};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   delete t;
@@ -2520,6 +2556,49 @@ int yk_track_create(yk_tracker* t, int s, const double* box, int dtype, int32_t 
     yk::set_error("yk_track_create: stream is at max_tracks capacity");
     return YK_ERR_CAPACITY;
   }
+  return YK_OK;
+}
+
+int yk_tracker_set_events(yk_tracker* t, int enable) {
+  YK_CHECK_ARG(t, "yk_tracker_set_events: NULL tracker");
+  yk::DeviceGuard guard(t->ctx->device);
+  if (!enable) {
+    t->dev.events = nullptr;  // the buffer stays allocated for a later enable
+    return YK_OK;
+  }
+  if (t->cfg.policy != YK_POLICY_ENHANCED || !t->split) {
+    yk::set_error("yk_tracker_set_events: the event log is written by the enhanced policy's two-launch step only");
+    return YK_ERR_STATE;
+  }
+  if (!t->d_events) {
+    const size_t bytes = (size_t)t->S * t->dev.T * sizeof(yk_track_event);
+    YK_HIP(hipMalloc((void**)&t->d_events, bytes));
+    YK_HIP(hipMemset(t->d_events, 0, bytes));
+    YK_HIP(hipDeviceSynchronize());
+  }
+  t->dev.events = t->d_events;
+  return YK_OK;
+}
+
+int yk_tracker_events(yk_tracker* t, int s, yk_track_event* host_events, int32_t* n_out, void* stream) {
+  YK_CHECK_ARG(t && host_events && n_out, "yk_tracker_events: NULL argument");
+  YK_CHECK_ARG(s >= 0 && s < t->S, "yk_tracker_events: stream index out of range");
+  if (!t->dev.events) {
+    yk::set_error("yk_tracker_events: the event log is off (yk_tracker_set_events)");
+    return YK_ERR_STATE;
+  }
+  yk::DeviceGuard guard(t->ctx->device);
+  hipStream_t st = (hipStream_t)stream;
+  int n = 0;
+  YK_HIP(hipMemcpyAsync(&n, t->dev.n_items + s, sizeof(int), hipMemcpyDeviceToHost, st));
+  YK_HIP(hipStreamSynchronize(st));
+  if (n < 0 || n > t->dev.T) n = 0;
+  if (n > 0) {
+    YK_HIP(hipMemcpyAsync(host_events, t->dev.events + (size_t)s * t->dev.T, n * sizeof(yk_track_event),
+                          hipMemcpyDeviceToHost, st));
+    YK_HIP(hipStreamSynchronize(st));
+  }
+  *n_out = n;
   return YK_OK;
 }
 

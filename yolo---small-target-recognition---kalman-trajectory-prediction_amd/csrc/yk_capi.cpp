@@ -43,6 +43,7 @@ int64_t yk_struct_size(int which) {
     case 8: return (int64_t)sizeof(yk_motion);
     case 9: return (int64_t)sizeof(yk_gmd_stats);
     case 10: return (int64_t)sizeof(yk_tensor);
+    case 11: return (int64_t)sizeof(yk_track_event);
     default: return -1;
   }
 }

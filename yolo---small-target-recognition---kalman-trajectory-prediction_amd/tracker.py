@@ -217,6 +217,18 @@ class MultiStreamTracker:
                 "yk_tracker_outputs")
         return rows.value, counts.value, stats.value
 
+    def set_events(self, enable: bool = True):
+        """Turn the per-step event log on / off (yk_tracker_set_events; enhanced policy)."""
+        L.check(L.lib().yk_tracker_set_events(self._h, int(bool(enable))), "yk_tracker_set_events")
+
+    def events(self, stream_index: int = 0) -> np.ndarray:
+        """The last step's event records of one stream (TRACK_EVENT_DTYPE, one per work item)."""
+        out = np.zeros(self.max_tracks, dtype=L.TRACK_EVENT_DTYPE)
+        n = C.c_int32()
+        L.check(L.lib().yk_tracker_events(self._h, int(stream_index), L.ptr(out), C.byref(n),
+                                          L.current_stream(self.device)), "yk_tracker_events")
+        return out[: n.value].copy()
+
     def phase_us(self, stream_index: int = 0):
         """Per-phase device time (µs) of the last step on one stream (wall clock of the stream's
         workgroup) and the association rounds used.  Single-workgroup step: predict, candidates,
@@ -257,6 +269,32 @@ class MultiStreamTracker:
         b = np.ascontiguousarray(np.asarray(box, dtype=np.float64)[:4])
         L.check(L.lib().yk_track_create(self._h, int(stream_index), L.ptr(b), int(dtype), int(track_num),
                                         int(max_lost_frames), L.current_stream(self.device)), "yk_track_create")
+
+
+def event_lines(ev: np.ndarray) -> list[str]:
+    """The console lines EnhancedMultiTargetTracker.update() prints for one step, from the step's
+    device event records (TRACK_EVENT_DTYPE), in the reference's order: the matched tracks that
+    were lost, in the greedy match order -- IoU descending, then row-major (detection) order, the
+    order _solve_assignment_problem appends pairs (enhanced_multi_target_tracker.py:234-270) --
+    each with AircraftKalmanTracker.update's line (enhanced_aircraft_kalman_tracker.py:271) then
+    the tracker's (:79); the newly unmatched tracks in list order (mark_as_lost's line, kf.py:313,
+    then :89); the new tracks in detection order (:101); the removed tracks in list order (:109)."""
+    lines = []
+    rec = ev[ev["kind"] == L.EV_RECOVERED]
+    for r in sorted(rec, key=lambda r: (-float(r["iou"]), int(r["det"]))):
+        tid = track_id_of(r["track_num"])
+        lines.append(f"目标 {tid} 重新检测到，丢失了 {int(r['lost_frames'])} 帧")
+        lines.append(f"跟踪器 {tid} 重新检测到，切换回检测模式")
+    for r in sorted(ev[ev["kind"] == L.EV_LOST], key=lambda r: int(r["list_pos"])):
+        tid = track_id_of(r["track_num"])
+        lines.append(f"目标 {tid} 丢失 - 位置: [{float(r['x']):.1f}, {float(r['y']):.1f}], "
+                     f"速度: [{float(r['vx']):.2f}, {float(r['vy']):.2f}], 运动置信度: {float(r['confidence']):.2f}")
+        lines.append(f"跟踪器 {tid} 丢失检测，切换到预测模式")
+    for r in sorted(ev[ev["kind"] == L.EV_CREATED], key=lambda r: int(r["list_pos"])):
+        lines.append(f"创建新跟踪器: {track_id_of(r['track_num'])}")
+    for r in sorted(ev[ev["deleted_tsu"] >= 0], key=lambda r: int(r["list_pos"])):
+        lines.append(f"删除跟踪器 {track_id_of(r['track_num'])} - 丢失时间: {int(r['deleted_tsu'])}帧")
+    return lines
 
 
 def _box_dtype(bbox):
@@ -491,7 +529,8 @@ class EnhancedMultiTargetTracker:
         self._stats = np.zeros(1, dtype=L.STATS_DTYPE)[0]
         self._stats["next_track_id"] = 1
         self._snap = None
-        if verbose:
+        if verbose:  # the reference prints its lifecycle messages (enhanced_multi_target_tracker.py:40,79-109)
+            self._core.set_events(True)
             print(f"增强版多目标跟踪器初始化完成 - 最大丢失容忍: {max_lost_frames}帧 ({max_lost_frames/30:.1f}秒)")
 
     @property
@@ -526,8 +565,11 @@ class EnhancedMultiTargetTracker:
         if int(self._stats["overflow"]):
             raise L.YKError(f"tracker capacity exceeded (max_tracks={self._core.max_tracks})")
         out = [_row_to_dict(r, track_id_of(r["track_num"])) for r in rows[0, : int(counts[0])]]
-        if self.verbose and self.frame_count % 100 == 0:
-            self._print_statistics()
+        if self.verbose:
+            for line in event_lines(self._core.events(0)):
+                print(line)
+            if self.frame_count % 100 == 0:
+                self._print_statistics()
         return out
 
     def _print_statistics(self):
@@ -538,6 +580,10 @@ class EnhancedMultiTargetTracker:
         print(f"总终止轨迹: {s['total_tracks_terminated']}")
         print(f"成功恢复次数: {s['successful_recoveries']}")
         print(f"长期预测次数: {s['long_term_predictions']}")
+        for t in self._snapshot():  # enhanced_multi_target_tracker.py:282-287, list order
+            status = "丢失" if t["is_lost"] else "正常"
+            print(f"  {track_id_of(t['track_num'])}: {status}, 年龄:{int(t['age'])}, "
+                  f"命中:{int(t['hits'])}, 丢失:{int(t['lost_frames'])}, 置信度:{float(t['prediction_confidence']):.2f}")
 
     def get_statistics(self):
         snap = self._snapshot()
