@@ -247,7 +247,9 @@ def test_tracker_event_messages_match_oracle(capsys, max_lost, min_hits, thr, fr
         kinds["delete"] += b.count("删除跟踪器")
         kinds["stats"] += b.count("=== 跟踪统计")
     print("EVENT_MESSAGES", max_lost, min_hits, thr, kinds)
-    assert kinds["lost"] > 0 and kinds["create"] > 0 and kinds["recover"] > 0
+    assert kinds["lost"] > 0 and kinds["create"] > 0
+    if max_lost > 0:  # (max_lost 0 removes every lost track at once: nothing can be recovered)
+        assert kinds["recover"] > 0
     if max_lost != 450:
         assert kinds["delete"] > 0
     if frames_n >= 100:
