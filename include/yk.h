@@ -122,6 +122,9 @@ typedef struct {
     double value[3];          /* jump px, velocity change px/f, size-change ratio     */
     double confidence, motion_consistency;
   } details[5];               /* oldest first                                         */
+  int32_t traj_count;         /* trajectory points appended since the track's creation (a history
+                               * reset adds 2^20): traj[] advanced by the difference since a
+                               * previous row of the same track, so a host can reuse its points */
 } yk_track_out;
 
 /* Full filter state of one live track (AircraftKalmanTracker attributes,

@@ -78,3 +78,49 @@ def test_event_lines_order_and_format():
         "跟踪器 T005 丢失检测，切换到预测模式",
         "创建新跟踪器: T012",
         "删除跟踪器 T005 - 丢失时间: 0帧", "删除跟踪器 T007 - 丢失时间: 151帧"]
+
+
+def test_rows_to_dicts_and_trajectory_cache_match_row_to_dict():
+    """tracker.rows_to_dicts (column-wise, with the TrajCache reusing the previous frame's points
+    by yk_track_out.traj_count) builds the same dicts -- values and types -- as the per-row
+    _row_to_dict, over a synthetic sequence of frames: windows growing to 30 points, 1-3 new
+    points per frame, a history reset (+2^20), new and vanished tracks."""
+    import numpy as np
+
+    from conftest import pkg
+
+    P = pkg()
+    L, T = P._lib, P.tracker
+    rng = np.random.default_rng(3)
+    hist = {}  # track -> (count, list of points)
+    cache = T.TrajCache()
+    for f in range(60):
+        live = sorted(set(rng.choice(40, 25, replace=False).tolist()) | {0, 1})
+        rows = np.zeros(len(live), dtype=L.TRACK_OUT_DTYPE)
+        for i, num in enumerate(live):
+            c, pts = hist.get(num, (0, []))
+            if f == 30 and num == 0:  # a motion-reset history restart
+                c, pts = c + (1 << 20), []
+            k = int(rng.integers(1, 4))
+            pts = pts + [(float(rng.normal()), float(rng.normal())) for _ in range(k)]
+            c += k
+            hist[num] = (c, pts)
+            w = pts[-30:]
+            rows[i]["track_num"] = num
+            rows[i]["traj_len"] = len(w)
+            rows[i]["traj_count"] = c
+            rows[i]["traj"][: len(w)] = w
+            rows[i]["bbox"] = rng.random(4)
+            rows[i]["time_since_update"] = int(rng.integers(0, 3))
+            rows[i]["status"] = int(rows[i]["time_since_update"] > 0)
+        got = T.rows_to_dicts(rows, cache)
+        want = [T._row_to_dict(r, T.track_id_of(r["track_num"])) for r in rows]
+        for a, b in zip(got, want):
+            assert a.keys() == b.keys()
+            for key in a:
+                if isinstance(b[key], np.ndarray):
+                    assert np.array_equal(a[key], b[key]) and a[key].dtype == b[key].dtype
+                else:
+                    assert a[key] == b[key] and type(a[key]) is type(b[key]), (key, a[key], b[key])
+        got[0]["trajectory"].append((1.0, 2.0))  # a caller mutating its list leaves the cache alone
+    assert T.rows_to_dicts(rows[:0], cache) == []

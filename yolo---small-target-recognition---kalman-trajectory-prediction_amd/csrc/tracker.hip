@@ -63,6 +63,7 @@ struct Slot {
   double th[TH][2];
   int age, hits, hit_streak, tsu, is_lost, lost_frames, track_num, max_lost;
   int vh_len, vh_head, th_len, th_head;
+  int th_cnt;  // trajectory points appended since creation (+2^20 at a history reset): yk_track_out.traj_count
   // YK_POLICY_MOTION_RESET (MotionResetKalmanTracker, motion_reset_kalman_tracker.py:28-65)
   int policy;
   int reset_count, last_reset;  // last_reset_frame: -999 at creation
@@ -91,6 +92,7 @@ struct LSlot {
   double (*th)[2];
   int age, hits, hit_streak, tsu, is_lost, lost_frames, track_num, max_lost;
   int vh_len, vh_head, th_len, th_head;
+  int th_cnt;
   int policy;
 };
 
@@ -187,6 +189,7 @@ __device__ void slot_init(S& s, const double* z, int track_num, int max_lost) {
   s.max_lost = max_lost;
   s.vh_len = s.vh_head = 0;
   s.th_len = s.th_head = 0;
+  s.th_cnt = 1;
   s.policy = 0;
   ring_push(s.th, TH, s.th_len, s.th_head, z[0], z[1]);
 }
@@ -209,6 +212,7 @@ __device__ void kf_predict(S& s) {
   s.age += 1;
   s.tsu += 1;
   ring_push(s.th, TH, s.th_len, s.th_head, s.x[0], s.x[1]);
+  s.th_cnt += 1;
 }
 
 // numpy's pairwise summation for a contiguous 1-D float64 array of n <= 128 elements
@@ -617,6 +621,7 @@ __device__ void cmc_reset(Slot& s, const DT* b, const double* val, int why, Num 
   }
   s.th_len = s.th_head = 0;
   ring_push(s.th, TH, s.th_len, s.th_head, z[0], z[1]);
+  s.th_cnt += 1 << 20;  // the history restarts: a host-side trajectory cache must not reuse points
   s.vh_len = s.vh_head = 0;
   s.ph_len = s.ph_head = 0;
   ph_push(s, z[0], z[1], sizeof(DT) == 4);
@@ -714,6 +719,7 @@ __device__ void kf_update(S& s, const DT* box, double* st) {
   st[2 * VS + at] = ang;
   const int base = len0 < VH ? 0 : 1;
   ring_push(s.th, TH, s.th_len, s.th_head, s.x[0], s.x[1]);
+  s.th_cnt += 1;
   analyze_motion(s, st + base, st + VS + base, st + 2 * VS + base, st + base);
 }
 
@@ -842,6 +848,7 @@ __device__ void track_info(S& s, yk_track_out& o, bool copy_traj = true) {
   }
   const int nt = s.th_len < TOUT ? s.th_len : TOUT;
   o.traj_len = nt;
+  o.traj_count = s.th_cnt;
   if (!copy_traj) return;  // the step kernel copies trajectories cooperatively
   int idx = s.th_head + (s.th_len - nt);
   if (idx >= TH) idx -= TH;
@@ -1406,6 +1413,7 @@ __device__ __forceinline__ void lslot_load(LSlot& l, Slot& g) {
   l.vh_head = g.vh_head;
   l.th_len = g.th_len;
   l.th_head = g.th_head;
+  l.th_cnt = g.th_cnt;
   l.policy = g.policy;
   lslot_bind(l, g);
 }
@@ -1434,6 +1442,7 @@ __device__ __forceinline__ void lslot_store(const LSlot& l, Slot& g) {
   g.vh_head = l.vh_head;
   g.th_len = l.th_len;
   g.th_head = l.th_head;
+  g.th_cnt = l.th_cnt;
   g.policy = l.policy;
 }
 

@@ -26,6 +26,27 @@ from . import arch as A
 from . import model as M
 from . import weights as Wt
 
+# committed conv plans (bench.py's plans/<scale>_<W>x<H>_i<imgsz>_b<batch>_<dtype>.json): a YOLO
+# engine applies the one for its geometry at batch 1 when it exists (YK_PLAN_DIR overrides)
+PLAN_DIR = os.environ.get("YK_PLAN_DIR", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                                      "plans"))
+
+
+class _EngineIO:
+    """Per-engine device / page-locked buffers of the batch path: the frames are staged through
+    one pinned buffer into one device buffer, the forward replays a native hipGraph per batch size
+    (yk_detect_graph; its key includes these fixed pointers), and counts come back through pinned
+    memory.  Results get their own copies of the detections (the buffers are reused)."""
+
+    def __init__(self, e: M.DeviceModel, max_batch: int, max_det: int):
+        p = e.prog
+        dev = torch.device("cuda", e.device)
+        self.frames = torch.empty((max_batch, p.frame_h, p.frame_w, 3), dtype=torch.uint8, device=dev)
+        self.host = torch.empty(self.frames.shape, dtype=torch.uint8, pin_memory=True)
+        self.dets = torch.empty((max_batch, max_det, 6), dtype=torch.float32, device=dev)
+        self.counts = torch.empty(max_batch, dtype=torch.int32, device=dev)
+        self.host_counts = torch.empty(max_batch, dtype=torch.int32, pin_memory=True)
+
 
 class Boxes:
     """engine/results.py Boxes: data (N, 6) = x1, y1, x2, y2, conf, cls."""
@@ -176,6 +197,8 @@ class YOLO:
         self.task = "detect"
         self.overrides = {"conf": 0.25, "iou": 0.7, "max_det": 300, "imgsz": 640}
         self._engines = {}
+        self._io = {}
+        self.plans = {}  # engine key -> conv plan file applied (None: the kernels' heuristic)
         self._lock = threading.Lock()
         self._staging = None
 
@@ -186,8 +209,28 @@ class YOLO:
         if e is None:
             prog = M.Program(self.arch, self.state_dict, frame_h, frame_w, imgsz, self.max_batch, self.dtype, max_det)
             e = M.DeviceModel(prog, self.device)
+            self.plans[key] = self._apply_plan(e, prog, imgsz)
             self._engines[key] = e
+            self._io[key] = _EngineIO(e, self.max_batch, max_det)
         return e
+
+    def _apply_plan(self, e: M.DeviceModel, prog: M.Program, imgsz):
+        """The committed batch-1 conv plan of this geometry (tuned kernels; held to the oracle
+        chain by tests/test_bench_pipeline_gpu.py) if one exists and fits the program."""
+        import json
+
+        if not self.arch.scale or not isinstance(imgsz, int):
+            return None
+        name = f"{self.arch.scale}_{prog.frame_w}x{prog.frame_h}_i{imgsz}_b1_{self.dtype}.json"
+        path = os.path.join(PLAN_DIR, name)
+        if not os.path.exists(path):
+            return None
+        with open(path) as f:
+            pl = json.load(f)
+        if pl.get("dtype", self.dtype) != self.dtype or len(pl.get("plan", ())) != len(prog.ops):
+            return None
+        e.load_plan(pl["batch"], pl["plan"])
+        return path
 
     # -- predict --------------------------------------------------------------------
     def __call__(self, source=None, stream: bool = False, **kwargs):
@@ -242,20 +285,26 @@ class YOLO:
         if c != 3 or frames[0].dtype != np.uint8:
             raise ValueError("frames must be uint8 HxWx3 (BGR)")
         t0 = time.perf_counter()
-        eng = self.engine(h, w, imgsz, max(max_det, 1))
+        md = max(max_det, 1)
+        eng = self.engine(h, w, imgsz, md)
+        io = self._io[(h, w, imgsz if isinstance(imgsz, int) else tuple(imgsz), md)]
         B = len(frames)
-        host = torch.from_numpy(np.ascontiguousarray(np.stack(frames)))
-        dev = host.to(f"cuda:{self.device}", non_blocking=False)
+        hb = io.host.numpy()
+        for b, f in enumerate(frames):  # page-locked staging, then one DMA of the batch
+            hb[b] = f
+        io.frames[:B].copy_(io.host[:B], non_blocking=True)
         t1 = time.perf_counter()
-        dets, counts = eng.detect(dev, conf, iou, max(max_det, 1))
-        cnt = counts.cpu().tolist()
+        eng.detect(io.frames[:B], conf, iou, md, io.dets[:B], io.counts[:B], graph=True)
+        io.host_counts[:B].copy_(io.counts[:B], non_blocking=True)
+        torch.cuda.current_stream(self.device).synchronize()
+        cnt = io.host_counts[:B].tolist()
         t2 = time.perf_counter()
         res = []
         for b in range(B):
             n = min(int(cnt[b]), max_det)
             if classes is not None and 0 not in classes:
                 n = 0  # the class filter ran before NMS in the reference: no candidate survives
-            d = dets[b, :n]
+            d = io.dets[b, :n].clone()  # the engine's buffer is reused by the next call
             res.append(Results(frames[b], paths[b], self.names, boxes=d))
         t3 = time.perf_counter()
         sp = {"preprocess": (t1 - t0) * 1e3 / B, "inference": (t2 - t1) * 1e3 / B, "postprocess": (t3 - t2) * 1e3 / B}

@@ -81,6 +81,73 @@ def _row_to_dict(r, track_id: str) -> dict:
     }
 
 
+class TrajCache:
+    """Trajectory lists of the previous frame, per track, so that a frame's dicts build only the
+    points the device appended since (yk_track_out.traj_count): the reference returns
+    ``list(trajectory_history)[-30:]`` afresh every frame (kf.py:382), i.e. the previous list
+    shifted by the one or two new centres; materialising all 30 points of every track as Python
+    floats each frame was most of the drop-in tracker's host time."""
+
+    def __init__(self):
+        self.d = {}
+
+    def lists(self, nums, counts, lens, traj):
+        """nums / counts / lens: lists per row; traj: [R, 30, 2] float64 (the rows' windows)."""
+        R = len(nums)
+        if R == 0:
+            self.d = {}
+            return []
+        rr = np.arange(R)[:, None]
+        ln = np.asarray(lens)
+        last = traj[rr, np.clip(ln[:, None] - 3 + np.arange(3), 0, traj.shape[1] - 1)].tolist()  # [R][3][2]
+        out, new = [], {}
+        for i in range(R):
+            n, c = lens[i], counts[i]
+            old = self.d.get(nums[i])
+            k = -1 if old is None else c - old[0]
+            if 0 <= k <= 3 and k <= n and n == min(len(old[1]) + k, traj.shape[1]):
+                lst = old[1] + [tuple(p) for p in last[i][3 - k:]] if k else old[1]
+                if len(lst) > n:
+                    lst = lst[len(lst) - n:]
+            else:
+                lst = list(map(tuple, traj[i, :n].tolist()))
+            new[nums[i]] = (c, lst)  # cached lists are never handed out (the caller may mutate its own)
+            out.append(list(lst))
+        self.d = new
+        return out
+
+
+def rows_to_dicts(rows, cache: TrajCache | None = None) -> list[dict]:
+    """yk_track_out rows -> the reference get_track_info() dicts (kf.py:366-383), column-wise:
+    each field is read once for all rows; the same values and types as _row_to_dict."""
+    R = len(rows)
+    if R == 0:
+        if cache is not None:
+            cache.d = {}
+        return []
+    nums = rows["track_num"].tolist()
+    tsu = rows["time_since_update"].tolist()
+    st, age, hits, hs = rows["status"].tolist(), rows["age"].tolist(), rows["hits"].tolist(), rows["hit_streak"].tolist()
+    conf, mc = rows["confidence"].tolist(), rows["motion_confidence"].tolist()
+    sp, di, stab = rows["speed"].tolist(), rows["direction"].tolist(), rows["is_stable_motion"].tolist()
+    bb = np.array(rows["bbox"], dtype=np.float64)  # fresh per frame: the dicts' arrays are views of it
+    ve = np.array(rows["velocity"], dtype=np.float64)
+    lens = rows["traj_len"].tolist()
+    traj = np.array(rows["traj"], dtype=np.float64)
+    if cache is not None:
+        trajs = cache.lists(nums, rows["traj_count"].tolist(), lens, traj)
+    else:
+        trajs = [list(map(tuple, traj[i, :lens[i]].tolist())) for i in range(R)]
+    out = []
+    for i in range(R):
+        k = tsu[i]
+        out.append({"track_id": f"T{nums[i]:03d}", "bbox": bb[i], "confidence": conf[i], "status": _STATUS[st[i]],
+                    "age": age[i], "hits": hits[i], "hit_streak": hs[i], "time_since_update": k, "lost_frames": k,
+                    "is_lost": k > 0, "trajectory": trajs[i], "velocity": ve[i], "motion_confidence": mc[i],
+                    "is_stable_motion": bool(stab[i]), "speed": sp[i], "direction": di[i]})
+    return out
+
+
 def track_id_of(num: int) -> str:
     return f"T{int(num):03d}"
 
@@ -146,9 +213,16 @@ class MultiStreamTracker:
         L.check(L.lib().yk_tracker_create(ctx, self.n_streams, C.byref(cfg), C.byref(h)), "yk_tracker_create")
         self._h = h
         S, T = self.n_streams, self.max_tracks
-        self.host_rows = np.zeros((S, T), dtype=L.TRACK_OUT_DTYPE)
-        self.host_counts = np.zeros(S, dtype=np.int32)
-        self.host_stats = np.zeros(S, dtype=L.STATS_DTYPE)
+        # page-locked host mirrors: the per-frame copies are DMA transfers, not staged ones
+        self._pin = {"rows": torch.zeros(S * T * L.TRACK_OUT_DTYPE.itemsize, dtype=torch.uint8, pin_memory=True),
+                     "counts": torch.zeros(S, dtype=torch.int32, pin_memory=True),
+                     "stats": torch.zeros(S * L.STATS_DTYPE.itemsize, dtype=torch.uint8, pin_memory=True),
+                     "in_counts": torch.zeros(S, dtype=torch.int32, pin_memory=True)}
+        self.host_rows = self._pin["rows"].numpy().view(L.TRACK_OUT_DTYPE).reshape(S, T)
+        self.host_counts = self._pin["counts"].numpy()
+        self.host_stats = self._pin["stats"].numpy().view(L.STATS_DTYPE)
+        self._pin_dets = {}
+        self._pin_evt = None
         dev = torch.device("cuda", self.device)
         self._dets = {L.YK_F32: torch.zeros((S, self.max_dets, 4), dtype=torch.float32, device=dev),
                       L.YK_F64: torch.zeros((S, self.max_dets, 4), dtype=torch.float64, device=dev)}
@@ -193,16 +267,23 @@ class MultiStreamTracker:
         dts = {a[1] for a in arrs if len(a[0])}
         dt = dts.pop() if len(dts) == 1 else (L.YK_F64 if dts else L.YK_F32)
         buf = self._dets[dt]
-        npdt = np.float32 if dt == L.YK_F32 else np.float64
-        host = np.zeros((self.n_streams, self.max_dets, 4), npdt)
-        cnt = np.zeros(self.n_streams, np.int32)
+        pin = self._pin_dets.get(dt)
+        if pin is None:
+            pin = self._pin_dets[dt] = torch.zeros(buf.shape, dtype=buf.dtype, pin_memory=True)
+        if self._pin_evt is not None:
+            self._pin_evt.synchronize()  # the previous step's copies out of the pinned buffers are done
+        host, cnt = pin.numpy(), self._pin["in_counts"].numpy()
         for s, (a, _) in enumerate(arrs):
             if len(a) > self.max_dets:
                 raise L.YKError(f"{len(a)} detections exceed max_dets={self.max_dets}")
             host[s, :len(a)] = a
             cnt[s] = len(a)
-        buf.copy_(torch.from_numpy(host))
-        self._counts.copy_(torch.from_numpy(cnt))
+        n = int(cnt.max()) if len(cnt) else 0
+        if n:  # only the rows the step reads (rows past a stream's count are never read)
+            buf[:, :n].copy_(pin[:, :n], non_blocking=True)
+        self._counts.copy_(self._pin["in_counts"], non_blocking=True)
+        self._pin_evt = torch.cuda.Event()
+        self._pin_evt.record(torch.cuda.current_stream(self.device))
         self.step_device(buf, self._counts, motion=motion)
 
     def download(self):
@@ -529,6 +610,7 @@ class EnhancedMultiTargetTracker:
         self._stats = np.zeros(1, dtype=L.STATS_DTYPE)[0]
         self._stats["next_track_id"] = 1
         self._snap = None
+        self._traj = TrajCache()
         if verbose:  # the reference prints its lifecycle messages (enhanced_multi_target_tracker.py:40,79-109)
             self._core.set_events(True)
             print(f"增强版多目标跟踪器初始化完成 - 最大丢失容忍: {max_lost_frames}帧 ({max_lost_frames/30:.1f}秒)")
@@ -564,7 +646,7 @@ class EnhancedMultiTargetTracker:
         self._snap = None
         if int(self._stats["overflow"]):
             raise L.YKError(f"tracker capacity exceeded (max_tracks={self._core.max_tracks})")
-        out = [_row_to_dict(r, track_id_of(r["track_num"])) for r in rows[0, : int(counts[0])]]
+        out = rows_to_dicts(rows[0, : int(counts[0])], self._traj)
         if self.verbose:
             for line in event_lines(self._core.events(0)):
                 print(line)
