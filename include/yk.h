@@ -253,8 +253,15 @@ int yk_track_create(yk_tracker* trk, int stream_index, const double* host_bbox, 
  * iterations / eps 0.01) into the current one, then the reference's median / 75th-percentile
  * inlier mean, magnitude thresholds and 3-vector direction consistency.  The OpenCV stages
  * follow OpenCV 4.x's published algorithms (cv2 is not available to pin them).
- * 'feature_matching' and 'hybrid' (ORB + RANSAC homography) are not built. */
-enum yk_gmd_method { YK_GMD_OPTICAL_FLOW = 0, YK_GMD_FEATURE_MATCHING = 1, YK_GMD_HYBRID = 2 };
+ * 'feature_matching' and 'hybrid' (ORB + RANSAC homography) are not built.
+ * YK_GMD_SPARSE_OPTFLOW is BoT-SORT's default global motion compensation instead
+ * (ultralytics/trackers/utils/gmc.py:278-345, GMC(method='sparseOptFlow', downscale=2)): gray,
+ * the 1/2 area downscale, goodFeaturesToTrack(1000, 0.01, 1, blockSize 3), calcOpticalFlowPyrLK
+ * (21x21, maxLevel 3) from the previous frame's corners, then estimateAffinePartial2D(RANSAC) with
+ * its Levenberg-Marquardt refinement; the result is a 2x3 warp per stream (yk_gmc_apply), not a
+ * yk_motion.  Frames must have even width and height. */
+enum yk_gmd_method { YK_GMD_OPTICAL_FLOW = 0, YK_GMD_FEATURE_MATCHING = 1, YK_GMD_HYBRID = 2,
+                     YK_GMD_SPARSE_OPTFLOW = 3 };
 /* One detect_motion() result (is_motion, motion_magnitude, motion_vector, should_reset). */
 typedef struct {
   int32_t valid;           /* 1: the stream had a frame this step                            */
@@ -292,9 +299,22 @@ int yk_gmd_outputs(yk_gmd* g, yk_motion** dev_motion);
 /* Copy the last results (and stats when host_stats != NULL) to the host; synchronous. */
 int yk_gmd_download(yk_gmd* g, yk_motion* host_motion, yk_gmd_stats* host_stats, void* stream);
 /* Diagnostics for parity tests: stream s's last corners (x, y), LK end points (x, y) and status
- * (host arrays of 200 entries); *n receives the corner count.  Synchronous. */
+ * (host arrays of 200 entries, 1000 for YK_GMD_SPARSE_OPTFLOW); *n receives the corner count.
+ * Synchronous. */
 int yk_gmd_points(yk_gmd* g, int stream_index, float* host_corners, float* host_next, uint8_t* host_status,
                   int32_t* n, void* stream);
+
+/* GMC.apply(frame) of a YK_GMD_SPARSE_OPTFLOW detector for every stream: dev_warp[n_streams][2][3]
+ * float64 (device; NULL: the detector's own buffer, yk_gmc_outputs).  The first frame of a
+ * stream, or one whose previous frame had no corners, gives the identity and stores the frame;
+ * <= 4 tracked points give the identity; a failed estimate gives the identity and keeps the
+ * previous frame (the reference's exception path, byte_tracker.py:334-338).  Asynchronous. */
+int yk_gmc_apply(yk_gmd* g, const uint8_t* dev_frames, double* dev_warp, void* stream);
+int yk_gmc_outputs(yk_gmd* g, double** dev_warp);
+/* Per-stream diagnostics of the last yk_gmc_apply: {tracked points, RANSAC inliers, RANSAC
+ * iterations, LM iterations, state (0 identity / first frame, 1 estimated, 2 too few points,
+ * 3 failed)} x n_streams int32 (host).  Synchronous. */
+int yk_gmc_info(yk_gmd* g, int32_t* host_info, void* stream);
 
 /* MotionCompensatedMultiTracker.update(detections, frame) (motion_compensated_multi_tracker.py
  * :75-121): yk_tracker_step of a YK_POLICY_MOTION_RESET tracker plus the global branch --
@@ -345,6 +365,12 @@ int yk_bt_reset(yk_bt* bt, void* stream);
 /* One update() of every stream.  dev_dets: [n_streams][max_dets][6] float32 rows x1 y1 x2 y2
  * conf cls (Boxes.data), dev_counts: [n_streams] rows used.  Asynchronous on `stream`. */
 int yk_bt_step(yk_bt* bt, const float* dev_dets, const int32_t* dev_counts, void* stream);
+/* yk_bt_step of a BoT-SORT tracker with its GMC: dev_warp[n_streams][2][3] float64 (yk_gmc_apply's
+ * output for the same frames) is applied to strack_pool and the unconfirmed tracks after the
+ * prediction (byte_tracker.py:333-340, STrack.multi_gmc :108-125); the covariances then become
+ * dense 8x8 (tracked to rounding against numpy's BLAS, not bit for bit).  NULL: yk_bt_step. */
+int yk_bt_step_warp(yk_bt* bt, const float* dev_dets, const int32_t* dev_counts, const double* dev_warp,
+                    void* stream);
 /* Device outputs of the last step: rows [n_streams][max_tracks][8] float32 = the reference's
  * result rows (x1 y1 x2 y2 track_id score cls idx) in tracked_stracks order; counts [n_streams]. */
 int yk_bt_outputs(yk_bt* bt, float** dev_rows, int32_t** dev_counts);

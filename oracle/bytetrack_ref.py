@@ -10,9 +10,9 @@ op a python float stays float32; lists mixing float32 scalars and python floats 
       update :205-236 (scipy.linalg.cho_factor / cho_solve, as the reference calls them)
   * STrack / BOTrack                         trackers/byte_tracker.py:16-237, bot_sort.py:21-153
   * BYTETracker.update and its list helpers  byte_tracker.py:299-485
-  * BOTSORT without ReID / GMC               bot_sort.py:156-249 (get_dists :227-240 with
-      with_reid False is iou_distance + fuse_score; GMC runs only when an image is passed and
-      needs cv2 -- absent here, so BOTSORT is stepped with img=None, as the reference skips GMC)
+  * BOTSORT without ReID                     bot_sort.py:156-249 (get_dists :227-240 with
+      with_reid False is iou_distance + fuse_score); with an image, its GMC (oracle/gmc_ref.py,
+      'sparseOptFlow' or 'none') and STrack.multi_gmc (byte_tracker.py:108-125, 333-340)
   * matching.iou_distance / fuse_score       trackers/utils/matching.py:64-157, with
       utils/metrics.py:23-52 bbox_ioa(iou=True) in float32
   * matching.linear_assignment (matching.py:20-61): by default the lap branch the reference
@@ -207,6 +207,22 @@ class Track:
         self.score, self.cls, self.idx = det.score, det.cls, det.idx
 
 
+def multi_gmc(tracks, H):
+    """STrack.multi_gmc (byte_tracker.py:108-125)."""
+    if tracks:
+        multi_mean = np.asarray([t.mean.copy() for t in tracks])
+        multi_cov = np.asarray([t.cov for t in tracks])
+        R = H[:2, :2]
+        R8x8 = np.kron(np.eye(4, dtype=float), R)
+        tr = H[:2, 2]
+        for i, (mean, cov) in enumerate(zip(multi_mean, multi_cov)):
+            mean = R8x8.dot(mean)
+            mean[:2] += tr
+            cov = R8x8.dot(cov).dot(R8x8.transpose())
+            tracks[i].mean = mean
+            tracks[i].cov = cov
+
+
 def multi_predict(tracks, kind):
     if not tracks:
         return
@@ -339,12 +355,19 @@ class RefTracker:
         self.kind = "xywh" if self.args.tracker_type == "botsort" else "xyah"
         self.ids = ids if ids is not None else IdCounter()
         self.max_time_lost = int(frame_rate / 30.0 * self.args.track_buffer)
+        self.gmc = None
+        if self.kind == "xywh":  # BOTSORT.__init__ (bot_sort.py:198)
+            from .gmc_ref import RefGMC
+
+            self.gmc = RefGMC(method=getattr(self.args, "gmc_method", "sparseOptFlow"))
         self.reset()
 
     def reset(self):
         self.tracked, self.lost, self.removed = [], [], []
         self.frame_id = 0
         self.ids.reset()
+        if self.gmc is not None:
+            self.gmc.reset_params()
 
     def _init_track(self, dets):
         if len(dets) == 0:
@@ -369,6 +392,13 @@ class RefTracker:
         tracked = [t for t in self.tracked if t.is_activated]
         pool = _joint(tracked, self.lost)
         multi_predict(pool, self.kind)
+        if self.gmc is not None and img is not None:  # byte_tracker.py:333-340
+            try:
+                warp = self.gmc.apply(img, None)
+            except Exception:
+                warp = np.eye(2, 3)
+            multi_gmc(pool, warp)
+            multi_gmc(unconfirmed, warp)
         m, u_track, u_det = linear_assignment(self._dists(pool, dets), thresh=a.match_thresh, use_lap=self.use_lap)
         for it, idt in m:
             t = pool[it]

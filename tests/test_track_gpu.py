@@ -28,7 +28,7 @@ def _expected(ref_det, trk, frame):
     """track.py:86-100 on the oracle chain for one frame: Results (N, 6) -> tracked (M, 7)."""
     want, _ = D.predict(ref_det, [frame], conf=0.1)
     det = want[0].numpy()
-    tracks = trk.update(R.Dets(det[:, :4], det[:, 4], det[:, 5]))
+    tracks = trk.update(R.Dets(det[:, :4], det[:, 4], det[:, 5]), frame)
     if len(tracks) == 0:
         return det
     out = tracks[:, :-1].astype(np.float32).copy()
@@ -37,14 +37,15 @@ def _expected(ref_det, trk, frame):
     return out
 
 
-@pytest.mark.parametrize("tracker", ["bytetrack.yaml", "botsort.yaml"])
+@pytest.mark.parametrize("tracker", ["bytetrack.yaml", "botsort.yaml", "botsort-none"])
 def test_yolo_track_persist_matches_oracle_chain(tracker):
     """for frame in video: model.track(frame, persist=True) -- 60 frames of a 24-target scene with
-    occlusions; one tracker kept across calls.  botsort.yaml runs with gmc_method: none (its
-    sparseOptFlow GMC needs cv2, absent here; the default config raises NotImplementedError)."""
+    occlusions; one tracker kept across calls.  botsort.yaml is the cfg default with its
+    sparseOptFlow GMC (device gmd.hip / oracle gmc_ref.py, both fed the frame as track.py:93 does);
+    botsort-none sets gmc_method: none (the identity warp)."""
     P = pkg()
     cfg = dict(R.BOTSORT_CFG if tracker.startswith("botsort") else R.BYTETRACK_CFG)
-    if cfg["tracker_type"] == "botsort":
+    if tracker == "botsort-none":
         cfg["gmc_method"] = "none"
     model = P.YOLO("yolov8s-small.yaml")
     ref_det = D.RefDetector(_layers(model.arch), model.state_dict, P.arch.detect_strides(model.arch))
@@ -74,14 +75,14 @@ def test_yolo_track_persist_matches_oracle_chain(tracker):
 def test_yolo_track_list_source_resets_per_image_and_default_cfg():
     """A list of frames is one LoadPilAndNumpy batch whose paths are image{i}.jpg: without persist
     the tracker resets at every new path (track.py:90-93), so every frame starts new tracks (ids
-    from 1); with persist the frames chain.  The cfg default (botsort.yaml, sparseOptFlow GMC)
-    raises because GMC needs cv2."""
+    from 1); with persist the frames chain.  The plain call uses the cfg default (botsort.yaml
+    with its sparseOptFlow GMC) and runs."""
     P = pkg()
     model = P.YOLO("yolov8s-small.yaml")
     sc = P.synth.Scene(seed=12, n_targets=16, n_frames=5)
     frames = [sc.frame(t) for t in range(4)]
-    with pytest.raises(NotImplementedError):
-        model.track(frames)
+    res0 = model.track(frames)  # defaults: botsort.yaml, GMC sparseOptFlow
+    assert len(res0) == 4 and any(r.boxes.is_track for r in res0)
     res = model.track(frames, tracker="bytetrack.yaml")
     for r in res:
         if r.boxes.is_track:

@@ -58,7 +58,7 @@ STATS_DTYPE = np.dtype([(k, np.int64) for k in (
     "current_active_tracks", "long_term_predictions", "successful_recoveries", "overflow",
     "individual_resets", "tracking_recoveries", "global_motion_events", "global_resets")])
 
-GMD_OPTICAL_FLOW, GMD_FEATURE_MATCHING, GMD_HYBRID = 0, 1, 2
+GMD_OPTICAL_FLOW, GMD_FEATURE_MATCHING, GMD_HYBRID, GMD_SPARSE_OPTFLOW = 0, 1, 2, 3
 GMD_METHODS = {"optical_flow": GMD_OPTICAL_FLOW, "feature_matching": GMD_FEATURE_MATCHING, "hybrid": GMD_HYBRID}
 # yk_track_event (include/yk.h): one record per work item of a step
 TRACK_EVENT_DTYPE = np.dtype([("kind", np.int32), ("track_num", np.int32), ("list_pos", np.int32), ("det", np.int32),
@@ -180,6 +180,7 @@ _SIGS = {
     "yk_bt_destroy": ([_vp], C.c_int),
     "yk_bt_reset": ([_vp, _vp], C.c_int),
     "yk_bt_step": ([_vp, _vp, _vp, _vp], C.c_int),
+    "yk_bt_step_warp": ([_vp, _vp, _vp, _vp, _vp], C.c_int),
     "yk_bt_outputs": ([_vp, C.POINTER(_vp), C.POINTER(_vp)], C.c_int),
     "yk_bt_download": ([_vp, _vp, _vp, _vp], C.c_int),
     "yk_gmd_create": ([_vp, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(_vp)], C.c_int),
@@ -191,6 +192,9 @@ _SIGS = {
     "yk_gmd_outputs": ([_vp, C.POINTER(_vp)], C.c_int),
     "yk_gmd_download": ([_vp, _vp, _vp, _vp], C.c_int),
     "yk_gmd_points": ([_vp, C.c_int, _vp, _vp, _vp, C.POINTER(_i32), _vp], C.c_int),
+    "yk_gmc_apply": ([_vp, _vp, _vp, _vp], C.c_int),
+    "yk_gmc_outputs": ([_vp, C.POINTER(_vp)], C.c_int),
+    "yk_gmc_info": ([_vp, _vp, _vp], C.c_int),
     "yk_tracker_step_motion": ([_vp, _vp, C.c_int, C.c_int, _vp, _vp, _vp], C.c_int),
     "yk_nms": ([_vp, _vp, C.c_int, C.c_int, _vp, C.c_int, C.c_float, C.c_int, _vp, _vp, _vp, _vp], C.c_int),
     "yk_nms_candidates": ([_vp, C.c_int, C.c_float, C.c_int, _vp, _vp, _vp, _vp], C.c_int),

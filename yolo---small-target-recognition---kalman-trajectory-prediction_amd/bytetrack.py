@@ -14,9 +14,12 @@ matching.linear_assignment follows its default lap branch (lap.lapjv with cost_l
 lists ascending); use_lap=False selects the scipy branch (matching.py:50-59).
 Track ids come from one counter shared by the streams of a BatchedTracker (the reference's
 BaseTrack._count is process-global); separate BYTETracker objects each own a counter, like
-separate processes.  BoT-SORT's ReID branch (with_reid) and its GMC (needs cv2 for every
-method but 'none') are not built: requesting them raises.  There is no CPU fallback: the
-library must load (YKError otherwise).
+separate processes.  BoT-SORT's GMC (gmc.py): 'sparseOptFlow' (the botsort.yaml default) runs
+on the device (csrc/gmd.hip yk_gmc_apply: corners, pyramidal LK, RANSAC + Levenberg-Marquardt
+estimateAffinePartial2D) and its warp is applied inside the step (yk_bt_step_warp); 'none' applies
+the identity, as the reference's GMC.apply returns np.eye(2, 3); 'orb' / 'sift' / 'ecc' (cv2
+feature / ECC internals) raise.  The ReID branch (with_reid) is not built.  There is no CPU
+fallback: the library must load (YKError otherwise).
 """
 from __future__ import annotations
 
@@ -93,16 +96,17 @@ class BatchedTracker:
     def reset(self):
         L.check(L.lib().yk_bt_reset(self._h, L.current_stream(self.device)), "yk_bt_reset")
 
-    def step_device(self, dets: torch.Tensor, counts: torch.Tensor):
-        """One update() of every stream from device-resident detections (no host round trip)."""
+    def step_device(self, dets: torch.Tensor, counts: torch.Tensor, warp: int | None = None):
+        """One update() of every stream from device-resident detections (no host round trip).
+        warp: device address of float64 [S][2][3] GMC warps (BoT-SORT), or None."""
         if dets.dtype != torch.float32 or dets.shape != (self.S, self.max_dets, 6) or not dets.is_contiguous():
             raise ValueError(f"dets must be a contiguous float32 tensor of shape {(self.S, self.max_dets, 6)}")
         if counts.dtype != torch.int32 or counts.shape != (self.S,):
             raise ValueError(f"counts must be an int32 tensor of shape ({self.S},)")
-        L.check(L.lib().yk_bt_step(self._h, C.c_void_p(dets.data_ptr()), C.c_void_p(counts.data_ptr()),
-                                   L.current_stream(self.device)), "yk_bt_step")
+        L.check(L.lib().yk_bt_step_warp(self._h, C.c_void_p(dets.data_ptr()), C.c_void_p(counts.data_ptr()),
+                                        C.c_void_p(warp or 0), L.current_stream(self.device)), "yk_bt_step")
 
-    def step(self, per_stream):
+    def step(self, per_stream, warp: int | None = None):
         """Host detections per stream (objects with .xyxy / .conf / .cls, or [n, 6] arrays)."""
         if len(per_stream) != self.S:
             raise ValueError(f"expected {self.S} streams, got {len(per_stream)}")
@@ -116,7 +120,7 @@ class BatchedTracker:
             cnt[s] = len(a)
         self.dets.copy_(torch.from_numpy(buf))
         self.counts.copy_(torch.from_numpy(cnt))
-        self.step_device(self.dets, self.counts)
+        self.step_device(self.dets, self.counts, warp)
 
     def download(self) -> list[np.ndarray]:
         L.check(L.lib().yk_bt_download(self._h, L.ptr(self._rows), L.ptr(self._cnt), L.current_stream(self.device)),
@@ -133,6 +137,96 @@ def _as_rows(r) -> np.ndarray:
                            np.asarray(r.cls, np.float32).reshape(-1, 1)], axis=1)
 
 
+class GMC:
+    """GMC(method='sparseOptFlow' | 'none', downscale=2) of ultralytics/trackers/utils/gmc.py:48-353
+    for n_streams streams on the device (yk_gmd with YK_GMD_SPARSE_OPTFLOW; created at the first
+    frame, when the frame size is known).  apply(raw_frame) returns the 2x3 float64 warp like the
+    reference; apply_device(frames) leaves it in HBM for the BoT-SORT step."""
+
+    def __init__(self, method: str = "sparseOptFlow", downscale: int = 2, n_streams: int = 1, device: int = 0):
+        if method not in ("sparseOptFlow", "none", None):
+            raise NotImplementedError(f"GMC method {method!r} needs cv2's ORB / SIFT / ECC internals (absent); "
+                                      "'sparseOptFlow' and 'none' are built")
+        if method == "sparseOptFlow" and downscale != 2:
+            raise NotImplementedError("GMC sparseOptFlow is built for downscale 2 (the INTER_AREA fast path)")
+        self.method, self.downscale, self.S, self.device = method, max(1, downscale), int(n_streams), int(device)
+        self._h = None
+        self._hw = None
+        dev = torch.device("cuda", self.device)
+        self.identity = torch.tensor([[1.0, 0.0, 0.0, 0.0, 1.0, 0.0]] * self.S, dtype=torch.float64, device=dev)
+        self.warp = torch.zeros((self.S, 6), dtype=torch.float64, device=dev)
+        self.frames = None
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            try:
+                L.lib().yk_gmd_destroy(h)
+            except Exception:
+                pass
+            self._h = None
+
+    def reset_params(self):
+        """gmc.py:347-353: forget the previous frame and keypoints."""
+        if self._h is not None:
+            L.check(L.lib().yk_gmd_reset(self._h, L.current_stream(self.device)), "yk_gmd_reset")
+
+    def _frames_device(self, frames) -> torch.Tensor:
+        if isinstance(frames, np.ndarray):
+            frames = torch.from_numpy(np.ascontiguousarray(frames))
+        if frames.dim() == 3:
+            frames = frames.unsqueeze(0)
+        if frames.dtype != torch.uint8 or frames.shape[0] != self.S or frames.shape[3] != 3:
+            raise ValueError(f"frames must be uint8 [{self.S}, H, W, 3] BGR")
+        if not frames.is_cuda:
+            if self.frames is None or self.frames.shape != frames.shape:
+                self.frames = torch.empty(frames.shape, dtype=torch.uint8, device=f"cuda:{self.device}")
+            self.frames.copy_(frames)
+            frames = self.frames
+        return frames.contiguous()
+
+    def apply_device(self, frames) -> int:
+        """GMC.apply of every stream's frame (uint8 [S, H, W, 3] BGR, host or device); returns the
+        device address of the float64 [S][2][3] warps."""
+        if self.method != "sparseOptFlow":
+            return self.identity.data_ptr()
+        f = self._frames_device(frames)
+        hw = (int(f.shape[1]), int(f.shape[2]))
+        if self._h is None or self._hw != hw:
+            if self._h is not None:
+                L.lib().yk_gmd_destroy(self._h)
+            h = C.c_void_p()
+            L.check(L.lib().yk_gmd_create(L.context(self.device), self.S, hw[0], hw[1], L.GMD_SPARSE_OPTFLOW,
+                                          C.byref(h)), "yk_gmd_create")
+            self._h, self._hw = h, hw
+        L.check(L.lib().yk_gmc_apply(self._h, C.c_void_p(f.data_ptr()), C.c_void_p(self.warp.data_ptr()),
+                                     L.current_stream(self.device)), "yk_gmc_apply")
+        return self.warp.data_ptr()
+
+    def apply(self, raw_frame, detections=None) -> np.ndarray:
+        """The 2x3 warp of one frame (stream 0), float64, like the reference's GMC.apply."""
+        self.apply_device(raw_frame)
+        src = self.warp if self.method == "sparseOptFlow" else self.identity
+        return src[0].cpu().numpy().reshape(2, 3)
+
+    def info(self) -> np.ndarray:
+        """[S, 5]: tracked points, RANSAC inliers, RANSAC iterations, LM iterations, state."""
+        out = np.zeros((self.S, 5), np.int32)
+        if self._h is not None:
+            L.check(L.lib().yk_gmc_info(self._h, L.ptr(out), L.current_stream(self.device)), "yk_gmc_info")
+        return out
+
+    def points(self, stream_index: int = 0):
+        """(corners [n, 2], LK end points [n, 2], status [n]) of the last apply (the previous frame's
+        keypoints tracked into the current one)."""
+        M = 1000
+        c, nx, st = np.zeros((M, 2), np.float32), np.zeros((M, 2), np.float32), np.zeros(M, np.uint8)
+        n = C.c_int32()
+        L.check(L.lib().yk_gmd_points(self._h, int(stream_index), L.ptr(c), L.ptr(nx), L.ptr(st), C.byref(n),
+                                      L.current_stream(self.device)), "yk_gmd_points")
+        return c[:n.value], nx[:n.value], st[:n.value]
+
+
 class BYTETracker:
     """BYTETracker(args, frame_rate=30) of ultralytics/trackers/byte_tracker.py:240 on the device."""
 
@@ -147,21 +241,26 @@ class BYTETracker:
             cfg = SimpleNamespace(**{**vars(cfg), "tracker_type": self.kind})
         self.args = cfg
         self._b = BatchedTracker(vars(cfg), 1, frame_rate, max_tracks, max_dets, device, use_lap)
+        # BOTSORT.__init__ (bot_sort.py:198): self.gmc = GMC(method=args.gmc_method)
+        self.gmc = GMC(getattr(cfg, "gmc_method", "none"), device=device) if self.kind == "botsort" else None
         self.frame_id = 0
 
     def reset(self):
         self._b.reset()
+        if self.gmc is not None:
+            self.gmc.reset_params()  # BOTSORT.reset (bot_sort.py:246-249)
         self.frame_id = 0
 
     def update(self, results, img=None, feats=None) -> np.ndarray:
-        if img is not None and self.kind == "botsort" and getattr(self.args, "gmc_method", "none") not in ("none", None):
-            raise NotImplementedError("BoT-SORT GMC needs cv2 (absent); pass img=None or gmc_method: none")
+        """byte_tracker.py:299-410: with an image, BoT-SORT applies its GMC warp (identity for
+        gmc_method 'none') to the predicted pool and the unconfirmed tracks (:333-340)."""
         self.frame_id += 1
-        self._b.step([results])
+        warp = self.gmc.apply_device(img) if (self.gmc is not None and img is not None) else None
+        self._b.step([results], warp)
         return self._b.download()[0]
 
 
 class BOTSORT(BYTETracker):
-    """BOTSORT(args, frame_rate=30) of ultralytics/trackers/bot_sort.py:156 without ReID / GMC."""
+    """BOTSORT(args, frame_rate=30) of ultralytics/trackers/bot_sort.py:156 with its GMC, without ReID."""
 
     kind = "botsort"

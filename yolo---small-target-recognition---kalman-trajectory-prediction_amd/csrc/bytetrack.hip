@@ -44,6 +44,8 @@ enum { NEW = 0, TRACKED = 1, LOST = 2, REMOVED = 3 };
 struct Slot {
   double mean[8];
   double P[16];  // per coordinate c: [4c] P[c][c], [4c+1] P[c][c+4], [4c+2] P[c+4][c], [4c+3] P[c+4][c+4]
+  double Pd[64]; // dense covariance (row-major 8x8) once a GMC warp coupled x / y (dense != 0)
+  int dense;
   double idx;    // detection index within its score subset (float64, the last element of the xywh row)
   float score, cls;
   int mean32;    // mean is still initiate()'s float32 array
@@ -65,6 +67,8 @@ struct Cfg {
   int lap;                        // linear_assignment branch: 1 lap.lapjv (default), 0 scipy
   double th_match_f64;            // match_thresh as the YAML's python float (lap's cost_limit)
 };
+
+// BoT-SORT's GMC (byte_tracker.py:333-340): the step's 2x3 warp per stream, or none
 
 struct Dev {
   Slot* slots;        // [S][T]
@@ -227,6 +231,7 @@ __device__ void kf_initiate(Slot& t, const float* m, bool xywh) {
     t.mean[c + 4] = 0.0;
   }
   t.mean32 = 1;
+  t.dense = 0;
   const float k2 = (float)(2 * WP), k10 = (float)(10 * WV);  // python float * np.float32 -> float32
   for (int c = 0; c < 4; ++c) {
     const float ref = xywh ? ((c & 1) ? m[3] : m[2]) : m[3];
@@ -284,6 +289,21 @@ __device__ void kf_predict(Slot& t, bool xywh, bool f32) {
       q[c + 4] = sv[c] * sv[c];
     }
   }
+  if (t.dense) {
+    // np.dot(F, P) then .dot(F.T) (+ motion_cov): every F row / column has one or two unit
+    // entries, so each product element is one rounded sum in any summation order
+    for (int c = 0; c < 4; ++c) t.mean[c] = t.mean[c] + t.mean[c + 4];
+    double L[64];
+    for (int i = 0; i < 8; ++i)
+      for (int j = 0; j < 8; ++j) L[8 * i + j] = i < 4 ? t.Pd[8 * i + j] + t.Pd[8 * (i + 4) + j] : t.Pd[8 * i + j];
+    for (int i = 0; i < 8; ++i)
+      for (int j = 0; j < 8; ++j) {
+        const double o = j < 4 ? L[8 * i + j] + L[8 * i + j + 4] : L[8 * i + j];
+        t.Pd[8 * i + j] = o + (i == j ? q[i] : 0.0);
+      }
+    t.mean32 = 0;
+    return;
+  }
   for (int c = 0; c < 4; ++c) {
     t.mean[c] = t.mean[c] + t.mean[c + 4];
     const double p = t.P[4 * c], a = t.P[4 * c + 1], b = t.P[4 * c + 2], v = t.P[4 * c + 3];
@@ -292,6 +312,103 @@ __device__ void kf_predict(Slot& t, bool xywh, bool f32) {
     t.P[4 * c + 2] = (b + v) + 0.0;
     t.P[4 * c + 3] = v + q[c + 4];
   }
+  t.mean32 = 0;
+}
+
+// Dense update (a covariance coupled by a GMC warp): project (H P H^T + R), scipy's
+// cho_factor (LAPACK dpotf2 order: dot, then the column scaled by 1 / L[j][j]) and cho_solve
+// (forward / backward substitution by the reciprocal diagonal), mean + innovation . K^T, and
+// P - K (S K^T) (multi_dot's order for equal costs).  numpy's BLAS kernels sum in their own
+// order, so this path agrees with the reference to rounding, not bit for bit (tests: 1e-6).
+__device__ void kf_update_dense(Slot& t, const float* meas, const double* r) {
+  double S[4][4], L[4][4] = {}, X[4][8], K[8][4];
+  for (int i = 0; i < 4; ++i)
+    for (int j = 0; j < 4; ++j) S[i][j] = t.Pd[8 * i + j] + (i == j ? r[i] : 0.0);
+  for (int j = 0; j < 4; ++j) {
+    double a = S[j][j];
+    for (int k = 0; k < j; ++k) a = a - L[j][k] * L[j][k];
+    L[j][j] = sqrt(a);
+    const double il = 1.0 / L[j][j];
+    for (int i = j + 1; i < 4; ++i) {
+      double v = S[i][j];
+      for (int k = 0; k < j; ++k) v = v - L[i][k] * L[j][k];
+      L[i][j] = v * il;
+    }
+  }
+  for (int j = 0; j < 8; ++j) {  // columns of (P H^T)^T
+    double y[4];
+    for (int i = 0; i < 4; ++i) {
+      double v = t.Pd[8 * j + i];
+      for (int k = 0; k < i; ++k) v = v - L[i][k] * y[k];
+      y[i] = v * (1.0 / L[i][i]);
+    }
+    for (int i = 3; i >= 0; --i) {
+      double v = y[i];
+      for (int k = i + 1; k < 4; ++k) v = v - L[k][i] * X[k][j];
+      X[i][j] = v * (1.0 / L[i][i]);
+    }
+  }
+  for (int j = 0; j < 8; ++j)
+    for (int c = 0; c < 4; ++c) K[j][c] = X[c][j];
+  double inn[4];
+  for (int c = 0; c < 4; ++c) inn[c] = (double)meas[c] - t.mean[c];
+  for (int i = 0; i < 8; ++i) {
+    double d = 0.0;
+    for (int c = 0; c < 4; ++c) d = d + inn[c] * K[i][c];
+    t.mean[i] = t.mean[i] + d;
+  }
+  double T[4][8];
+  for (int a = 0; a < 4; ++a)
+    for (int j = 0; j < 8; ++j) {
+      double v = 0.0;
+      for (int b = 0; b < 4; ++b) v = v + S[a][b] * K[j][b];
+      T[a][j] = v;
+    }
+  for (int i = 0; i < 8; ++i)
+    for (int j = 0; j < 8; ++j) {
+      double v = 0.0;
+      for (int a = 0; a < 4; ++a) v = v + K[i][a] * T[a][j];
+      t.Pd[8 * i + j] = t.Pd[8 * i + j] - v;
+    }
+  t.mean32 = 0;
+}
+
+// STrack.multi_gmc (byte_tracker.py:108-125) of one track: mean = R8x8 . mean, mean[:2] += t,
+// P = R8x8 . P . R8x8^T with R8x8 = kron(I4, H[:2, :2]); the covariance becomes dense (the warp
+// couples x and y).  The mean's two products are rounded separately (dgemv's lanes); the
+// covariance products accumulate with fma (dgemm's k loop) -- OpenBLAS's kernels, unpinned.
+__device__ void kf_gmc(Slot& t, const double* Hw) {
+  const double R00 = Hw[0], R01 = Hw[1], R10 = Hw[3], R11 = Hw[4];
+  if (!t.dense) {
+    for (int k = 0; k < 64; ++k) t.Pd[k] = 0.0;
+    for (int c = 0; c < 4; ++c) {
+      t.Pd[9 * c] = t.P[4 * c];
+      t.Pd[8 * c + c + 4] = t.P[4 * c + 1];
+      t.Pd[8 * (c + 4) + c] = t.P[4 * c + 2];
+      t.Pd[9 * (c + 4)] = t.P[4 * c + 3];
+    }
+    t.dense = 1;
+  }
+  for (int p = 0; p < 4; ++p) {
+    const double m0 = t.mean[2 * p], m1 = t.mean[2 * p + 1];
+    t.mean[2 * p] = R00 * m0 + R01 * m1;
+    t.mean[2 * p + 1] = R10 * m0 + R11 * m1;
+  }
+  t.mean[0] = t.mean[0] + Hw[2];
+  t.mean[1] = t.mean[1] + Hw[5];
+  double A[64];
+  for (int p = 0; p < 4; ++p)
+    for (int j = 0; j < 8; ++j) {
+      const double a = t.Pd[8 * (2 * p) + j], b = t.Pd[8 * (2 * p + 1) + j];
+      A[8 * (2 * p) + j] = fma(R01, b, R00 * a);
+      A[8 * (2 * p + 1) + j] = fma(R11, b, R10 * a);
+    }
+  for (int i = 0; i < 8; ++i)
+    for (int q = 0; q < 4; ++q) {
+      const double a = A[8 * i + 2 * q], b = A[8 * i + 2 * q + 1];
+      t.Pd[8 * i + 2 * q] = fma(b, R01, a * R00);
+      t.Pd[8 * i + 2 * q + 1] = fma(b, R11, a * R10);
+    }
   t.mean32 = 0;
 }
 
@@ -311,6 +428,10 @@ __device__ void kf_update(Slot& t, const float* meas, bool xywh) {
       const double s = c == 2 && !xywh ? 1e-1 : WP * (xywh ? ((c & 1) ? t.mean[3] : t.mean[2]) : t.mean[3]);
       r[c] = s * s;
     }
+  }
+  if (t.dense) {
+    kf_update_dense(t, meas, r);
+    return;
   }
   for (int c = 0; c < 4; ++c) {
     const double p = t.P[4 * c], a = t.P[4 * c + 1], b = t.P[4 * c + 2], v = t.P[4 * c + 3];
@@ -639,7 +760,8 @@ __device__ void apply_match(Slot& t, const Lds& L, int d, int frame, bool xywh, 
   *refound = !was_tracked;
 }
 
-__global__ void __launch_bounds__(NT) bt_step_kernel(Dev g, const float* __restrict__ dets, const int* __restrict__ counts) {
+__global__ void __launch_bounds__(NT) bt_step_kernel(Dev g, const float* __restrict__ dets, const int* __restrict__ counts,
+                                                     const double* __restrict__ warp) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int s = blockIdx.x, tid = threadIdx.x;
   const int T = g.T, Dm = g.D;
@@ -738,6 +860,11 @@ __global__ void __launch_bounds__(NT) bt_step_kernel(Dev g, const float* __restr
     }
   }
   __syncthreads();
+  if (warp) {  // GMC (byte_tracker.py:333-340): multi_gmc(strack_pool, warp), multi_gmc(unconfirmed, warp)
+    const double* Hw = warp + (size_t)s * 6;
+    for (int i = tid; i < npool + nun; i += NT) kf_gmc(slots[i < npool ? L.pool[i] : L.unc[i - npool]], Hw);
+    __syncthreads();
+  }
   int nact = 0, nref = 0, nlnew = 0, nrnew = 0;
   // first association: strack_pool x high detections, fused IoU cost, match_thresh (:342-353)
   for (int i = tid; i < npool; i += NT) track_xyxy(slots[L.pool[i]], xywh, &L.txy[4 * i]);
@@ -1115,10 +1242,15 @@ int yk_bt_reset(yk_bt* t, void* stream) {
 }
 
 int yk_bt_step(yk_bt* t, const float* dets, const int32_t* counts, void* stream) {
+  return yk_bt_step_warp(t, dets, counts, nullptr, stream);
+}
+
+int yk_bt_step_warp(yk_bt* t, const float* dets, const int32_t* counts, const double* warp, void* stream) {
   YK_CHECK_ARG(t && dets && counts, "yk_bt_step: NULL argument");
+  YK_CHECK_ARG(!warp || t->dev.cfg.xywh, "yk_bt_step_warp: a GMC warp needs the BoT-SORT tracker");
   yk::DeviceGuard guard(t->ctx->device);
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(yk::bt::bt_step_kernel, dim3(t->S), dim3(yk::bt::NT), t->lds, st, t->dev, dets, counts);
+  hipLaunchKernelGGL(yk::bt::bt_step_kernel, dim3(t->S), dim3(yk::bt::NT), t->lds, st, t->dev, dets, counts, warp);
   hipLaunchKernelGGL(yk::bt::bt_ids_kernel, dim3(t->S), dim3(64), 0, st, t->dev, t->S);
   hipLaunchKernelGGL(yk::bt::bt_ids_advance_kernel, dim3(1), dim3(64), 0, st, t->dev, t->S);
   YK_HIP(hipGetLastError());

@@ -25,6 +25,17 @@
 // The OpenCV stages follow OpenCV 4.x's algorithms as restated in oracle/gmd_ref.py (cv2 itself
 // is absent, so that restatement is unpinned); these kernels reproduce the restatement bit for
 // bit.  Compiled with -ffp-contract=off: every float expression rounds like the C++ / numpy one.
+//
+// YK_GMD_SPARSE_OPTFLOW (BoT-SORT's GMC, ultralytics/trackers/utils/gmc.py:278-345) runs the same
+// stages with the GMC's parameters on the half-resolution gray image -- gray_down_kernel (gray of
+// each 2x2 block, then cv2.resize's INTER_AREA fast path (a+b+c+d+2) >> 2), eig_kernel<3>
+// (blockSize 3), select_top_kernel (minDistance 1 keeps every local maximum: the 1000 largest keys
+// in goodFeaturesToTrack order), lk_kernel -- and gmc_kernel: estimateAffinePartial2D (RANSAC with
+// cv::RNG, closed-form 2-point similarity, float32 errors, RANSACUpdateNumIters; then the
+// Levenberg-Marquardt refinement) restated in oracle/gmc_ref.py.  Each stream keeps its previous
+// frame in the pyramid buffer sel[s]; the new frame goes to sel[s] ^ 1 and sel flips at the end of
+// the call (not after a failed GMC estimate, which keeps the previous frame like the reference's
+// exception path).
 #include <cfloat>
 #include <climits>
 
@@ -37,6 +48,7 @@ constexpr int WIN = 21;                      // lk_params winSize
 constexpr int WAREA = WIN * WIN;             // 441 window pixels
 constexpr int NSLOT = (WAREA + 63) / 64;     // 7 window pixels per lane
 constexpr int MAXC = 200;                    // feature_params maxCorners
+constexpr int MAXC_G = 1000;                 // GMC feature_params maxCorners (gmc.py:78-80)
 constexpr int MINDIST2 = 225;                // minDistance^2 (corners sit on integer pixels)
 constexpr int MAXLV = 3;                     // lk_params maxLevel
 constexpr int MAXIT = 30;                    // criteria count
@@ -55,7 +67,7 @@ struct Geo {
 };
 
 struct State {
-  int has_prev;
+  int has_prev;  // GlobalMotionDetector: a previous frame is stored (first_frame otherwise)
   int mv_len, mv_head;
   float mv[MVQ][2];
   long long total, motion_events, reset_triggers;
@@ -78,6 +90,12 @@ struct Dev {
   State* st;               // [S]
   yk_motion* out;          // [S]
   float thr_motion, thr_reset, thr_reset_cons;
+  int* sel;                // [S] pyramid buffer holding the stream's previous frame
+  int mode;                // 0 GlobalMotionDetector, 1 GMC sparseOptFlow
+  int maxc;                // corners per stream (MAXC / MAXC_G): stride of corners / next / status
+  int W0, H0;              // input frame size (GMC: twice geo.W / geo.H)
+  double* warp;            // [S][6] GMC warp
+  int* info;               // [S][5] GMC diagnostics (yk_gmc_info)
 };
 
 __device__ __forceinline__ int refl(int i, int n) {  // BORDER_REFLECT_101, |overflow| < n
@@ -102,18 +120,36 @@ __device__ __forceinline__ long long wave_sum64(long long v) {
 }
 
 // ---------------------------------------------------------------- frame ingest
-__global__ void __launch_bounds__(256) gray_kernel(Dev g, const unsigned char* __restrict__ frames, int cur) {
-  const int s = blockIdx.y;
+__device__ __forceinline__ int gray_of(const unsigned char* p) {
+  return (p[0] * 1868 + p[1] * 9617 + p[2] * 4899 + (1 << 13)) >> 14;
+}
+__global__ void __launch_bounds__(256) gray_kernel(Dev g, const unsigned char* __restrict__ frames) {
+  const int s = blockIdx.y, cur = g.sel[s] ^ 1;
   const long long n = (long long)g.geo.W * g.geo.H;
   const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
   const unsigned char* p = frames + ((long long)s * n + i) * 3;
-  const int v = (p[0] * 1868 + p[1] * 9617 + p[2] * 4899 + (1 << 13)) >> 14;
-  g.pyr[cur][(long long)s * g.geo.per + i] = (unsigned char)v;
+  g.pyr[cur][(long long)s * g.geo.per + i] = (unsigned char)gray_of(p);
 }
 
-__global__ void __launch_bounds__(256) pyrdown_kernel(Dev g, int cur, int l) {
-  const int s = blockIdx.z;
+// GMC: cvtColor(BGR2GRAY) then cv2.resize(gray, (W / 2, H / 2)): INTER_LINEAR at an exact 1/2
+// scale is resize.cpp's INTER_AREA fast path, (a + b + c + d + 2) >> 2 of each 2x2 block
+// (gmc.py:296-301; oracle/gmc_ref.py area_down2)
+__global__ void __launch_bounds__(256) gray_down_kernel(Dev g, const unsigned char* __restrict__ frames) {
+  const int s = blockIdx.y, cur = g.sel[s] ^ 1;
+  const int W = g.geo.W, H = g.geo.H, W0 = g.W0;
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long long)W * H) return;
+  const int y = (int)(i / W), x = (int)(i - (long long)y * W);
+  const unsigned char* f = frames + (long long)s * W0 * g.H0 * 3;
+  const unsigned char* r0 = f + ((long long)(2 * y) * W0 + 2 * x) * 3;
+  const unsigned char* r1 = r0 + (long long)W0 * 3;
+  const int v = gray_of(r0) + gray_of(r0 + 3) + gray_of(r1) + gray_of(r1 + 3);
+  g.pyr[cur][(long long)s * g.geo.per + i] = (unsigned char)((v + 2) >> 2);
+}
+
+__global__ void __launch_bounds__(256) pyrdown_kernel(Dev g, int l) {
+  const int s = blockIdx.z, cur = g.sel[s] ^ 1;
   const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = blockIdx.y * 16 + (threadIdx.x >> 4);
   const int dw = g.geo.lw[l], dh = g.geo.lh[l], sw = g.geo.lw[l - 1], sh = g.geo.lh[l - 1];
   if (x >= dw || y >= dh) return;
@@ -135,8 +171,8 @@ __global__ void __launch_bounds__(256) pyrdown_kernel(Dev g, int cur, int l) {
 }
 
 // calcSharrDeriv: vertical [3 10 3] / [-1 0 1], then horizontal [-1 0 1] / [3 10 3], reflect-101.
-__global__ void __launch_bounds__(256) scharr_kernel(Dev g, int cur, int l) {
-  const int s = blockIdx.z;
+__global__ void __launch_bounds__(256) scharr_kernel(Dev g, int l) {
+  const int s = blockIdx.z, cur = g.sel[s] ^ 1;
   const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = blockIdx.y * 16 + (threadIdx.x >> 4);
   const int w = g.geo.lw[l], h = g.geo.lh[l];
   if (x >= w || y >= h) return;
@@ -162,30 +198,33 @@ __global__ void clear_kernel(Dev g) {
   }
 }
 
-// cornerMinEigenVal on a 16x16 output tile: the 22x22 Sobel-product halo (box radius 3; the
-// products outside the image are those of the reflected pixel, like boxFilter's reflect-101
-// border over the product image), 7-wide horizontal then vertical integer sums.  The gray pixels
-// the Sobel taps of those products read -- rows / columns [o - 1, o + 23) of the image, each
-// product at its reflected position with Sobel's own reflect-101 neighbours -- are staged in LDS
-// once (coalesced rows), so a product costs LDS reads instead of eight global byte loads.
-__global__ void __launch_bounds__(256) eig_kernel(Dev g, int prev) {
-  __shared__ int gt[24][25];
-  __shared__ int pxx[22][23], pxy[22][23], pyy[22][23];
-  __shared__ int hxx[22][17], hxy[22][17], hyy[22][17];
+// cornerMinEigenVal on a 16x16 output tile: the (16 + BS - 1)^2 Sobel-product halo (box radius
+// BS / 2; the products outside the image are those of the reflected pixel, like boxFilter's
+// reflect-101 border over the product image), BS-wide horizontal then vertical integer sums.  The
+// gray pixels the Sobel taps of those products read -- rows / columns [o - 1, o + 16 + BS) of the
+// image, each product at its reflected position with Sobel's own reflect-101 neighbours -- are
+// staged in LDS once (coalesced rows), so a product costs LDS reads instead of eight global byte
+// loads.  BS = 7: GlobalMotionDetector (global_motion_detector.py:49-55); 3: GMC (gmc.py:78-80).
+template <int BS>
+__global__ void __launch_bounds__(256) eig_kernel(Dev g) {
+  constexpr int R = BS / 2, PN = 16 + 2 * R, GN = PN + 2;
+  __shared__ int gt[GN][GN + 1];
+  __shared__ int pxx[PN][PN + 1], pxy[PN][PN + 1], pyy[PN][PN + 1];
+  __shared__ int hxx[PN][17], hxy[PN][17], hyy[PN][17];
   __shared__ unsigned wmax[4];
   const int s = blockIdx.z, W = g.geo.W, H = g.geo.H, tid = threadIdx.x;
-  const unsigned char* img = g.pyr[prev] + (long long)s * g.geo.per;
-  const int ox = blockIdx.x * 16 - 3, oy = blockIdx.y * 16 - 3;
+  const unsigned char* img = g.pyr[g.sel[s]] + (long long)s * g.geo.per;
+  const int ox = blockIdx.x * 16 - R, oy = blockIdx.y * 16 - R;
   const int gy0 = oy - 1, gx0 = ox - 1;  // LDS tile origin (image coordinates)
-  for (int i = tid; i < 24 * 24; i += 256) {
-    const int ry = i / 24, rx = i - ry * 24;
+  for (int i = tid; i < GN * GN; i += 256) {
+    const int ry = i / GN, rx = i - ry * GN;
     const int y = gy0 + ry, x = gx0 + rx;
     gt[ry][rx] = (y >= 0 && y < H && x >= 0 && x < W) ? (int)img[(long long)y * W + x] : 0;
   }
   __syncthreads();
-  auto cl = [](int v) { return v < 0 ? 0 : (v > 23 ? 23 : v); };  // only outputs outside the image clamp
-  for (int i = tid; i < 22 * 22; i += 256) {
-    const int ry = i / 22, rx = i - ry * 22;
+  auto cl = [](int v) { return v < 0 ? 0 : (v > GN - 1 ? GN - 1 : v); };  // only outputs outside the image clamp
+  for (int i = tid; i < PN * PN; i += 256) {
+    const int ry = i / PN, rx = i - ry * PN;
     const int y = refl_c(oy + ry, H), x = refl_c(ox + rx, W);
     const int ya = cl(refl(y - 1, H) - gy0), yb = cl(y - gy0), yc = cl(refl(y + 1, H) - gy0);
     const int xm = cl(refl(x - 1, W) - gx0), xc = cl(x - gx0), xp = cl(refl(x + 1, W) - gx0);
@@ -196,11 +235,11 @@ __global__ void __launch_bounds__(256) eig_kernel(Dev g, int prev) {
     pyy[ry][rx] = iy * iy;
   }
   __syncthreads();
-  for (int i = tid; i < 22 * 16; i += 256) {
+  for (int i = tid; i < PN * 16; i += 256) {
     const int ry = i >> 4, cx = i & 15;
     int a = 0, b = 0, c = 0;
 #pragma unroll
-    for (int k = 0; k < 7; ++k) {
+    for (int k = 0; k < BS; ++k) {
       a += pxx[ry][cx + k];
       b += pxy[ry][cx + k];
       c += pyy[ry][cx + k];
@@ -213,7 +252,7 @@ __global__ void __launch_bounds__(256) eig_kernel(Dev g, int prev) {
   const int tx = tid & 15, ty = tid >> 4;
   int sxx = 0, sxy = 0, syy = 0;
 #pragma unroll
-  for (int k = 0; k < 7; ++k) {
+  for (int k = 0; k < BS; ++k) {
     sxx += hxx[ty + k][tx];
     sxy += hxy[ty + k][tx];
     syy += hyy[ty + k][tx];
@@ -221,7 +260,8 @@ __global__ void __launch_bounds__(256) eig_kernel(Dev g, int prev) {
   const int x = blockIdx.x * 16 + tx, y = blockIdx.y * 16 + ty;
   unsigned m = 0u;
   if (x < W && y < H) {
-    const double s2 = 1.0 / (7140.0 * 7140.0);  // (1 / (4 * blockSize * 255))^2
+    constexpr double sc = 4.0 * BS * 255.0;
+    const double s2 = 1.0 / (sc * sc);  // (1 / (4 * blockSize * 255))^2
     const float cxx = (float)((double)sxx * s2), cxy = (float)((double)sxy * s2), cyy = (float)((double)syy * s2);
     const float a = cxx * 0.5f, c = cyy * 0.5f, d = a - c;
     const float e = (a + c) - sqrtf(d * d + cxy * cxy);
@@ -513,8 +553,71 @@ __global__ void __launch_bounds__(NTS) select_kernel(Dev g) {
   }
   __syncthreads();
   const int na = L.misc[S_NA];
-  for (int i = tid; i < na; i += NTS) g.corners[s * MAXC + i] = make_float2((float)L.ax[i], (float)L.ay[i]);
+  for (int i = tid; i < na; i += NTS) g.corners[s * g.maxc + i] = make_float2((float)L.ax[i], (float)L.ay[i]);
   if (tid == 0) g.ncorners[s] = na;
+}
+
+// GMC (minDistance 1): goodFeaturesToTrack's greedy pass keeps every candidate (distinct pixels are
+// >= 1 apart; featureselect.cpp tests dx*dx + dy*dy < minDistance^2), so its corners are the
+// MAXC_G largest keys in (value desc, address desc) order: the MAXC_G-th largest key by radix
+// select, the keys >= it gathered and bitonic-sorted descending in LDS.
+__global__ void __launch_bounds__(NTS) select_top_kernel(Dev g) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  SelLds L = carve_sel(smem);
+  const int s = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+  const int W = g.geo.W;
+  const long long HW = (long long)W * g.geo.H;
+  const unsigned long long* keys = g.cand + s * HW;
+  int n = g.ncand[s];
+  if (n > HW) n = (int)HW;
+  const bool all = n <= MAXC_G;
+  const unsigned long long K = all ? 0ull : kth_largest(keys, n, 0ull, false, MAXC_G, L);
+  if (tid == 0) L.misc[S_CNT] = 0;
+  __syncthreads();
+  for (int base = 0; base < n; base += NTS) {
+    const int i = base + tid;
+    unsigned long long key = 0ull;
+    bool in = false;
+    if (i < n) {
+      key = keys[i];
+      in = all || key >= K;
+    }
+    const unsigned long long mask = __ballot(in);
+    if (mask) {
+      const int leader = __ffsll((long long)mask) - 1;
+      int b = 0;
+      if (lane == leader) b = atomicAdd(&L.misc[S_CNT], __popcll(mask));
+      b = __shfl(b, leader);
+      if (in) L.keys[b + __popcll(mask & ((1ull << lane) - 1ull))] = key;
+    }
+  }
+  __syncthreads();
+  const int m = L.misc[S_CNT];
+  int P = 2;
+  while (P < m) P <<= 1;
+  for (int i = m + tid; i < P; i += NTS) L.keys[i] = 0ull;
+  __syncthreads();
+  for (int k = 2; k <= P; k <<= 1)
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = tid; i < P; i += NTS) {
+        const int ixj = i ^ j;
+        if (ixj > i) {
+          const unsigned long long a = L.keys[i], b = L.keys[ixj];
+          const bool desc = (i & k) == 0;
+          if (desc ? a < b : a > b) {
+            L.keys[i] = b;
+            L.keys[ixj] = a;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  for (int i = tid; i < m; i += NTS) {
+    const unsigned a = (unsigned)(L.keys[i] & 0xffffffffull);
+    const int y = (int)(a / (unsigned)W), x = (int)(a - (unsigned)y * (unsigned)W);
+    g.corners[s * g.maxc + i] = make_float2((float)x, (float)y);
+  }
+  if (tid == 0) g.ncorners[s] = m;
 }
 
 // ---------------------------------------------------------------- calcOpticalFlowPyrLK
@@ -527,12 +630,13 @@ __device__ __forceinline__ void lk_weights(float a, float b, int& w00, int& w01,
 }
 
 // One wavefront per corner (4 corners per workgroup); all control flow is wave-uniform.
-__global__ void __launch_bounds__(256) lk_kernel(Dev g, int prev, int cur) {
+__global__ void __launch_bounds__(256) lk_kernel(Dev g) {
   const int s = blockIdx.y, lane = threadIdx.x & 63;
   const int p = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (p >= g.ncorners[s]) return;
+  const int prev = g.sel[s], cur = prev ^ 1;
   const Geo& G = g.geo;
-  const float2 pt = g.corners[s * MAXC + p];
+  const float2 pt = g.corners[s * g.maxc + p];
   const unsigned char* Ib = g.pyr[prev] + (long long)s * G.per;
   const short2* Db = g.der[prev] + (long long)s * G.per;
   const unsigned char* Jb = g.pyr[cur] + (long long)s * G.per;
@@ -649,8 +753,8 @@ __global__ void __launch_bounds__(256) lk_kernel(Dev g, int prev, int cur) {
     }
   }
   if (lane == 0) {
-    g.next[s * MAXC + p] = nxt;
-    g.status[s * MAXC + p] = (unsigned char)status;
+    g.next[s * g.maxc + p] = nxt;
+    g.status[s * g.maxc + p] = (unsigned char)status;
   }
 }
 
@@ -676,6 +780,7 @@ __global__ void __launch_bounds__(256) finish_kernel(Dev g, yk_motion* __restric
       r.consistency = -1.0f;
       out[s] = r;
       S.has_prev = 1;
+      g.sel[s] ^= 1;  // this frame is the next call's previous one
     }
     return;
   }
@@ -683,9 +788,9 @@ __global__ void __launch_bounds__(256) finish_kernel(Dev g, yk_motion* __restric
   // status == 1 compaction in corner order (n <= 200 < 256 threads)
   int flag = 0;
   float mvx = 0.0f, mvy = 0.0f;
-  if (tid < n && n >= 20 && g.status[s * MAXC + tid]) {
+  if (tid < n && n >= 20 && g.status[s * g.maxc + tid]) {
     flag = 1;
-    const float2 a = g.corners[s * MAXC + tid], b = g.next[s * MAXC + tid];
+    const float2 a = g.corners[s * g.maxc + tid], b = g.next[s * g.maxc + tid];
     mvx = b.x - a.x;  // next_points - prev_points (:140)
     mvy = b.y - a.y;
   }
@@ -726,7 +831,7 @@ __global__ void __launch_bounds__(256) finish_kernel(Dev g, yk_motion* __restric
     if (tid < ng) sd[rank_of(dist, ng, tid)] = dist[tid];
     __syncthreads();
   }
-  if (tid != 0) return;
+  if (tid != 0) return;  // (tid 0 flips sel at the end)
   yk_motion r{};
   r.valid = 1;
   r.consistency = -1.0f;
@@ -803,6 +908,357 @@ __global__ void __launch_bounds__(256) finish_kernel(Dev g, yk_motion* __restric
   S.reset_triggers += r.should_reset;
   S.avg = (S.avg * (float)(S.total - 1) + r.magnitude) / (float)S.total;
   out[s] = r;
+  g.sel[s] ^= 1;
+}
+
+// ---------------------------------------------------------------- GMC: estimateAffinePartial2D
+// oracle/gmc_ref.py restates OpenCV 4.x ptsetreg.cpp / levmarq.cpp; this kernel reproduces that
+// restatement operation for operation (-ffp-contract=off).  One workgroup per stream: thread 0
+// runs the sequential parts (cv::RNG, the 2-point kernel, the RANSAC bookkeeping, the 4x4 LM
+// solves), every thread the per-point work; sums over points use lane_sum's order (lane t adds
+// points t, t + 256, ... in turn, then a pairwise tree over the 256 lanes).
+constexpr int GT = 256;
+constexpr unsigned long long RNG_COEFF = 4164903690ull;
+
+__device__ __forceinline__ unsigned rng_next(unsigned long long& st) {
+  st = (unsigned long long)(unsigned)st * RNG_COEFF + (unsigned)(st >> 32);
+  return (unsigned)st;
+}
+__device__ __forceinline__ int rng_uniform(unsigned long long& st, int a, int b) {
+  return a == b ? a : (int)(rng_next(st) % (unsigned)(b - a) + (unsigned)a);
+}
+
+// RANSACUpdateNumIters (pow(x, 2) of a double is x * x correctly rounded, as glibc's pow)
+__device__ int ransac_update_num_iters(double p, double ep, int max_iters) {
+  p = p < 0.0 ? 0.0 : (p > 1.0 ? 1.0 : p);
+  ep = ep < 0.0 ? 0.0 : (ep > 1.0 ? 1.0 : ep);
+  double num = 1.0 - p;
+  num = num > DBL_MIN ? num : DBL_MIN;
+  const double q = 1.0 - ep;
+  double denom = 1.0 - q * q;
+  if (denom < DBL_MIN) return 0;
+  num = log(num);
+  denom = log(denom);
+  if (denom >= 0 || -num >= (double)max_iters * (-denom)) return max_iters;
+  return (int)rint(num / denom);
+}
+
+// Cholesky solve of a 4x4 SPD system in oracle/gmc_ref.py chol_solve4's order
+__device__ void chol_solve4(const double A[4][4], const double* b, double* x) {
+  double L[4][4] = {};
+  for (int j = 0; j < 4; ++j) {
+    double sj = A[j][j];
+    for (int k = 0; k < j; ++k) sj = sj - L[j][k] * L[j][k];
+    L[j][j] = sj > 0.0 ? sqrt(sj) : __builtin_nan("");
+    for (int i = j + 1; i < 4; ++i) {
+      double si = A[i][j];
+      for (int k = 0; k < j; ++k) si = si - L[i][k] * L[j][k];
+      L[i][j] = si / L[j][j];
+    }
+  }
+  double y[4];
+  for (int i = 0; i < 4; ++i) {
+    double si = b[i];
+    for (int k = 0; k < i; ++k) si = si - L[i][k] * y[k];
+    y[i] = si / L[i][i];
+  }
+  for (int i = 3; i >= 0; --i) {
+    double si = y[i];
+    for (int k = i + 1; k < 4; ++k) si = si - L[k][i] * x[k];
+    x[i] = si / L[i][i];
+  }
+}
+
+// lane_sum of NQ per-thread partials: red[q][GT] in LDS, pairwise tree; result in red[q][0]
+template <int NQ>
+__device__ __forceinline__ void tree_reduce(double (*red)[GT]) {
+  for (int o = GT / 2; o >= 1; o >>= 1) {
+    __syncthreads();
+    if ((int)threadIdx.x < o)
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) red[q][threadIdx.x] = red[q][threadIdx.x] + red[q][threadIdx.x + o];
+  }
+  __syncthreads();
+}
+
+enum { G_GO = 0, G_GOOD = 1, G_RECOMP = 2, G_N = 3 };
+
+__global__ void __launch_bounds__(GT) gmc_kernel(Dev g, double* __restrict__ out) {
+  __shared__ float fx[MAXC_G], fy[MAXC_G], tx[MAXC_G], ty[MAXC_G];  // tracked points; then the inliers first
+  __shared__ double red[9][GT];
+  __shared__ double xs[4], xds[4];  // LM parameters (a, b, tx, ty): current / trial
+  __shared__ float F[6];
+  __shared__ int wcnt[GT / 64], misc[8];
+  const int s = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  State& S = g.st[s];
+  double H[6] = {1.0, 0.0, 0.0, 0.0, 1.0, 0.0};
+  int state = 0, npts = 0, max_good = 0, rit = 0, lit = 0;
+  bool flip = true;
+  const bool have = S.has_prev && g.ncorners[s] > 0;  // gmc.py:306-311 (first frame / no previous keypoints)
+  if (have) {
+    // the points with status 1, in corner order (gmc.py:317-324)
+    const int n = g.ncorners[s];
+    int base = 0;
+    for (int c0 = 0; c0 < n; c0 += GT) {
+      const int i = c0 + tid;
+      const int f = i < n && g.status[s * g.maxc + i] ? 1 : 0;
+      const unsigned long long bm = __ballot(f);
+      if (lane == 0) wcnt[wave] = __popcll(bm);
+      __syncthreads();
+      int pos = base + __popcll(bm & ((1ull << lane) - 1ull)), tot = 0;
+      for (int w = 0; w < GT / 64; ++w) {
+        pos += w < wave ? wcnt[w] : 0;
+        tot += wcnt[w];
+      }
+      if (f) {
+        const float2 a = g.corners[s * g.maxc + i], b = g.next[s * g.maxc + i];
+        fx[pos] = a.x;
+        fy[pos] = a.y;
+        tx[pos] = b.x;
+        ty[pos] = b.y;
+      }
+      base += tot;
+      __syncthreads();
+    }
+    npts = base;
+    state = 2;  // "not enough matching points": the identity (gmc.py:327-336)
+  }
+  if (have && npts > 4) {
+    // ---- RANSACPointSetRegistrator::run (modelPoints 2, threshold 3, confidence 0.99, 2000 iterations)
+    const float thr = (float)(3.0 * 3.0);
+    unsigned long long rng = ~0ull;  // RNG((uint64)-1)
+    int niters = 2000;
+    double M[6] = {0, 0, 0, 0, 0, 0}, best[6] = {0, 0, 0, 0, 0, 0};
+    for (;;) {
+      if (tid == 0) {
+        misc[G_GO] = rit < niters;
+        if (rit < niters) {
+          const int i0 = rng_uniform(rng, 0, npts);
+          int i1 = rng_uniform(rng, 0, npts);
+          while (i1 == i0) i1 = rng_uniform(rng, 0, npts);
+          // AffinePartial2DEstimatorCallback::runKernel
+          const double x1 = fx[i0], y1 = fy[i0], x2 = fx[i1], y2 = fy[i1];
+          const double X1 = tx[i0], Y1 = ty[i0], X2 = tx[i1], Y2 = ty[i1];
+          const double d = 1. / ((x1 - x2) * (x1 - x2) + (y1 - y2) * (y1 - y2));
+          const double S0 = d * ((X1 - X2) * (x1 - x2) + (Y1 - Y2) * (y1 - y2));
+          const double S1 = d * ((Y1 - Y2) * (x1 - x2) - (X1 - X2) * (y1 - y2));
+          const double S2 = d * ((Y1 - Y2) * (x1 * y2 - x2 * y1) - (X1 * y2 - X2 * y1) * (y1 - y2) - (X1 * x2 - X2 * x1) * (x1 - x2));
+          const double S3 = d * (-(X1 - X2) * (x1 * y2 - x2 * y1) - (Y1 * x2 - Y2 * x1) * (x1 - x2) - (Y1 * y2 - Y2 * y1) * (y1 - y2));
+          M[0] = S0; M[1] = -S1; M[2] = S2; M[3] = S1; M[4] = S0; M[5] = S3;
+          for (int k = 0; k < 6; ++k) F[k] = (float)M[k];
+        }
+      }
+      __syncthreads();
+      if (!misc[G_GO]) break;
+      int c = 0;  // findInliers: err <= thr^2 (float32 error, computeError)
+      for (int i = tid; i < npts; i += GT) {
+        const float a = F[0] * fx[i] + F[1] * fy[i] + F[2] - tx[i];
+        const float b = F[3] * fx[i] + F[4] * fy[i] + F[5] - ty[i];
+        c += (a * a + b * b) <= thr ? 1 : 0;
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
+      if (lane == 0) wcnt[wave] = c;
+      __syncthreads();
+      if (tid == 0) {
+        int good = 0;
+        for (int w = 0; w < GT / 64; ++w) good += wcnt[w];
+        if (good > (max_good > 1 ? max_good : 1)) {
+          for (int k = 0; k < 6; ++k) best[k] = M[k];
+          max_good = good;
+          niters = ransac_update_num_iters(0.99, (double)(npts - good) / npts, niters);
+        }
+        ++rit;
+      }
+      __syncthreads();
+    }
+    if (tid == 0) {
+      misc[G_GOOD] = max_good;
+      for (int k = 0; k < 6; ++k) F[k] = (float)best[k];
+      xs[0] = best[0];  // Hvec = (H[0], H[3], H[2], H[5]) (ptsetreg.cpp estimateAffinePartial2D)
+      xs[1] = best[3];
+      xs[2] = best[2];
+      xs[3] = best[5];
+    }
+    __syncthreads();
+    max_good = misc[G_GOOD];
+    if (max_good <= 0) {
+      state = 3;  // cv2 returns None: the identity, the previous frame kept
+      flip = false;
+    } else {
+      state = 1;
+      // compressElems: the best model's inliers first, in order (the mask recomputed from it)
+      float ix[4], iy[4], jx[4], jy[4];
+      int mine[4];
+      const int nchunk = (npts + GT - 1) / GT;
+      for (int k = 0; k < nchunk; ++k) {
+        const int i = k * GT + tid;
+        mine[k] = 0;
+        if (i < npts) {
+          ix[k] = fx[i];
+          iy[k] = fy[i];
+          jx[k] = tx[i];
+          jy[k] = ty[i];
+          const float a = F[0] * fx[i] + F[1] * fy[i] + F[2] - tx[i];
+          const float b = F[3] * fx[i] + F[4] * fy[i] + F[5] - ty[i];
+          mine[k] = (a * a + b * b) <= thr ? 1 : 0;
+        }
+      }
+      __syncthreads();
+      int nin = 0;
+      for (int k = 0; k < nchunk; ++k) {
+        const unsigned long long bm = __ballot(mine[k]);
+        if (lane == 0) wcnt[wave] = __popcll(bm);
+        __syncthreads();
+        int pos = nin + __popcll(bm & ((1ull << lane) - 1ull)), tot = 0;
+        for (int w = 0; w < GT / 64; ++w) {
+          pos += w < wave ? wcnt[w] : 0;
+          tot += wcnt[w];
+        }
+        if (mine[k]) {
+          fx[pos] = ix[k];
+          fy[pos] = iy[k];
+          tx[pos] = jx[k];
+          ty[pos] = jy[k];
+        }
+        nin += tot;
+        __syncthreads();
+      }
+      // ---- LMSolverImpl::run on (a, b, tx, ty), 10 iterations, eps FLT_EPSILON
+      // normal(x): J^T J, J^T r, |r|^2 and max |r| at xs, summed in lane_sum order
+      auto normal = [&](const double* h) {
+        double q[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+        for (int i = tid; i < nin; i += GT) {
+          const double Mx = fx[i], My = fy[i];
+          const double rx = ((h[0] * Mx - h[1] * My) + h[2]) - (double)tx[i];
+          const double ry = ((h[1] * Mx + h[0] * My) + h[3]) - (double)ty[i];
+          q[0] = q[0] + (Mx * Mx + My * My);
+          q[1] = q[1] + Mx;
+          q[2] = q[2] + My;
+          q[3] = q[3] + (Mx * rx + My * ry);
+          q[4] = q[4] + ((-My) * rx + Mx * ry);
+          q[5] = q[5] + rx;
+          q[6] = q[6] + ry;
+          q[7] = q[7] + (rx * rx + ry * ry);
+          q[8] = fmax(q[8], fmax(fabs(rx), fabs(ry)));
+        }
+        for (int k = 0; k < 9; ++k) red[k][tid] = q[k];
+        for (int o = GT / 2; o >= 1; o >>= 1) {
+          __syncthreads();
+          if (tid < o) {
+            for (int k = 0; k < 8; ++k) red[k][tid] = red[k][tid] + red[k][tid + o];
+            red[8][tid] = fmax(red[8][tid], red[8][tid + o]);
+          }
+        }
+        __syncthreads();
+      };
+      auto sumsq = [&](const double* h) {  // |r|^2 at h
+        double q = 0.0;
+        for (int i = tid; i < nin; i += GT) {
+          const double Mx = fx[i], My = fy[i];
+          const double rx = ((h[0] * Mx - h[1] * My) + h[2]) - (double)tx[i];
+          const double ry = ((h[1] * Mx + h[0] * My) + h[3]) - (double)ty[i];
+          q = q + (rx * rx + ry * ry);
+        }
+        red[0][tid] = q;
+        tree_reduce<1>(red);
+      };
+      double A[4][4], v[4], D[4], Sc = 0.0, rinf = 0.0, lam = 1.0, lc = 0.75;
+      const double nd = (double)nin;
+      auto take = [&]() {  // thread 0: A, v, S, max |r| from the reduction
+        const double sxx = red[0][0], sx = red[1][0], sy = red[2][0];
+        const double a[4][4] = {{sxx, 0.0, sx, sy}, {0.0, sxx, -sy, sx}, {sx, -sy, nd, 0.0}, {sy, sx, 0.0, nd}};
+        for (int i = 0; i < 4; ++i)
+          for (int j = 0; j < 4; ++j) A[i][j] = a[i][j];
+        for (int k = 0; k < 4; ++k) v[k] = red[3 + k][0];
+        rinf = red[8][0];
+      };
+      normal(xs);
+      if (tid == 0) {
+        take();
+        Sc = red[7][0];
+        for (int i = 0; i < 4; ++i) D[i] = A[i][i];
+      }
+      for (;;) {
+        double d[4];
+        if (tid == 0) {
+          double Ap[4][4];
+          for (int i = 0; i < 4; ++i)
+            for (int j = 0; j < 4; ++j) Ap[i][j] = A[i][j];
+          for (int i = 0; i < 4; ++i) Ap[i][i] = Ap[i][i] + lam * D[i];
+          chol_solve4(Ap, v, d);
+          for (int k = 0; k < 4; ++k) xds[k] = xs[k] - d[k];
+        }
+        __syncthreads();
+        sumsq(xds);
+        if (tid == 0) {
+          const double Sd = red[0][0];
+          double temp[4];
+          for (int i = 0; i < 4; ++i)
+            temp[i] = (A[i][0] * d[0] + A[i][1] * d[1] + A[i][2] * d[2] + A[i][3] * d[3]) * -1.0 + 2.0 * v[i];
+          const double dS = d[0] * temp[0] + d[1] * temp[1] + d[2] * temp[2] + d[3] * temp[3];
+          const double R = (Sc - Sd) / (fabs(dS) > DBL_EPSILON ? dS : 1.0);
+          if (R > 0.75) {
+            lam *= 0.5;
+            if (lam < lc) lam = 0.0;
+          } else if (R < 0.25) {
+            const double t = d[0] * v[0] + d[1] * v[1] + d[2] * v[2] + d[3] * v[3];
+            double nu = (Sd - Sc) / (fabs(t) > DBL_EPSILON ? t : 1.0) + 2.0;
+            nu = fmin(fmax(nu, 2.0), 10.0);
+            if (lam == 0.0) {
+              double mx = DBL_EPSILON;
+              for (int i = 0; i < 4; ++i) {
+                double e[4] = {0.0, 0.0, 0.0, 0.0}, c[4];
+                e[i] = 1.0;
+                chol_solve4(A, e, c);
+                mx = fmax(mx, fabs(c[i]));
+              }
+              lam = lc = 1.0 / mx;
+              nu *= 0.5;
+            }
+            lam *= nu;
+          }
+          misc[G_RECOMP] = Sd < Sc;
+          if (Sd < Sc) {
+            Sc = Sd;
+            for (int k = 0; k < 4; ++k) xs[k] = xds[k];
+          }
+        }
+        __syncthreads();
+        if (misc[G_RECOMP]) {
+          normal(xs);
+          if (tid == 0) take();
+        }
+        if (tid == 0) {
+          ++lit;
+          double dinf = 0.0;
+          for (int k = 0; k < 4; ++k) dinf = fmax(dinf, fabs(d[k]));
+          misc[G_GO] = lit < 10 && dinf >= (double)FLT_EPSILON && rinf >= (double)FLT_EPSILON;
+        }
+        __syncthreads();
+        if (!misc[G_GO]) break;
+      }
+      if (tid == 0) {  // H = [[a, -b, tx], [b, a, ty]], translation scaled back by the downscale 2
+        H[0] = xs[0];
+        H[1] = -xs[1];
+        H[2] = xs[2] * 2.0;
+        H[3] = xs[1];
+        H[4] = xs[0];
+        H[5] = xs[3] * 2.0;
+      }
+    }
+  }
+  if (tid == 0) {
+    for (int k = 0; k < 6; ++k) out[s * 6 + k] = H[k];
+    int* inf = g.info + s * 5;
+    inf[0] = npts;
+    inf[1] = max_good;
+    inf[2] = rit;
+    inf[3] = lit;
+    inf[4] = state;
+    S.has_prev = 1;
+    if (flip) g.sel[s] ^= 1;
+  }
 }
 
 __global__ void state_reset_kernel(Dev g, int stats_only) {
@@ -811,6 +1267,7 @@ __global__ void state_reset_kernel(Dev g, int stats_only) {
   State& S = g.st[s];
   if (!stats_only) {
     S.has_prev = 0;
+    g.sel[s] = 0;
     S.mv_len = S.mv_head = 0;
     yk_motion r{};
     r.consistency = -1.0f;
@@ -828,7 +1285,6 @@ using yk::gmd::Dev;
 struct yk_gmd {
   yk_ctx* ctx;
   Dev dev;
-  int cur;
   long long frames;
 };
 
@@ -839,19 +1295,29 @@ int yk_gmd_create(yk_ctx* ctx, int n_streams, int height, int width, int method,
   YK_CHECK_ARG(n_streams >= 1 && n_streams <= 65535, "yk_gmd_create: n_streams out of range");
   YK_CHECK_ARG(height >= 32 && width >= 32 && (long long)height * width <= (1ll << 28),
                "yk_gmd_create: frame size out of range (32 .. 2^28 pixels)");
-  YK_CHECK_ARG(method == YK_GMD_OPTICAL_FLOW || method == YK_GMD_FEATURE_MATCHING || method == YK_GMD_HYBRID,
+  YK_CHECK_ARG(method == YK_GMD_OPTICAL_FLOW || method == YK_GMD_FEATURE_MATCHING || method == YK_GMD_HYBRID ||
+                   method == YK_GMD_SPARSE_OPTFLOW,
                "yk_gmd_create: unknown motion detection method");
-  YK_CHECK_ARG(method == YK_GMD_OPTICAL_FLOW,
+  YK_CHECK_ARG(method == YK_GMD_OPTICAL_FLOW || method == YK_GMD_SPARSE_OPTFLOW,
                "yk_gmd_create: 'feature_matching' / 'hybrid' (ORB + RANSAC homography) are not built; use "
                "'optical_flow'");
+  const bool gmc = method == YK_GMD_SPARSE_OPTFLOW;
+  YK_CHECK_ARG(!gmc || (height % 2 == 0 && width % 2 == 0 && height >= 64 && width >= 64),
+               "yk_gmd_create: GMC sparseOptFlow needs even frame sizes >= 64 (the 1/2 area downscale)");
   yk::DeviceGuard guard(ctx->device);
   auto* g = new yk_gmd{};
   g->ctx = ctx;
   Dev& d = g->dev;
   d.S = n_streams;
+  d.mode = gmc ? 1 : 0;
+  d.maxc = gmc ? yk::gmd::MAXC_G : yk::gmd::MAXC;
+  d.W0 = width;
+  d.H0 = height;
   yk::gmd::Geo& G = d.geo;
-  G.W = width;
-  G.H = height;
+  G.W = gmc ? width / 2 : width;  // the GMC works on the downscaled gray image (gmc.py:300-301)
+  G.H = gmc ? height / 2 : height;
+  width = G.W;
+  height = G.H;
   // buildOpticalFlowPyramid: stop before a level whose size would be <= winSize
   G.levels = 0;
   G.lw[0] = width;
@@ -885,12 +1351,16 @@ int yk_gmd_create(yk_ctx* ctx, int n_streams, int height, int width, int method,
   A((void**)&d.emax, S * sizeof(unsigned));
   A((void**)&d.cand, S * HW * sizeof(unsigned long long));
   A((void**)&d.ncand, S * sizeof(int));
-  A((void**)&d.corners, S * yk::gmd::MAXC * sizeof(float2));
+  A((void**)&d.corners, S * d.maxc * sizeof(float2));
   A((void**)&d.ncorners, S * sizeof(int));
-  A((void**)&d.next, S * yk::gmd::MAXC * sizeof(float2));
-  A((void**)&d.status, S * yk::gmd::MAXC);
+  A((void**)&d.next, S * d.maxc * sizeof(float2));
+  A((void**)&d.status, S * d.maxc);
   A((void**)&d.st, S * sizeof(yk::gmd::State));
   A((void**)&d.out, S * sizeof(yk_motion));
+  A((void**)&d.sel, S * sizeof(int));
+  A((void**)&d.warp, S * 6 * sizeof(double));
+  A((void**)&d.info, S * 5 * sizeof(int));
+  if (e == hipSuccess) e = hipMemset(d.info, 0, S * 5 * sizeof(int));
   if (e == hipSuccess) e = hipMemset(d.ncorners, 0, S * sizeof(int));
   if (e != hipSuccess) {
     yk::set_error(std::string("yk_gmd_create: hipMalloc failed: ") + hipGetErrorString(e));
@@ -898,6 +1368,8 @@ int yk_gmd_create(yk_ctx* ctx, int n_streams, int height, int width, int method,
     return YK_ERR_HIP;
   }
   if (hipFuncSetAttribute((const void*)yk::gmd::select_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)yk::gmd::SEL_LDS) != hipSuccess ||
+      hipFuncSetAttribute((const void*)yk::gmd::select_top_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)yk::gmd::SEL_LDS) != hipSuccess)
     (void)hipGetLastError();
   int rc = yk_gmd_reset(g, nullptr);
@@ -915,7 +1387,7 @@ int yk_gmd_destroy(yk_gmd* g) {
   yk::DeviceGuard guard(g->ctx->device);
   Dev& d = g->dev;
   void* ptrs[] = {d.pyr[0], d.pyr[1], d.der[0], d.der[1], d.eig, d.emax, d.cand, d.ncand, d.corners,
-                  d.ncorners, d.next, d.status, d.st, d.out};
+                  d.ncorners, d.next, d.status, d.st, d.out, d.sel, d.warp, d.info};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   delete g;
@@ -929,7 +1401,6 @@ int yk_gmd_reset(yk_gmd* g, void* stream) {
                      g->dev, 0);
   YK_HIP(hipGetLastError());
   g->frames = 0;
-  g->cur = 0;
   return YK_OK;
 }
 
@@ -950,34 +1421,79 @@ int yk_gmd_set_thresholds(yk_gmd* g, double global_motion_threshold, double rese
   return YK_OK;
 }
 
-int yk_gmd_detect(yk_gmd* g, const uint8_t* frames, yk_motion* out, void* stream) {
-  YK_CHECK_ARG(g && frames, "yk_gmd_detect: NULL argument");
-  yk::DeviceGuard guard(g->ctx->device);
+// the stages both methods share: new frame's gray pyramid + derivatives, then (from the second
+// frame on) corners of the previous frame and their Lucas-Kanade flow to the new one
+static void gmd_front(yk_gmd* g, const uint8_t* frames, hipStream_t st) {
   const Dev& d = g->dev;
   const yk::gmd::Geo& G = d.geo;
-  hipStream_t st = (hipStream_t)stream;
-  const int cur = g->cur, prev = cur ^ 1, S = d.S;
+  const int S = d.S;
   const long long HW = (long long)G.W * G.H;
-  hipLaunchKernelGGL(yk::gmd::gray_kernel, dim3((unsigned)((HW + 255) / 256), S), dim3(256), 0, st, d, frames, cur);
+  if (d.mode)
+    hipLaunchKernelGGL(yk::gmd::gray_down_kernel, dim3((unsigned)((HW + 255) / 256), S), dim3(256), 0, st, d, frames);
+  else
+    hipLaunchKernelGGL(yk::gmd::gray_kernel, dim3((unsigned)((HW + 255) / 256), S), dim3(256), 0, st, d, frames);
   for (int l = 1; l <= G.levels; ++l)
     hipLaunchKernelGGL(yk::gmd::pyrdown_kernel, dim3((G.lw[l] + 15) / 16, (G.lh[l] + 15) / 16, S), dim3(256), 0, st,
-                       d, cur, l);
+                       d, l);
   for (int l = 0; l <= G.levels; ++l)
     hipLaunchKernelGGL(yk::gmd::scharr_kernel, dim3((G.lw[l] + 15) / 16, (G.lh[l] + 15) / 16, S), dim3(256), 0, st,
-                       d, cur, l);
+                       d, l);
   if (g->frames > 0) {
     hipLaunchKernelGGL(yk::gmd::clear_kernel, dim3((S + 255) / 256), dim3(256), 0, st, d);
-    hipLaunchKernelGGL(yk::gmd::eig_kernel, dim3((G.W + 15) / 16, (G.H + 15) / 16, S), dim3(256), 0, st, d, prev);
+    if (d.mode)
+      hipLaunchKernelGGL(yk::gmd::eig_kernel<3>, dim3((G.W + 15) / 16, (G.H + 15) / 16, S), dim3(256), 0, st, d);
+    else
+      hipLaunchKernelGGL(yk::gmd::eig_kernel<7>, dim3((G.W + 15) / 16, (G.H + 15) / 16, S), dim3(256), 0, st, d);
     hipLaunchKernelGGL(yk::gmd::cand_kernel, dim3((unsigned)((HW + 256 * yk::gmd::CPX - 1) / (256 * yk::gmd::CPX)), S),
                        dim3(256), 0, st, d);
-    hipLaunchKernelGGL(yk::gmd::select_kernel, dim3(S), dim3(yk::gmd::NTS), yk::gmd::SEL_LDS, st, d);
-    hipLaunchKernelGGL(yk::gmd::lk_kernel, dim3(yk::gmd::MAXC / 4, S), dim3(256), 0, st, d, prev, cur);
+    if (d.mode)
+      hipLaunchKernelGGL(yk::gmd::select_top_kernel, dim3(S), dim3(yk::gmd::NTS), yk::gmd::SEL_LDS, st, d);
+    else
+      hipLaunchKernelGGL(yk::gmd::select_kernel, dim3(S), dim3(yk::gmd::NTS), yk::gmd::SEL_LDS, st, d);
+    hipLaunchKernelGGL(yk::gmd::lk_kernel, dim3(d.maxc / 4, S), dim3(256), 0, st, d);
   }
-  hipLaunchKernelGGL(yk::gmd::finish_kernel, dim3(S), dim3(256), 0, st, d, out ? out : d.out);
-  if (out) YK_HIP(hipMemcpyAsync(d.out, out, S * sizeof(yk_motion), hipMemcpyDeviceToDevice, st));
+}
+
+int yk_gmd_detect(yk_gmd* g, const uint8_t* frames, yk_motion* out, void* stream) {
+  YK_CHECK_ARG(g && frames, "yk_gmd_detect: NULL argument");
+  YK_CHECK_ARG(g->dev.mode == 0, "yk_gmd_detect: a YK_GMD_SPARSE_OPTFLOW detector computes warps (yk_gmc_apply)");
+  yk::DeviceGuard guard(g->ctx->device);
+  const Dev& d = g->dev;
+  hipStream_t st = (hipStream_t)stream;
+  gmd_front(g, frames, st);
+  hipLaunchKernelGGL(yk::gmd::finish_kernel, dim3(d.S), dim3(256), 0, st, d, out ? out : d.out);
+  if (out) YK_HIP(hipMemcpyAsync(d.out, out, d.S * sizeof(yk_motion), hipMemcpyDeviceToDevice, st));
   YK_HIP(hipGetLastError());
-  g->cur ^= 1;
   g->frames += 1;
+  return YK_OK;
+}
+
+int yk_gmc_apply(yk_gmd* g, const uint8_t* frames, double* warp, void* stream) {
+  YK_CHECK_ARG(g && frames, "yk_gmc_apply: NULL argument");
+  YK_CHECK_ARG(g->dev.mode == 1, "yk_gmc_apply: the detector was not created with YK_GMD_SPARSE_OPTFLOW");
+  yk::DeviceGuard guard(g->ctx->device);
+  const Dev& d = g->dev;
+  hipStream_t st = (hipStream_t)stream;
+  gmd_front(g, frames, st);
+  hipLaunchKernelGGL(yk::gmd::gmc_kernel, dim3(d.S), dim3(yk::gmd::GT), 0, st, d, warp ? warp : d.warp);
+  if (warp) YK_HIP(hipMemcpyAsync(d.warp, warp, d.S * 6 * sizeof(double), hipMemcpyDeviceToDevice, st));
+  YK_HIP(hipGetLastError());
+  g->frames += 1;
+  return YK_OK;
+}
+
+int yk_gmc_outputs(yk_gmd* g, double** dev_warp) {
+  YK_CHECK_ARG(g && dev_warp, "yk_gmc_outputs: NULL argument");
+  *dev_warp = g->dev.warp;
+  return YK_OK;
+}
+
+int yk_gmc_info(yk_gmd* g, int32_t* host_info, void* stream) {
+  YK_CHECK_ARG(g && host_info, "yk_gmc_info: NULL argument");
+  yk::DeviceGuard guard(g->ctx->device);
+  hipStream_t st = (hipStream_t)stream;
+  YK_HIP(hipMemcpyAsync(host_info, g->dev.info, g->dev.S * 5 * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+  YK_HIP(hipStreamSynchronize(st));
   return YK_OK;
 }
 
@@ -1021,7 +1537,7 @@ int yk_gmd_points(yk_gmd* g, int s, float* host_corners, float* host_next, uint8
   YK_CHECK_ARG(s >= 0 && s < g->dev.S, "yk_gmd_points: stream index out of range");
   yk::DeviceGuard guard(g->ctx->device);
   hipStream_t st = (hipStream_t)stream;
-  const int M = yk::gmd::MAXC;
+  const int M = g->dev.maxc;
   YK_HIP(hipMemcpyAsync(n, g->dev.ncorners + s, sizeof(int), hipMemcpyDeviceToHost, st));
   YK_HIP(hipMemcpyAsync(host_corners, g->dev.corners + (size_t)s * M, M * sizeof(float2), hipMemcpyDeviceToHost, st));
   YK_HIP(hipMemcpyAsync(host_next, g->dev.next + (size_t)s * M, M * sizeof(float2), hipMemcpyDeviceToHost, st));

@@ -320,17 +320,14 @@ class YOLO:
         sources); on_predict_postprocess_end resets it when the source path changes (unless
         persist), updates it with the result's boxes and replaces the result by the tracked subset
         with boxes [x1, y1, x2, y2, id, conf, cls] (track.py:66-100).  `tracker`: 'botsort.yaml'
-        (the cfg default) / 'bytetrack.yaml' / a YAML path / dict; BoT-SORT's GMC needs cv2 (absent):
-        use gmc_method: none, or bytetrack."""
+        (the cfg default, with its sparseOptFlow GMC on the device) / 'bytetrack.yaml' / a YAML
+        path / dict.  The frame goes to the tracker's update (track.py:93, im0s[i]) for the GMC."""
         from . import bytetrack as BT
 
         kwargs["conf"] = kwargs.get("conf") or 0.1
         kwargs["batch"] = kwargs.get("batch") or 1
         if not (persist and getattr(self, "trackers", None)):
             cfg = BT.load_tracker_cfg(tracker)
-            if cfg.tracker_type == "botsort" and getattr(cfg, "gmc_method", None) not in (None, "none"):
-                raise NotImplementedError(f"BoT-SORT GMC '{cfg.gmc_method}' needs cv2 (absent here): use "
-                                          "tracker='bytetrack.yaml' or a botsort YAML with gmc_method: none")
             kind = BT.BOTSORT if cfg.tracker_type == "botsort" else BT.BYTETracker
             self.trackers = [kind(cfg, frame_rate=30, device=self.device)]
             self.vid_path = [None]
@@ -341,7 +338,7 @@ class YOLO:
             if not persist and self.vid_path[0] != vid_path:
                 trk.reset()
                 self.vid_path[0] = vid_path
-            tracks = trk.update(r.boxes.cpu().numpy())
+            tracks = trk.update(r.boxes.cpu().numpy(), r.orig_img)
             if len(tracks) == 0:
                 continue
             idx = tracks[:, -1].astype(int)
