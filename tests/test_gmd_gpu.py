@@ -193,8 +193,8 @@ def test_motion_compensated_tracker_with_frames():
 
 
 def test_many_candidates_take_the_windowed_selection():
-    """Pixel noise has tens of thousands of local maxima: more than one LDS sort window (16384
-    keys), so the radix-select windows of select_kernel are exercised."""
+    """Pixel noise has tens of thousands of local maxima: many LDS sort windows (2048 keys each,
+    more than 16384 candidates), so the radix-select windows of select_kernel are exercised."""
     from oracle import gmd_ref as G
 
     rng = np.random.default_rng(11)

@@ -13,7 +13,7 @@
 //                   per covariance entry, per-stream max by an ordered-bits atomicMax
 //   cand_kernel     TOZERO threshold at 0.01 * max, 3x3 dilate test, interior local maxima
 //                   appended as 64-bit keys (value bits, address) with wave-aggregated atomics
-//   select_kernel   one workgroup per stream: keys sorted descending in LDS (bitonic, 16384 at
+//   select_kernel   one workgroup per stream: keys sorted descending in LDS (bitonic, 2048 at
 //                   a time; a radix select cuts larger candidate sets into windows), then the
 //                   greedy minDistance-15 pass (1024 candidates tested in parallel against the
 //                   kept corners, in-chunk conflicts resolved in order by one wave) to 200 corners
@@ -53,7 +53,9 @@ constexpr int MINDIST2 = 225;                // minDistance^2 (corners sit on in
 constexpr int MAXLV = 3;                     // lk_params maxLevel
 constexpr int MAXIT = 30;                    // criteria count
 constexpr double EPS2 = 0.01 * 0.01;         // criteria eps, squared by calcOpticalFlowPyrLK
-constexpr int CAP = 16384;                   // candidate keys sorted in LDS at once
+constexpr int CAP = 2048;                    // candidate keys select_kernel sorts in LDS per window:
+                                             // the greedy pass usually reaches maxCorners inside the
+                                             // first window (round 3 sorted 16384 at once)
 constexpr int NTS = 1024;                    // select_kernel threads
 constexpr int MVQ = 5;                       // motion_vectors deque(maxlen=5)
 constexpr float F_PI = 3.14159274101257324f;       // np.pi cast to float32 (NEP 50)
