@@ -88,7 +88,7 @@ def test_botsort_with_gmc_matches_oracle(method):
     for f in range(len(frames)):
         d = dets[f]
         got = dev.update(d, frames[f])
-        want = ref.update(BR.Dets(d[:, :4], d[:, 4], d[:, 5]), frames[f])
+        want = ref.update(BR.Dets(d[:, :4], d[:, 4], d[:, 5]), frames[f]).reshape(-1, 8)
         assert got.shape == want.shape, (f, got.shape, want.shape)
         np.testing.assert_array_equal(got[:, 4:], want[:, 4:], err_msg=f"frame {f}: id / score / cls / idx")
         if len(want):
