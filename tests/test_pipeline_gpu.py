@@ -52,12 +52,22 @@ def test_stream_pipeline_fp32_matches_oracle_chain():
                 np.testing.assert_allclose(o["confidence"], r["confidence"], rtol=1e-4)
 
 
-def _driver_scene(P, n_frames):
+# Scene seed of the strict driver-loop test.  The scene's tracks include many coasting
+# duplicates, so some frames' greedy association is decided by IoU gaps far below the fp32
+# detector's chain-to-chain IoU spread (~1e-6): seed 4's oracle chain has a 3.8e-8 gap (frame 89)
+# and a 2.8e-7 one at frame 75 where two duplicate tracks swap (tools/driver_diag.py).  A strict
+# chain test only measures parity on a scene whose oracle chain is decided by margins well above
+# that spread; seed 8's smallest margin is 1.5e-5 (tools/driver_scene_margin.py), asserted below.
+DRIVER_SEED = 8
+DRIVER_MIN_MARGIN = 1e-5
+
+
+def _driver_scene(P, n_frames, seed=DRIVER_SEED):
     """40 targets over n_frames with the lifecycle events the driver's statistics count: the
     scene's own occlusion bursts, plus targets forced out for 1-3 frames (lost -> recovered) and
     three forced out from frame 3 to the end (their tracks reach the 150-miss deletion unless a
     neighbouring detection keeps them alive; at least one is deleted)."""
-    sc = P.synth.Scene(seed=4, n_targets=40, n_frames=n_frames + 1)
+    sc = P.synth.Scene(seed=seed, n_targets=40, n_frames=n_frames + 1)
     for k, (t0, L) in enumerate(((6, 1), (9, 2), (14, 3), (20, 2), (31, 1), (44, 3))):
         sc.visible[t0:t0 + L, k] = False
     sc.visible[3:, 37:40] = False
@@ -87,7 +97,7 @@ def test_reference_driver_loop_through_compat_packages(tmp_path):
     P = pkg()
     FR = P.frames
     F = 160
-    sc = _driver_scene(P, F)
+    sc = _driver_scene(P, F, DRIVER_SEED)
     frames = np.stack([sc.frame(t) for t in range(F)])
     np.save(tmp_path / "seq.npy", frames)
     # --- the driver, as written (aircraft_detection_tracking.py:45-52, 58-161) ---------------------
@@ -143,20 +153,22 @@ def test_reference_driver_loop_through_compat_packages(tmp_path):
     # detector -> oracle tracker): decisions identical, boxes within 1e-4 of the box's scale; and on
     # every frame they also equal the oracle tracker fed the GPU's own detections (1e-9,
     # test_tracker_gpu.compare_frame).
-    from gpu_helpers import dets_match
+    from gpu_helpers import assign_margin, dets_match
     from test_tracker_gpu import compare_frame
 
     ref = D.RefDetector(_layers(model.arch), model.state_dict, P.arch.detect_strides(model.arch))
     trk = RefMultiTracker(150, 1, 0.1, stable_ties=True, fast_iou=True)
     iso = RefMultiTracker(150, 1, 0.1, stable_ties=True, fast_iou=True)
     torch.set_num_threads(max(1, min(16, len(os.sched_getaffinity(0)))))
-    n_tracks, box_rel = 0, 0.0
+    n_tracks, box_rel, margin = 0, 0.0, np.inf
     for t in range(F):
         want, _ = D.predict(ref, [frames[t]])
         wd = want[0][:, :5].numpy()
         got_d, ours = per_frame[t]
         assert dets_match(got_d, wd) == "same", (f"frame {t}: detections differ from the oracle's", got_d, wd)
         rb = trk.update([[b[0], b[1], b[2], b[3], b[4]] for b in wd])
+        if trk.last_iou is not None:
+            margin = min(margin, assign_margin(trk.last_iou, 0.1))
         assert decisions(ours) == decisions(rb), t
         for o, r in zip(ours, rb):
             scale = float(np.max(np.abs(r["bbox"])))
@@ -166,12 +178,13 @@ def test_reference_driver_loop_through_compat_packages(tmp_path):
             n_tracks += 1
         compare_frame(ours, iso.update([[b[0], b[1], b[2], b[3], b[4]] for b in got_d]), f"isolated tracker frame {t}")
     assert n_tracks == sum(len(per_frame[t][1]) for t in range(F))  # every output of every frame compared
+    assert margin >= DRIVER_MIN_MARGIN, margin  # the scene is well conditioned for a strict comparison
     st = iso.stats
     assert st["total_tracks_terminated"] >= 1 and st["successful_recoveries"] > 0, st  # deletion + recovery ran
     assert tracker.get_statistics()["total_tracks_terminated"] == st["total_tracks_terminated"]
     assert trk.stats == st  # the oracle chain and the isolated oracle tracker agree too
     assert detection_frames > 0 and prediction_frames > 0 and state_changes > 0
-    print("DRIVER_LOOP", {"frames": F, "chain_track_outputs_compared": n_tracks, "max_box_rel_dev": box_rel,
+    print("DRIVER_LOOP", {"frames": F, "chain_track_outputs_compared": n_tracks, "max_box_rel_dev": box_rel, "min_assign_margin": margin,
                           "stats": dict(st), "state_changes": state_changes})
 
 

@@ -86,7 +86,7 @@ TRACK_OUT_DTYPE = np.dtype([
     ("reset_count", np.int32), ("frames_since_reset", np.int32), ("reason_count", np.int32, (3,)),
     ("n_details", np.int32), ("motion_consistency", np.float64), ("reset_confidence_sum", np.float64),
     ("motion_consistency_sum", np.float64), ("details", RESET_DETAIL_DTYPE, (5,)),
-    ("traj_count", np.int32)], align=True)
+    ("traj_count", np.int32), ("reserved", np.int32)], align=True)
 
 TRACK_STATE_DTYPE = np.dtype([
     ("track_num", np.int32), ("age", np.int32), ("hits", np.int32), ("hit_streak", np.int32),

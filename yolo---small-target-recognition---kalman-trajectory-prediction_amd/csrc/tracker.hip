@@ -849,6 +849,7 @@ __device__ void track_info(S& s, yk_track_out& o, bool copy_traj = true) {
   const int nt = s.th_len < TOUT ? s.th_len : TOUT;
   o.traj_len = nt;
   o.traj_count = s.th_cnt;
+  o.reserved = 0;
   if (!copy_traj) return;  // the step kernel copies trajectories cooperatively
   int idx = s.th_head + (s.th_len - nt);
   if (idx >= TH) idx -= TH;

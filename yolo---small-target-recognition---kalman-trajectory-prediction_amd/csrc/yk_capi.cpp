@@ -1,4 +1,9 @@
 // Context handling, error reporting and the engine-file loader of the C ABI (include/yk.h).
+#include <execinfo.h>
+#include <signal.h>
+#include <unistd.h>
+
+#include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <vector>
@@ -19,8 +24,40 @@ int yk_abi_version(void) { return YK_ABI_VERSION; }
 
 const char* yk_last_error(void) { return yk::g_last_error.c_str(); }
 
+namespace {
+// Diagnostics (YK_SEGV_TRACE=1 at context creation): a SIGSEGV prints the native stack to stderr,
+// then the previous handler (Python's faulthandler, or the default action) runs.
+struct sigaction g_prev_segv;
+void segv_trace(int sig, siginfo_t* info, void* uc) {
+  void* frames[64];
+  const int n = backtrace(frames, 64);
+  static const char hdr[] = "[yk] SIGSEGV native stack:\n";
+  (void)!write(2, hdr, sizeof hdr - 1);
+  backtrace_symbols_fd(frames, n, 2);
+  if (g_prev_segv.sa_flags & SA_SIGINFO) {
+    if (g_prev_segv.sa_sigaction) g_prev_segv.sa_sigaction(sig, info, uc);
+  } else if (g_prev_segv.sa_handler != SIG_DFL && g_prev_segv.sa_handler != SIG_IGN) {
+    g_prev_segv.sa_handler(sig);
+  }
+  signal(sig, SIG_DFL);
+  raise(sig);
+}
+void maybe_install_segv_trace() {
+  static bool done = false;
+  if (done || !getenv("YK_SEGV_TRACE")) return;
+  done = true;
+  struct sigaction sa;
+  memset(&sa, 0, sizeof sa);
+  sa.sa_sigaction = segv_trace;
+  sa.sa_flags = SA_SIGINFO;
+  sigemptyset(&sa.sa_mask);
+  sigaction(SIGSEGV, &sa, &g_prev_segv);
+}
+}  // namespace
+
 int yk_ctx_create(int device, yk_ctx** out) {
   YK_CHECK_ARG(out != nullptr, "yk_ctx_create: out is NULL");
+  maybe_install_segv_trace();
   int n = 0;
   YK_HIP(hipGetDeviceCount(&n));
   YK_CHECK_ARG(device >= 0 && device < n, "yk_ctx_create: device index out of range");

@@ -78,6 +78,11 @@ class StreamPipeline:
         self.models = [self.model] + [M.DeviceModel(self.prog, self.device) for _ in range(self.D - 1)]
         self.frame_slots = [self.frames] + [torch.zeros_like(self.frames) for _ in range(self.D - 1)]
         self.det_streams = [None] + [torch.cuda.Stream(dev) for _ in range(self.D - 1)]
+        if self.D > 1:
+            # forwards in flight are the concurrency: one lane per graph (bench.py's default too).
+            # Multi-lane (forked) graphs of several in-flight slots plus other live models were
+            # seen to crash the HIP runtime inside hipGraphLaunch (tools/graph_lanes_repro.py, round 4)
+            self.set_schedule(1, 1)
         self.gmd = None
         if motion_method is not None:
             if tracker_policy != 1:
