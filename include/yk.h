@@ -294,7 +294,8 @@ int yk_gmd_reset_stats(yk_gmd* g, void* stream);
 int yk_gmd_set_thresholds(yk_gmd* g, double global_motion_threshold, double reset_motion_threshold);
 /* detect_motion() on frame s of dev_frames ([n_streams][height][width][3] uint8) for every
  * stream; results in dev_motion[n_streams] (device memory; NULL: the detector's own buffer,
- * see yk_gmd_outputs).  Asynchronous on `stream`. */
+ * see yk_gmd_outputs, which holds the last call's results either way).  Asynchronous on
+ * `stream`. */
 int yk_gmd_detect(yk_gmd* g, const uint8_t* dev_frames, yk_motion* dev_motion, void* stream);
 int yk_gmd_outputs(yk_gmd* g, yk_motion** dev_motion);
 /* Copy the last results (and stats when host_stats != NULL) to the host; synchronous. */

@@ -49,6 +49,8 @@ def main():
             for npt in (1, 2, 4):
                 for sp in (0, 64):
                     cands.append((3, nnt, npt | (mode << 4) | sp))
+                    if mode == 1 and sp:  # block loop: 2 / 4 pixel blocks per workgroup
+                        cands += [(3, nnt, npt | (mode << 4) | sp | nb) for nb in (128, 256)]
     for ne in (1, 2):
         for npt in (1, 2, 4):
             for wm in (0, 1):

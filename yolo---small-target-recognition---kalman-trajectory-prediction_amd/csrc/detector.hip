@@ -902,7 +902,6 @@ struct FastArgs {
   int r_cstride, r_coff;
   int act;
   int xcd;
-  int nb;                        // pixel blocks per workgroup (WS only; 1 otherwise)
   unsigned long long* tstamp;  // diagnostics (YK_FAST_TS): per-workgroup [start, end] wall clock
   int tstamp_cap;              // workgroups the tstamp buffer holds (3 entries each)
 };
@@ -958,7 +957,7 @@ constexpr int fastw_skd(int nnt, int npt) { return nnt * npt >= 8 ? 2 : 4; }
 // NE = output-channel tiles this workgroup computes: NNT, or fewer for the last channel group of
 // an op whose n_tiles is not a multiple of NNT (its missing tiles cost no loads and no MFMAs;
 // each body is straight-line code, the dispatch is one scalar branch per workgroup).
-template <class Tr, int NE, int NPT, bool WS, int SKD, bool MB>
+template <class Tr, int NE, int NPT, bool WS, int SKD>
 __device__ __forceinline__ void conv_fast_body(const FastArgs& a, int2 blk, int nt0) {
   using T = typename Tr::T;
   constexpr int ESZ = (int)sizeof(T);
@@ -968,15 +967,6 @@ __device__ __forceinline__ void conv_fast_body(const FastArgs& a, int2 blk, int 
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int kg = lane >> 4, col = lane & 15;
   const int nk = a.k_steps;
-  // pixel blocks of this workgroup: [bx, bend) (MB: the a.nb > 1 instantiation, WS only)
-  static_assert(!MB || WS, "block loop only with waves splitting K");
-  constexpr int BPX = WS ? 16 * NPT : 64 * NPT;
-  int bx = MB ? blk.x * a.nb : blk.x;
-  int bend = bx + 1;
-  if constexpr (MB) {
-    const int nbx = (a.M + BPX - 1) / BPX;
-    bend = bx + a.nb < nbx ? bx + a.nb : nbx;
-  }
   const int wg_lin = blockIdx.y * gridDim.x + blockIdx.x;
   if (a.tstamp && tid == 0 && wg_lin < a.tstamp_cap) a.tstamp[3 * wg_lin] = wall_clock64();
   {
@@ -993,10 +983,9 @@ __device__ __forceinline__ void conv_fast_body(const FastArgs& a, int2 blk, int 
   const __amdgpu_buffer_rsrc_t wr = make_srd(a.wblob, a.wbytes);
   const int hw = a.out_h * a.out_w;
   unsigned vo0[NPT], vo1[NPT], vm[NPT];
-  int pbase = 0;
+  const int pbase = WS ? blk.x * (16 * NPT) : (blk.x * 4 + wave) * (16 * NPT);
   // the lane's window origins in both sources and its 9-bit tap mask, per pixel fragment
-  auto set_block = [&](int b_x) {
-    pbase = WS ? b_x * (16 * NPT) : (b_x * 4 + wave) * (16 * NPT);
+  {
 #pragma unroll
     for (int t = 0; t < NPT; ++t) {
       const int p = pbase + t * 16 + col;
@@ -1017,8 +1006,7 @@ __device__ __forceinline__ void conv_fast_body(const FastArgs& a, int2 blk, int 
                          ((iy0 + 2 >= 0 && iy0 + 2 < a.in_h) ? cm << 6 : 0u);
       vm[t] = pv ? m : 0u;  // 1x1 convs use tap 0 = the pixel itself
     }
-  };
-  set_block(bx);
+  }
   f32x4 acc[NE][NPT];
 #pragma unroll
   for (int i = 0; i < NE; ++i)
@@ -1072,205 +1060,176 @@ __device__ __forceinline__ void conv_fast_body(const FastArgs& a, int2 blk, int 
   }
   WF wb[SKD][NE];
   uint4 xb[SKD][NPT];
-  // a block's first SKD steps of loads (issued before the previous block's epilogue)
-  auto issue_first = [&]() {
+  int ks = k0;
+  if (k1 - k0 >= 2 * SKD) {
+    // prologue and steady state issue the loads in the same pinned order (MFMAs of step d,
+    // then step d + SKD's loads), so the waitcnt pass sees one consistent FIFO of SKD steps
 #pragma unroll
     for (int d = 0; d < SKD; ++d) {
       __builtin_amdgcn_sched_barrier(0);
-      if (k0 + d < k1) load_step(k0 + d, wb[d], xb[d]);
+      load_step(k0 + d, wb[d], xb[d]);
     }
-  };
-  if constexpr (MB) issue_first();
-  for (bool first = true;; first = false) {
-    int ks = k0;
-    if (k1 - k0 >= 2 * SKD) {
-      // prologue (MB: issued ahead) and steady state issue the loads in the same pinned order
-      // (MFMAs of step d, then step d + SKD's loads), so the waitcnt pass sees one consistent
-      // FIFO of SKD steps
-      if constexpr (!MB) {
+    for (; ks + 2 * SKD <= k1; ks += SKD) {
+      if constexpr (Tr::kScaled) {
+        // FP8: step pairs (d, d + 1) on one block-scaled K=128 MFMA, then both refills
+#pragma unroll
+        for (int d = 0; d < SKD; d += 2) {
+          __builtin_amdgcn_sched_barrier(0);
+          const int2 e0 = tab[(ks + d + SKD) * 4 + kg], e1 = tab[(ks + d + 1 + SKD) * 4 + kg];
+#pragma unroll
+          for (int i = 0; i < NE; ++i)
+#pragma unroll
+            for (int t = 0; t < NPT; ++t)
+              acc[i][t] = mma2<Tr>(wb[d][i], wb[d + 1][i], xb[d][t], xb[d + 1][t], acc[i][t]);
+          __builtin_amdgcn_sched_barrier(0);
+          issue(ks + d + SKD, e0, wb[d], xb[d]);
+          issue(ks + d + 1 + SKD, e1, wb[d + 1], xb[d + 1]);
+        }
+      } else {
 #pragma unroll
         for (int d = 0; d < SKD; ++d) {
           __builtin_amdgcn_sched_barrier(0);
-          load_step(k0 + d, wb[d], xb[d]);
+          const int2 e = tab[(ks + d + SKD) * 4 + kg];  // LDS read in flight over the MFMAs
+          step_mma(wb[d], xb[d]);
+          __builtin_amdgcn_sched_barrier(0);
+          issue(ks + d + SKD, e, wb[d], xb[d]);
         }
       }
-      for (; ks + 2 * SKD <= k1; ks += SKD) {
-        if constexpr (Tr::kScaled) {
-          // FP8: step pairs (d, d + 1) on one block-scaled K=128 MFMA, then both refills
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (Tr::kScaled) {
 #pragma unroll
-          for (int d = 0; d < SKD; d += 2) {
-            __builtin_amdgcn_sched_barrier(0);
-            const int2 e0 = tab[(ks + d + SKD) * 4 + kg], e1 = tab[(ks + d + 1 + SKD) * 4 + kg];
+      for (int d = 0; d < SKD; d += 2)
+#pragma unroll
+        for (int i = 0; i < NE; ++i)
+#pragma unroll
+          for (int t = 0; t < NPT; ++t) acc[i][t] = mma2<Tr>(wb[d][i], wb[d + 1][i], xb[d][t], xb[d + 1][t], acc[i][t]);
+    } else {
+#pragma unroll
+      for (int d = 0; d < SKD; ++d) step_mma(wb[d], xb[d]);
+    }
+    ks += SKD;
+  }
+  // short K ranges (the split-K waves of the low-resolution layers own 3-11 steps) and the
+  // tail: up to SKD steps of loads in flight, refilled as each step's MFMAs consume them
+  // (ks and k1 are wave-uniform: the guards are scalar branches)
+  if (ks < k1) {
+#pragma unroll
+    for (int d = 0; d < SKD; ++d)
+      if (ks + d < k1) load_step(ks + d, wb[d], xb[d]);
+    for (; ks < k1; ks += SKD) {
+      if constexpr (Tr::kScaled) {
+        const uint4 z = make_uint4(0u, 0u, 0u, 0u);  // an odd last step pairs with zeros
+#pragma unroll
+        for (int d = 0; d < SKD; d += 2) {
+          if (ks + d < k1) {
+            const bool two = ks + d + 1 < k1;
 #pragma unroll
             for (int i = 0; i < NE; ++i)
 #pragma unroll
               for (int t = 0; t < NPT; ++t)
-                acc[i][t] = mma2<Tr>(wb[d][i], wb[d + 1][i], xb[d][t], xb[d + 1][t], acc[i][t]);
-            __builtin_amdgcn_sched_barrier(0);
-            issue(ks + d + SKD, e0, wb[d], xb[d]);
-            issue(ks + d + 1 + SKD, e1, wb[d + 1], xb[d + 1]);
-          }
-        } else {
-#pragma unroll
-          for (int d = 0; d < SKD; ++d) {
-            __builtin_amdgcn_sched_barrier(0);
-            const int2 e = tab[(ks + d + SKD) * 4 + kg];  // LDS read in flight over the MFMAs
-            step_mma(wb[d], xb[d]);
-            __builtin_amdgcn_sched_barrier(0);
-            issue(ks + d + SKD, e, wb[d], xb[d]);
+                acc[i][t] = mma2<Tr>(wb[d][i], two ? wb[d + 1][i] : z, xb[d][t], two ? xb[d + 1][t] : z, acc[i][t]);
+            if (ks + d + SKD < k1) load_step(ks + d + SKD, wb[d], xb[d]);
+            if (two && ks + d + 1 + SKD < k1) load_step(ks + d + 1 + SKD, wb[d + 1], xb[d + 1]);
           }
         }
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      if constexpr (Tr::kScaled) {
-#pragma unroll
-        for (int d = 0; d < SKD; d += 2)
-#pragma unroll
-          for (int i = 0; i < NE; ++i)
-#pragma unroll
-            for (int t = 0; t < NPT; ++t) acc[i][t] = mma2<Tr>(wb[d][i], wb[d + 1][i], xb[d][t], xb[d + 1][t], acc[i][t]);
       } else {
 #pragma unroll
-        for (int d = 0; d < SKD; ++d) step_mma(wb[d], xb[d]);
-      }
-      ks += SKD;
-    }
-    // short K ranges (the split-K waves of the low-resolution layers own 3-11 steps) and the
-    // tail: up to SKD steps of loads in flight, refilled as each step's MFMAs consume them
-    // (ks and k1 are wave-uniform: the guards are scalar branches)
-    if (ks < k1) {
-      if (!MB || ks != k0) {
-#pragma unroll
-        for (int d = 0; d < SKD; ++d)
-          if (ks + d < k1) load_step(ks + d, wb[d], xb[d]);
-      }
-      for (; ks < k1; ks += SKD) {
-        if constexpr (Tr::kScaled) {
-          const uint4 z = make_uint4(0u, 0u, 0u, 0u);  // an odd last step pairs with zeros
-#pragma unroll
-          for (int d = 0; d < SKD; d += 2) {
-            if (ks + d < k1) {
-              const bool two = ks + d + 1 < k1;
-#pragma unroll
-              for (int i = 0; i < NE; ++i)
-#pragma unroll
-                for (int t = 0; t < NPT; ++t)
-                  acc[i][t] = mma2<Tr>(wb[d][i], two ? wb[d + 1][i] : z, xb[d][t], two ? xb[d + 1][t] : z, acc[i][t]);
-              if (ks + d + SKD < k1) load_step(ks + d + SKD, wb[d], xb[d]);
-              if (two && ks + d + 1 + SKD < k1) load_step(ks + d + 1 + SKD, wb[d + 1], xb[d + 1]);
-            }
-          }
-        } else {
-#pragma unroll
-          for (int d = 0; d < SKD; ++d) {
-            if (ks + d < k1) {
-              step_mma(wb[d], xb[d]);
-              if (ks + d + SKD < k1) load_step(ks + d + SKD, wb[d], xb[d]);
-            }
+        for (int d = 0; d < SKD; ++d) {
+          if (ks + d < k1) {
+            step_mma(wb[d], xb[d]);
+            if (ks + d + SKD < k1) load_step(ks + d + SKD, wb[d], xb[d]);
           }
         }
       }
     }
-    const int pcur = pbase;
-    const bool more = MB && bx + 1 < bend;
-    if (!more && a.tstamp && tid == 0 && wg_lin < a.tstamp_cap) a.tstamp[3 * wg_lin + 1] = wall_clock64();
-    if constexpr (WS) {
-      // partial tiles to LDS; each wave then finishes the (tile, fragment) slots q = 4 j + wave.
-      // The slots' bias and residual loads go out before the next block's first K steps (vmcnt
-      // retires in order), whose loads then fly over this block's reduction and epilogue.
-      f32x4* red = (f32x4*)(smem + (((size_t)nk * 4 * 8 + 15) & ~(size_t)15));
-      if (!first) __syncthreads();  // every wave is done reading the previous block's partials
+  }
+  if (a.tstamp && tid == 0 && wg_lin < a.tstamp_cap) a.tstamp[3 * wg_lin + 1] = wall_clock64();
+  if constexpr (WS) {
+    // partial tiles to LDS; each wave then finishes the (tile, fragment) slots q = 4 j + wave,
+    // with the slots' bias and residual loads in flight over the barrier (runtime slot
+    // indices: no acc registers live in the epilogue)
+    f32x4* red = (f32x4*)(smem + (((size_t)nk * 4 * 8 + 15) & ~(size_t)15));
 #pragma unroll
-      for (int i = 0; i < NE; ++i)
+    for (int i = 0; i < NE; ++i)
 #pragma unroll
-        for (int t = 0; t < NPT; ++t) red[((wave * NE + i) * NPT + t) * 64 + lane] = acc[i][t];
-      constexpr int J = (NE * NPT + 3) / 4;
-      float4 sb[J], ss[J];
-      float rv[J][4];
+      for (int t = 0; t < NPT; ++t) red[((wave * NE + i) * NPT + t) * 64 + lane] = acc[i][t];
+    constexpr int J = (NE * NPT + 3) / 4;
+    float4 sb[J], ss[J];
+    float rv[J][4];
 #pragma unroll
-      for (int j = 0; j < J; ++j) {
-        const int q = j * 4 + wave, i = q / NPT, t = q - i * NPT;
-        const int n0 = (nt0 + i) * 16 + kg * 4, p = pcur + t * 16 + col;
-        const bool ok = q < NE * NPT && nt0 + i < a.n_tiles && n0 < a.cout && p < a.M;
-        sb[j] = ok ? *(const float4*)(a.bias + n0) : make_float4(0.f, 0.f, 0.f, 0.f);
-        if constexpr (Tr::kScaled) ss[j] = dq4<Tr>(a.bias, a.n_tiles, ok ? n0 : 0);
-        if (a.res && ok) load4((const T*)a.res + (size_t)p * a.r_cstride + a.r_coff + n0, rv[j]);
+    for (int j = 0; j < J; ++j) {
+      const int q = j * 4 + wave, i = q / NPT, t = q - i * NPT;
+      const int n0 = (nt0 + i) * 16 + kg * 4, p = pbase + t * 16 + col;
+      const bool ok = q < NE * NPT && nt0 + i < a.n_tiles && n0 < a.cout && p < a.M;
+      sb[j] = ok ? *(const float4*)(a.bias + n0) : make_float4(0.f, 0.f, 0.f, 0.f);
+      if constexpr (Tr::kScaled) ss[j] = dq4<Tr>(a.bias, a.n_tiles, ok ? n0 : 0);
+      if (a.res && ok) load4((const T*)a.res + (size_t)p * a.r_cstride + a.r_coff + n0, rv[j]);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      const int q = j * 4 + wave, i = q / NPT, t = q - i * NPT;
+      const int n0 = (nt0 + i) * 16 + kg * 4, p = pbase + t * 16 + col;
+      if (!(q < NE * NPT && nt0 + i < a.n_tiles && n0 < a.cout && p < a.M)) continue;
+      f32x4 v4 = red[((0 * NE + i) * NPT + t) * 64 + lane];
+#pragma unroll
+      for (int w = 1; w < 4; ++w) {
+        const f32x4 u = red[((w * NE + i) * NPT + t) * 64 + lane];
+        v4[0] += u[0];
+        v4[1] += u[1];
+        v4[2] += u[2];
+        v4[3] += u[3];
       }
-      if (more) {
-        set_block(bx + 1);
-        issue_first();
+      float v[4] = {v4[0] + sb[j].x, v4[1] + sb[j].y, v4[2] + sb[j].z, v4[3] + sb[j].w};
+      if constexpr (Tr::kScaled) {
+        v[0] = v4[0] * ss[j].x + sb[j].x;
+        v[1] = v4[1] * ss[j].y + sb[j].y;
+        v[2] = v4[2] * ss[j].z + sb[j].z;
+        v[3] = v4[3] * ss[j].w + sb[j].w;
       }
-      __syncthreads();
+      if (a.act) {
 #pragma unroll
-      for (int j = 0; j < J; ++j) {
-        const int q = j * 4 + wave, i = q / NPT, t = q - i * NPT;
-        const int n0 = (nt0 + i) * 16 + kg * 4, p = pcur + t * 16 + col;
-        if (!(q < NE * NPT && nt0 + i < a.n_tiles && n0 < a.cout && p < a.M)) continue;
-        f32x4 v4 = red[((0 * NE + i) * NPT + t) * 64 + lane];
+        for (int e = 0; e < 4; ++e) v[e] = silu<Tr::kExact>(v[e]);
+      }
+      if (a.res) {
 #pragma unroll
-        for (int w = 1; w < 4; ++w) {
-          const f32x4 u = red[((w * NE + i) * NPT + t) * 64 + lane];
-          v4[0] += u[0];
-          v4[1] += u[1];
-          v4[2] += u[2];
-          v4[3] += u[3];
-        }
-        float v[4] = {v4[0] + sb[j].x, v4[1] + sb[j].y, v4[2] + sb[j].z, v4[3] + sb[j].w};
+        for (int e = 0; e < 4; ++e) v[e] = rv[j][e] + v[e];
+      }
+      store4((T*)a.dst + (size_t)p * a.d_cstride + a.d_coff + n0, v);
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < NE; ++i) {
+      const int nt = nt0 + i;
+      if (nt >= a.n_tiles) break;
+      const int n0 = nt * 16 + kg * 4;
+      if (n0 >= a.cout) continue;
+#pragma unroll
+      for (int t = 0; t < NPT; ++t) {
+        const int p = pbase + t * 16 + col;
+        if (p >= a.M) continue;
+        const f32x4 v4 = acc[i][t];
+        float v[4] = {v4[0] + bb[i].x, v4[1] + bb[i].y, v4[2] + bb[i].z, v4[3] + bb[i].w};
         if constexpr (Tr::kScaled) {
-          v[0] = v4[0] * ss[j].x + sb[j].x;
-          v[1] = v4[1] * ss[j].y + sb[j].y;
-          v[2] = v4[2] * ss[j].z + sb[j].z;
-          v[3] = v4[3] * ss[j].w + sb[j].w;
+          v[0] = v4[0] * sc[i].x + bb[i].x;
+          v[1] = v4[1] * sc[i].y + bb[i].y;
+          v[2] = v4[2] * sc[i].z + bb[i].z;
+          v[3] = v4[3] * sc[i].w + bb[i].w;
         }
         if (a.act) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] = silu<Tr::kExact>(v[e]);
         }
         if (a.res) {
+          float r[4];
+          load4((const T*)a.res + (size_t)p * a.r_cstride + a.r_coff + n0, r);
 #pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = rv[j][e] + v[e];
+          for (int e = 0; e < 4; ++e) v[e] = r[e] + v[e];
         }
         store4((T*)a.dst + (size_t)p * a.d_cstride + a.d_coff + n0, v);
       }
-    } else {
-#pragma unroll
-      for (int i = 0; i < NE; ++i) {
-        const int nt = nt0 + i;
-        if (nt >= a.n_tiles) break;
-        const int n0 = nt * 16 + kg * 4;
-        if (n0 >= a.cout) continue;
-#pragma unroll
-        for (int t = 0; t < NPT; ++t) {
-          const int p = pcur + t * 16 + col;
-          if (p >= a.M) continue;
-          const f32x4 v4 = acc[i][t];
-          float v[4] = {v4[0] + bb[i].x, v4[1] + bb[i].y, v4[2] + bb[i].z, v4[3] + bb[i].w};
-          if constexpr (Tr::kScaled) {
-            v[0] = v4[0] * sc[i].x + bb[i].x;
-            v[1] = v4[1] * sc[i].y + bb[i].y;
-            v[2] = v4[2] * sc[i].z + bb[i].z;
-            v[3] = v4[3] * sc[i].w + bb[i].w;
-          }
-          if (a.act) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] = silu<Tr::kExact>(v[e]);
-          }
-          if (a.res) {
-            float r[4];
-            load4((const T*)a.res + (size_t)p * a.r_cstride + a.r_coff + n0, r);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] = r[e] + v[e];
-          }
-          store4((T*)a.dst + (size_t)p * a.d_cstride + a.d_coff + n0, v);
-        }
-      }
     }
-    if (!more) break;
-    ++bx;
-#pragma unroll
-    for (int i = 0; i < NE; ++i)
-#pragma unroll
-      for (int t = 0; t < NPT; ++t) acc[i][t] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
   if (a.tstamp && tid == 0 && wg_lin < a.tstamp_cap) a.tstamp[3 * wg_lin + 2] = wall_clock64();
 }
@@ -1281,24 +1240,23 @@ __device__ __forceinline__ void conv_fast_body(const FastArgs& a, int2 blk, int 
 // Measured (round 3, fp32 headline): 2 lets the large split tiles drop their AGPR accumulators and
 // run two waves per SIMD without spills, but the headline does not move (5,279 vs 5,264 frames/s:
 // those kernels are bound by the split VALU work, not by occupancy); 3 spills (-32 %).
-// MB: the block-loop instantiation (plan nb > 1, split fp32 with waves splitting K only)
-template <class Tr, int NNT, int NPT, bool WS, int SKD, bool MB = false>
+template <class Tr, int NNT, int NPT, bool WS, int SKD>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(YK_FAST_WPE))) conv_fast_kernel(FastArgs a) {
   const int2 blk = xcd_block(a.xcd);
   const int nt0 = blk.y * NNT;
   const int rem = a.n_tiles - nt0;
   if constexpr (NNT == 1) {
-    conv_fast_body<Tr, 1, NPT, WS, SKD, MB>(a, blk, nt0);
+    conv_fast_body<Tr, 1, NPT, WS, SKD>(a, blk, nt0);
   } else {
     if (rem >= NNT) {
-      conv_fast_body<Tr, NNT, NPT, WS, SKD, MB>(a, blk, nt0);
+      conv_fast_body<Tr, NNT, NPT, WS, SKD>(a, blk, nt0);
     } else if (rem == 1) {
-      conv_fast_body<Tr, 1, NPT, WS, SKD, MB>(a, blk, nt0);
+      conv_fast_body<Tr, 1, NPT, WS, SKD>(a, blk, nt0);
     } else if constexpr (NNT > 2) {
       if (rem == 2 || NNT == 3)
-        conv_fast_body<Tr, 2, NPT, WS, SKD, MB>(a, blk, nt0);
+        conv_fast_body<Tr, 2, NPT, WS, SKD>(a, blk, nt0);
       else
-        conv_fast_body<Tr, (NNT > 3 ? 3 : 1), NPT, WS, SKD, MB>(a, blk, nt0);
+        conv_fast_body<Tr, (NNT > 3 ? 3 : 1), NPT, WS, SKD>(a, blk, nt0);
     }
   }
 }
@@ -3421,9 +3379,6 @@ void set_fast_attr() {
   constexpr int SKD = fast_skd(NNT, NPT);
   (void)hipFuncSetAttribute((const void*)conv_fast_kernel<Tr, NNT, NPT, WS, SKD>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
-  if constexpr (WS && std::is_same_v<Tr, F32S>)
-    (void)hipFuncSetAttribute((const void*)conv_fast_kernel<Tr, NNT, NPT, WS, SKD, true>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
 }
 template <class Tr, int NNT, int NPT>
 void set_fastw_attr() {
@@ -3505,10 +3460,6 @@ void set_tile_attrs() {
 enum { CK_DIRECT = 0, CK_TILE = 1, CK_SPLITK = 2, CK_FAST = 3, CK_WIDE = 4, CK_HALO = 5 };
 // CK_FAST plan npt bit: the F32 build's op runs the F32S split-MFMA body (every mode)
 constexpr int kSplitBit = 64;
-// CK_FAST npt bits 7-8 (waves-split-K mode only): log2 of the pixel blocks one workgroup runs
-// in sequence, each block's first K steps of loads in flight over the previous block's epilogue
-constexpr int kNbShift = 7;
-inline int fast_nb_log(int npt) { return (npt >> kNbShift) & 3; }
 // CK_WIDE plan: nnt in {2, 4} (output-channel tiles per workgroup), npt unused
 // CK_HALO plan (F32 build): nnt = NE in {1, 2}, npt = NPT | WM << 4 with NPT in {1, 2, 4}
 // CK_FAST plan: nnt in {1, 2, 3, 4}, npt = NPT | (WS << 4) with NPT in {1, 2, 4}
@@ -3718,16 +3669,7 @@ template <class Tr, int NNT, int NPT, bool WS>
 void launch_fast_t(const FastArgs& a, hipStream_t st) {
   constexpr int SKD = fast_skd(NNT, NPT);
   const int px = WS ? 16 * NPT : 64 * NPT;
-  const int nbx = (a.M + px - 1) / px;
-  if constexpr (WS && std::is_same_v<Tr, F32S>) {
-    if (a.nb > 1) {
-      dim3 grid((nbx + a.nb - 1) / a.nb, (a.n_tiles + NNT - 1) / NNT);
-      hipLaunchKernelGGL((conv_fast_kernel<Tr, NNT, NPT, WS, SKD, true>), grid, dim3(256),
-                         fast_lds(a.k_steps, NNT, NPT, WS), st, a);
-      return;
-    }
-  }
-  dim3 grid(nbx, (a.n_tiles + NNT - 1) / NNT);
+  dim3 grid((a.M + px - 1) / px, (a.n_tiles + NNT - 1) / NNT);
   hipLaunchKernelGGL((conv_fast_kernel<Tr, NNT, NPT, WS, SKD>), grid, dim3(256), fast_lds(a.k_steps, NNT, NPT, WS), st,
                      a);
 }
@@ -3773,18 +3715,12 @@ void launch_fastw(const FastArgs& a, int nnt, int npt, hipStream_t st) {
 template <class Tr>
 void launch_fast(const FastArgs& a, const ConvPlan& p, hipStream_t st) {
   const int mode = (p.npt >> 4) & 3;
-  FastArgs b = a;
-  b.nb = 1;
   if (mode == 2) {
-    launch_fastw<Tr>(b, p.nnt, p.npt & 15, st);
+    launch_fastw<Tr>(a, p.nnt, p.npt & 15, st);
     return;
   }
-  if (mode == 1) {
-    b.nb = 1 << fast_nb_log(p.npt);
-    launch_fast_w<Tr, true>(b, p.nnt, p.npt & 15, st);
-  } else {
-    launch_fast_w<Tr, false>(b, p.nnt, p.npt & 15, st);
-  }
+  if (mode == 1) launch_fast_w<Tr, true>(a, p.nnt, p.npt & 15, st);
+  else launch_fast_w<Tr, false>(a, p.nnt, p.npt & 15, st);
 }
 
 template <int NE, int NPT, int WM, int KS>
@@ -4207,9 +4143,6 @@ const char* op_kernel_name(const yk_model* m, const yk_op& op) {
     if (cp.npt & kSplitBit) tn = "F32S";
     if (mode == 2)
       snprintf(buf, sizeof buf, "conv_fastw_kernel<yk::det::%s, %d, %d, %d>", tn, cp.nnt, npt, skd);
-    else if (mode == 1 && fast_nb_log(cp.npt))
-      snprintf(buf, sizeof buf, "conv_fast_kernel<yk::det::%s, %d, %d, true, %d> nb%d", tn, cp.nnt, npt, skd,
-               1 << fast_nb_log(cp.npt));
     else
       snprintf(buf, sizeof buf, "conv_fast_kernel<yk::det::%s, %d, %d, %s, %d>", tn, cp.nnt, npt,
                mode ? "true" : "false", skd);
@@ -4927,11 +4860,9 @@ int yk_model_set_plan(yk_model* m, int op_index, int batch, int kind, int nnt, i
   YK_CHECK_ARG(kind != CK_WIDE || ((nnt == 2 || nnt == 4) && (npt == 0 || npt == 4 || npt == 8)),
                "yk_model_set_plan: wide conv nnt must be 2 or 4, npt (waves) 0, 4 or 8");
   YK_CHECK_ARG(kind != CK_FAST || (nnt >= 1 && nnt <= 4 && ((npt & 15) == 1 || (npt & 15) == 2 || (npt & 15) == 4) &&
-                                   ((npt >> 4) & 3) <= 2 && (npt & ~(kSplitBit | 63 | (3 << kNbShift))) == 0 &&
-                                   fast_nb_log(npt) <= 2 &&
-                                   (fast_nb_log(npt) == 0 || (((npt >> 4) & 3) == 1 && (npt & kSplitBit)))),
+                                   ((npt >> 4) & 3) <= 2 && (npt & ~(kSplitBit | 63)) == 0),
                "yk_model_set_plan: table conv needs nnt in [1, 4], npt in {1, 2, 4} (+16: waves split K, +32: LDS-shared "
-               "weights, +64: split-bf16 MFMA, +128 / +256: 2 / 4 pixel blocks per workgroup, split waves-split-K only)");
+               "weights, +64: split-bf16 MFMA)");
   YK_CHECK_ARG(kind != CK_FAST || !(npt & kSplitBit) || m->wsplit,
                "yk_model_set_plan: the split-bf16 MFMA variant (+64) needs the fp32 build");
   YK_CHECK_ARG(kind != CK_TILE || nnt == 0 || nnt == 1, "yk_model_set_plan: tiled conv nnt must be 0 or 1 (LDS-resident weights)");
@@ -5003,12 +4934,9 @@ int yk_model_autotune(yk_model* m, const uint8_t* frames, int batch, float conf,
             const long px = mode == 1 ? 16 * npt : 64 * npt;
             const long wgs = ((long)bt * op.out_h * op.out_w + px - 1) / px * ((op.n_tiles + nnt - 1) / nnt);
             if (wgs < 64) continue;
-            for (int nbl = 0; nbl < (mode == 1 ? 3 : 1); ++nbl) {
-              if (nbl && wgs < (256L << nbl)) break;  // a block loop only where it leaves >= 256 workgroups
-              const int v = npt | (mode << 4) | (nbl << kNbShift);
-              if (!nbl) cands.push_back({CK_FAST, nnt, v});
-              if (m->wsplit && m->ws_off[i] >= 0 && m->autotune_split) cands.push_back({CK_FAST, nnt, v | kSplitBit});
-            }
+            cands.push_back({CK_FAST, nnt, npt | (mode << 4)});
+            if (m->wsplit && m->ws_off[i] >= 0 && m->autotune_split)
+              cands.push_back({CK_FAST, nnt, npt | (mode << 4) | kSplitBit});
           }
     if (m->wkslot && m->wk_off[i] >= 0 && m->autotune_split)
       for (int wm = 0; wm < 2; ++wm)

@@ -18,7 +18,7 @@
 //                   greedy minDistance-15 pass (1024 candidates tested in parallel against the
 //                   kept corners, in-chunk conflicts resolved in order by one wave) to 200 corners
 //   lk_kernel       pyramidal Lucas-Kanade, one wavefront per corner: the 21x21 window is 7
-//                   pixels per lane in registers, window sums are exact int64 wave reductions
+//                   pixels per lane in registers, window sums are exact (DPP row sums, then int64)
 //   finish_kernel   the reference's numpy post-processing per stream: median, 75th percentile
 //                   inliers, float32 mean / norm, thresholds, 3-vector direction consistency,
 //                   GlobalMotionDetector.stats
@@ -115,10 +115,16 @@ __device__ __forceinline__ unsigned ord_bits(float f) {
 __device__ __forceinline__ float unord_bits(unsigned o) {
   return __uint_as_float((o & 0x80000000u) ? (o & 0x7fffffffu) : ~o);
 }
-__device__ __forceinline__ long long wave_sum64(long long v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-  return v;
+// Exact wave sum of per-lane int32 values whose 16-lane partial sums stay inside int32 (the LK
+// window sums: |per-lane| < 2^27): butterflies within each 16-lane row on DPP (no LDS round
+// trips), then the four row sums added in int64 on the scalar unit.  Wave-uniform callers only.
+__device__ __forceinline__ long long wave_sum_rows(int v) {
+  v += __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, false);   // quad_perm [1, 0, 3, 2]
+  v += __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xF, 0xF, false);   // quad_perm [2, 3, 0, 1]
+  v += __builtin_amdgcn_update_dpp(0, v, 0x124, 0xF, 0xF, false);  // row_ror 4
+  v += __builtin_amdgcn_update_dpp(0, v, 0x128, 0xF, 0xF, false);  // row_ror 8
+  return ((long long)__builtin_amdgcn_readlane(v, 0) + (long long)__builtin_amdgcn_readlane(v, 16)) +
+         ((long long)__builtin_amdgcn_readlane(v, 32) + (long long)__builtin_amdgcn_readlane(v, 48));
 }
 
 // ---------------------------------------------------------------- frame ingest
@@ -702,9 +708,10 @@ __global__ void __launch_bounds__(256) lk_kernel(Dev g) {
         s22 += Dy[k] * Dy[k];
       }
     }
-    const float A11 = (float)wave_sum64(s11) * fs;
-    const float A12 = (float)wave_sum64(s12) * fs;
-    const float A22 = (float)wave_sum64(s22) * fs;
+    // |Dx|, |Dy| <= 4080 (Scharr of 8-bit pixels): a lane's 7 products < 2^27, a row's 16 < 2^31
+    const float A11 = (float)wave_sum_rows(s11) * fs;
+    const float A12 = (float)wave_sum_rows(s12) * fs;
+    const float A22 = (float)wave_sum_rows(s22) * fs;
     const float Dd = A11 * A22 - A12 * A12;
     const float dd = A11 - A22;
     const float mine = ((A22 + A11) - sqrtf(dd * dd + (4.0f * A12) * A12)) / (float)(2 * WIN * WIN);
@@ -713,6 +720,9 @@ __global__ void __launch_bounds__(256) lk_kernel(Dev g) {
       continue;
     }
     const float Di = 1.0f / Dd;
+    int woff[NSLOT];  // the slot's pixel offset from the window origin at this level
+#pragma unroll
+    for (int k = 0; k < NSLOT; ++k) woff[k] = wy[k] >= 0 ? wy[k] * cols + wx[k] : 0;
     float nx = cx - half, ny = cy - half;
     float pdx = 0.0f, pdy = 0.0f;
     for (int j = 0; j < MAXIT; ++j) {
@@ -724,21 +734,35 @@ __global__ void __launch_bounds__(256) lk_kernel(Dev g) {
       int v00, v01, v10, v11;
       lk_weights(nx - (float)jx, ny - (float)jy, v00, v01, v10, v11);
       int b1 = 0, b2 = 0;
+      if (jx >= 0 && jx + WIN < cols && jy >= 0 && jy + WIN < rows) {  // window and its +1 inside
+        const unsigned char* base = J + (long long)jy * cols + jx;
 #pragma unroll
-      for (int k = 0; k < NSLOT; ++k) {
-        if (wy[k] >= 0) {
-          const int X = jx + wx[k], Y = jy + wy[k];
-          const int x0 = refl(X, cols), x1 = refl(X + 1, cols);
-          const unsigned char* r0 = J + (long long)refl(Y, rows) * cols;
-          const unsigned char* r1 = J + (long long)refl(Y + 1, rows) * cols;
-          const int jv = (r0[x0] * v00 + r0[x1] * v01 + r1[x0] * v10 + r1[x1] * v11 + 256) >> 9;
-          const int diff = jv - Iv[k];
-          b1 += diff * Dx[k];
-          b2 += diff * Dy[k];
+        for (int k = 0; k < NSLOT; ++k) {
+          if (wy[k] >= 0) {
+            const unsigned char* q = base + woff[k];
+            const int jv = (q[0] * v00 + q[1] * v01 + q[cols] * v10 + q[cols + 1] * v11 + 256) >> 9;
+            const int diff = jv - Iv[k];
+            b1 += diff * Dx[k];
+            b2 += diff * Dy[k];
+          }
+        }
+      } else {  // reflect-101 at the border
+#pragma unroll
+        for (int k = 0; k < NSLOT; ++k) {
+          if (wy[k] >= 0) {
+            const int X = jx + wx[k], Y = jy + wy[k];
+            const int x0 = refl(X, cols), x1 = refl(X + 1, cols);
+            const unsigned char* r0 = J + (long long)refl(Y, rows) * cols;
+            const unsigned char* r1 = J + (long long)refl(Y + 1, rows) * cols;
+            const int jv = (r0[x0] * v00 + r0[x1] * v01 + r1[x0] * v10 + r1[x1] * v11 + 256) >> 9;
+            const int diff = jv - Iv[k];
+            b1 += diff * Dx[k];
+            b2 += diff * Dy[k];
+          }
         }
       }
-      const float fb1 = (float)wave_sum64(b1) * fs;
-      const float fb2 = (float)wave_sum64(b2) * fs;
+      const float fb1 = (float)wave_sum_rows(b1) * fs;
+      const float fb2 = (float)wave_sum_rows(b2) * fs;
       const float dx = (A12 * fb2 - A22 * fb1) * Di;
       const float dy = (A12 * fb1 - A11 * fb2) * Di;
       nx += dx;
@@ -781,6 +805,7 @@ __global__ void __launch_bounds__(256) finish_kernel(Dev g, yk_motion* __restric
       r.first_frame = 1;
       r.consistency = -1.0f;
       out[s] = r;
+      if (out != g.out) g.out[s] = r;  // the detector's own record stays "the last detect" too
       S.has_prev = 1;
       g.sel[s] ^= 1;  // this frame is the next call's previous one
     }
@@ -910,6 +935,7 @@ __global__ void __launch_bounds__(256) finish_kernel(Dev g, yk_motion* __restric
   S.reset_triggers += r.should_reset;
   S.avg = (S.avg * (float)(S.total - 1) + r.magnitude) / (float)S.total;
   out[s] = r;
+  if (out != g.out) g.out[s] = r;
   g.sel[s] ^= 1;
 }
 

@@ -63,12 +63,13 @@ class BatchedMotionDetector:
         L.check(L.lib().yk_gmd_set_thresholds(self._h, float(global_motion_threshold), float(reset_motion_threshold)),
                 "yk_gmd_set_thresholds")
 
-    def detect_device(self, frames: torch.Tensor | None = None):
-        """detect_motion on every stream's frame (device uint8 [S, H, W, 3] BGR)."""
+    def detect_device(self, frames: torch.Tensor | None = None, out: int = 0):
+        """detect_motion on every stream's frame (device uint8 [S, H, W, 3] BGR).  out: device
+        address of a yk_motion[S] record to write instead of the detector's own (motion_ptr)."""
         f = self.frames if frames is None else frames
         if f.dtype != torch.uint8 or tuple(f.shape) != (self.S, self.H, self.W, 3) or not f.is_contiguous():
             raise ValueError(f"frames must be a contiguous uint8 tensor of shape {(self.S, self.H, self.W, 3)}")
-        L.check(L.lib().yk_gmd_detect(self._h, L.ptr(f), C.c_void_p(0), L.current_stream(self.device)),
+        L.check(L.lib().yk_gmd_detect(self._h, L.ptr(f), C.c_void_p(out), L.current_stream(self.device)),
                 "yk_gmd_detect")
 
     def detect_host(self, frames):
