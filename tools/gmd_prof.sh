@@ -11,6 +11,6 @@ timeout -k 10 400 python -u -m pytest tests/test_gmd_gpu.py tests/test_gmc_gpu.p
 tail -1 $O/pytest.log
 timeout -k 10 200 python -u tools/gmd_bench.py --streams 8 > $O/gmd_bench.txt 2>&1 || { echo "bench failed"; tail -20 $O/gmd_bench.txt; exit 1; }
 grep -v amdgpu.ids $O/gmd_bench.txt
-timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $O/prof -o gmd -- python -u tools/gmd_bench.py --streams 8 --steps 100 > $O/gmd_prof.log 2>&1 || { echo "rocprof failed"; tail -20 $O/gmd_prof.log; exit 1; }
+timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o gmd -- python -u tools/gmd_bench.py --streams 8 --steps 100 > $O/gmd_prof.log 2>&1 || { echo "rocprof failed"; tail -20 $O/gmd_prof.log; exit 1; }
 f=$(find $O/prof -name "*kernel_stats.csv" | head -1)
 [ -n "$f" ] && cut -d, -f1-4 "$f" | head -16

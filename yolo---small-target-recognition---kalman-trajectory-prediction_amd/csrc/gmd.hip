@@ -293,8 +293,10 @@ __global__ void __launch_bounds__(256) eig_kernel(Dev g) {
 }
 
 // CPX pixels per thread (a workgroup covers 256 * CPX consecutive pixels); the workgroup's
-// candidates take one global atomic (per-stream counter), not one per wave.
-constexpr int CPX = 4;
+// candidates take one global atomic (per-stream counter), not one per wave.  Same-address
+// atomics serialise at L2, so fewer, larger workgroups: 16 pixels a thread = 80 atomics per
+// 640x512 stream (4: 320, ~33 µs for 8 streams, round 4 profile).
+constexpr int CPX = 16;
 __global__ void __launch_bounds__(256) cand_kernel(Dev g) {
   __shared__ int wcnt[4], wbase[4];
   const int s = blockIdx.y, W = g.geo.W, H = g.geo.H, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -361,7 +363,7 @@ struct SelLds {
   int* cok;                  // [NTS]
   int* cx;                   // [NTS]
   int* cy;                   // [NTS]
-  int* hist;                 // [256]
+  int* hist;                 // [NTS / 64][256]: one histogram per wave (no cross-wave atomics)
   int* misc;                 // [8]
 };
 __device__ __forceinline__ SelLds carve_sel(char* base) {
@@ -379,24 +381,45 @@ __device__ __forceinline__ SelLds carve_sel(char* base) {
   L.cy = (int*)base;
   base += 4 * NTS;
   L.hist = (int*)base;
-  base += 4 * 256;
+  base += 4 * 256 * (NTS / 64);
   L.misc = (int*)base;
   return L;
 }
-constexpr size_t SEL_LDS = sizeof(unsigned long long) * CAP + 4 * (2 * MAXC + 3 * NTS + 256 + 8);
+constexpr size_t SEL_LDS = sizeof(unsigned long long) * CAP + 4 * (2 * MAXC + 3 * NTS + 256 * (NTS / 64) + 8);
 enum { S_CNT = 0, S_NA = 1, S_D = 2, S_K = 3, S_REM = 4 };
 
-// The k-th largest key among keys < U (all keys when !has_u): radix select, 8 bits a pass.
+// Key scans keep KU global loads in flight per thread: one workgroup per stream walks every
+// candidate key of its image several times, so each scan is load-latency-bound otherwise.
+constexpr int KU = 8;
+
+// The k-th largest key among keys < U (all keys when !has_u): radix select, 8 bits a pass.  The
+// candidates of one image share their top digits (similar eigenvalues), so one shared histogram
+// would serialise every key of a pass on a single LDS address: each wave counts into its own.
 __device__ unsigned long long kth_largest(const unsigned long long* keys, int n, unsigned long long U, bool has_u,
                                           int k, SelLds& L) {
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, wave = tid >> 6;
+  constexpr int NW = NTS / 64;
   unsigned long long prefix = 0ull, mask = 0ull;
   for (int shift = 56; shift >= 0; shift -= 8) {
-    for (int i = tid; i < 256; i += NTS) L.hist[i] = 0;
+    for (int i = tid; i < 256 * NW; i += NTS) L.hist[i] = 0;
     __syncthreads();
-    for (int i = tid; i < n; i += NTS) {
-      const unsigned long long key = keys[i];
-      if ((!has_u || key < U) && (key & mask) == prefix) atomicAdd(&L.hist[(key >> shift) & 255], 1);
+    for (int i0 = tid; i0 < n; i0 += KU * NTS) {  // KU loads in flight, then their counts
+      unsigned long long kk[KU];
+#pragma unroll
+      for (int u = 0; u < KU; ++u) kk[u] = i0 + u * NTS < n ? keys[i0 + u * NTS] : 0ull;
+#pragma unroll
+      for (int u = 0; u < KU; ++u) {
+        const unsigned long long key = kk[u];
+        if (i0 + u * NTS < n && (!has_u || key < U) && (key & mask) == prefix)
+          atomicAdd(&L.hist[wave * 256 + ((key >> shift) & 255)], 1);
+      }
+    }
+    __syncthreads();
+    for (int i = tid; i < 256; i += NTS) {
+      int c = 0;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) c += L.hist[w * 256 + i];
+      L.hist[i] = c;  // (wave 0's own count is read before this thread overwrites it)
     }
     __syncthreads();
     if (tid == 0) {
@@ -438,7 +461,13 @@ __global__ void __launch_bounds__(NTS) select_kernel(Dev g) {
       if (tid == 0) L.misc[S_REM] = 0;
       __syncthreads();
       int c = 0;
-      for (int i = tid; i < n; i += NTS) c += keys[i] < U ? 1 : 0;
+      for (int i0 = tid; i0 < n; i0 += KU * NTS) {
+        unsigned long long kk[KU];
+#pragma unroll
+        for (int u = 0; u < KU; ++u) kk[u] = i0 + u * NTS < n ? keys[i0 + u * NTS] : ~0ull;
+#pragma unroll
+        for (int u = 0; u < KU; ++u) c += kk[u] < U ? 1 : 0;
+      }
       if (c) atomicAdd(&L.misc[S_REM], c);
       __syncthreads();
       rem = L.misc[S_REM];
@@ -447,21 +476,22 @@ __global__ void __launch_bounds__(NTS) select_kernel(Dev g) {
     const unsigned long long K = last ? 0ull : kth_largest(keys, n, U, has_u, CAP, L);
     if (tid == 0) L.misc[S_CNT] = 0;
     __syncthreads();
-    for (int base = 0; base < n; base += NTS) {  // gather the window [K, U)
-      const int i = base + tid;
-      unsigned long long key = 0ull;
-      bool in = false;
-      if (i < n) {
-        key = keys[i];
-        in = (!has_u || key < U) && (last || key >= K);
-      }
-      const unsigned long long mask = __ballot(in);
-      if (mask) {
-        const int leader = __ffsll((long long)mask) - 1;
-        int b = 0;
-        if (lane == leader) b = atomicAdd(&L.misc[S_CNT], __popcll(mask));
-        b = __shfl(b, leader);
-        if (in) L.keys[b + __popcll(mask & ((1ull << lane) - 1ull))] = key;
+    for (int b0 = 0; b0 < n; b0 += KU * NTS) {  // gather the window [K, U)
+      unsigned long long kk[KU];
+#pragma unroll
+      for (int u = 0; u < KU; ++u) kk[u] = b0 + u * NTS + tid < n ? keys[b0 + u * NTS + tid] : 0ull;
+#pragma unroll
+      for (int u = 0; u < KU; ++u) {
+        const unsigned long long key = kk[u];
+        const bool in = b0 + u * NTS + tid < n && (!has_u || key < U) && (last || key >= K);
+        const unsigned long long mask = __ballot(in);
+        if (mask) {
+          const int leader = __ffsll((long long)mask) - 1;
+          int b = 0;
+          if (lane == leader) b = atomicAdd(&L.misc[S_CNT], __popcll(mask));
+          b = __shfl(b, leader);
+          if (in) L.keys[b + __popcll(mask & ((1ull << lane) - 1ull))] = key;
+        }
       }
     }
     __syncthreads();
@@ -509,46 +539,47 @@ __global__ void __launch_bounds__(NTS) select_kernel(Dev g) {
       L.cy[tid] = y;
       __syncthreads();
       if (wave == 0) {  // in-chunk conflicts, in sorted order
-        // The chunk's candidates 64 at a time in registers (lane l holds candidate c0 + l); the
-        // ones that passed the test against the earlier chunks' corners are walked in order
-        // through a ballot mask, and the corners accepted in this chunk stay in registers (lane
-        // l, slot k holds accepted corner na0 + l + 64 k; at most MAXC < 256 of them).
+        // 64 candidates at a time (lane l holds candidate c0 + l): tested against the corners
+        // this chunk accepted so far (LDS, [na0, na)), the conflicts among the 64 as one mask per
+        // lane (bit j: an earlier candidate j of the block within minDistance), then the block's
+        // greedy decisions on the scalar unit from those masks -- one serial step per candidate
+        // that passed, instead of one broadcast-and-ballot round each.
         int na = na0;
         const int cm = m - base < NTS ? m - base : NTS;
-        int rx[4] = {0, 0, 0, 0}, ry[4] = {0, 0, 0, 0};
         for (int c0 = 0; c0 < cm && na < MAXC; c0 += 64) {
           const int c = c0 + lane;
-          const bool okc = c < cm && L.cok[c] != 0;
+          bool okc = c < cm && L.cok[c] != 0;
           const int xl = okc ? L.cx[c] : 0, yl = okc ? L.cy[c] : 0;
-          unsigned long long todo = __ballot(okc);
-          while (todo != 0ull && na < MAXC) {
+          bool conflict = false;
+          for (int q = na0; q < na; ++q) {
+            const int dx = xl - L.ax[q], dy = yl - L.ay[q];
+            conflict |= dx * dx + dy * dy < MINDIST2;
+          }
+          okc = okc && !conflict;
+          unsigned long long mk = 0ull;
+          for (int j = 0; j < 64; ++j) {
+            const int dx = xl - __builtin_amdgcn_readlane(xl, j), dy = yl - __builtin_amdgcn_readlane(yl, j);
+            if (j < lane && dx * dx + dy * dy < MINDIST2) mk |= 1ull << j;
+          }
+          const unsigned mlo = (unsigned)mk, mhi = (unsigned)(mk >> 32);
+          unsigned long long todo = __ballot(okc), acc = 0ull;
+          int nacc = 0;
+          while (todo != 0ull && na + nacc < MAXC) {
             const int b = __ffsll((long long)todo) - 1;
             todo &= todo - 1ull;
-            const int xc = __builtin_amdgcn_readlane(xl, b), yc = __builtin_amdgcn_readlane(yl, b);
-            const int nin = na - na0;
-            bool conflict = false;
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-              if (lane + 64 * k < nin) {
-                const int dx = xc - rx[k], dy = yc - ry[k];
-                conflict |= dx * dx + dy * dy < MINDIST2;
-              }
-            if (__ballot(conflict) == 0ull) {
-              if (lane == (nin & 63)) {
-#pragma unroll
-                for (int k = 0; k < 4; ++k)
-                  if ((nin >> 6) == k) {
-                    rx[k] = xc;
-                    ry[k] = yc;
-                  }
-              }
-              if (lane == 0) {
-                L.ax[na] = xc;
-                L.ay[na] = yc;
-              }
-              ++na;
+            const unsigned long long mb = ((unsigned long long)__builtin_amdgcn_readlane(mhi, b) << 32) |
+                                          (unsigned)__builtin_amdgcn_readlane(mlo, b);
+            if ((mb & acc) == 0ull) {
+              acc |= 1ull << b;
+              ++nacc;
             }
           }
+          if ((acc >> lane) & 1ull) {
+            const int idx = na + __popcll(acc & ((1ull << lane) - 1ull));
+            L.ax[idx] = xl;
+            L.ay[idx] = yl;
+          }
+          na += nacc;
         }
         if (lane == 0) L.misc[S_NA] = na;
       }
@@ -582,21 +613,22 @@ __global__ void __launch_bounds__(NTS) select_top_kernel(Dev g) {
   const unsigned long long K = all ? 0ull : kth_largest(keys, n, 0ull, false, MAXC_G, L);
   if (tid == 0) L.misc[S_CNT] = 0;
   __syncthreads();
-  for (int base = 0; base < n; base += NTS) {
-    const int i = base + tid;
-    unsigned long long key = 0ull;
-    bool in = false;
-    if (i < n) {
-      key = keys[i];
-      in = all || key >= K;
-    }
-    const unsigned long long mask = __ballot(in);
-    if (mask) {
-      const int leader = __ffsll((long long)mask) - 1;
-      int b = 0;
-      if (lane == leader) b = atomicAdd(&L.misc[S_CNT], __popcll(mask));
-      b = __shfl(b, leader);
-      if (in) L.keys[b + __popcll(mask & ((1ull << lane) - 1ull))] = key;
+  for (int b0 = 0; b0 < n; b0 += KU * NTS) {
+    unsigned long long kk[KU];
+#pragma unroll
+    for (int u = 0; u < KU; ++u) kk[u] = b0 + u * NTS + tid < n ? keys[b0 + u * NTS + tid] : 0ull;
+#pragma unroll
+    for (int u = 0; u < KU; ++u) {
+      const unsigned long long key = kk[u];
+      const bool in = b0 + u * NTS + tid < n && (all || key >= K);
+      const unsigned long long mask = __ballot(in);
+      if (mask) {
+        const int leader = __ffsll((long long)mask) - 1;
+        int b = 0;
+        if (lane == leader) b = atomicAdd(&L.misc[S_CNT], __popcll(mask));
+        b = __shfl(b, leader);
+        if (in) L.keys[b + __popcll(mask & ((1ull << lane) - 1ull))] = key;
+      }
     }
   }
   __syncthreads();
@@ -638,6 +670,7 @@ __device__ __forceinline__ void lk_weights(float a, float b, int& w00, int& w01,
 }
 
 // One wavefront per corner (4 corners per workgroup); all control flow is wave-uniform.
+// (Staging each level's search region in LDS was measured slower: 111 -> 159 µs for 8 streams.)
 __global__ void __launch_bounds__(256) lk_kernel(Dev g) {
   const int s = blockIdx.y, lane = threadIdx.x & 63;
   const int p = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -805,7 +838,6 @@ __global__ void __launch_bounds__(256) finish_kernel(Dev g, yk_motion* __restric
       r.first_frame = 1;
       r.consistency = -1.0f;
       out[s] = r;
-      if (out != g.out) g.out[s] = r;  // the detector's own record stays "the last detect" too
       S.has_prev = 1;
       g.sel[s] ^= 1;  // this frame is the next call's previous one
     }
@@ -935,7 +967,6 @@ __global__ void __launch_bounds__(256) finish_kernel(Dev g, yk_motion* __restric
   S.reset_triggers += r.should_reset;
   S.avg = (S.avg * (float)(S.total - 1) + r.magnitude) / (float)S.total;
   out[s] = r;
-  if (out != g.out) g.out[s] = r;
   g.sel[s] ^= 1;
 }
 

@@ -17,7 +17,7 @@ identical to the serial order (the tracker still sees frames in order on one str
 tracker) adds the global camera-motion branch of MotionCompensatedMultiTracker.update(dets,
 frame) (motion_compensated_multi_tracker.py:94-121): GlobalMotionDetector on every stream's
 frame (motion.BatchedMotionDetector, gmd.hip), whose device results the tracker step consumes:
-serial, right before the tracker step; pipelined, on its own high-priority stream as soon as the
+serial, right before the tracker step; pipelined, on its own stream as soon as the
 slot's frames are in, writing one motion record per detection buffer.  The frame slot is not
 refilled before that detector has read it.
 
@@ -30,8 +30,6 @@ parallel branches inside one captured graph execute one after the other, so a se
 independent graph on another stream is what fills the idle CUs (tools/inflight.py: 1.45x).
 """
 from __future__ import annotations
-
-import os
 
 import numpy as np
 
@@ -68,11 +66,9 @@ class StreamPipeline:
         self._counts = torch.zeros((self.nb, self.S), dtype=torch.int32, device=dev)
         self._k = 0  # detection buffer the next step writes
         self.pipelined = bool(pipelined)
-        # the tracker stream is a serial chain (motion detection + tracker step per frame) of small,
-        # latency-bound launches: high priority, so its workgroups are dispatched ahead of the
-        # in-flight forwards' instead of queueing behind them (YK_TRK_PRIORITY=0 turns it off)
-        prio = -1 if os.environ.get("YK_TRK_PRIORITY", "1") != "0" else 0
-        self.trk_stream = torch.cuda.Stream(dev, priority=prio) if self.pipelined else None
+        # (a high-priority tracker stream halved the bf16 line, 12,301 -> 5,974 frames/s, and the
+        # CMC line with it: profiles/r04_cmc_ab.txt; default priority everywhere)
+        self.trk_stream = torch.cuda.Stream(dev) if self.pipelined else None
         self._ev_det = [torch.cuda.Event() for _ in range(self.nb)]
         self._ev_trk = [torch.cuda.Event() for _ in range(self.nb)]
         self._trk_pending = [False] * self.nb
@@ -106,7 +102,7 @@ class StreamPipeline:
         # overlaps the tracker step of t and both overlap the forwards in flight
         self.gmd_stream = None
         if self.gmd is not None and self.pipelined:
-            self.gmd_stream = torch.cuda.Stream(dev, priority=prio)
+            self.gmd_stream = torch.cuda.Stream(dev)
             self._motion = torch.zeros((self.nb, self.S * L.MOTION_DTYPE.itemsize), dtype=torch.uint8, device=dev)
             self._ev_in = [torch.cuda.Event() for _ in range(self.D)]
 
