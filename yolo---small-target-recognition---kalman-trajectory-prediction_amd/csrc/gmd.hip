@@ -179,8 +179,10 @@ __global__ void __launch_bounds__(256) pyrdown_kernel(Dev g, int l) {
 }
 
 // calcSharrDeriv: vertical [3 10 3] / [-1 0 1], then horizontal [-1 0 1] / [3 10 3], reflect-101.
-__global__ void __launch_bounds__(256) scharr_kernel(Dev g, int l) {
-  const int s = blockIdx.z, cur = g.sel[s] ^ 1;
+// Every level of every stream in one launch (blockIdx.z = stream * (levels + 1) + level; the
+// grid covers level 0, smaller levels' out-of-range tiles return at once).
+__global__ void __launch_bounds__(256) scharr_kernel(Dev g) {
+  const int nl = g.geo.levels + 1, s = blockIdx.z / nl, l = blockIdx.z - s * nl, cur = g.sel[s] ^ 1;
   const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = blockIdx.y * 16 + (threadIdx.x >> 4);
   const int w = g.geo.lw[l], h = g.geo.lh[l];
   if (x >= w || y >= h) return;
@@ -1494,9 +1496,8 @@ static void gmd_front(yk_gmd* g, const uint8_t* frames, hipStream_t st) {
   for (int l = 1; l <= G.levels; ++l)
     hipLaunchKernelGGL(yk::gmd::pyrdown_kernel, dim3((G.lw[l] + 15) / 16, (G.lh[l] + 15) / 16, S), dim3(256), 0, st,
                        d, l);
-  for (int l = 0; l <= G.levels; ++l)
-    hipLaunchKernelGGL(yk::gmd::scharr_kernel, dim3((G.lw[l] + 15) / 16, (G.lh[l] + 15) / 16, S), dim3(256), 0, st,
-                       d, l);
+  hipLaunchKernelGGL(yk::gmd::scharr_kernel, dim3((G.lw[0] + 15) / 16, (G.lh[0] + 15) / 16, S * (G.levels + 1)),
+                     dim3(256), 0, st, d);
   if (g->frames > 0) {
     hipLaunchKernelGGL(yk::gmd::clear_kernel, dim3((S + 255) / 256), dim3(256), 0, st, d);
     if (d.mode)
