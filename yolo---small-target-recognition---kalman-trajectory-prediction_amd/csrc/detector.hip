@@ -61,20 +61,16 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 // range of work items ordered (pixel tile major, channel group minor): sibling channel groups of a
 // pixel tile and neighbouring pixel tiles (the rows a 3x3 window shares) meet in one L2 instead of
 // being fetched once per XCD.  Placement only: the mapping is a bijection either way.
-// on = 1: XCD k runs a contiguous range of (pixel block, channel group) items in pixel-major
-// order (a block's channel groups on one XCD: its activations are fetched into one L2);
-// on = 2: the same in channel-group-major order (a group's weights are fetched into ~1 + 8 / G
-// L2s instead of all 8; chosen by the host for weight-heavy launches, xcd_order).
+// XCD k runs a contiguous range of (pixel block, channel group) items in pixel-major order (a
+// block's channel groups on one XCD: its activations are fetched into one L2).  (Round 4: a
+// channel-group-major order for the weight-heavy P5 convs cut their PMC bytes 3.73x -> 3.18x of
+// algorithmic but not their time, 25.3 vs 25.8 µs; not kept.)
 __device__ __forceinline__ int2 xcd_block(int on) {
   if (!on) return make_int2(blockIdx.x, blockIdx.y);
   const int gx = gridDim.x, gy = gridDim.y, n = gx * gy;
   const int L = blockIdx.y * gx + blockIdx.x;
   const int k = L & 7, i = L >> 3, q = n >> 3, r = n & 7;
   const int item = k * q + (k < r ? k : r) + i;
-  if (on == 2) {
-    const int ty = item / gx;
-    return make_int2(item - ty * gx, ty);
-  }
   const int px = item / gy;
   return make_int2(px, item - px * gy);
 }
@@ -3720,17 +3716,6 @@ void launch_fastw(const FastArgs& a, int nnt, int npt, hipStream_t st) {
 }
 // plan.npt = NPT | mode << 4: mode 0 per-wave pixels, 1 = the four waves split K (WS),
 // 2 = per-wave pixels with the weight fragments shared through LDS (conv_fastw_kernel)
-// XCD placement of a table-conv launch (xcd_block): L2 fetches of pixel-major placement ~ A + 8 W
-// (every XCD sees every channel group's weights), of group-major ~ G A + (1 + 8 / G) W, with A the
-// input activations, W the packed weights, G the channel groups (gridDim.y).
-int xcd_order(int xcd, const yk_op& op, const ConvPlan& cp, long M, int esz, int wb_per_lane) {
-  if (xcd != 1) return xcd;
-  const int cin = op.src_ch[0] + (op.n_src > 1 ? op.src_ch[1] : 0);
-  const double A = (double)M * cin * esz, W = (double)op.n_tiles * op.k_steps * 64 * wb_per_lane;
-  const int G = (op.n_tiles + cp.nnt - 1) / cp.nnt;
-  return G * A + (1.0 + 8.0 / G) * W < A + 8.0 * W ? 2 : 1;
-}
-
 template <class Tr>
 void launch_fast(const FastArgs& a, const ConvPlan& p, hipStream_t st) {
   const int mode = (p.npt >> 4) & 3;
@@ -3998,8 +3983,7 @@ int launch_op(yk_model* m, const yk_op& op, const uint8_t* frames, int B, float 
           f.r_cstride = a.r_cstride;
           f.r_coff = a.r_coff;
           f.act = a.act;
-          f.xcd = xcd_order(m->xcd, op, cp, a.M, esz_of(m->desc.act_dtype),
-                            std::is_same<Tr, F32>::value && (cp.npt & kSplitBit) ? 32 : 16);
+          f.xcd = m->xcd;
           f.tstamp = (m->ts && (int)(&op - m->ops.data()) == m->ts_op) ? m->ts : nullptr;
           f.tstamp_cap = kTsCap;
           if constexpr (std::is_same<Tr, F32>::value) {
