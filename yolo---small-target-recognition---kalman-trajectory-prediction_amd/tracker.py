@@ -97,16 +97,22 @@ class TrajCache:
         if R == 0:
             self.d = {}
             return []
-        rr = np.arange(R)[:, None]
-        ln = np.asarray(lens)
-        last = traj[rr, np.clip(ln[:, None] - 3 + np.arange(3), 0, traj.shape[1] - 1)].tolist()  # [R][3][2]
+        # every row's newest point in one gather (the usual one-point advance); more than one new
+        # point reads the row itself
+        lp = traj[np.arange(R), np.maximum(np.asarray(lens) - 1, 0)]
+        last = list(zip(lp[:, 0].tolist(), lp[:, 1].tolist()))
         out, new = [], {}
         for i in range(R):
             n, c = lens[i], counts[i]
             old = self.d.get(nums[i])
             k = -1 if old is None else c - old[0]
             if 0 <= k <= 3 and k <= n and n == min(len(old[1]) + k, traj.shape[1]):
-                lst = old[1] + [tuple(p) for p in last[i][3 - k:]] if k else old[1]
+                if k == 0:
+                    lst = old[1]
+                elif k == 1:
+                    lst = old[1] + [last[i]]
+                else:
+                    lst = old[1] + list(map(tuple, traj[i, n - k:n].tolist()))
                 if len(lst) > n:
                     lst = lst[len(lst) - n:]
             else:
@@ -138,12 +144,13 @@ def rows_to_dicts(rows, cache: TrajCache | None = None) -> list[dict]:
         trajs = cache.lists(nums, rows["traj_count"].tolist(), lens, traj)
     else:
         trajs = [list(map(tuple, traj[i, :lens[i]].tolist())) for i in range(R)]
+    bbs, ves = list(bb), list(ve)  # row views, made in C
     out = []
     for i in range(R):
         k = tsu[i]
-        out.append({"track_id": f"T{nums[i]:03d}", "bbox": bb[i], "confidence": conf[i], "status": _STATUS[st[i]],
+        out.append({"track_id": f"T{nums[i]:03d}", "bbox": bbs[i], "confidence": conf[i], "status": _STATUS[st[i]],
                     "age": age[i], "hits": hits[i], "hit_streak": hs[i], "time_since_update": k, "lost_frames": k,
-                    "is_lost": k > 0, "trajectory": trajs[i], "velocity": ve[i], "motion_confidence": mc[i],
+                    "is_lost": k > 0, "trajectory": trajs[i], "velocity": ves[i], "motion_confidence": mc[i],
                     "is_stable_motion": bool(stab[i]), "speed": sp[i], "direction": di[i]})
     return out
 
