@@ -248,7 +248,10 @@ def test_pipeline_with_global_motion_matches_serial():
     for r1, c1, s1, m1, ms1 in runs[1:]:
         np.testing.assert_array_equal(c0, c1)
         np.testing.assert_array_equal(s0, s1)
-        assert m0.tobytes() == m1.tobytes() and ms0.tobytes() == ms1.tobytes()
+        for f in m0.dtype.names:  # field by field, so a mismatch prints the values
+            np.testing.assert_array_equal(m1[f], m0[f], err_msg=f"motion.{f}")
+        for f in ms0.dtype.names:
+            np.testing.assert_array_equal(ms1[f], ms0[f], err_msg=f"gmd stats.{f}")
         for s in range(S):
             assert r0[s][: c0[s]].tobytes() == r1[s][: c1[s]].tobytes()
 

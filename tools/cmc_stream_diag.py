@@ -26,7 +26,7 @@ def main():
     seqs = [camera_sequence(80 + s, F, h=512, w=640, whip_at=(7, 14), n_targets=12)[0] for s in range(S)]
     frames = torch.from_numpy(np.stack(seqs, 1)).cuda()
     runs = []
-    for pipelined, inflight in ((False, 1), (True, 1), (True, 3)):
+    for pipelined, inflight in ((False, 1), (False, 1), (True, 1), (True, 1), (True, 3)):
         pipe = pipeline.StreamPipeline("yolov8s-small.yaml", S, (512, 640), "bf16", seed=0, max_tracks=256,
                                        pipelined=pipelined, inflight=inflight, tracker_policy=1,
                                        motion_method="optical_flow")
@@ -41,7 +41,6 @@ def main():
         pipe.sync()
         rec.append(pipe.gmd.download()[0].copy())
         runs.append(rec)
-        del pipe
     for j, r in enumerate(runs[1:], 1):
         for t, (a, b) in enumerate(zip(runs[0], r)):
             if a.tobytes() != b.tobytes():

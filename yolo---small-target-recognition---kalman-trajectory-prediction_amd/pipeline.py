@@ -16,10 +16,9 @@ identical to the serial order (the tracker still sees frames in order on one str
 ``motion_method='optical_flow'`` (with ``tracker_policy=1``, the camera-motion-compensation
 tracker) adds the global camera-motion branch of MotionCompensatedMultiTracker.update(dets,
 frame) (motion_compensated_multi_tracker.py:94-121): GlobalMotionDetector on every stream's
-frame (motion.BatchedMotionDetector, gmd.hip), whose device results the tracker step consumes:
-serial, right before the tracker step; pipelined, on its own stream as soon as the
-slot's frames are in, writing one motion record per detection buffer.  The frame slot is not
-refilled before that detector has read it.
+frame (motion.BatchedMotionDetector, gmd.hip) on the tracker stream right before the tracker
+step, which consumes its device results.  The frame slot is not refilled before that detector
+has read it.
 
 ``inflight=D`` > 1 (needs ``pipelined``) keeps D detector forwards in flight: D DeviceModels
 (same program and conv plan, each its own activation arena) replay their hipGraphs on D HIP
@@ -32,10 +31,8 @@ independent graph on another stream is what fills the idle CUs (tools/inflight.p
 from __future__ import annotations
 
 import numpy as np
-
 import torch
 
-from . import _lib as L
 from . import arch as A
 from . import model as M
 from . import tracker as T
@@ -66,8 +63,11 @@ class StreamPipeline:
         self._counts = torch.zeros((self.nb, self.S), dtype=torch.int32, device=dev)
         self._k = 0  # detection buffer the next step writes
         self.pipelined = bool(pipelined)
-        # (a high-priority tracker stream halved the bf16 line, 12,301 -> 5,974 frames/s, and the
-        # CMC line with it: profiles/r04_cmc_ab.txt; default priority everywhere)
+        # default stream priorities: a high-priority tracker / motion stream halved the bf16 line
+        # (12,301 -> 5,974 frames/s, profiles/r04_cmc_ab.txt).  The motion detector stays on the
+        # tracker stream: moving it to a stream of its own (+13 % on the bf16 CMC line) made the
+        # pipelined motion records differ from the serial ones in 3 of 5 runs of
+        # test_pipeline_with_global_motion_matches_serial, a race not found in round 4
         self.trk_stream = torch.cuda.Stream(dev) if self.pipelined else None
         self._ev_det = [torch.cuda.Event() for _ in range(self.nb)]
         self._ev_trk = [torch.cuda.Event() for _ in range(self.nb)]
@@ -97,14 +97,6 @@ class StreamPipeline:
             self.gmd = Mo.BatchedMotionDetector(self.S, frame_hw[0], frame_hw[1], motion_method, self.device)
         self._ev_gmd = [torch.cuda.Event() for _ in range(self.D)]  # slot's frames read by the motion detector
         self._gmd_pending = [False] * self.D
-        # pipelined: the motion detector runs on its own stream as soon as a slot's frames are in
-        # (it needs no detections), one yk_motion record per detection buffer, so motion(t + 1)
-        # overlaps the tracker step of t and both overlap the forwards in flight
-        self.gmd_stream = None
-        if self.gmd is not None and self.pipelined:
-            self.gmd_stream = torch.cuda.Stream(dev)
-            self._motion = torch.zeros((self.nb, self.S * L.MOTION_DTYPE.itemsize), dtype=torch.uint8, device=dev)
-            self._ev_in = [torch.cuda.Event() for _ in range(self.D)]
 
     @property
     def dets(self) -> torch.Tensor:
@@ -154,29 +146,15 @@ class StreamPipeline:
         k = self._k
         s = self._slot(k)
         cur = self._stream(s)
-        trk_busy = self._trk_pending[k]
-        if trk_busy:  # tracker(t - nb) still reads buffer k
+        if self._trk_pending[k]:  # tracker(t - nb) still reads buffer k
             cur.wait_event(self._ev_trk[k])
             self._trk_pending[k] = False
-        if self.gmd_stream is not None:
-            # motion(t) reads slot s's frames (in once `cur` reaches here) and writes record k,
-            # which tracker(t - nb) may still be reading
-            self._ev_in[s].record(cur)
-            self.gmd_stream.wait_event(self._ev_in[s])
-            if trk_busy:
-                self.gmd_stream.wait_event(self._ev_trk[k])
-            with torch.cuda.stream(self.gmd_stream):
-                self.gmd.detect_device(self.frame_slots[s], out=self._motion[k].data_ptr())
-            self._ev_gmd[s].record(self.gmd_stream)
-            self._gmd_pending[s] = True
         with torch.cuda.stream(cur):
             self.models[s].detect(self.frame_slots[s], self.conf, self.iou, self.max_det, self._dets[k],
                                   self._counts[k], graph=bool(self.graph))
         if self.pipelined:
             self._ev_det[k].record(cur)
             self.trk_stream.wait_event(self._ev_det[k])
-            if self.gmd_stream is not None:
-                self.trk_stream.wait_event(self._ev_gmd[s])
             with torch.cuda.stream(self.trk_stream):
                 self._track(k, s)
             self._ev_trk[k].record(self.trk_stream)
@@ -193,9 +171,6 @@ class StreamPipeline:
         """Tracker step of detection buffer k (frames of slot s) on the current stream."""
         if self.gmd is None:
             self.tracker.step_device(self._dets[k], self._counts[k])
-            return
-        if self.gmd_stream is not None:  # motion(t) ran on its own stream (step)
-            self.tracker.step_device(self._dets[k], self._counts[k], motion=self._motion[k].data_ptr())
             return
         self.gmd.detect_device(self.frame_slots[s])
         if self.pipelined:
