@@ -102,8 +102,9 @@ def parse():
                     help="with --tracker motion_reset: also run GlobalMotionDetector('optical_flow') on every frame "
                          "(MotionCompensatedMultiTracker.update(dets, frame)); no CPU baseline (the oracle's numpy "
                          "restatement of cv2's optical flow is not a stand-in for cv2's speed)")
-    ap.add_argument("--inflight", type=int, default=4, choices=range(1, 9),
-                    help="detector forwards in flight (each a batch of all streams, own graph + HIP stream)")
+    ap.add_argument("--inflight", type=int, default=None, choices=range(1, 9),
+                    help="detector forwards in flight (each a batch of all streams, own graph + HIP stream); "
+                         "default 4, 6 with --gmd (profiles/r04_inflight_sweep.txt)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=25.0, help="CPU-baseline sample bound (default threads)")
     ap.add_argument("--cpu-all-seconds", type=float, default=10.0, help="CPU-baseline sample bound (all cores)")
@@ -112,7 +113,13 @@ def parse():
     ap.add_argument("--save-plans", action="store_true", help="write every leg's conv plan to plans/<workload>.json")
     ap.add_argument("--plan-in", default="", help="conv plan (json) of the headline leg (default: plans/<workload>.json)")
     ap.add_argument("--dump-ops", default="", help="write per-op device times (json) to this path")
-    return ap.parse_args()
+    a = ap.parse_args()
+    if a.inflight is None:
+        # the motion detector and the motion-reset step lengthen the tracker stream; two more
+        # forwards in flight hide it (bf16 CMC 8,883 -> 10,115, fp32 4,586 -> 5,118 frames/s), while
+        # the plain lines are flat from 4 to 8 (profiles/r04_inflight_sweep.txt)
+        a.inflight = 6 if a.gmd else 4
+    return a
 
 
 # ---------------------------------------------------------------------------- ranks
