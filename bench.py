@@ -104,7 +104,7 @@ def parse():
                          "restatement of cv2's optical flow is not a stand-in for cv2's speed)")
     ap.add_argument("--inflight", type=int, default=None, choices=range(1, 9),
                     help="detector forwards in flight (each a batch of all streams, own graph + HIP stream); "
-                         "default 4, 6 with --gmd (profiles/r04_inflight_sweep.txt)")
+                         "default 4")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=25.0, help="CPU-baseline sample bound (default threads)")
     ap.add_argument("--cpu-all-seconds", type=float, default=10.0, help="CPU-baseline sample bound (all cores)")
@@ -115,10 +115,10 @@ def parse():
     ap.add_argument("--dump-ops", default="", help="write per-op device times (json) to this path")
     a = ap.parse_args()
     if a.inflight is None:
-        # the motion detector and the motion-reset step lengthen the tracker stream; two more
-        # forwards in flight hide it (bf16 CMC 8,883 -> 10,115, fp32 4,586 -> 5,118 frames/s), while
-        # the plain lines are flat from 4 to 8 (profiles/r04_inflight_sweep.txt)
-        a.inflight = 6 if a.gmd else 4
+        # 4 for every line: six forwards in flight lift the CMC lines (bf16 8,883 -> 10,115 frames/s)
+        # but the motion records then differ from the serial pipeline's in float rounding
+        # (profiles/r04_inflight_sweep.txt), so the CMC line is not measured there
+        a.inflight = 4
     return a
 
 
