@@ -24,6 +24,56 @@ pipeline = importlib.import_module(PKG + ".pipeline")
 L = importlib.import_module(PKG + "._lib")
 
 
+class IsolatedMotionPipeline(pipeline.StreamPipeline):
+    """--isolate: the motion detector of step t waits for every detector slot stream (all forwards
+    up to t done) and forward(t + 1) waits for it, so no forward overlaps the motion kernels."""
+
+    def step(self):
+        k = self._k
+        s = self._slot(k)
+        cur = self._stream(s)
+        if self._trk_pending[k]:
+            cur.wait_event(self._ev_trk[k])
+            self._trk_pending[k] = False
+        if getattr(self, "_ev_motion_done", None) is not None:
+            cur.wait_event(self._ev_motion_done)
+        with torch.cuda.stream(cur):
+            self.models[s].detect(self.frame_slots[s], self.conf, self.iou, self.max_det, self._dets[k],
+                                  self._counts[k], graph=bool(self.graph))
+        self._ev_det[k].record(cur)
+        for j in range(self.D):
+            self.trk_stream.wait_stream(self._stream(j))
+        with torch.cuda.stream(self.trk_stream):
+            self.gmd.detect_device(self.frame_slots[s])
+            self._ev_gmd[s].record(self.trk_stream)
+            self._gmd_pending[s] = True
+            ev = torch.cuda.Event()
+            ev.record(self.trk_stream)
+            self._ev_motion_done = ev
+            self.tracker.step_device(self._dets[k], self._counts[k], motion=self.gmd.motion_ptr)
+        if self.step_hook is not None:
+            self.step_hook(self, k, cur, self.trk_stream)
+        self._ev_trk[k].record(self.trk_stream)
+        self._trk_pending[k] = True
+        self._k = (k + 1) % self.nb
+
+
+class PrivateFramePipeline(pipeline.StreamPipeline):
+    """--private: the motion detector reads its own copy of the step's frames, made on the tracker
+    stream from the caller's (never rewritten) source tensor instead of the detector slot."""
+
+    def run(self, frames):
+        self._src = frames
+        super().run(frames)
+
+    def _track(self, k, s):
+        if getattr(self, "_gbuf", None) is None:
+            self._gbuf = torch.empty_like(self.frames)
+        self._gbuf.copy_(self._src, non_blocking=True)
+        self.gmd.detect_device(self._gbuf)
+        self.tracker.step_device(self._dets[k], self._counts[k], motion=self.gmd.motion_ptr)
+
+
 def main():
     from gmd_helpers import camera_sequence
     from gpu_helpers import d2d_async
@@ -31,6 +81,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--inflight", type=int, default=6)
     ap.add_argument("--reps", type=int, default=6)
+    ap.add_argument("--isolate", action="store_true", help="no forward overlaps the motion kernels")
+    ap.add_argument("--private", action="store_true", help="motion reads a tracker-stream copy of the frames")
     a = ap.parse_args()
     S, F = 3, 20
     seqs = [camera_sequence(80 + s, F, h=512, w=640, whip_at=(7, 14), n_targets=12)[0] for s in range(S)]
@@ -38,7 +90,12 @@ def main():
     nbytes = S * L.MOTION_DTYPE.itemsize
 
     def run(pipelined, inflight):
-        pipe = pipeline.StreamPipeline("yolov8s-small.yaml", S, (512, 640), "bf16", seed=0, max_tracks=256,
+        cls = pipeline.StreamPipeline
+        if pipelined and a.isolate:
+            cls = IsolatedMotionPipeline
+        elif pipelined and a.private:
+            cls = PrivateFramePipeline
+        pipe = cls("yolov8s-small.yaml", S, (512, 640), "bf16", seed=0, max_tracks=256,
                                        pipelined=pipelined, inflight=inflight, tracker_policy=1,
                                        motion_method="optical_flow")
         rec = torch.zeros((F, nbytes), dtype=torch.uint8, device="cuda")
@@ -54,6 +111,16 @@ def main():
         for t in range(F):
             pipe.run(frames[t])
         pipe.sync()
+        # every frame buffer must still hold the frame last copied into it
+        held = [(f"slot{(F - 1 - j) % pipe.D if pipe.D > 1 else 0}", pipe.frame_slots[(F - 1 - j) % pipe.D], frames[F - 1 - j])
+                for j in range(pipe.D)]
+        if getattr(pipe, "_gbuf", None) is not None:
+            held.append(("private", pipe._gbuf, frames[F - 1]))
+        for name, buf, want in held:
+            nbad = int((buf != want).sum())
+            if nbad:
+                idx = (buf != want).flatten().nonzero()[:4].flatten().tolist()
+                print(f"    {name}: {nbad} bytes differ from the frame copied in, first at {idx}", flush=True)
         return np.frombuffer(rec.cpu().numpy().tobytes(), dtype=L.MOTION_DTYPE).reshape(F, S)
 
     ref = run(False, 1)
@@ -76,7 +143,7 @@ def main():
                 print(f"    {name:9s} serial {ref[t][name].tolist()}  pipelined {got[t][name].tolist()}", flush=True)
         else:
             print(f"rep {r}: identical", flush=True)
-    print(f"inflight={a.inflight}: {bad} of {a.reps} runs differ", flush=True)
+    print(f"inflight={a.inflight}{' isolated' if a.isolate else ''}{' private' if a.private else ''}: {bad} of {a.reps} runs differ", flush=True)
 
 
 if __name__ == "__main__":
