@@ -298,6 +298,11 @@ int yk_gmd_set_thresholds(yk_gmd* g, double global_motion_threshold, double rese
  * `stream`. */
 int yk_gmd_detect(yk_gmd* g, const uint8_t* dev_frames, yk_motion* dev_motion, void* stream);
 int yk_gmd_outputs(yk_gmd* g, yk_motion** dev_motion);
+/* Diagnostics: device addresses of the last call's corners (float x, y [S][max_corners]), LK end
+ * points (float x, y [S][max_corners]), status (uint8 [S][max_corners]) and corner counts
+ * (int32 [S]), so a harness can copy them in stream order (tools/gmd_step_diff.py). */
+int yk_gmd_debug_buffers(yk_gmd* g, void** dev_corners, void** dev_next, void** dev_status, int32_t** dev_ncorners,
+                         int32_t* max_corners);
 /* Copy the last results (and stats when host_stats != NULL) to the host; synchronous. */
 int yk_gmd_download(yk_gmd* g, yk_motion* host_motion, yk_gmd_stats* host_stats, void* stream);
 /* Diagnostics for parity tests: stream s's last corners (x, y), LK end points (x, y) and status

@@ -99,10 +99,19 @@ def main():
                                        pipelined=pipelined, inflight=inflight, tracker_policy=1,
                                        motion_method="optical_flow")
         rec = torch.zeros((F, nbytes), dtype=torch.uint8, device="cuda")
+        ptrs = [C.c_void_p() for _ in range(4)]
+        M = C.c_int32()
+        L.check(L.lib().yk_gmd_debug_buffers(pipe.gmd._h, *[C.byref(q) for q in ptrs], C.byref(M)), "debug buffers")
+        M = M.value
+        cor = torch.zeros((F, S, M, 2), dtype=torch.float32, device="cuda")
+        nxt = torch.zeros((F, S, M, 2), dtype=torch.float32, device="cuda")
         step = [0]
 
         def hook(p, k, det_stream, trk_stream):
-            d2d_async(rec[step[0]].data_ptr(), p.gmd.motion_ptr, nbytes, trk_stream)
+            t = step[0]
+            d2d_async(rec[t].data_ptr(), p.gmd.motion_ptr, nbytes, trk_stream)
+            d2d_async(cor[t].data_ptr(), ptrs[0].value, S * M * 8, trk_stream)
+            d2d_async(nxt[t].data_ptr(), ptrs[1].value, S * M * 8, trk_stream)
             step[0] += 1
 
         pipe.frames.copy_(frames[0])
@@ -121,12 +130,27 @@ def main():
             if nbad:
                 idx = (buf != want).flatten().nonzero()[:4].flatten().tolist()
                 print(f"    {name}: {nbad} bytes differ from the frame copied in, first at {idx}", flush=True)
-        return np.frombuffer(rec.cpu().numpy().tobytes(), dtype=L.MOTION_DTYPE).reshape(F, S)
+        return (np.frombuffer(rec.cpu().numpy().tobytes(), dtype=L.MOTION_DTYPE).reshape(F, S), cor.cpu().numpy(),
+                nxt.cpu().numpy())
 
-    ref = run(False, 1)
+    ref, rcor, rnxt = run(False, 1)
     bad = 0
     for r in range(a.reps):
-        got = run(True, a.inflight)
+        got, gcor, gnxt = run(True, a.inflight)
+        # first step whose corners / LK end points differ (any stream), before the motion record
+        for t in range(F):
+            # the first n_corners entries of each stream (the rest is not written by that step)
+            live = np.arange(rcor.shape[2])[None, :, None] < ref[t]["n_corners"][:, None, None]
+            dc = np.argwhere((rcor[t] != gcor[t]) & live)
+            dn = np.argwhere((rnxt[t] != gnxt[t]) & live)
+            if len(dc) or len(dn):
+                what = "corners" if len(dc) else "lk_next"
+                s_, i_ = (dc if len(dc) else dn)[0][:2]
+                src = (rcor, gcor) if len(dc) else (rnxt, gnxt)
+                print(f"rep {r}: first {what} difference at step {t} stream {s_} point {i_} "
+                      f"({len(dc)} corner / {len(dn)} end-point values differ): serial {src[0][t, s_, i_].tolist()} "
+                      f"pipelined {src[1][t, s_, i_].tolist()}", flush=True)
+                break
         first = None
         for t in range(F):
             for f in ref.dtype.names:

@@ -1563,6 +1563,18 @@ int yk_gmd_outputs(yk_gmd* g, yk_motion** dev_motion) {
   return YK_OK;
 }
 
+int yk_gmd_debug_buffers(yk_gmd* g, void** dev_corners, void** dev_next, void** dev_status, int32_t** dev_ncorners,
+                         int32_t* max_corners) {
+  YK_CHECK_ARG(g && dev_corners && dev_next && dev_status && dev_ncorners && max_corners,
+               "yk_gmd_debug_buffers: NULL argument");
+  *dev_corners = g->dev.corners;
+  *dev_next = g->dev.next;
+  *dev_status = g->dev.status;
+  *dev_ncorners = g->dev.ncorners;
+  *max_corners = g->dev.maxc;
+  return YK_OK;
+}
+
 int yk_gmd_download(yk_gmd* g, yk_motion* host_motion, yk_gmd_stats* host_stats, void* stream) {
   YK_CHECK_ARG(g && host_motion, "yk_gmd_download: NULL argument");
   yk::DeviceGuard guard(g->ctx->device);
