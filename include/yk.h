@@ -303,6 +303,9 @@ int yk_gmd_outputs(yk_gmd* g, yk_motion** dev_motion);
  * (int32 [S]), so a harness can copy them in stream order (tools/gmd_step_diff.py). */
 int yk_gmd_debug_buffers(yk_gmd* g, void** dev_corners, void** dev_next, void** dev_status, int32_t** dev_ncorners,
                          int32_t* max_corners);
+/* Diagnostics: the two gray-pyramid buffers (uint8 [S][per]) and Scharr-derivative buffers (int16 x, y
+ * [S][per]) the calls alternate between; per = pixels of every level of one stream. */
+int yk_gmd_debug_pyramids(yk_gmd* g, void** dev_pyr0, void** dev_pyr1, void** dev_der0, void** dev_der1, int64_t* per);
 /* Copy the last results (and stats when host_stats != NULL) to the host; synchronous. */
 int yk_gmd_download(yk_gmd* g, yk_motion* host_motion, yk_gmd_stats* host_stats, void* stream);
 /* Diagnostics for parity tests: stream s's last corners (x, y), LK end points (x, y) and status

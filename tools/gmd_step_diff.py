@@ -103,6 +103,12 @@ def main():
         M = C.c_int32()
         L.check(L.lib().yk_gmd_debug_buffers(pipe.gmd._h, *[C.byref(q) for q in ptrs], C.byref(M)), "debug buffers")
         M = M.value
+        pp = [C.c_void_p() for _ in range(4)]
+        per = C.c_int64()
+        L.check(L.lib().yk_gmd_debug_pyramids(pipe.gmd._h, *[C.byref(q) for q in pp], C.byref(per)), "pyramids")
+        per = per.value
+        pyr = torch.zeros((F, 2, S * per), dtype=torch.uint8, device="cuda")
+        der = torch.zeros((F, 2, S * per * 4), dtype=torch.uint8, device="cuda")
         cor = torch.zeros((F, S, M, 2), dtype=torch.float32, device="cuda")
         nxt = torch.zeros((F, S, M, 2), dtype=torch.float32, device="cuda")
         step = [0]
@@ -112,6 +118,9 @@ def main():
             d2d_async(rec[t].data_ptr(), p.gmd.motion_ptr, nbytes, trk_stream)
             d2d_async(cor[t].data_ptr(), ptrs[0].value, S * M * 8, trk_stream)
             d2d_async(nxt[t].data_ptr(), ptrs[1].value, S * M * 8, trk_stream)
+            for j in range(2):
+                d2d_async(pyr[t, j].data_ptr(), pp[j].value, S * per, trk_stream)
+                d2d_async(der[t, j].data_ptr(), pp[2 + j].value, S * per * 4, trk_stream)
             step[0] += 1
 
         pipe.frames.copy_(frames[0])
@@ -131,12 +140,18 @@ def main():
                 idx = (buf != want).flatten().nonzero()[:4].flatten().tolist()
                 print(f"    {name}: {nbad} bytes differ from the frame copied in, first at {idx}", flush=True)
         return (np.frombuffer(rec.cpu().numpy().tobytes(), dtype=L.MOTION_DTYPE).reshape(F, S), cor.cpu().numpy(),
-                nxt.cpu().numpy())
+                nxt.cpu().numpy(), pyr.cpu().numpy(), der.cpu().numpy())
 
-    ref, rcor, rnxt = run(False, 1)
+    ref, rcor, rnxt, rpyr, rder = run(False, 1)
     bad = 0
     for r in range(a.reps):
-        got, gcor, gnxt = run(True, a.inflight)
+        got, gcor, gnxt, gpyr, gder = run(True, a.inflight)
+        for t in range(1, F):  # first step whose pyramid / derivative buffers differ (both written)
+            bp = [int((rpyr[t, j] != gpyr[t, j]).sum()) for j in range(2)]
+            bd = [int((rder[t, j] != gder[t, j]).sum()) for j in range(2)]
+            if any(bp) or any(bd):
+                print(f"rep {r}: pyramid bytes differing at step {t}: pyr {bp} der {bd}", flush=True)
+                break
         # first step whose corners / LK end points differ (any stream), before the motion record
         for t in range(F):
             # the first n_corners entries of each stream (the rest is not written by that step)

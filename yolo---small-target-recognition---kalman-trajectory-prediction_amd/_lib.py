@@ -192,6 +192,8 @@ _SIGS = {
     "yk_gmd_outputs": ([_vp, C.POINTER(_vp)], C.c_int),
     "yk_gmd_debug_buffers": ([_vp, C.POINTER(_vp), C.POINTER(_vp), C.POINTER(_vp), C.POINTER(_vp), C.POINTER(_i32)],
                              C.c_int),
+    "yk_gmd_debug_pyramids": ([_vp, C.POINTER(_vp), C.POINTER(_vp), C.POINTER(_vp), C.POINTER(_vp),
+                               C.POINTER(C.c_int64)], C.c_int),
     "yk_gmd_download": ([_vp, _vp, _vp, _vp], C.c_int),
     "yk_gmd_points": ([_vp, C.c_int, _vp, _vp, _vp, C.POINTER(_i32), _vp], C.c_int),
     "yk_gmc_apply": ([_vp, _vp, _vp, _vp], C.c_int),

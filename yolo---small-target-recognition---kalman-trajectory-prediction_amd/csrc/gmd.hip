@@ -1575,6 +1575,16 @@ int yk_gmd_debug_buffers(yk_gmd* g, void** dev_corners, void** dev_next, void** 
   return YK_OK;
 }
 
+int yk_gmd_debug_pyramids(yk_gmd* g, void** dev_pyr0, void** dev_pyr1, void** dev_der0, void** dev_der1, int64_t* per) {
+  YK_CHECK_ARG(g && dev_pyr0 && dev_pyr1 && dev_der0 && dev_der1 && per, "yk_gmd_debug_pyramids: NULL argument");
+  *dev_pyr0 = g->dev.pyr[0];
+  *dev_pyr1 = g->dev.pyr[1];
+  *dev_der0 = g->dev.der[0];
+  *dev_der1 = g->dev.der[1];
+  *per = g->dev.geo.per;
+  return YK_OK;
+}
+
 int yk_gmd_download(yk_gmd* g, yk_motion* host_motion, yk_gmd_stats* host_stats, void* stream) {
   YK_CHECK_ARG(g && host_motion, "yk_gmd_download: NULL argument");
   yk::DeviceGuard guard(g->ctx->device);
