@@ -83,6 +83,7 @@ def main():
     ap.add_argument("--reps", type=int, default=6)
     ap.add_argument("--isolate", action="store_true", help="no forward overlaps the motion kernels")
     ap.add_argument("--private", action="store_true", help="motion reads a tracker-stream copy of the frames")
+    ap.add_argument("--serial", action="store_true", help="repetitions run the serial pipeline too (baseline noise)")
     a = ap.parse_args()
     S, F = 3, 20
     seqs = [camera_sequence(80 + s, F, h=512, w=640, whip_at=(7, 14), n_targets=12)[0] for s in range(S)]
@@ -145,7 +146,7 @@ def main():
     ref, rcor, rnxt, rpyr, rder = run(False, 1)
     bad = 0
     for r in range(a.reps):
-        got, gcor, gnxt, gpyr, gder = run(True, a.inflight)
+        got, gcor, gnxt, gpyr, gder = run(False, 1) if a.serial else run(True, a.inflight)
         for t in range(1, F):  # first step whose pyramid / derivative buffers differ (both written)
             bp = [int((rpyr[t, j] != gpyr[t, j]).sum()) for j in range(2)]
             bd = [int((rder[t, j] != gder[t, j]).sum()) for j in range(2)]
@@ -182,7 +183,7 @@ def main():
                 print(f"    {name:9s} serial {ref[t][name].tolist()}  pipelined {got[t][name].tolist()}", flush=True)
         else:
             print(f"rep {r}: identical", flush=True)
-    print(f"inflight={a.inflight}{' isolated' if a.isolate else ''}{' private' if a.private else ''}: {bad} of {a.reps} runs differ", flush=True)
+    print(f"inflight={a.inflight}{' isolated' if a.isolate else ''}{' private' if a.private else ''}{' serial' if a.serial else ''}: {bad} of {a.reps} runs differ", flush=True)
 
 
 if __name__ == "__main__":
