@@ -173,6 +173,14 @@ int yk_tracker_outputs(yk_tracker* trk, yk_track_out** dev_rows, int32_t** dev_c
 int yk_tracker_download(yk_tracker* trk, yk_track_out* host_rows, int32_t* host_counts,
                         yk_tracker_stats* host_stats, void* stream);
 
+/* Enqueue the same copies without waiting: counts, stats and the first `rows_per_stream` rows of
+ * every stream (host_rows[s * max_tracks ...]; max_tracks copies every row, live or not, since the
+ * counts are not known on the host yet) on `stream`, page-locked destinations expected.  Nothing
+ * is synchronised: the host reads them after an event / stream sync of its own.  The per-step
+ * "tracker output to the host" of a pipelined loop (bench.py). */
+int yk_tracker_download_async(yk_tracker* trk, yk_track_out* host_rows, int32_t* host_counts,
+                              yk_tracker_stats* host_stats, int rows_per_stream, void* stream);
+
 /* Profiling: 32 words of stream s's last step (host_ticks holds 32).  wall_clock64 (100 MHz)
  * timestamps at the phase boundaries -- single-workgroup step: [0] start, [1] predict, [2] IoU
  * candidates, [3] greedy rounds, [4] update / mark_lost, [5] new tracks, [6] delete, [7] outputs;

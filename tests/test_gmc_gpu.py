@@ -99,3 +99,26 @@ def test_botsort_with_gmc_matches_oracle(method):
     print("BOTSORT_GMC", method, {"rows": n_rows, "max_box_dev_px": maxdev})
     # without compensation the fast pan loses its tracks (that is what GMC is for): fewer rows
     assert n_rows > (200 if method == "sparseOptFlow" else 100)
+
+
+def test_gmc_reset_params_then_apply():
+    """GMC.reset_params() (gmc.py:347-353) mid-sequence: the next apply is a first frame again (the
+    identity, every wave of gmc_kernel on the same branch -- ADVICE r4: has_prev was read by every
+    thread while thread 0 set it), and the frames after it match a fresh restatement fed from the
+    reset on."""
+    P = pkg()
+    frames, _ = camera_sequence(3, 12, h=512, w=640, whip_at=(8,))
+    dev = _gmc(P)
+    for fr in frames[:5]:
+        dev.apply(fr)
+    dev.reset_params()
+    ref = R.RefGMC()
+    for f, fr in enumerate(frames[5:]):
+        H = dev.apply(fr)
+        Hr = ref.apply(fr)
+        if f == 0:
+            np.testing.assert_array_equal(H, np.eye(2, 3))
+            assert int(dev.info()[0][4]) == 0
+            continue
+        assert int(dev.info()[0][4]) == 1, (f, dev.info())
+        np.testing.assert_allclose(H, Hr, rtol=1e-9, atol=1e-9, err_msg=f"frame {f} after reset: warp")

@@ -74,6 +74,16 @@ for s in ${STEPS:-pytest bench}; do
         YK_LIB=$PWD/yolo---small-target-recognition---kalman-trajectory-prediction_amd/$L timeout -k 10 200 python -u bench.py --steps 100 --secondary none --no-cpu-baseline $BARGS --dump-ops $O/ops_$L.json > $O/bench_$L.json 2> $O/bench_$L.err || { echo "bench $L failed"; tail -20 $O/bench_$L.err; exit 1; }
         python3 -c "import json; d=json.load(open('$O/bench_$L.json')); print('$L', d['value'], d['ms_per_step'], d['roofline']['kernel'], d['roofline']['avg_launch_us'])"
       done ;;
+    graphkeep)
+      timeout -k 10 120 tools/_graph_fork_repro keep 8 4 > $O/graph_keep.log 2>&1; rc=$?; tail -2 $O/graph_keep.log; [ $rc -eq 0 ] || { echo "graph repro keep rc=$rc"; exit 1; } ;;
+    graphdestroy)
+      timeout -k 10 120 tools/_graph_fork_repro destroy 8 4 > $O/graph_destroy.log 2>&1; rc=$?; tail -2 $O/graph_destroy.log; echo "graph repro destroy rc=$rc"; [ $rc -eq 0 ] || exit 1 ;;
+    lanes)
+      timeout -k 10 300 python -u tools/graph_lanes_repro.py alive > $O/graph_lanes.log 2>&1 || { echo "graph_lanes_repro failed"; tail -20 $O/graph_lanes.log; exit 1; }
+      tail -2 $O/graph_lanes.log ;;
+    stepdiff)
+      timeout -k 10 600 python -u tools/gmd_step_diff.py --inflight ${SD_INFLIGHT:-6} --reps ${SD_REPS:-10} > $O/stepdiff.log 2>&1 || { echo "stepdiff failed"; tail -20 $O/stepdiff.log; exit 1; }
+      tail -15 $O/stepdiff.log ;;
     smoke)
       timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1 || { echo "smoke failed"; tail -20 $O/smoke.txt; exit 1; }
       tail -3 $O/smoke.txt ;;

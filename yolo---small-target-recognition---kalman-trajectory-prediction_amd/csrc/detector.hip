@@ -3160,6 +3160,7 @@ struct yk_model {
   std::vector<Task> tasks;
   std::vector<char> lane_used;              // lanes that run at least one task
   std::vector<hipStream_t> aux;             // lanes 1..groups*lanes-1
+  hipStream_t cap = nullptr;                // graph-capture stream, kept for the model's lifetime
   std::vector<hipEvent_t> ev;               // per task + fork + joins
   // per-op conv plan chosen by yk_model_autotune (kind < 0: not tuned, use the heuristic)
   std::vector<std::array<int, 3>> tuned;    // {kind, nnt, npt}
@@ -4567,6 +4568,8 @@ hipError_t set_schedule(yk_model* m, int groups, int lanes) {
   for (auto& kv : m->graphs) (void)hipGraphExecDestroy(kv.second);
   m->graphs.clear();
   for (hipStream_t s : m->aux) (void)hipStreamDestroy(s);
+  if (m->cap) (void)hipStreamDestroy(m->cap);
+  m->cap = nullptr;
   for (hipEvent_t v : m->ev) (void)hipEventDestroy(v);
   m->aux.clear();
   m->ev.clear();
@@ -4751,6 +4754,7 @@ int yk_model_destroy(yk_model* m) {
   yk::DeviceGuard guard(m->ctx->device);
   for (auto& kv : m->graphs) (void)hipGraphExecDestroy(kv.second);
   for (hipStream_t s : m->aux) (void)hipStreamDestroy(s);
+  if (m->cap) (void)hipStreamDestroy(m->cap);
   for (hipEvent_t v : m->ev) (void)hipEventDestroy(v);
   if (m->arena) (void)hipFree(m->arena);
   void* ptrs[] = {m->blob, m->cand, m->cand_count, m->slot_of, m->gkeys, m->gbox, m->gflag, m->dets, m->counts, m->ktab,
@@ -4779,8 +4783,12 @@ int yk_detect_graph(yk_model* m, const uint8_t* frames, int batch, float conf, f
   auto key = std::make_tuple(batch, conf, iou, max_det, (const void*)frames, (void*)dets, (void*)counts);
   auto it = m->graphs.find(key);
   if (it == m->graphs.end()) {
-    hipStream_t cap;
-    YK_HIP(hipStreamCreateWithFlags(&cap, hipStreamNonBlocking));
+    // one capture stream per model, alive as long as the model and its graphs: round 4 created a
+    // stream per capture and destroyed it right after hipStreamEndCapture, and multi-lane graphs
+    // (forked onto m->aux) then crashed inside hipGraphLaunch once several models were alive
+    // (tools/graph_fork_repro.hip reproduces that pattern in pure HIP)
+    if (!m->cap) YK_HIP(hipStreamCreateWithFlags(&m->cap, hipStreamNonBlocking));
+    hipStream_t cap = m->cap;
     hipGraph_t g;
     const bool dbg = getenv("YK_DEBUG_GRAPH") != nullptr;
     YK_HIP(hipStreamBeginCapture(cap, hipStreamCaptureModeThreadLocal));
@@ -4789,7 +4797,6 @@ int yk_detect_graph(yk_model* m, const uint8_t* frames, int batch, float conf, f
     if (dbg) fprintf(stderr, "[yk] ops recorded rc=%d\n", rc);
     hipError_t ce = hipStreamEndCapture(cap, &g);
     if (dbg) fprintf(stderr, "[yk] capture ended: %s\n", hipGetErrorString(ce));
-    (void)hipStreamDestroy(cap);
     if (rc != YK_OK) return rc;
     if (ce != hipSuccess) {
       yk::set_error(std::string("yk_detect_graph: capture failed: ") + hipGetErrorString(ce));

@@ -126,6 +126,14 @@ __device__ __forceinline__ long long wave_sum_rows(int v) {
   return ((long long)__builtin_amdgcn_readlane(v, 0) + (long long)__builtin_amdgcn_readlane(v, 16)) +
          ((long long)__builtin_amdgcn_readlane(v, 32) + (long long)__builtin_amdgcn_readlane(v, 48));
 }
+// The same for per-lane values < 2^28 in magnitude (LK's b1 / b2: |diff| <= 8160, |D| <= 4080, 7
+// products per lane), whose 16-lane rows can leave int32: v = hi * 2^16 + lo with lo in [0, 2^16),
+// both halves summed exactly by wave_sum_rows, recombined in int64.
+__device__ __forceinline__ long long wave_sum_rows_wide(int v) {
+  const long long h = wave_sum_rows(v >> 16);
+  const long long l = wave_sum_rows(v & 0xffff);
+  return h * 65536 + l;
+}
 
 // ---------------------------------------------------------------- frame ingest
 __device__ __forceinline__ int gray_of(const unsigned char* p) {
@@ -731,13 +739,21 @@ __global__ void __launch_bounds__(256) lk_kernel(Dev g) {
         Iv[k] = (r0[x0] * w00 + r0[x1] * w01 + r1[x0] * w10 + r1[x1] * w11 + 256) >> 9;
         const bool ix0 = X >= 0 && X < cols, ix1 = X + 1 >= 0 && X + 1 < cols;
         const bool iy0 = Y >= 0 && Y < rows, iy1 = Y + 1 >= 0 && Y + 1 < rows;
-        const short2 z = make_short2(0, 0);
-        const short2 d00 = (iy0 && ix0) ? D[(long long)Y * cols + X] : z;
-        const short2 d01 = (iy0 && ix1) ? D[(long long)Y * cols + X + 1] : z;
-        const short2 d10 = (iy1 && ix0) ? D[(long long)(Y + 1) * cols + X] : z;
-        const short2 d11 = (iy1 && ix1) ? D[(long long)(Y + 1) * cols + X + 1] : z;
-        Dx[k] = (d00.x * w00 + d01.x * w01 + d10.x * w10 + d11.x * w11 + 8192) >> 14;
-        Dy[k] = (d00.y * w00 + d01.y * w01 + d10.y * w10 + d11.y * w11 + 8192) >> 14;
+        // (dx, dy) as one packed int32 load, 0 outside the level.  Round 4 wrote `cond ? D[i] : z`
+        // with a local short2 z: the compiler turned that into a select between &D[i] and the
+        // address of a stack copy of z, i.e. FLAT loads through a private-aperture pointer (8 bytes
+        // of scratch) -- the one scratch user of the motion chain, and the only place its results
+        // depended on what ran beside it (LK end points of border windows differing from the
+        // serial run while forwards with spilling conv kernels ran concurrently).  No scratch now.
+        const int* Dw = (const int*)D;
+        const int e00 = (iy0 && ix0) ? Dw[(long long)Y * cols + X] : 0;
+        const int e01 = (iy0 && ix1) ? Dw[(long long)Y * cols + X + 1] : 0;
+        const int e10 = (iy1 && ix0) ? Dw[(long long)(Y + 1) * cols + X] : 0;
+        const int e11 = (iy1 && ix1) ? Dw[(long long)(Y + 1) * cols + X + 1] : 0;
+        auto lo = [](int e) { return (int)(short)(e & 0xffff); };  // short2.x (little endian)
+        auto hi = [](int e) { return e >> 16; };                   // short2.y
+        Dx[k] = (lo(e00) * w00 + lo(e01) * w01 + lo(e10) * w10 + lo(e11) * w11 + 8192) >> 14;
+        Dy[k] = (hi(e00) * w00 + hi(e01) * w01 + hi(e10) * w10 + hi(e11) * w11 + 8192) >> 14;
         s11 += Dx[k] * Dx[k];
         s12 += Dx[k] * Dy[k];
         s22 += Dy[k] * Dy[k];
@@ -796,8 +812,8 @@ __global__ void __launch_bounds__(256) lk_kernel(Dev g) {
           }
         }
       }
-      const float fb1 = (float)wave_sum_rows(b1) * fs;
-      const float fb2 = (float)wave_sum_rows(b2) * fs;
+      const float fb1 = (float)wave_sum_rows_wide(b1) * fs;
+      const float fb2 = (float)wave_sum_rows_wide(b2) * fs;
       const float dx = (A12 * fb2 - A22 * fb1) * Di;
       const float dy = (A12 * fb1 - A11 * fb2) * Di;
       nx += dx;
@@ -831,9 +847,15 @@ __device__ __forceinline__ int rank_of(const float* v, int n, int i) {
 __global__ void __launch_bounds__(256) finish_kernel(Dev g, yk_motion* __restrict__ out) {
   __shared__ float vx[MAXC], vy[MAXC], sx[MAXC], sy[MAXC], dist[MAXC], sd[MAXC];
   __shared__ int wcnt[4];
+  __shared__ int hv[2];
   const int s = blockIdx.x, tid = threadIdx.x;
   State& S = g.st[s];
-  if (!S.has_prev) {  // first frame: only stored (:77-80)
+  if (tid == 0) {  // read once before thread 0 sets has_prev below: every wave takes the same branch
+    hv[0] = S.has_prev;
+    hv[1] = g.ncorners[s];
+  }
+  __syncthreads();
+  if (!hv[0]) {  // first frame: only stored (:77-80)
     if (tid == 0) {
       yk_motion r{};
       r.valid = 1;
@@ -845,7 +867,7 @@ __global__ void __launch_bounds__(256) finish_kernel(Dev g, yk_motion* __restric
     }
     return;
   }
-  const int n = g.ncorners[s];
+  const int n = hv[1];
   // status == 1 compaction in corner order (n <= 200 < 256 threads)
   int flag = 0;
   float mvx = 0.0f, mvy = 0.0f;
@@ -1055,10 +1077,18 @@ __global__ void __launch_bounds__(GT) gmc_kernel(Dev g, double* __restrict__ out
   double H[6] = {1.0, 0.0, 0.0, 0.0, 1.0, 0.0};
   int state = 0, npts = 0, max_good = 0, rit = 0, lit = 0;
   bool flip = true;
-  const bool have = S.has_prev && g.ncorners[s] > 0;  // gmc.py:306-311 (first frame / no previous keypoints)
+  // has_prev / ncorners read once, by one thread, before anything of this launch writes them: thread 0
+  // sets has_prev at the end, and every wave must take the same branch (the RANSAC / LM loops below are
+  // driven by LDS words only thread 0 writes)
+  if (tid == 0) {
+    misc[G_N] = S.has_prev;
+    misc[G_N + 1] = g.ncorners[s];
+  }
+  __syncthreads();
+  const bool have = misc[G_N] && misc[G_N + 1] > 0;  // gmc.py:306-311 (first frame / no previous keypoints)
   if (have) {
     // the points with status 1, in corner order (gmc.py:317-324)
-    const int n = g.ncorners[s];
+    const int n = misc[G_N + 1];
     int base = 0;
     for (int c0 = 0; c0 < n; c0 += GT) {
       const int i = c0 + tid;
@@ -1328,6 +1358,7 @@ __global__ void state_reset_kernel(Dev g, int stats_only) {
   State& S = g.st[s];
   if (!stats_only) {
     S.has_prev = 0;
+    g.ncorners[s] = 0;
     g.sel[s] = 0;
     S.mv_len = S.mv_head = 0;
     yk_motion r{};

@@ -2497,6 +2497,27 @@ int yk_tracker_download(yk_tracker* t, yk_track_out* host_rows, int32_t* host_co
   return YK_OK;
 }
 
+int yk_tracker_download_async(yk_tracker* t, yk_track_out* host_rows, int32_t* host_counts,
+                              yk_tracker_stats* host_stats, int rows_per_stream, void* stream) {
+  YK_CHECK_ARG(t && host_counts, "yk_tracker_download_async: NULL argument");
+  YK_CHECK_ARG(rows_per_stream >= 0 && rows_per_stream <= t->dev.T,
+               "yk_tracker_download_async: rows_per_stream out of [0, max_tracks]");
+  yk::DeviceGuard guard(t->ctx->device);
+  hipStream_t st = (hipStream_t)stream;
+  YK_HIP(hipMemcpyAsync(host_counts, t->dev.counts, t->S * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+  if (host_stats)
+    YK_HIP(hipMemcpyAsync(host_stats, t->dev.stats, t->S * sizeof(yk_tracker_stats), hipMemcpyDeviceToHost, st));
+  if (host_rows && rows_per_stream > 0) {
+    const size_t pitch = (size_t)t->dev.T * sizeof(yk_track_out);
+    if (rows_per_stream == t->dev.T)
+      YK_HIP(hipMemcpyAsync(host_rows, t->dev.rows, pitch * t->S, hipMemcpyDeviceToHost, st));
+    else
+      YK_HIP(hipMemcpy2DAsync(host_rows, pitch, t->dev.rows, pitch, rows_per_stream * sizeof(yk_track_out), t->S,
+                              hipMemcpyDeviceToHost, st));
+  }
+  return YK_OK;
+}
+
 int yk_tracker_snapshot(yk_tracker* t, int s, yk_track_state* host_states, int32_t* n_out, void* stream) {
   YK_CHECK_ARG(t && host_states && n_out, "yk_tracker_snapshot: NULL argument");
   YK_CHECK_ARG(s >= 0 && s < t->S, "yk_tracker_snapshot: stream index out of range");

@@ -183,21 +183,33 @@ class StreamPipeline:
         torch.cuda.synchronize(self.device)
 
     def run(self, frames: torch.Tensor):
-        """frames [S, H, W, 3] uint8 (device) -> one step.  The copy runs on the slot's detector
-        stream, after that slot's previous forward has read its frames, and after whatever the
-        caller's current stream enqueued before this call (the producer of `frames`)."""
+        """frames [S, H, W, 3] uint8 (device, or page-locked host memory: the frame in host memory
+        the driver loop starts from) -> one step.  The copy runs on the slot's detector stream,
+        after that slot's previous forward has read its frames, and after whatever the caller's
+        current stream enqueued before this call (the producer of `frames`); the forward that reads
+        the slot follows it on the same stream.  A host source must stay unchanged until that copy
+        has run (the caller's buffer; see download_async for the matching output side)."""
         s = self._slot(self._k)
         st = self._stream(s)
         cur = torch.cuda.current_stream(self.device)
         if st != cur:
             st.wait_stream(cur)
-            frames.record_stream(st)  # the allocator keeps `frames` alive until the copy ran
+            if frames.is_cuda:
+                frames.record_stream(st)  # the allocator keeps `frames` alive until the copy ran
         if self._gmd_pending[s]:  # the motion detector (tracker stream) still reads this slot's frames
             st.wait_event(self._ev_gmd[s])
             self._gmd_pending[s] = False
         with torch.cuda.stream(st):
             self.frame_slots[s].copy_(frames, non_blocking=True)
         self.step()
+
+    def download_async(self, rows, counts, stats, rows_per_stream=None):
+        """Enqueue the tracker output of the most recent step into page-locked host buffers
+        (rows [S * max_tracks] yk_track_out bytes, counts int32 [S], stats [S] yk_tracker_stats)
+        on the tracker stream, behind that step; no host wait.  The host reads them after
+        sync() (or an event recorded on the tracker stream after this call)."""
+        st = self.trk_stream if self.pipelined else torch.cuda.current_stream(self.device)
+        self.tracker.download_async(rows, counts, stats, rows_per_stream, stream=st.cuda_stream)
 
     def download(self):
         """Tracker results of the most recent step (rows, counts, stats; host arrays).  Waits for

@@ -299,6 +299,23 @@ class MultiStreamTracker:
                                             L.ptr(self.host_stats), st), "yk_tracker_download")
         return self.host_rows, self.host_counts, self.host_stats
 
+    def download_async(self, rows: torch.Tensor, counts: torch.Tensor, stats: torch.Tensor | None = None,
+                       rows_per_stream: int | None = None, stream=None):
+        """Enqueue counts, stats and the first rows_per_stream (default: every) rows of each stream
+        into page-locked host tensors (yk_tracker_download_async); nothing waits."""
+        S, T = self.n_streams, self.max_tracks
+        if not (rows.is_pinned() and counts.is_pinned() and (stats is None or stats.is_pinned())):
+            raise ValueError("download_async needs page-locked host tensors")
+        if rows.numel() * rows.element_size() < S * T * L.TRACK_OUT_DTYPE.itemsize or counts.numel() < S:
+            raise ValueError("download_async: host buffers too small")
+        if stats is not None and stats.numel() * stats.element_size() < S * L.STATS_DTYPE.itemsize:
+            raise ValueError("download_async: stats buffer too small")
+        n = T if rows_per_stream is None else int(rows_per_stream)
+        st = L.current_stream(self.device) if stream is None else C.c_void_p(stream)
+        L.check(L.lib().yk_tracker_download_async(self._h, C.c_void_p(rows.data_ptr()), C.c_void_p(counts.data_ptr()),
+                                                  C.c_void_p(stats.data_ptr() if stats is not None else 0), n, st),
+                "yk_tracker_download_async")
+
     def device_outputs(self):
         rows, counts, stats = C.c_void_p(), C.c_void_p(), C.c_void_p()
         L.check(L.lib().yk_tracker_outputs(self._h, C.byref(rows), C.byref(counts), C.byref(stats)),
