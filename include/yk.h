@@ -306,14 +306,6 @@ int yk_gmd_set_thresholds(yk_gmd* g, double global_motion_threshold, double rese
  * `stream`. */
 int yk_gmd_detect(yk_gmd* g, const uint8_t* dev_frames, yk_motion* dev_motion, void* stream);
 int yk_gmd_outputs(yk_gmd* g, yk_motion** dev_motion);
-/* Diagnostics: device addresses of the last call's corners (float x, y [S][max_corners]), LK end
- * points (float x, y [S][max_corners]), status (uint8 [S][max_corners]) and corner counts
- * (int32 [S]), so a harness can copy them in stream order (tools/gmd_step_diff.py). */
-int yk_gmd_debug_buffers(yk_gmd* g, void** dev_corners, void** dev_next, void** dev_status, int32_t** dev_ncorners,
-                         int32_t* max_corners);
-/* Diagnostics: the two gray-pyramid buffers (uint8 [S][per]) and Scharr-derivative buffers (int16 x, y
- * [S][per]) the calls alternate between; per = pixels of every level of one stream. */
-int yk_gmd_debug_pyramids(yk_gmd* g, void** dev_pyr0, void** dev_pyr1, void** dev_der0, void** dev_der1, int64_t* per);
 /* Copy the last results (and stats when host_stats != NULL) to the host; synchronous. */
 int yk_gmd_download(yk_gmd* g, yk_motion* host_motion, yk_gmd_stats* host_stats, void* stream);
 /* Diagnostics for parity tests: stream s's last corners (x, y), LK end points (x, y) and status
@@ -403,7 +395,8 @@ int yk_bt_download(yk_bt* bt, float* host_rows, int32_t* host_counts, void* stre
  * (utils/ops.py:105-184).  The host builds the program (parse_model rules + weight
  * packing, see arch.py / model.py); the library executes it.
  */
-enum yk_act_dtype { YK_ACT_BF16 = 0, YK_ACT_F32 = 1, YK_ACT_FP8 = 2 };  /* FP8: OCP e4m3 activations + weights */
+/* FP8: OCP e4m3 activations + weights; F16: IEEE binary16 (predict(half=True), nn/autobackend.py:215) */
+enum yk_act_dtype { YK_ACT_BF16 = 0, YK_ACT_F32 = 1, YK_ACT_FP8 = 2, YK_ACT_F16 = 3 };
 enum yk_op_kind {
   YK_K_CONV_INPUT = 0, /* first conv, reads uint8 BGR frames (fused letterbox/RGB//255)    */
   YK_K_CONV = 1,       /* implicit-GEMM conv (+bias, SiLU, residual, concat/upsample read)   */

@@ -9,10 +9,11 @@ import pytest
 from conftest import REPO, pkg
 
 HEADER = os.path.join(REPO, "include", "yk.h")
+DIAG_HEADER = os.path.join(REPO, "include", "yk_diag.h")
 
 
-def declared_functions():
-    src = open(HEADER).read()
+def declared_functions(path=HEADER):
+    src = open(path).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     names = re.findall(r"^\s*(?:const\s+)?[A-Za-z_][A-Za-z0-9_]*\s*\*?\s+\*?(yk_[a-z0-9_]+)\s*\(", src, flags=re.M)
     return sorted(set(names))
@@ -29,10 +30,18 @@ def test_library_exports_every_declared_symbol():
 
     lib_mod = import_module(pkg().__name__ + "._lib")
     lib = lib_mod.lib()  # loads libyk.so (raises if missing)
-    for n in declared_functions():
+    for n in declared_functions() + declared_functions(DIAG_HEADER):
         assert hasattr(lib, n), f"libyk.so does not export {n}"
     # the python binding covers every declared function too
     assert set(declared_functions()) <= set(lib_mod.exported_symbols())
+
+
+def test_diagnostics_stay_out_of_the_product_header():
+    """yk_gmd_debug_* (stream-order copies of the motion detector's internals for parity tools)
+    live in yk_diag.h, not in the boundary header (VERDICT r4 hygiene)."""
+    diag = declared_functions(DIAG_HEADER)
+    assert {"yk_gmd_debug_buffers", "yk_gmd_debug_pyramids"} <= set(diag)
+    assert not set(diag) & set(declared_functions())
 
 
 def test_struct_sizes_match_python_mirrors():

@@ -139,6 +139,27 @@ def test_bf16_detections_close_to_oracle(scale):
         assert float((best > 0.5).float().mean()) >= 0.9
 
 
+@pytest.mark.parametrize("scale", ["s", "n"])
+def test_fp16_detections_close_to_oracle(scale):
+    """fp16 build (predict(half=True): the reference's model.half()): binary16 weights and
+    activations on the f16 MFMA.  binary16 keeps 11 significant bits (bf16: 8), so the bar is
+    tighter than bf16's: the same count within 10 % and 95 % of the oracle's boxes matched at
+    IoU > 0.5; every layer within 2e-2 of the fp32 oracle (max-normalised)."""
+    s = setup(scale=scale, dtype="fp16")
+    for layer in (0, 2, 9, 15, 21):
+        e = rel_err(s["dm"].layer_nchw(layer, s["B"]), s["ref"].outputs[layer])
+        assert e < 2e-2, (layer, e)
+    for b in range(s["B"]):
+        ref = s["res"][b]
+        n = int(s["counts"][b])
+        ours = s["dets"][b, :n]
+        assert abs(n - len(ref)) <= max(2, int(0.10 * len(ref)))
+        if len(ref) == 0:
+            continue
+        iou = _box_iou(ref[:, :4], ours[:, :4])
+        assert float((iou.max(1).values > 0.5).float().mean()) >= 0.95
+
+
 def test_fp32_scale_n_and_padded_frame():
     """LetterBox padding path: a 640x500 frame is centred with 6 rows of 114 top and bottom."""
     s = setup(scale="n", dtype="fp32", frame_hw=(500, 640), K=12)

@@ -122,3 +122,16 @@ def test_gmc_reset_params_then_apply():
             continue
         assert int(dev.info()[0][4]) == 1, (f, dev.info())
         np.testing.assert_allclose(H, Hr, rtol=1e-9, atol=1e-9, err_msg=f"frame {f} after reset: warp")
+
+
+def test_gmc_odd_frame_size_falls_back_to_identity():
+    """An odd frame (1242x375, KITTI-like) is outside the restated exact-1/2 downscale: GMC returns
+    the identity with one RuntimeWarning instead of failing, every frame."""
+    P = pkg()
+    dev = _gmc(P)
+    rng = np.random.default_rng(0)
+    fr = rng.integers(0, 255, (375, 1242, 3), dtype=np.uint8)
+    with pytest.warns(RuntimeWarning, match="not even"):
+        H = dev.apply(fr)
+    np.testing.assert_array_equal(H, np.eye(2, 3))
+    np.testing.assert_array_equal(dev.apply(np.roll(fr, 3, axis=1)), np.eye(2, 3))

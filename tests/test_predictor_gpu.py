@@ -35,6 +35,16 @@ def _close(r, ref):
     np.testing.assert_allclose(got[:, 4], ref[:, 4].numpy(), rtol=1e-4, atol=1e-6)
 
 
+def _iou_np(a, b):
+    lt = np.maximum(a[:, None, :2], b[None, :, :2])
+    rb = np.minimum(a[:, None, 2:4], b[None, :, 2:4])
+    wh = np.clip(rb - lt, 0, None)
+    inter = wh[..., 0] * wh[..., 1]
+    aa = (a[:, 2] - a[:, 0]) * (a[:, 3] - a[:, 1])
+    ab = (b[:, 2] - b[:, 0]) * (b[:, 3] - b[:, 1])
+    return inter / (aa[:, None] + ab[None] - inter)
+
+
 def test_predict_kwargs_match_oracle():
     P = pkg()
     model = P.YOLO("yolov8s-small.yaml", dtype="fp32")
@@ -52,8 +62,16 @@ def test_predict_kwargs_match_oracle():
     # classes= filters before NMS (nms.py:128-132): single-class head -> all or nothing
     assert len(model(frames[0], classes=[0])[0].boxes) == len(model(frames[0])[0].boxes) > 0
     assert len(model(frames[0], classes=[1])[0].boxes) == 0
-    with pytest.raises(NotImplementedError):
-        model(frames[0], half=True)
+    # half=True: the fp16 build (AutoBackend(fp16=True) -> model.half()), its own engine; the
+    # detections agree with the fp32 ones to fp16 rounding
+    rh = model(frames, half=True, verbose=False)
+    assert any(k[-1] == "fp16" for k in model._engines)
+    for r16, r32 in zip(rh, model(frames, verbose=False)):
+        a, b = r16.boxes.data.cpu().numpy(), r32.boxes.data.cpu().numpy()
+        assert abs(len(a) - len(b)) <= max(2, len(b) // 10)
+        if len(b):
+            iou = _iou_np(b[:, :4], a[:, :4])
+            assert (iou.max(1) > 0.5).mean() >= 0.95
     with pytest.raises(AssertionError):
         model(frames[0], conf=1.5)
 

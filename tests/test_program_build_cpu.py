@@ -26,7 +26,8 @@ def _build_c(L, sd, scale, dtype, fh, fw, imgsz, max_batch):
 
 @pytest.mark.parametrize("scale,dtype,hw,imgsz", [("s", "fp32", (512, 640), 640), ("n", "fp32", (512, 640), 640),
                                                   ("s", "bf16", (500, 640), 640), ("s", "fp8", (1024, 1280), 1280),
-                                                  ("n", "bf16", (480, 720), 640), ("s", "fp32", (1024, 1280), 640)])
+                                                  ("n", "bf16", (480, 720), 640), ("s", "fp32", (1024, 1280), 640),
+                                                  ("s", "fp16", (512, 640), 640)])
 def test_program_build_matches_python_program(scale, dtype, hw, imgsz):
     P = pkg()
     import importlib

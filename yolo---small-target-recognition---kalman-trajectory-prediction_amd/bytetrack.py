@@ -192,6 +192,18 @@ class GMC:
             return self.identity.data_ptr()
         f = self._frames_device(frames)
         hw = (int(f.shape[1]), int(f.shape[2]))
+        if hw[0] % 2 or hw[1] % 2 or min(hw) < 64:
+            # the device GMC restates cv2.resize's exact-1/2 INTER_AREA fast path only; an odd or tiny
+            # frame (e.g. 1242x375) would take cv2's general INTER_LINEAR path, not restated here.
+            # Like the reference's identity fallbacks (gmc.py:155-158, 297-311) the warp is then the identity,
+            # with one warning, instead of failing the whole track() call.
+            if not getattr(self, "_warned_size", False):
+                import warnings
+
+                warnings.warn(f"GMC sparseOptFlow: frame size {hw[1]}x{hw[0]} is not even and >= 64; "
+                              "using the identity warp for this stream", RuntimeWarning, stacklevel=2)
+                self._warned_size = True
+            return self.identity.data_ptr()
         if self._h is None or self._hw != hw:
             if self._h is not None:
                 L.lib().yk_gmd_destroy(self._h)

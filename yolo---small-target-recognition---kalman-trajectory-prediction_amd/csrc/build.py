@@ -39,7 +39,7 @@ SOURCES = [
     ("bytetrack.hip", ["-ffp-contract=off"]),
     ("gmd.hip", ["-ffp-contract=off"]),
 ]
-HEADERS = ["yk_internal.h", os.path.join("..", "..", "include", "yk.h")]
+HEADERS = ["yk_internal.h", os.path.join("..", "..", "include", "yk.h"), os.path.join("..", "..", "include", "yk_diag.h")]
 
 
 def _hipcc() -> str:

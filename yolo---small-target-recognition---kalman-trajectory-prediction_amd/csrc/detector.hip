@@ -53,6 +53,7 @@ namespace yk {
 namespace det {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 // Workgroup -> (pixel tile, channel group), XCD-aware.  The dispatcher deals workgroups (linear id,
@@ -87,6 +88,16 @@ __device__ __forceinline__ unsigned short f2bf(float f) {
 struct BF16 {
   using T = unsigned short;
   static constexpr int EPL = 8;  // k elements per lane per K-step (16x16x32: 4 groups x 8)
+  static constexpr bool kExact = false;
+  static constexpr bool kScaled = false;
+  static constexpr bool kSplit = false;
+};
+// fp16 twin of BF16 (predict(half=True): the reference's model.half(), nn/autobackend.py:215):
+// IEEE binary16 weights and activations on v_mfma_f32_16x16x32_f16 (the bf16 rate on gfx950),
+// fp32 accumulation, the same layouts, tables and kernels.
+struct F16 {
+  using T = _Float16;
+  static constexpr int EPL = 8;
   static constexpr bool kExact = false;
   static constexpr bool kScaled = false;
   static constexpr bool kSplit = false;
@@ -155,6 +166,10 @@ template <>
 __device__ __forceinline__ f32x4 mma<BF16>(const uint4& w, const uint4& x, f32x4 acc) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, w), __builtin_bit_cast(bf16x8, x),
                                                  acc, 0, 0, 0);
+}
+template <>
+__device__ __forceinline__ f32x4 mma<F16>(const uint4& w, const uint4& x, f32x4 acc) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, w), __builtin_bit_cast(f16x8, x), acc, 0, 0, 0);
 }
 template <>
 __device__ __forceinline__ f32x4 mma<FP8>(const uint4& w, const uint4& x, f32x4 acc) {
@@ -291,6 +306,18 @@ __device__ __forceinline__ void store4(unsigned short* p, const float v[4]) {
   *(uint2*)p = o;
 }
 __device__ __forceinline__ void store4(float* p, const float v[4]) { *(float4*)p = make_float4(v[0], v[1], v[2], v[3]); }
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+// f32 -> f16 round-to-nearest-even (v_cvt_f16_f32), overflow to +-inf like torch's .half()
+__device__ __forceinline__ void store4(_Float16* p, const float v[4]) {
+  *(f16x4*)p = f16x4{(_Float16)v[0], (_Float16)v[1], (_Float16)v[2], (_Float16)v[3]};
+}
+__device__ __forceinline__ void load4(const _Float16* p, float v[4]) {
+  const f16x4 h = *(const f16x4*)p;
+  v[0] = (float)h[0];
+  v[1] = (float)h[1];
+  v[2] = (float)h[2];
+  v[3] = (float)h[3];
+}
 // f32 -> e4m3 with round-to-nearest-even (v_cvt_pk_fp8_f32), saturated to the finite range
 __device__ __forceinline__ float sat448(float v) { return __builtin_amdgcn_fmed3f(v, -448.f, 448.f); }
 __device__ __forceinline__ void store4(unsigned char* p, const float v[4]) {
@@ -2154,14 +2181,17 @@ __global__ void __launch_bounds__(256) conv_input_mfma_kernel(InputArgs a) {
     xs[2][ry][rx] = v2;
   }
   __syncthreads();
-  // A fragments: rows = output channels nt*16 + col, K = kg*8 + e (k = c*9 + ky*3 + kx)
-  bf16x8 wa[2];
+  // A fragments: rows = output channels nt*16 + col, K = kg*8 + e (k = c*9 + ky*3 + kx); the
+  // fp16 build rounds them to binary16 and runs the f16 MFMA (uint8 values are exact in both)
+  using E = std::conditional_t<std::is_same<Tr, F16>::value, _Float16, __bf16>;
+  typedef E e8 __attribute__((ext_vector_type(8)));
+  e8 wa[2];
   int xoff[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     const int k = kg * 8 + e;
-    wa[0][e] = (__bf16)(k < 27 ? ws[col * 27 + k] : 0.f);
-    wa[1][e] = (__bf16)(k < 27 ? ws[(16 + col) * 27 + k] : 0.f);
+    wa[0][e] = (E)(k < 27 ? ws[col * 27 + k] : 0.f);
+    wa[1][e] = (E)(k < 27 ? ws[(16 + col) * 27 + k] : 0.f);
     const int c = k / 9, tap = k - c * 9, ky = tap / 3, kx = tap - ky * 3;
     xoff[e] = k < 27 ? (c * TI + ky) * TP + col * s + kx : -1;
   }
@@ -2170,11 +2200,16 @@ __global__ void __launch_bounds__(256) conv_input_mfma_kernel(InputArgs a) {
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int roff = (wave * 4 + r) * s * TP;
-    bf16x8 xb;
+    e8 xb;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) xb[e] = (__bf16)(xoff[e] >= 0 ? xsf[xoff[e] + roff] : 0.f);
-    acc[0][r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[0], xb, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-    acc[1][r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[1], xb, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+    for (int e = 0; e < 8; ++e) xb[e] = (E)(xoff[e] >= 0 ? xsf[xoff[e] + roff] : 0.f);
+    if constexpr (std::is_same<Tr, F16>::value) {
+      acc[0][r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wa[0], xb, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      acc[1][r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wa[1], xb, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+    } else {
+      acc[0][r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[0], xb, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      acc[1][r] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[1], xb, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+    }
   }
   const int ox = tx0 + col;
 #pragma unroll
@@ -3196,10 +3231,12 @@ struct yk_model {
 
 namespace {
 
-int esz_of(int dtype) { return dtype == YK_ACT_F32 ? 4 : dtype == YK_ACT_FP8 ? 1 : 2; }
+int esz_of(int dtype) { return dtype == YK_ACT_F32 ? 4 : dtype == YK_ACT_FP8 ? 1 : 2; }  // BF16 / F16: 2
 size_t act_bytes(const yk_model* m) { return (size_t)esz_of(m->desc.act_dtype); }
 // trait name as rocprofv3 demangles it
-const char* tr_name(int dtype) { return dtype == YK_ACT_F32 ? "F32" : dtype == YK_ACT_FP8 ? "FP8" : "BF16"; }
+const char* tr_name(int dtype) {
+  return dtype == YK_ACT_F32 ? "F32" : dtype == YK_ACT_FP8 ? "FP8" : dtype == YK_ACT_F16 ? "F16" : "BF16";
+}
 
 // Base of image b0 of a buffer whose per-image extent is h x w x c_stride elements.
 void* img_ptr(const yk_model* m, int buf, int h, int w, int cstride, int b0) {
@@ -3438,13 +3475,18 @@ void set_tile_attrs() {
   set_halo_attr_n<1>();
   set_halo_attr_n<2>();
   set_tile_attrs_t<BF16>();
+  set_tile_attrs_t<F16>();
   set_tile_attrs_t<F32>();
   set_wide_attr_n<BF16, 2>();
   set_wide_attr_n<BF16, 4>();
+  set_wide_attr_n<F16, 2>();
+  set_wide_attr_n<F16, 4>();
   set_wide_attr_n<F32, 2>();
   set_wide_attr_n<F32, 4>();
   set_fast_attr_w<BF16, false>();
   set_fast_attr_w<BF16, true>();
+  set_fast_attr_w<F16, false>();
+  set_fast_attr_w<F16, true>();
   set_fast_attr_w<F32, false>();
   set_fast_attr_w<F32, true>();
   set_fast_attr_w<F32S, false>();
@@ -3455,6 +3497,8 @@ void set_tile_attrs() {
   set_fast_attr_w<FP8, true>();
   (void)hipFuncSetAttribute((const void*)sppf_lds_kernel<FP8, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, kSppfLdsBytes);
   (void)hipFuncSetAttribute((const void*)sppf_lds_kernel<BF16, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, kSppfLdsBytes);
+  (void)hipFuncSetAttribute((const void*)sppf_lds_kernel<F16, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, kSppfLdsBytes);
+  (void)hipFuncSetAttribute((const void*)sppf_lds_kernel<F16, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, kSppfLdsBytes);
   (void)hipFuncSetAttribute((const void*)sppf_lds_kernel<F32, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, kSppfLdsBytes);
   (void)hipFuncSetAttribute((const void*)sppf_lds_kernel<FP8, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, kSppfLdsBytes);
   (void)hipFuncSetAttribute((const void*)sppf_lds_kernel<BF16, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, kSppfLdsBytes);
@@ -4104,6 +4148,7 @@ int launch_any(yk_model* m, const yk_op& op, const uint8_t* frames, int B, float
   switch (m->desc.act_dtype) {
     case YK_ACT_F32: return launch_op<F32>(m, op, frames, B, conf, st);
     case YK_ACT_FP8: return launch_op<FP8>(m, op, frames, B, conf, st);
+    case YK_ACT_F16: return launch_op<F16>(m, op, frames, B, conf, st);
     default: return launch_op<BF16>(m, op, frames, B, conf, st);
   }
 }
@@ -4336,6 +4381,7 @@ int detect_impl(yk_model* m, const uint8_t* frames, int B, float conf, float iou
   frames = input_frames(m, frames, B, st);
   int rc = D.act_dtype == YK_ACT_F32   ? run_dag<F32>(m, frames, B, conf, st)
            : D.act_dtype == YK_ACT_FP8 ? run_dag<FP8>(m, frames, B, conf, st)
+           : D.act_dtype == YK_ACT_F16 ? run_dag<F16>(m, frames, B, conf, st)
                                        : run_dag<BF16>(m, frames, B, conf, st);
   if (rc != YK_OK) return rc;
   return launch_nms(m, B, iou, max_det, dets, counts, st);
@@ -4601,7 +4647,8 @@ int yk_model_create(yk_ctx* ctx, const yk_model_desc* desc, const void* host_blo
   YK_CHECK_ARG(desc->max_batch >= 1 && desc->n_anchors > 0 && desc->max_det >= 1, "yk_model_create: bad sizes");
   YK_CHECK_ARG(desc->nc == 1, "yk_model_create: only single-class detection heads are supported");
   YK_CHECK_ARG(desc->max_det <= 2048, "yk_model_create: max_det must be <= 2048");
-  YK_CHECK_ARG(desc->act_dtype == YK_ACT_BF16 || desc->act_dtype == YK_ACT_F32 || desc->act_dtype == YK_ACT_FP8,
+  YK_CHECK_ARG(desc->act_dtype == YK_ACT_BF16 || desc->act_dtype == YK_ACT_F32 || desc->act_dtype == YK_ACT_FP8 ||
+                   desc->act_dtype == YK_ACT_F16,
                "yk_model_create: bad act dtype");
   for (int i = 0; i < desc->n_ops; ++i) {
     const yk_op& op = desc->ops[i];

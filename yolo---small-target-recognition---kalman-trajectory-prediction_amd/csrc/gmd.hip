@@ -40,6 +40,15 @@
 #include <climits>
 
 #include "yk_internal.h"
+#include "yk_diag.h"
+
+// Diagnostic builds (csrc/build.py YK_DEFINES="-DYK_GMD_DIAG=<mask>"; the product is 0):
+//     1  lk_kernel window sums through LDS (no DPP row sums, no v_readlane)
+//     2  system-scope release at the end of the pyramid / derivative producers, acquire at
+//        the start of lk_kernel
+#ifndef YK_GMD_DIAG
+#define YK_GMD_DIAG 0
+#endif
 
 namespace yk {
 namespace gmd {
@@ -126,6 +135,18 @@ __device__ __forceinline__ long long wave_sum_rows(int v) {
   return ((long long)__builtin_amdgcn_readlane(v, 0) + (long long)__builtin_amdgcn_readlane(v, 16)) +
          ((long long)__builtin_amdgcn_readlane(v, 32) + (long long)__builtin_amdgcn_readlane(v, 48));
 }
+// Diagnostic twin of wave_sum_rows: the wave's 64 values through the wave's own LDS row, every
+// lane adding all of them in int64 (no DPP, no cross-lane register reads).
+__device__ __forceinline__ long long wave_sum_lds(int v, int* row) {
+  const int lane = threadIdx.x & 63;
+  row[lane] = v;
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+  __builtin_amdgcn_wave_barrier();
+  long long t = 0;
+  for (int i = 0; i < 64; ++i) t += row[i];
+  __builtin_amdgcn_wave_barrier();
+  return t;
+}
 // The same for per-lane values < 2^28 in magnitude (LK's b1 / b2: |diff| <= 8160, |D| <= 4080, 7
 // products per lane), whose 16-lane rows can leave int32: v = hi * 2^16 + lo with lo in [0, 2^16),
 // both halves summed exactly by wave_sum_rows, recombined in int64.
@@ -146,6 +167,7 @@ __global__ void __launch_bounds__(256) gray_kernel(Dev g, const unsigned char* _
   if (i >= n) return;
   const unsigned char* p = frames + ((long long)s * n + i) * 3;
   g.pyr[cur][(long long)s * g.geo.per + i] = (unsigned char)gray_of(p);
+  if (YK_GMD_DIAG & 2) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
 }
 
 // GMC: cvtColor(BGR2GRAY) then cv2.resize(gray, (W / 2, H / 2)): INTER_LINEAR at an exact 1/2
@@ -162,6 +184,7 @@ __global__ void __launch_bounds__(256) gray_down_kernel(Dev g, const unsigned ch
   const unsigned char* r1 = r0 + (long long)W0 * 3;
   const int v = gray_of(r0) + gray_of(r0 + 3) + gray_of(r1) + gray_of(r1 + 3);
   g.pyr[cur][(long long)s * g.geo.per + i] = (unsigned char)((v + 2) >> 2);
+  if (YK_GMD_DIAG & 2) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
 }
 
 __global__ void __launch_bounds__(256) pyrdown_kernel(Dev g, int l) {
@@ -184,6 +207,7 @@ __global__ void __launch_bounds__(256) pyrdown_kernel(Dev g, int l) {
     acc += k[i] * r;
   }
   g.pyr[cur][(long long)s * g.geo.per + g.geo.loff[l] + (long long)y * dw + x] = (unsigned char)((acc + 128) >> 8);
+  if (YK_GMD_DIAG & 2) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
 }
 
 // calcSharrDeriv: vertical [3 10 3] / [-1 0 1], then horizontal [-1 0 1] / [3 10 3], reflect-101.
@@ -205,6 +229,7 @@ __global__ void __launch_bounds__(256) scharr_kernel(Dev g) {
   const int dx = t0(xp) - t0(xm);
   const int dy = (t1(xp) + t1(xm)) * 3 + t1(x) * 10;
   g.der[cur][base + (long long)y * w + x] = make_short2((short)dx, (short)dy);
+  if (YK_GMD_DIAG & 2) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
 }
 
 // ---------------------------------------------------------------- goodFeaturesToTrack
@@ -684,6 +709,11 @@ __device__ __forceinline__ void lk_weights(float a, float b, int& w00, int& w01,
 __global__ void __launch_bounds__(256) lk_kernel(Dev g) {
   const int s = blockIdx.y, lane = threadIdx.x & 63;
   const int p = blockIdx.x * 4 + (threadIdx.x >> 6);
+  __shared__ int red_lds[(YK_GMD_DIAG & 1) ? 4 : 1][64];
+  int* red = red_lds[(YK_GMD_DIAG & 1) ? (threadIdx.x >> 6) : 0];
+  if (YK_GMD_DIAG & 2) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  auto wsum = [&](int v) { return (YK_GMD_DIAG & 1) ? wave_sum_lds(v, red) : wave_sum_rows(v); };
+  auto wsum_wide = [&](int v) { return (YK_GMD_DIAG & 1) ? wave_sum_lds(v, red) : wave_sum_rows_wide(v); };
   if (p >= g.ncorners[s]) return;
   const int prev = g.sel[s], cur = prev ^ 1;
   const Geo& G = g.geo;
@@ -760,9 +790,9 @@ __global__ void __launch_bounds__(256) lk_kernel(Dev g) {
       }
     }
     // |Dx|, |Dy| <= 4080 (Scharr of 8-bit pixels): a lane's 7 products < 2^27, a row's 16 < 2^31
-    const float A11 = (float)wave_sum_rows(s11) * fs;
-    const float A12 = (float)wave_sum_rows(s12) * fs;
-    const float A22 = (float)wave_sum_rows(s22) * fs;
+    const float A11 = (float)wsum(s11) * fs;
+    const float A12 = (float)wsum(s12) * fs;
+    const float A22 = (float)wsum(s22) * fs;
     const float Dd = A11 * A22 - A12 * A12;
     const float dd = A11 - A22;
     const float mine = ((A22 + A11) - sqrtf(dd * dd + (4.0f * A12) * A12)) / (float)(2 * WIN * WIN);
@@ -812,8 +842,8 @@ __global__ void __launch_bounds__(256) lk_kernel(Dev g) {
           }
         }
       }
-      const float fb1 = (float)wave_sum_rows_wide(b1) * fs;
-      const float fb2 = (float)wave_sum_rows_wide(b2) * fs;
+      const float fb1 = (float)wsum_wide(b1) * fs;
+      const float fb2 = (float)wsum_wide(b2) * fs;
       const float dx = (A12 * fb2 - A22 * fb1) * Di;
       const float dy = (A12 * fb1 - A11 * fb2) * Di;
       nx += dx;

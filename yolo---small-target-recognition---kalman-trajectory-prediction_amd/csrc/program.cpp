@@ -365,6 +365,12 @@ struct Builder {
         const uint16_t h = f2bf(ord[j]);
         memcpy(&P.packed[2 * j], &h, 2);
       }
+    } else if (dtype == YK_ACT_F16) {  // torch .half(): IEEE binary16, round to nearest even
+      P.packed.resize(nel * 2);
+      for (size_t j = 0; j < nel; ++j) {
+        const _Float16 h = (_Float16)ord[j];
+        memcpy(&P.packed[2 * j], &h, 2);
+      }
     } else {
       P.packed.resize(nel * 4);
       memcpy(P.packed.data(), ord.data(), nel * 4);
@@ -644,8 +650,8 @@ extern "C" {
 int yk_program_build(const yk_weights* weights, char scale, int act_dtype, int frame_h, int frame_w, int imgsz,
                      int max_batch, int max_det, yk_program** out) {
   YK_CHECK_ARG(weights && out && (weights->n == 0 || weights->tensors), "yk_program_build: NULL argument");
-  YK_CHECK_ARG(act_dtype == YK_ACT_BF16 || act_dtype == YK_ACT_F32 || act_dtype == YK_ACT_FP8,
-               "yk_program_build: act_dtype must be YK_ACT_BF16, YK_ACT_F32 or YK_ACT_FP8");
+  YK_CHECK_ARG(act_dtype == YK_ACT_BF16 || act_dtype == YK_ACT_F32 || act_dtype == YK_ACT_FP8 || act_dtype == YK_ACT_F16,
+               "yk_program_build: act_dtype must be YK_ACT_BF16, YK_ACT_F32, YK_ACT_FP8 or YK_ACT_F16");
   YK_CHECK_ARG(frame_h > 0 && frame_w > 0 && imgsz >= 32 && imgsz % 32 == 0 && max_batch >= 1 && max_det >= 1,
                "yk_program_build: bad frame size, imgsz (a multiple of 32), max_batch or max_det");
   *out = nullptr;

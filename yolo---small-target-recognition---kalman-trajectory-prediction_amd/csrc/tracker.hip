@@ -63,7 +63,8 @@ struct Slot {
   double th[TH][2];
   int age, hits, hit_streak, tsu, is_lost, lost_frames, track_num, max_lost;
   int vh_len, vh_head, th_len, th_head;
-  int th_cnt;  // trajectory points appended since creation (+2^20 at a history reset): yk_track_out.traj_count
+  unsigned th_cnt;  // trajectory points appended since creation (+2^20 at a history reset), mod 2^32:
+                    // yk_track_out.traj_count (unsigned: a long-lived track's count wraps, defined)
   // YK_POLICY_MOTION_RESET (MotionResetKalmanTracker, motion_reset_kalman_tracker.py:28-65)
   int policy;
   int reset_count, last_reset;  // last_reset_frame: -999 at creation
@@ -92,7 +93,7 @@ struct LSlot {
   double (*th)[2];
   int age, hits, hit_streak, tsu, is_lost, lost_frames, track_num, max_lost;
   int vh_len, vh_head, th_len, th_head;
-  int th_cnt;
+  unsigned th_cnt;
   int policy;
 };
 
@@ -848,7 +849,7 @@ __device__ void track_info(S& s, yk_track_out& o, bool copy_traj = true) {
   }
   const int nt = s.th_len < TOUT ? s.th_len : TOUT;
   o.traj_len = nt;
-  o.traj_count = s.th_cnt;
+  o.traj_count = (int32_t)s.th_cnt;  // two's-complement view of the mod-2^32 count
   o.reserved = 0;
   if (!copy_traj) return;  // the step kernel copies trajectories cooperatively
   int idx = s.th_head + (s.th_len - nt);

@@ -31,8 +31,8 @@ from . import letterbox as LB
 from . import weights as Wt
 
 YK_K_CONV_INPUT, YK_K_CONV, YK_K_SPPF_POOL, YK_K_DETECT = range(4)
-ACT = {"bf16": 0, "fp32": 1, "fp8": 2}
-ESZ = {"bf16": 2, "fp32": 4, "fp8": 1}
+ACT = {"bf16": 0, "fp32": 1, "fp8": 2, "fp16": 3}
+ESZ = {"bf16": 2, "fp32": 4, "fp8": 1, "fp16": 2}
 
 
 def phys(c: int, align: int = 8) -> int:
@@ -94,6 +94,11 @@ def letterbox_geometry(frame_h, frame_w, imgsz=640, stride=32):
 def _bf16_bits(a: np.ndarray) -> np.ndarray:
     """float32 -> bfloat16 bit patterns, round-to-nearest-even (torch's conversion)."""
     return torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32)).to(torch.bfloat16).view(torch.int16).numpy()
+
+
+def _f16_bits(a: np.ndarray) -> np.ndarray:
+    """float32 -> IEEE binary16 bits, round to nearest even (torch's .half())."""
+    return np.ascontiguousarray(a, dtype=np.float32).astype(np.float16).view(np.int16)
 
 
 def _fp8_bits(a: np.ndarray) -> np.ndarray:
@@ -203,7 +208,7 @@ class Program:
             packed = _fp8_bits(P)
             bias = np.concatenate([bias, dq])
         else:
-            packed = _bf16_bits(P) if self.dtype == "bf16" else P
+            packed = _bf16_bits(P) if self.dtype == "bf16" else _f16_bits(P) if self.dtype == "fp16" else P
         tab = []
         pad = k // 2
         for q in range(K // 8):
@@ -669,6 +674,10 @@ class DeviceModel:
             raw = np.zeros(n, np.int16)
             _memcpy_d2h(raw, ptr.value)
             out = torch.from_numpy(raw).view(torch.bfloat16).float().numpy()
+        elif self.prog.dtype == "fp16":
+            raw = np.zeros(n, np.float16)
+            _memcpy_d2h(raw, ptr.value)
+            out = raw.astype(np.float32)
         elif self.prog.dtype == "fp8":
             raw = np.zeros(n, np.uint8)
             _memcpy_d2h(raw, ptr.value)

@@ -160,7 +160,10 @@ class YOLO:
     torch.save (loaded with weights_only=True).  ``dtype``: 'fp32' (the default: fp32-grade
     arithmetic with the reference's exact SiLU, so the unchanged driver gets the reference's
     decisions up to fp32 near-ties), or the explicit opt-ins
-    'bf16' / 'fp8' (faster, not parity-capable: their detections differ from the reference's)."""
+    'bf16' / 'fp8' (faster, not parity-capable: their detections differ from the reference's).
+    ``predict(half=True)`` runs the fp16 build (the reference's AutoBackend(fp16=True) ->
+    model.half(), nn/autobackend.py:215, engine/predictor.py:172): binary16 weights and
+    activations on the f16 matrix cores, fp32 accumulation, its own engine per geometry."""
 
     def __init__(self, model: str = "yolov8s-small.yaml", task=None, verbose: bool = False, *, weights=None,
                  dtype: str = "fp32", device: int = 0, seed: int = 0, max_batch: int = 8):
@@ -203,11 +206,16 @@ class YOLO:
         self._staging = None
 
     # -- engines ------------------------------------------------------------------
-    def engine(self, frame_h: int, frame_w: int, imgsz=640, max_det: int = 300) -> M.DeviceModel:
-        key = (frame_h, frame_w, imgsz if isinstance(imgsz, int) else tuple(imgsz), max_det)
+    def _key(self, frame_h, frame_w, imgsz, max_det, dtype=None):
+        k = (frame_h, frame_w, imgsz if isinstance(imgsz, int) else tuple(imgsz), max_det)
+        return k if dtype in (None, self.dtype) else k + (dtype,)
+
+    def engine(self, frame_h: int, frame_w: int, imgsz=640, max_det: int = 300, dtype=None) -> M.DeviceModel:
+        dtype = self.dtype if dtype is None else dtype
+        key = self._key(frame_h, frame_w, imgsz, max_det, dtype)
         e = self._engines.get(key)
         if e is None:
-            prog = M.Program(self.arch, self.state_dict, frame_h, frame_w, imgsz, self.max_batch, self.dtype, max_det)
+            prog = M.Program(self.arch, self.state_dict, frame_h, frame_w, imgsz, self.max_batch, dtype, max_det)
             e = M.DeviceModel(prog, self.device)
             self.plans[key] = self._apply_plan(e, prog, imgsz)
             self._engines[key] = e
@@ -221,13 +229,18 @@ class YOLO:
 
         if not self.arch.scale or not isinstance(imgsz, int):
             return None
-        name = f"{self.arch.scale}_{prog.frame_w}x{prog.frame_h}_i{imgsz}_b1_{self.dtype}.json"
-        path = os.path.join(PLAN_DIR, name)
+        dt = prog.dtype
+        path = os.path.join(PLAN_DIR, f"{self.arch.scale}_{prog.frame_w}x{prog.frame_h}_i{imgsz}_b1_{dt}.json")
+        if dt == "fp16" and not os.path.exists(path):
+            # the fp16 build runs the bf16 build's kernels with the f16 MFMA (same shapes, same rate):
+            # the committed bf16 plan is its plan too
+            dt = "bf16"
+            path = os.path.join(PLAN_DIR, f"{self.arch.scale}_{prog.frame_w}x{prog.frame_h}_i{imgsz}_b1_bf16.json")
         if not os.path.exists(path):
             return None
         with open(path) as f:
             pl = json.load(f)
-        if pl.get("dtype", self.dtype) != self.dtype or len(pl.get("plan", ())) != len(prog.ops):
+        if pl.get("dtype", dt) != dt or len(pl.get("plan", ())) != len(prog.ops):
             return None
         e.load_plan(pl["batch"], pl["plan"])
         return path
@@ -244,9 +257,7 @@ class YOLO:
         max_det = self.overrides["max_det"] if max_det is None else max_det
         assert 0 <= conf <= 1, f"Invalid Confidence threshold {conf}, valid values are between 0.0 and 1.0"
         assert 0 <= iou <= 1, f"Invalid IoU {iou}, valid values are between 0.0 and 1.0"
-        if half:
-            raise NotImplementedError("half=True (fp16 weights/activations) is not built on this path; the 16-bit "
-                                      "build is YOLO(..., dtype='bf16')")
+        dtype = "fp16" if half else None  # AutoBackend(fp16=half): model.half() (nn/autobackend.py:215)
         if self.arch.nc != 1:
             raise NotImplementedError("only single-class detection heads are on this path")
         # nc == 1: every candidate is class 0, so non_max_suppression's class filter (utils/nms.py:128-132),
@@ -262,7 +273,7 @@ class YOLO:
             out = []
             for i in range(0, len(frames), self.max_batch):
                 out.extend(self._predict_batch(frames[i:i + self.max_batch], conf, iou, imgsz, max_det, classes,
-                                               paths[i:i + self.max_batch]))
+                                               paths[i:i + self.max_batch], dtype))
         return iter(out) if stream else out
 
     @staticmethod
@@ -273,21 +284,21 @@ class YOLO:
 
         return FR.load_source(source)
 
-    def _predict_batch(self, frames, conf, iou, imgsz, max_det, classes, paths=None):
+    def _predict_batch(self, frames, conf, iou, imgsz, max_det, classes, paths=None, dtype=None):
         paths = paths or [f"image{b}.jpg" for b in range(len(frames))]
         shapes = {f.shape for f in frames}
         if len(shapes) != 1:
             out = []
             for f, p in zip(frames, paths):
-                out.extend(self._predict_batch([f], conf, iou, imgsz, max_det, classes, [p]))
+                out.extend(self._predict_batch([f], conf, iou, imgsz, max_det, classes, [p], dtype))
             return out
         h, w, c = frames[0].shape
         if c != 3 or frames[0].dtype != np.uint8:
             raise ValueError("frames must be uint8 HxWx3 (BGR)")
         t0 = time.perf_counter()
         md = max(max_det, 1)
-        eng = self.engine(h, w, imgsz, md)
-        io = self._io[(h, w, imgsz if isinstance(imgsz, int) else tuple(imgsz), md)]
+        eng = self.engine(h, w, imgsz, md, dtype)
+        io = self._io[self._key(h, w, imgsz, md, dtype)]
         B = len(frames)
         hb = io.host.numpy()
         for b, f in enumerate(frames):  # page-locked staging, then one DMA of the batch

@@ -105,7 +105,7 @@ class TrajCache:
         for i in range(R):
             n, c = lens[i], counts[i]
             old = self.d.get(nums[i])
-            k = -1 if old is None else c - old[0]
+            k = -1 if old is None else (c - old[0]) % (1 << 32)  # traj_count wraps mod 2^32 on the device
             if 0 <= k <= 3 and k <= n and n == min(len(old[1]) + k, traj.shape[1]):
                 if k == 0:
                     lst = old[1]
