@@ -173,10 +173,10 @@ int yk_tracker_outputs(yk_tracker* trk, yk_track_out** dev_rows, int32_t** dev_c
 int yk_tracker_download(yk_tracker* trk, yk_track_out* host_rows, int32_t* host_counts,
                         yk_tracker_stats* host_stats, void* stream);
 
-/* Enqueue the same copies without waiting: counts, stats and the first `rows_per_stream` rows of
- * every stream (host_rows[s * max_tracks ...]; max_tracks copies every row, live or not, since the
- * counts are not known on the host yet) on `stream`, page-locked destinations expected.  Nothing
- * is synchronised: the host reads them after an event / stream sync of its own.  The per-step
+/* Enqueue the same transfer without waiting: one kernel on `stream` writes counts, stats and the
+ * live rows of every stream (at most `rows_per_stream` of them; host_rows[s * max_tracks ...])
+ * straight into the page-locked host buffers (YK_ERR_ARG for pageable memory).  Nothing is
+ * synchronised: the host reads them after an event / stream sync of its own.  The per-step
  * "tracker output to the host" of a pipelined loop (bench.py). */
 int yk_tracker_download_async(yk_tracker* trk, yk_track_out* host_rows, int32_t* host_counts,
                               yk_tracker_stats* host_stats, int rows_per_stream, void* stream);

@@ -200,3 +200,25 @@ def score_ties(pred: torch.Tensor, conf: float = 0.25) -> int:
     output [5, A]: non_max_suppression's scores.sort (utils/nms.py:264) is unstable on them."""
     s = pred[4][pred[4] > conf]
     return int(s.numel() - torch.unique(s).numel())
+
+
+def lost_conf_spread(track, delta: float, samples: int = 8, seed: int = 0) -> float:
+    """How far a lost track's reported confidence (get_lost_prediction -> long_term_predict,
+    kf.py:205-247, 319-333) moves when every entry of its velocity history moves by ~delta
+    (Gaussian, per component): the conditioning of that confidence.  Through the direction
+    statistics (arctan2 of near-zero velocities) and the 0.3 / 0.5 thresholds a confidence can
+    swing by far more than its inputs; two fp32 chains whose velocities differ by delta cannot be
+    held closer than this.  `track` is an oracle RefTrack; nothing of it is modified."""
+    import copy
+    from collections import deque
+
+    rng = np.random.default_rng(seed)
+    _, c0 = copy.deepcopy(track).get_lost_prediction()
+    spread = 0.0
+    for _ in range(samples):
+        t2 = copy.deepcopy(track)
+        t2.velocity_history = deque([np.asarray(v, np.float64) + rng.normal(0.0, delta, 2) for v in track.velocity_history],
+                                    maxlen=track.velocity_history.maxlen)
+        _, c = t2.get_lost_prediction()
+        spread = max(spread, abs(float(c) - float(c0)))
+    return spread

@@ -19,7 +19,8 @@ import pytest
 import torch
 
 from conftest import pkg
-from gpu_helpers import StepRecorder, decisions, dets_match, near_tie_boxes, score_ties, track_dicts
+from gpu_helpers import (StepRecorder, decisions, dets_match, lost_conf_spread, near_tie_boxes, score_ties,
+                         track_dicts)
 from oracle import detector_ref as D
 from oracle.tracker_ref import RefMultiTracker
 
@@ -30,6 +31,7 @@ S, F, TARGETS = 8, 160, 40  # bench.py config 3's streams and targets
 # (relative) -- below the resolution of fp32 convolutions that differ only in summation order
 # (layer activations ~3e-6 apart, max-normalised; tools/split_ab.py)
 TIE_REL = 1e-5
+CONF_TOL = 1e-4  # north_star: floats within 1e-4 (confidences are in [0, 1])
 PLANS = {"exact_r2": "plans/exp/s_640x512_i640_b8_fp32_exact_r2.json",  # round-2 exact-f32 MFMA plan
          "committed": "plans/s_640x512_i640_b8_fp32.json"}              # bench.py's plan (split-bf16 / halo)
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -151,7 +153,7 @@ def check_chain(chain, plan_path, parity_record=False):
     S, F = chain["S"], chain["F"]
     dets, counts, rows, tcounts, stats = _run_gpu("fp32", chain["frames"], plan_path)
     assert int(stats[-1]["overflow"].sum()) == 0
-    conf_dev, box_rel, n_tracks, n_outputs = 0.0, 0.0, 0, 0
+    conf_dev, conf_dev_well, box_rel, n_tracks, n_outputs, ill_conf = 0.0, 0.0, 0.0, 0, 0, []
     flips, flip_scores, order_ties = [], [], []
     ctrk = [RefMultiTracker(150, 1, 0.1, stable_ties=True, fast_iou=True) for _ in range(S)]  # resynced chain
     iso = [RefMultiTracker(150, 1, 0.1, stable_ties=True, fast_iou=True) for _ in range(S)]
@@ -181,7 +183,20 @@ def check_chain(chain, plan_path, parity_record=False):
                 dev = float(np.max(np.abs(o["bbox"] - r["bbox"])))
                 assert dev <= 1e-4 * scale + 1e-3, (t, s, o["bbox"], r["bbox"])
                 box_rel = max(box_rel, dev / max(scale, 1.0))
-                conf_dev = max(conf_dev, abs(o["confidence"] - r["confidence"]))
+                dc = abs(o["confidence"] - r["confidence"])
+                conf_dev = max(conf_dev, dc)
+                if dc > CONF_TOL:
+                    # only a lost track whose confidence is ill conditioned at the chains' own velocity
+                    # difference may exceed the float bar (north_star 1e-4): counted, printed
+                    dv = float(np.max(np.abs(np.asarray(o["velocity"]) - np.asarray(r["velocity"]))))
+                    tr = next(x for x in ctrk[s].trackers if x.track_id == r["track_id"])
+                    spread = lost_conf_spread(tr, max(2.0 * dv, 1e-7))
+                    assert r["status"] == "predicted" and spread >= 0.5 * dc, \
+                        (t, s, r["track_id"], o["confidence"], r["confidence"], dv, spread)
+                    ill_conf.append({"frame": t, "stream": s, "track": int(r["track_id"]), "dev": dc,
+                                     "velocity_dev": dv, "spread": spread})
+                else:
+                    conf_dev_well = max(conf_dev_well, dc)
                 n_tracks += 1
             n_outputs += len(ours)
             # the tracker alone, on the GPU's detections (float32 rows, as the driver builds them)
@@ -195,6 +210,7 @@ def check_chain(chain, plan_path, parity_record=False):
                "near_tie_flip_frames": flips, "order_ties": len(order_ties), "order_tie_frames": order_ties,
                "oracle_near_tie_boxes": int(sum(len(b) for fr in chain["near"] for b in fr)),
                "max_box_rel_dev": box_rel, "max_confidence_abs_dev": conf_dev,
+               "max_confidence_abs_dev_well_conditioned": conf_dev_well, "ill_conditioned_confidences": len(ill_conf),
                "oracle_tie_frames": chain["tie_frames"], "nms_early_exit": _run_gpu.nms,
                "nms_score_ties": chain["nms_score_ties"], "terminated": chain["terminated"]}
     print("BENCH_PIPELINE_FP32", json.dumps(summary))
@@ -205,6 +221,9 @@ def check_chain(chain, plan_path, parity_record=False):
         assert rec.get("near_tie_flips") == len(flips) and rec.get("order_ties") == len(order_ties), \
             (rec, flips, order_ties)
     assert _run_gpu.nms["images"] == S * F  # every frame's NMS ran once on the device
+    for ic in ill_conf[:10]:
+        print("ILL_CONDITIONED_CONFIDENCE", json.dumps(ic))
+    assert conf_dev_well <= CONF_TOL  # every well-conditioned confidence at the float bar
     assert conf_dev <= 1e-2
     return summary
 

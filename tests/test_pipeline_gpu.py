@@ -74,17 +74,12 @@ def _driver_scene(P, n_frames, seed=DRIVER_SEED):
     return sc
 
 
-@pytest.mark.timeout(900)
-def test_reference_driver_loop_through_compat_packages(tmp_path):
+def _run_driver(tmp_path, seed, F=160):
     """kalman/aircraft_detection_tracking.py:45-161 run unchanged through the compat imports --
     ``YOLO(model_path)`` with no dtype argument (so the drop-in default), frames read through the
     VideoCapture-like reader (a .npy frame stack, since no codec is in the image), the per-frame
-    body of :88-131, the visualizer and the VideoWriter-like sink -- held to the oracle under the
-    strict chain bar: every frame's detections equal the torch-CPU fp32 detector's row for row,
-    the track dicts equal the oracle chain (detector -> numpy RefMultiTracker(150, 1, 0.1)) on
-    every frame -- decisions (id, status, age, hits, tsu) identical, boxes within 1e-4 of the
-    box's scale -- and equal the oracle tracker fed the GPU's detections.  No near-tie
-    allowance.  160 frames so the 150-miss deletion happens inside the loop."""
+    body of :88-131, the visualizer and the VideoWriter-like sink.  Returns what the chain check
+    needs: the model, the frames and every frame's (float32 detections, track dicts)."""
     sys.path.insert(0, os.path.join(REPO, pkg().__name__, "compat"))
     try:
         from kalman.enhanced_multi_target_tracker import EnhancedMultiTargetTracker
@@ -92,12 +87,10 @@ def test_reference_driver_loop_through_compat_packages(tmp_path):
         from ultralytics import YOLO
     finally:
         sys.path.pop(0)
-    from gpu_helpers import decisions
 
     P = pkg()
     FR = P.frames
-    F = 160
-    sc = _driver_scene(P, F, DRIVER_SEED)
+    sc = _driver_scene(P, F, seed)
     frames = np.stack([sc.frame(t) for t in range(F)])
     np.save(tmp_path / "seq.npy", frames)
     # --- the driver, as written (aircraft_detection_tracking.py:45-52, 58-161) ---------------------
@@ -147,45 +140,96 @@ def test_reference_driver_loop_through_compat_packages(tmp_path):
     out.release()
     assert frame_count == F and tracker.frame_count == F
     assert results[0].boxes.xyxy.is_cuda and results[0].orig_shape == (512, 640)
-    # --- the oracle chain on the same frames -----------------------------------------------------
-    # Strict chain bar, no near-tie allowance: per frame, the detections equal the oracle's row for
-    # row (1e-4 relative, 1e-3 px; scores 1e-4); the track dicts equal the oracle chain's (oracle
-    # detector -> oracle tracker): decisions identical, boxes within 1e-4 of the box's scale; and on
-    # every frame they also equal the oracle tracker fed the GPU's own detections (1e-9,
-    # test_tracker_gpu.compare_frame).
-    from gpu_helpers import assign_margin, dets_match
+    assert detection_frames > 0 and prediction_frames > 0 and state_changes > 0
+    return dict(model=model, frames=frames, per_frame=per_frame, tracker=tracker, state_changes=state_changes)
+
+
+def _check_driver_chain(run, assoc_tie_margin=None):
+    """The oracle chain on the driver's frames: per frame the detections equal the oracle's row for
+    row (1e-4 relative, 1e-3 px; scores 1e-4); the track dicts equal the oracle chain's (oracle
+    detector -> oracle RefMultiTracker(150, 1, 0.1)): decisions identical, boxes within 1e-4 of
+    the box's scale; and on every frame they equal the oracle tracker fed the GPU's own detections
+    (1e-9, test_tracker_gpu.compare_frame).
+
+    assoc_tie_margin=None: strict, no allowance.  A number: the association near-tie policy (the
+    NMS near-tie policy of tests/test_bench_pipeline_gpu.py applied to the tracker) -- a frame
+    whose decisions differ from the oracle chain's is accepted only when that frame's oracle
+    greedy association had a pick decided by less than assoc_tie_margin (gpu_helpers.assign_margin:
+    the IoU gap to the free pair it beat, or to the gate); it is counted, both chains' IoUs of
+    the differing tracks are printed, and the oracle chain is resynced to the GPU's pick (its
+    tracker takes the state of the oracle tracker fed the GPU's detections, which equals the
+    device tracker at 1e-9), so every later frame is still compared."""
+    import copy
+
+    from gpu_helpers import assign_margin, decisions, dets_match
     from test_tracker_gpu import compare_frame
 
+    P = pkg()
+    model, frames, per_frame = run["model"], run["frames"], run["per_frame"]
+    F = len(per_frame)
     ref = D.RefDetector(_layers(model.arch), model.state_dict, P.arch.detect_strides(model.arch))
     trk = RefMultiTracker(150, 1, 0.1, stable_ties=True, fast_iou=True)
     iso = RefMultiTracker(150, 1, 0.1, stable_ties=True, fast_iou=True)
     torch.set_num_threads(max(1, min(16, len(os.sched_getaffinity(0)))))
-    n_tracks, box_rel, margin = 0, 0.0, np.inf
+    n_tracks, box_rel, margin, flips = 0, 0.0, np.inf, []
     for t in range(F):
         want, _ = D.predict(ref, [frames[t]])
         wd = want[0][:, :5].numpy()
         got_d, ours = per_frame[t]
         assert dets_match(got_d, wd) == "same", (f"frame {t}: detections differ from the oracle's", got_d, wd)
         rb = trk.update([[b[0], b[1], b[2], b[3], b[4]] for b in wd])
-        if trk.last_iou is not None:
-            margin = min(margin, assign_margin(trk.last_iou, 0.1))
-        assert decisions(ours) == decisions(rb), t
+        fm = assign_margin(trk.last_iou, 0.1) if trk.last_iou is not None else np.inf
+        margin = min(margin, fm)
+        ri = iso.update([[b[0], b[1], b[2], b[3], b[4]] for b in got_d])
+        compare_frame(ours, ri, f"isolated tracker frame {t}")
+        if decisions(ours) != decisions(rb):
+            assert assoc_tie_margin is not None and fm < assoc_tie_margin, \
+                (f"frame {t}: association decisions differ (oracle margin {fm:.3g})", decisions(ours), decisions(rb))
+            ids = {d[0] for d in set(decisions(ours)) ^ set(decisions(rb))}
+            flips.append({"frame": t, "oracle_margin": fm, "tracks": sorted(int(i) for i in ids),
+                          "oracle_iou_max": [float(trk.last_iou.max())], "gpu_chain_iou_max": [float(iso.last_iou.max())]})
+            print("ASSOC_NEAR_TIE_FLIP", flips[-1])
+            trk = copy.deepcopy(iso)  # resync: the oracle chain continues from the GPU's pick
+            continue
         for o, r in zip(ours, rb):
             scale = float(np.max(np.abs(r["bbox"])))
             dev = float(np.max(np.abs(np.asarray(o["bbox"]) - r["bbox"])))
             assert dev <= 1e-4 * scale + 1e-3, (t, o["track_id"], o["bbox"], r["bbox"])
             box_rel = max(box_rel, dev / max(scale, 1.0))
             n_tracks += 1
-        compare_frame(ours, iso.update([[b[0], b[1], b[2], b[3], b[4]] for b in got_d]), f"isolated tracker frame {t}")
-    assert n_tracks == sum(len(per_frame[t][1]) for t in range(F))  # every output of every frame compared
-    assert margin >= DRIVER_MIN_MARGIN, margin  # the scene is well conditioned for a strict comparison
     st = iso.stats
     assert st["total_tracks_terminated"] >= 1 and st["successful_recoveries"] > 0, st  # deletion + recovery ran
-    assert tracker.get_statistics()["total_tracks_terminated"] == st["total_tracks_terminated"]
-    assert trk.stats == st  # the oracle chain and the isolated oracle tracker agree too
-    assert detection_frames > 0 and prediction_frames > 0 and state_changes > 0
-    print("DRIVER_LOOP", {"frames": F, "chain_track_outputs_compared": n_tracks, "max_box_rel_dev": box_rel, "min_assign_margin": margin,
-                          "stats": dict(st), "state_changes": state_changes})
+    assert run["tracker"].get_statistics()["total_tracks_terminated"] == st["total_tracks_terminated"]
+    return dict(frames=F, chain_track_outputs_compared=n_tracks, max_box_rel_dev=box_rel, min_assign_margin=margin,
+                assoc_near_tie_flips=flips, stats=dict(st), oracle_chain_stats=dict(trk.stats),
+                state_changes=run["state_changes"])
+
+
+@pytest.mark.timeout(900)
+def test_reference_driver_loop_through_compat_packages(tmp_path):
+    """The reference driver loop (see _run_driver) held to the oracle chain under the strict bar:
+    no near-tie allowance at all, on a scene whose oracle chain is decided by association margins
+    >= DRIVER_MIN_MARGIN (asserted).  160 frames so the 150-miss deletion happens inside the loop."""
+    out = _check_driver_chain(_run_driver(tmp_path, DRIVER_SEED))
+    F = out["frames"]
+    assert out["chain_track_outputs_compared"] > 0
+    assert out["min_assign_margin"] >= DRIVER_MIN_MARGIN, out["min_assign_margin"]  # well conditioned
+    assert out["oracle_chain_stats"] == out["stats"]  # the oracle chain and the isolated oracle tracker agree
+    print("DRIVER_LOOP", {k: v for k, v in out.items() if k != "assoc_near_tie_flips"}, F)
+
+
+@pytest.mark.timeout(900)
+def test_reference_driver_loop_ill_conditioned_scene_counted_ties(tmp_path):
+    """The same driver loop on the rounds-2/3 scene (seed 4), whose many coasting duplicate tracks
+    give association margins of 3.8e-8 (frame 89) and 2.8e-7 (frame 75) -- below the ~1e-6 IoU
+    spread of two fp32 detector chains, so no implementation can be held to the oracle's pick there.
+    Under the association near-tie policy (_check_driver_chain): every frame compared, a differing
+    frame accepted only at an oracle margin < 1e-5, counted and resynced; at most 3 such frames."""
+    out = _check_driver_chain(_run_driver(tmp_path, 4), assoc_tie_margin=1e-5)
+    print("DRIVER_LOOP_SEED4", {k: v for k, v in out.items() if k != "assoc_near_tie_flips"},
+          "flips", len(out["assoc_near_tie_flips"]))
+    assert out["min_assign_margin"] < 1e-5  # the scene really is ill conditioned
+    assert len(out["assoc_near_tie_flips"]) <= 3, out["assoc_near_tie_flips"]
 
 
 def test_pipelined_tracker_stream_matches_serial():

@@ -130,6 +130,11 @@ def main():
         for t in range(F):
             pipe.run(frames[t])
         pipe.sync()
+        info = np.zeros((S, 5), np.int32)  # diag builds (YK_GMD_DIAG 4 / 8): LK self-consistency counters
+        L.check(L.lib().yk_gmc_info(pipe.gmd._h, L.ptr(info), L.current_stream(0)), "yk_gmc_info")
+        if info[:, :2].any():
+            print(f"    LK recompute mismatches: same wave {info[:, 0].tolist()}  second launch {info[:, 1].tolist()}",
+                  flush=True)
         # every frame buffer must still hold the frame last copied into it
         held = [(f"slot{(F - 1 - j) % pipe.D if pipe.D > 1 else 0}", pipe.frame_slots[(F - 1 - j) % pipe.D], frames[F - 1 - j])
                 for j in range(pipe.D)]

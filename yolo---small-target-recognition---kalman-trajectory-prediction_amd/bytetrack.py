@@ -217,8 +217,8 @@ class GMC:
 
     def apply(self, raw_frame, detections=None) -> np.ndarray:
         """The 2x3 warp of one frame (stream 0), float64, like the reference's GMC.apply."""
-        self.apply_device(raw_frame)
-        src = self.warp if self.method == "sparseOptFlow" else self.identity
+        ptr = self.apply_device(raw_frame)
+        src = self.identity if ptr == self.identity.data_ptr() else self.warp
         return src[0].cpu().numpy().reshape(2, 3)
 
     def info(self) -> np.ndarray:

@@ -46,6 +46,12 @@
 //     1  lk_kernel window sums through LDS (no DPP row sums, no v_readlane)
 //     2  system-scope release at the end of the pyramid / derivative producers, acquire at
 //        the start of lk_kernel
+//     4  lk_kernel solves every corner twice in a row, counting differing answers in info[s][0]
+//     8  a second lk_kernel launch re-solves every corner and counts answers differing from the
+//        first launch's in info[s][1] (the kernel template's diag bit picks the role)
+//    16  ordering probe: every wave of the pyramid / derivative producers adds 1 to info[0][2] after
+//        an agent-scope release; lk_kernel's waves check on entry that every producer wave of
+//        this call has (info[0][3] counts the waves that found fewer)
 #ifndef YK_GMD_DIAG
 #define YK_GMD_DIAG 0
 #endif
@@ -107,7 +113,16 @@ struct Dev {
   int W0, H0;              // input frame size (GMC: twice geo.W / geo.H)
   double* warp;            // [S][6] GMC warp
   int* info;               // [S][5] GMC diagnostics (yk_gmc_info)
+  int diag_expect;         // YK_GMD_DIAG 16: producer waves launched so far, this call's included
 };
+// YK_GMD_DIAG 16: one count per producer wave, after its stores are released
+#define GMD_PRODUCER_DONE()                                                                       \
+  do {                                                                                            \
+    if (YK_GMD_DIAG & 16) {                                                                       \
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");                                          \
+      if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(g.info + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); \
+    }                                                                                             \
+  } while (0)
 
 __device__ __forceinline__ int refl(int i, int n) {  // BORDER_REFLECT_101, |overflow| < n
   i = i < 0 ? -i : i;
@@ -164,10 +179,12 @@ __global__ void __launch_bounds__(256) gray_kernel(Dev g, const unsigned char* _
   const int s = blockIdx.y, cur = g.sel[s] ^ 1;
   const long long n = (long long)g.geo.W * g.geo.H;
   const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (i >= n) return;
-  const unsigned char* p = frames + ((long long)s * n + i) * 3;
-  g.pyr[cur][(long long)s * g.geo.per + i] = (unsigned char)gray_of(p);
-  if (YK_GMD_DIAG & 2) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  if (i < n) {
+    const unsigned char* p = frames + ((long long)s * n + i) * 3;
+    g.pyr[cur][(long long)s * g.geo.per + i] = (unsigned char)gray_of(p);
+    if (YK_GMD_DIAG & 2) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  }
+  GMD_PRODUCER_DONE();
 }
 
 // GMC: cvtColor(BGR2GRAY) then cv2.resize(gray, (W / 2, H / 2)): INTER_LINEAR at an exact 1/2
@@ -177,21 +194,23 @@ __global__ void __launch_bounds__(256) gray_down_kernel(Dev g, const unsigned ch
   const int s = blockIdx.y, cur = g.sel[s] ^ 1;
   const int W = g.geo.W, H = g.geo.H, W0 = g.W0;
   const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (i >= (long long)W * H) return;
-  const int y = (int)(i / W), x = (int)(i - (long long)y * W);
-  const unsigned char* f = frames + (long long)s * W0 * g.H0 * 3;
-  const unsigned char* r0 = f + ((long long)(2 * y) * W0 + 2 * x) * 3;
-  const unsigned char* r1 = r0 + (long long)W0 * 3;
-  const int v = gray_of(r0) + gray_of(r0 + 3) + gray_of(r1) + gray_of(r1 + 3);
-  g.pyr[cur][(long long)s * g.geo.per + i] = (unsigned char)((v + 2) >> 2);
-  if (YK_GMD_DIAG & 2) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  if (i < (long long)W * H) {
+    const int y = (int)(i / W), x = (int)(i - (long long)y * W);
+    const unsigned char* f = frames + (long long)s * W0 * g.H0 * 3;
+    const unsigned char* r0 = f + ((long long)(2 * y) * W0 + 2 * x) * 3;
+    const unsigned char* r1 = r0 + (long long)W0 * 3;
+    const int v = gray_of(r0) + gray_of(r0 + 3) + gray_of(r1) + gray_of(r1 + 3);
+    g.pyr[cur][(long long)s * g.geo.per + i] = (unsigned char)((v + 2) >> 2);
+    if (YK_GMD_DIAG & 2) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  }
+  GMD_PRODUCER_DONE();
 }
 
 __global__ void __launch_bounds__(256) pyrdown_kernel(Dev g, int l) {
   const int s = blockIdx.z, cur = g.sel[s] ^ 1;
   const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = blockIdx.y * 16 + (threadIdx.x >> 4);
   const int dw = g.geo.lw[l], dh = g.geo.lh[l], sw = g.geo.lw[l - 1], sh = g.geo.lh[l - 1];
-  if (x >= dw || y >= dh) return;
+  if (x < dw && y < dh) {
   const unsigned char* src = g.pyr[cur] + (long long)s * g.geo.per + g.geo.loff[l - 1];
   const int k[5] = {1, 4, 6, 4, 1};
   int xs[5];
@@ -208,6 +227,8 @@ __global__ void __launch_bounds__(256) pyrdown_kernel(Dev g, int l) {
   }
   g.pyr[cur][(long long)s * g.geo.per + g.geo.loff[l] + (long long)y * dw + x] = (unsigned char)((acc + 128) >> 8);
   if (YK_GMD_DIAG & 2) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  }
+  GMD_PRODUCER_DONE();
 }
 
 // calcSharrDeriv: vertical [3 10 3] / [-1 0 1], then horizontal [-1 0 1] / [3 10 3], reflect-101.
@@ -706,12 +727,21 @@ __device__ __forceinline__ void lk_weights(float a, float b, int& w00, int& w01,
 
 // One wavefront per corner (4 corners per workgroup); all control flow is wave-uniform.
 // (Staging each level's search region in LDS was measured slower: 111 -> 159 µs for 8 streams.)
+template <int CHECK>
 __global__ void __launch_bounds__(256) lk_kernel(Dev g) {
   const int s = blockIdx.y, lane = threadIdx.x & 63;
   const int p = blockIdx.x * 4 + (threadIdx.x >> 6);
   __shared__ int red_lds[(YK_GMD_DIAG & 1) ? 4 : 1][64];
   int* red = red_lds[(YK_GMD_DIAG & 1) ? (threadIdx.x >> 6) : 0];
   if (YK_GMD_DIAG & 2) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  if ((YK_GMD_DIAG & 16) && !CHECK && (threadIdx.x & 63) == 0) {
+    const int done = __hip_atomic_load(g.info + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (done < g.diag_expect) {
+      __hip_atomic_fetch_add(g.info + 3, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      printf("[lk order] s %d wave %d: %d of %d producer waves done at entry\n", blockIdx.y,
+             (int)(blockIdx.x * 4 + (threadIdx.x >> 6)), done, g.diag_expect);
+    }
+  }
   auto wsum = [&](int v) { return (YK_GMD_DIAG & 1) ? wave_sum_lds(v, red) : wave_sum_rows(v); };
   auto wsum_wide = [&](int v) { return (YK_GMD_DIAG & 1) ? wave_sum_lds(v, red) : wave_sum_rows_wide(v); };
   if (p >= g.ncorners[s]) return;
@@ -730,8 +760,25 @@ __global__ void __launch_bounds__(256) lk_kernel(Dev g) {
   }
   const float half = (float)((WIN - 1) * 0.5);
   const float fs = 1.0f / (float)(1 << 20);
-  float2 nxt = pt;
-  int status = 1;
+  float2 nxt = pt, nxt0 = pt;
+  int status = 1, status0 = 1;
+  // diag 4: per-lane rolling hashes of every value the pass loads (I window + derivatives, J
+  // samples) and the iterations it ran, to tell a memory difference from a compute difference
+  unsigned long long hI = 0, hJ = 0, hI0 = 0, hJ0 = 0;
+  int nit = 0, nit0 = 0;
+  // diag 4: every wave solves its corner twice in a row and counts a differing second answer
+  for (int rep = 0; rep < ((YK_GMD_DIAG & 4) ? 2 : 1); ++rep) {
+  if (rep == 1) {
+    nxt0 = nxt;
+    status0 = status;
+    nxt = pt;
+    status = 1;
+    hI0 = hI;
+    hJ0 = hJ;
+    nit0 = nit;
+    hI = hJ = 0;
+    nit = 0;
+  }
   for (int l = G.levels; l >= 0; --l) {
     const int cols = G.lw[l], rows = G.lh[l];
     const unsigned char* I = Ib + G.loff[l];
@@ -784,6 +831,8 @@ __global__ void __launch_bounds__(256) lk_kernel(Dev g) {
         auto hi = [](int e) { return e >> 16; };                   // short2.y
         Dx[k] = (lo(e00) * w00 + lo(e01) * w01 + lo(e10) * w10 + lo(e11) * w11 + 8192) >> 14;
         Dy[k] = (hi(e00) * w00 + hi(e01) * w01 + hi(e10) * w10 + hi(e11) * w11 + 8192) >> 14;
+        if (YK_GMD_DIAG & 4)
+          hI = hI * 1000003ull + (unsigned long long)(unsigned)((Iv[k] * 65599 + Dx[k]) * 131 + Dy[k] + l * 7 + k);
         s11 += Dx[k] * Dx[k];
         s12 += Dx[k] * Dy[k];
         s22 += Dy[k] * Dy[k];
@@ -822,6 +871,7 @@ __global__ void __launch_bounds__(256) lk_kernel(Dev g) {
           if (wy[k] >= 0) {
             const unsigned char* q = base + woff[k];
             const int jv = (q[0] * v00 + q[1] * v01 + q[cols] * v10 + q[cols + 1] * v11 + 256) >> 9;
+            if (YK_GMD_DIAG & 4) hJ = hJ * 1000003ull + (unsigned long long)(unsigned)(jv * 31 + j * 7 + l);
             const int diff = jv - Iv[k];
             b1 += diff * Dx[k];
             b2 += diff * Dy[k];
@@ -836,12 +886,14 @@ __global__ void __launch_bounds__(256) lk_kernel(Dev g) {
             const unsigned char* r0 = J + (long long)refl(Y, rows) * cols;
             const unsigned char* r1 = J + (long long)refl(Y + 1, rows) * cols;
             const int jv = (r0[x0] * v00 + r0[x1] * v01 + r1[x0] * v10 + r1[x1] * v11 + 256) >> 9;
+            if (YK_GMD_DIAG & 4) hJ = hJ * 1000003ull + (unsigned long long)(unsigned)(jv * 31 + j * 7 + l + 1000);
             const int diff = jv - Iv[k];
             b1 += diff * Dx[k];
             b2 += diff * Dy[k];
           }
         }
       }
+      if (YK_GMD_DIAG & 4) ++nit;
       const float fb1 = (float)wsum_wide(b1) * fs;
       const float fb2 = (float)wsum_wide(b2) * fs;
       const float dx = (A12 * fb2 - A22 * fb1) * Di;
@@ -858,6 +910,23 @@ __global__ void __launch_bounds__(256) lk_kernel(Dev g) {
       pdx = dx;
       pdy = dy;
     }
+  }
+  }  // rep
+  if (YK_GMD_DIAG & 4) {
+    const unsigned long long dI = __ballot(hI != hI0), dJ = __ballot(hJ != hJ0);
+    const bool differ = nxt.x != nxt0.x || nxt.y != nxt0.y || status != status0;
+    if (lane == 0 && (differ || dI || dJ)) {
+      atomicAdd(g.info + s * 5, 1);
+      printf("[lk diag] s %d p %d pt (%.3f %.3f): pass1 (%.6f %.6f) st %d it %d | pass2 (%.6f %.6f) st %d it %d | "
+             "I-hash lanes differ %016llx J-hash lanes differ %016llx\n",
+             s, p, pt.x, pt.y, nxt0.x, nxt0.y, status0, nit0, nxt.x, nxt.y, status, nit, dI, dJ);
+    }
+  }
+  if (CHECK && lane == 0) {  // second launch (diag 8): compare with the first launch's answer
+    const float2 f = g.next[s * g.maxc + p];
+    if (f.x != nxt.x || f.y != nxt.y || g.status[s * g.maxc + p] != (unsigned char)status)
+      atomicAdd(g.info + s * 5 + 1, 1);
+    return;
   }
   if (lane == 0) {
     g.next[s * g.maxc + p] = nxt;
@@ -1546,7 +1615,7 @@ int yk_gmd_set_thresholds(yk_gmd* g, double global_motion_threshold, double rese
 // the stages both methods share: new frame's gray pyramid + derivatives, then (from the second
 // frame on) corners of the previous frame and their Lucas-Kanade flow to the new one
 static void gmd_front(yk_gmd* g, const uint8_t* frames, hipStream_t st) {
-  const Dev& d = g->dev;
+  Dev& d = g->dev;
   const yk::gmd::Geo& G = d.geo;
   const int S = d.S;
   const long long HW = (long long)G.W * G.H;
@@ -1554,9 +1623,12 @@ static void gmd_front(yk_gmd* g, const uint8_t* frames, hipStream_t st) {
     hipLaunchKernelGGL(yk::gmd::gray_down_kernel, dim3((unsigned)((HW + 255) / 256), S), dim3(256), 0, st, d, frames);
   else
     hipLaunchKernelGGL(yk::gmd::gray_kernel, dim3((unsigned)((HW + 255) / 256), S), dim3(256), 0, st, d, frames);
-  for (int l = 1; l <= G.levels; ++l)
+  if (YK_GMD_DIAG & 16) d.diag_expect += (int)((HW + 255) / 256) * S * 4;
+  for (int l = 1; l <= G.levels; ++l) {
     hipLaunchKernelGGL(yk::gmd::pyrdown_kernel, dim3((G.lw[l] + 15) / 16, (G.lh[l] + 15) / 16, S), dim3(256), 0, st,
                        d, l);
+    if (YK_GMD_DIAG & 16) d.diag_expect += ((G.lw[l] + 15) / 16) * ((G.lh[l] + 15) / 16) * S * 4;
+  }
   hipLaunchKernelGGL(yk::gmd::scharr_kernel, dim3((G.lw[0] + 15) / 16, (G.lh[0] + 15) / 16, S * (G.levels + 1)),
                      dim3(256), 0, st, d);
   if (g->frames > 0) {
@@ -1571,7 +1643,8 @@ static void gmd_front(yk_gmd* g, const uint8_t* frames, hipStream_t st) {
       hipLaunchKernelGGL(yk::gmd::select_top_kernel, dim3(S), dim3(yk::gmd::NTS), yk::gmd::SEL_LDS, st, d);
     else
       hipLaunchKernelGGL(yk::gmd::select_kernel, dim3(S), dim3(yk::gmd::NTS), yk::gmd::SEL_LDS, st, d);
-    hipLaunchKernelGGL(yk::gmd::lk_kernel, dim3(d.maxc / 4, S), dim3(256), 0, st, d);
+    hipLaunchKernelGGL(yk::gmd::lk_kernel<0>, dim3(d.maxc / 4, S), dim3(256), 0, st, d);
+    if (YK_GMD_DIAG & 8) hipLaunchKernelGGL(yk::gmd::lk_kernel<1>, dim3(d.maxc / 4, S), dim3(256), 0, st, d);
   }
 }
 

@@ -2268,6 +2268,28 @@ __global__ void track_create_kernel(Dev g, int s, const double* in_box, int trac
   *status = 0;
 }
 
+// Tracker output pushed to page-locked host memory by the device (yk_tracker_download_async): one
+// workgroup per stream writes its count, its stats and only its LIVE rows (count[s] of them, known
+// here and not on the host) with 8-byte stores through the host-mapped pointers -- one small
+// launch instead of three copy-engine / blit transfers of every row slot.
+__global__ void __launch_bounds__(256) push_out_kernel(Dev g, int S, int T, int rows_per_stream, yk_track_out* rows,
+                                                       int32_t* counts, yk_tracker_stats* stats) {
+  const int s = blockIdx.x;
+  if (s >= S) return;
+  const int c = g.counts[s];
+  if (threadIdx.x == 0) {
+    counts[s] = c;
+    if (stats) stats[s] = g.stats[s];
+  }
+  if (!rows) return;
+  const int n = c < rows_per_stream ? c : rows_per_stream;
+  static_assert(sizeof(yk_track_out) % 8 == 0, "8-byte row copies");
+  constexpr int W = (int)(sizeof(yk_track_out) / 8);
+  const uint2* src = (const uint2*)(g.rows + (size_t)s * T);
+  uint2* dst = (uint2*)(rows + (size_t)s * T);
+  for (int i = threadIdx.x; i < n * W; i += blockDim.x) dst[i] = src[i];
+}
+
 }  // namespace trk
 }  // namespace yk
 
@@ -2505,17 +2527,24 @@ int yk_tracker_download_async(yk_tracker* t, yk_track_out* host_rows, int32_t* h
                "yk_tracker_download_async: rows_per_stream out of [0, max_tracks]");
   yk::DeviceGuard guard(t->ctx->device);
   hipStream_t st = (hipStream_t)stream;
-  YK_HIP(hipMemcpyAsync(host_counts, t->dev.counts, t->S * sizeof(int32_t), hipMemcpyDeviceToHost, st));
-  if (host_stats)
-    YK_HIP(hipMemcpyAsync(host_stats, t->dev.stats, t->S * sizeof(yk_tracker_stats), hipMemcpyDeviceToHost, st));
-  if (host_rows && rows_per_stream > 0) {
-    const size_t pitch = (size_t)t->dev.T * sizeof(yk_track_out);
-    if (rows_per_stream == t->dev.T)
-      YK_HIP(hipMemcpyAsync(host_rows, t->dev.rows, pitch * t->S, hipMemcpyDeviceToHost, st));
-    else
-      YK_HIP(hipMemcpy2DAsync(host_rows, pitch, t->dev.rows, pitch, rows_per_stream * sizeof(yk_track_out), t->S,
-                              hipMemcpyDeviceToHost, st));
+  // the device writes the host buffers itself: they must be page-locked memory mapped into the
+  // device's address space; the kernel gets the device-side address of each (never a raw host one)
+  void* dp[3] = {nullptr, nullptr, nullptr};
+  const void* hp[3] = {host_rows, host_counts, host_stats};
+  for (int i = 0; i < 3; ++i) {
+    if (!hp[i] || (i == 0 && rows_per_stream == 0)) continue;
+    hipPointerAttribute_t at;
+    const hipError_t e = hipPointerGetAttributes(&at, hp[i]);
+    if (e != hipSuccess || at.type != hipMemoryTypeHost || !at.devicePointer) {
+      (void)hipGetLastError();
+      yk::set_error("yk_tracker_download_async: host buffers must be page-locked, device-mapped memory");
+      return YK_ERR_ARG;
+    }
+    dp[i] = at.devicePointer;
   }
+  hipLaunchKernelGGL(yk::trk::push_out_kernel, dim3(t->S), dim3(256), 0, st, t->dev, t->S, t->dev.T,
+                     rows_per_stream, (yk_track_out*)dp[0], (int32_t*)dp[1], (yk_tracker_stats*)dp[2]);
+  YK_HIP(hipGetLastError());
   return YK_OK;
 }
 

@@ -97,6 +97,13 @@ class StreamPipeline:
             self.gmd = Mo.BatchedMotionDetector(self.S, frame_hw[0], frame_hw[1], motion_method, self.device)
         self._ev_gmd = [torch.cuda.Event() for _ in range(self.D)]  # slot's frames read by the motion detector
         self._gmd_pending = [False] * self.D
+        # host-frame prefetch (run(..., next_frames=)): the next step's upload runs on its own copy
+        # stream one step ahead, behind the forward that last read that slot
+        self.copy_stream = torch.cuda.Stream(dev) if self.D > 1 else None
+        self._ev_fwd = [torch.cuda.Event() for _ in range(self.D)]  # slot's last forward enqueued
+        self._fwd_pending = [False] * self.D
+        self._ev_copy = [torch.cuda.Event() for _ in range(self.D)]
+        self._prefetched = [None] * self.D  # data_ptr of the host frames being uploaded into the slot
 
     @property
     def dets(self) -> torch.Tensor:
@@ -152,6 +159,8 @@ class StreamPipeline:
         with torch.cuda.stream(cur):
             self.models[s].detect(self.frame_slots[s], self.conf, self.iou, self.max_det, self._dets[k],
                                   self._counts[k], graph=bool(self.graph))
+        self._ev_fwd[s].record(cur)
+        self._fwd_pending[s] = True
         if self.pipelined:
             self._ev_det[k].record(cur)
             self.trk_stream.wait_event(self._ev_det[k])
@@ -182,26 +191,52 @@ class StreamPipeline:
         """Wait for every launched step (detector and tracker streams)."""
         torch.cuda.synchronize(self.device)
 
-    def run(self, frames: torch.Tensor):
+    def run(self, frames: torch.Tensor, next_frames: torch.Tensor | None = None):
         """frames [S, H, W, 3] uint8 (device, or page-locked host memory: the frame in host memory
         the driver loop starts from) -> one step.  The copy runs on the slot's detector stream,
         after that slot's previous forward has read its frames, and after whatever the caller's
         current stream enqueued before this call (the producer of `frames`); the forward that reads
         the slot follows it on the same stream.  A host source must stay unchanged until that copy
-        has run (the caller's buffer; see download_async for the matching output side)."""
+        has run (the caller's buffer; see download_async for the matching output side).
+
+        next_frames (page-locked host, inflight > 1): the NEXT step's frames, already decoded (a
+        video driver reads ahead).  Their upload is issued now, on the copy stream, into the next
+        step's slot once the forward that last read that slot has run; the next run() is then
+        handed the same tensor and its forward only waits for that copy's event.  Every frame still
+        crosses PCIe once, inside the caller's loop; the upload of step t + 1 overlaps step t."""
         s = self._slot(self._k)
         st = self._stream(s)
         cur = torch.cuda.current_stream(self.device)
-        if st != cur:
-            st.wait_stream(cur)
-            if frames.is_cuda:
-                frames.record_stream(st)  # the allocator keeps `frames` alive until the copy ran
-        if self._gmd_pending[s]:  # the motion detector (tracker stream) still reads this slot's frames
-            st.wait_event(self._ev_gmd[s])
-            self._gmd_pending[s] = False
-        with torch.cuda.stream(st):
-            self.frame_slots[s].copy_(frames, non_blocking=True)
+        if self._prefetched[s] is not None:
+            if frames.is_cuda or frames.data_ptr() != self._prefetched[s]:
+                raise ValueError("run(): the previous call prefetched other frames for this step (next_frames)")
+            st.wait_event(self._ev_copy[s])
+            self._prefetched[s] = None
+        else:
+            if st != cur:
+                st.wait_stream(cur)
+                if frames.is_cuda:
+                    frames.record_stream(st)  # the allocator keeps `frames` alive until the copy ran
+            if self._gmd_pending[s]:  # the motion detector (tracker stream) still reads this slot's frames
+                st.wait_event(self._ev_gmd[s])
+                self._gmd_pending[s] = False
+            with torch.cuda.stream(st):
+                self.frame_slots[s].copy_(frames, non_blocking=True)
         self.step()
+        if next_frames is not None:
+            if next_frames.is_cuda or self.copy_stream is None:
+                raise ValueError("next_frames: page-locked host frames and inflight > 1")
+            s2 = self._slot(self._k)
+            cs = self.copy_stream
+            if self._fwd_pending[s2]:  # the forward that last read slot s2
+                cs.wait_event(self._ev_fwd[s2])
+            if self._gmd_pending[s2]:  # and the motion detector's read of it
+                cs.wait_event(self._ev_gmd[s2])
+                self._gmd_pending[s2] = False
+            with torch.cuda.stream(cs):
+                self.frame_slots[s2].copy_(next_frames, non_blocking=True)
+            self._ev_copy[s2].record(cs)
+            self._prefetched[s2] = next_frames.data_ptr()
 
     def download_async(self, rows, counts, stats, rows_per_stream=None):
         """Enqueue the tracker output of the most recent step into page-locked host buffers
