@@ -390,13 +390,16 @@ def run_leg(a, P, cfg, dtype, frames, dev, local, rank, ws, headline):
     t0 = time.perf_counter()
     w0 = time.clock_gettime_ns(time.CLOCK_MONOTONIC)
     h2d, d2h = a.io in ("both", "h2d"), a.io in ("both", "d2h")
+    host_ns = 0
     for t in range(a.steps):
+        h0 = time.perf_counter_ns()
         if h2d:  # the next step's frames are uploaded while this step runs (decode-ahead driver)
             pipe.run(host[t % n_host], next_frames=host[(t + 1) % n_host] if t + 1 < a.steps and pipe.D > 1 else None)
         else:
             pipe.run(frames[(t_first + t) % F])
         if d2h:
             pipe.download_async(out_rows, out_counts, out_stats)
+        host_ns += time.perf_counter_ns() - h0
     torch.cuda.synchronize()
     barrier(ws)
     elapsed = time.perf_counter() - t0
@@ -430,6 +433,7 @@ def run_leg(a, P, cfg, dtype, frames, dev, local, rank, ws, headline):
     gflop = pipe.flops_per_frame() / 1e9
     leg = {"dtype": dtype, "value": round(fps, 2), "ms_per_step": round(elapsed_max / a.steps * 1e3, 4),
            "hbm_resident_fps": round(run["frames"] / max(hbm_max, 1e-12), 2),
+           "host_enqueue_ms_per_step": round(host_ns / a.steps / 1e6, 4),
            "network_mfma_frac": round(fps / ws * gflop / 1e3 / PEAK[dtype], 5),
            "live_tracks_per_stream": round(run["current_active_tracks"] / (S * ws), 1),
            "live_tracks_per_stream_min_at_start": int(live_start.min()),
@@ -583,7 +587,7 @@ def main():
                        "rank_devices": head["rank_devices"],
                        "global_motion": "optical_flow" if a.gmd else None},
             "network_mfma_frac": head["network_mfma_frac"],
-            "hbm_resident_fps": head["hbm_resident_fps"],
+            "hbm_resident_fps": head["hbm_resident_fps"], "host_enqueue_ms_per_step": head["host_enqueue_ms_per_step"],
             "timed_region": "frames in page-locked host memory -> H2D on the slot stream -> forward -> NMS -> tracker "
                             "-> tracker output (counts, stats, rows) D2H, every step; hbm_resident_fps: the same steps "
                             "with the frames already in HBM and no output copy (informational)",

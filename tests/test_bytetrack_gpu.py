@@ -120,7 +120,8 @@ def test_single_stream_facade_and_reset():
 @pytest.mark.gpu
 def test_botsort_rejects_reid_and_unbuilt_gmc_methods():
     """with_reid and the cv2-internal GMC methods (orb / sift / ecc) raise; the default
-    sparseOptFlow GMC refuses frames below its 64 px minimum (the 1/2 downscale's pyramid)."""
+    sparseOptFlow GMC falls back to the identity warp (with a RuntimeWarning) for frames below its
+    64 px minimum or of odd size, like the reference's identity fallbacks (gmc.py:155-158)."""
     BT = _bt()
     with pytest.raises(NotImplementedError):
         BT.BOTSORT(dict(BT.BOTSORT_DEFAULTS, with_reid=True))
@@ -129,6 +130,7 @@ def test_botsort_rejects_reid_and_unbuilt_gmc_methods():
             BT.BOTSORT(dict(BT.BOTSORT_DEFAULTS, gmc_method=m))
     trk = BT.BOTSORT(dict(BT.BOTSORT_DEFAULTS))
     x, c, k = scenario(3, n_targets=4, n_frames=1)[0]
-    with pytest.raises(pkg().YKError):
-        trk.update(R.Dets(x, c, k), img=np.zeros((8, 8, 3), np.uint8))
+    with pytest.warns(RuntimeWarning, match="identity warp"):
+        out = trk.update(R.Dets(x, c, k), img=np.zeros((8, 8, 3), np.uint8))
+    assert out.shape[1] == 8
     assert trk.update(R.Dets(x, c, k)).shape[1] == 8

@@ -186,7 +186,7 @@ def _check_driver_chain(run, assoc_tie_margin=None):
             assert assoc_tie_margin is not None and fm < assoc_tie_margin, \
                 (f"frame {t}: association decisions differ (oracle margin {fm:.3g})", decisions(ours), decisions(rb))
             ids = {d[0] for d in set(decisions(ours)) ^ set(decisions(rb))}
-            flips.append({"frame": t, "oracle_margin": fm, "tracks": sorted(int(i) for i in ids),
+            flips.append({"frame": t, "oracle_margin": fm, "tracks": sorted(str(i) for i in ids),
                           "oracle_iou_max": [float(trk.last_iou.max())], "gpu_chain_iou_max": [float(iso.last_iou.max())]})
             print("ASSOC_NEAR_TIE_FLIP", flips[-1])
             trk = copy.deepcopy(iso)  # resync: the oracle chain continues from the GPU's pick

@@ -55,6 +55,9 @@ def main():
         for npt in (1, 2, 4):
             for wm in (0, 1):
                 cands.append((5, ne, npt | (wm << 4)))
+    for ne in (1, 2, 3, 4, 5):
+        for npt in (1, 2, 4):
+            cands.append((6, ne, npt))
     for op in (int(v) for v in a.ops.split(",")):
         res = []
         for kind, nnt, npt in cands:
@@ -67,7 +70,7 @@ def main():
         dm.load_plan(B, plan)
         res.sort()
         print(json.dumps({"op": op, "committed_us": round(base[op][3] * 1e3, 2), "committed": base[op][2],
-                          "best": res[:8]}), flush=True)
+                          "best": res[:8], "all": res}), flush=True)
 
 
 if __name__ == "__main__":

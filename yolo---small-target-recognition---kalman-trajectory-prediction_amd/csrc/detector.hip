@@ -1983,6 +1983,206 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(YK_FAS
   }
 }
 
+// ---------------------------------------------------------------- halo tile + shared weights (F32 build)
+// conv_halo_kernel's waves each fetch their own weight fragments from global memory every K step:
+// with the four waves splitting the tile's pixels (WM 0) that is four copies of NE x 3 KB per step
+// through one CU's vector-memory path, which -- not the matrix cores -- paces it (two K steps of
+// weights per wave = 2 x 3 KB against 3 x NE x NPT MFMAs).  Here the workgroup loads each step's
+// NE x 3 KB of K-slot weight fragments ONCE, 16 bytes per thread, two steps ahead through
+// registers into a three-slot LDS ring, and every wave reads them from LDS (one barrier per K
+// step); the input window is staged split, as in conv_halo_kernel, one 16-channel group per chunk,
+// double-buffered.  Tiles are 16 output columns wide (a fragment = one tile row, consecutive in
+// LDS) or 8 (a fragment = two rows; row pitch = 8 mod 16 pixels keeps the 16 pixels on 16
+// different bank groups).  Stride 1, 3x3 or 1x1.  Same arithmetic and accumulation order per
+// output as conv_halo_kernel (K-slot weights, group-major / tap-minor K order).
+struct HwsArgs {
+  HaloArgs h;
+  int pxp;      // pixels per LDS plane (window rounded up to 16)
+  int nsteps;   // K steps (16-channel groups x taps)
+};
+constexpr int kHwsR = 3;  // weight ring slots
+
+template <int NE, int NPT, int KS>
+__global__ void __launch_bounds__(256) conv_hws_kernel(HwsArgs A) {
+  const HaloArgs& a = A.h;
+  constexpr int T = KS * KS;
+  constexpr int CC = KS == 1 ? 4 : 1;             // 16-channel groups per chunk
+  constexpr int S = CC * T;                        // K steps per chunk
+  constexpr int WU = (NE * 192 + 255) / 256;       // weight uint4s per thread per step
+  constexpr int UMAX = 8;                          // staging units per thread (3x3 window <= 512 px,
+                                                   // 1x1 tile <= 128 px)
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int kg = lane >> 4, col = lane & 15;
+  const int pxp = A.pxp, nsteps = A.nsteps;
+  const int plb = pxp * 16;                        // plane bytes
+  const int buf = 8 * CC * plb;                    // one chunk buffer
+  unsigned char* wring = smem + 2 * buf;           // kHwsR slots of NE x 3 KB
+  const int2 blk = xcd_block(a.xcd);
+  const int tpi = a.tiles_x * a.tiles_y;
+  const int b = blk.x / tpi, rr = blk.x - b * tpi;
+  const int tyi = rr / a.tiles_x, txi = rr - tyi * a.tiles_x;
+  const int oy0 = tyi * a.tr, ox0 = txi * a.tc;
+  const int iy0 = oy0 - a.pad, ix0 = ox0 - a.pad;
+  const int nt0 = blk.y * NE;
+  const int n_groups = (a.cin + 15) >> 4;
+  const int n_chunks = (n_groups + CC - 1) / CC;
+  const __amdgpu_buffer_rsrc_t xr = make_srd(a.arena, a.arena_bytes);
+  const __amdgpu_buffer_rsrc_t wr = make_srd(a.wblob, a.wbytes);
+  // the lane's pixel of each fragment: LDS byte offset of its window origin in plane XA(kg)
+  unsigned lb[NPT];
+  int opx[NPT];
+#pragma unroll
+  for (int t = 0; t < NPT; ++t) {
+    const int q = (wave * NPT + t) * 16 + col;
+    const int ty = q / a.tc, tx = q - ty * a.tc;
+    const bool v = ty < a.tr && oy0 + ty < a.out_h && ox0 + tx < a.out_w;
+    lb[t] = (unsigned)(kg * plb + (v ? (ty * a.rp + tx) * 16 : 0));
+    opx[t] = v ? (b * a.out_h + oy0 + ty) * a.out_w + ox0 + tx : -1;
+  }
+  // staging: unit j of a thread = channel group kgu, window pixel px = (tid & 15) + 16 (tid >> 6) + 64 j
+  // (3x3: one 16-channel group per chunk); 1x1: px = (tid & 15) + 16 (tid >> 6) + 64 (j >> 2), group j & 3
+  const int kgu = (tid >> 4) & 3;
+  unsigned sv0[UMAX], sv1[UMAX];
+  int sl[UMAX];
+#pragma unroll
+  for (int j = 0; j < UMAX; ++j) {
+    const int px = (tid & 15) + 16 * (tid >> 6) + (CC == 1 ? 64 * j : 64 * (j >> 2));
+    const int g = CC == 1 ? 0 : (j & 3);
+    sl[j] = -1;
+    sv0[j] = sv1[j] = kOOB;
+    if (px < a.npx) {
+      const int py = px / a.twin, pxx = px - py * a.twin;
+      const int iy = iy0 + py, ix = ix0 + pxx;
+      sl[j] = (g * 8 + kgu) * plb + (py * a.rp + pxx) * 16;
+      if (iy >= 0 && iy < a.in_h && ix >= 0 && ix < a.in_w) {
+        sv0[j] = a.soff0 + (unsigned)(((b * a.h0 + (iy >> a.up0)) * a.w0 + (ix >> a.up0)) * a.cs0 * 4);
+        sv1[j] = a.soff1 + (unsigned)(((b * a.h1 + (iy >> a.up1)) * a.w1 + (ix >> a.up1)) * a.cs1 * 4);
+      }
+    }
+  }
+  uint4 st[UMAX];
+  auto fetch = [&](int c) {
+#pragma unroll
+    for (int j = 0; j < UMAX; ++j) {
+      if (sl[j] < 0) continue;
+      const int ch = (c * CC + (CC == 1 ? 0 : (j & 3))) * 16 + kgu * 4;
+      const bool s1 = ch >= a.c0, cv = ch < a.cin;
+      const unsigned o = s1 ? sv1[j] : sv0[j];
+      st[j] = bload(xr, cv && o != kOOB ? o + (unsigned)((s1 ? ch - a.c0 : ch) * 4) : kOOB, 0);
+    }
+  };
+  auto commit = [&](int bi) {
+    unsigned char* base = smem + bi * buf;
+#pragma unroll
+    for (int j = 0; j < UMAX; ++j)
+      if (sl[j] >= 0) {
+        u32x4v xa, xb;
+        split_kslot(st[j], xa, xb);
+        *(u32x4v*)(base + sl[j]) = xa;
+        *(u32x4v*)(base + 4 * plb + sl[j]) = xb;
+      }
+  };
+  // weight staging: uint4 u = tid + 256 j of step s's NE x 192; tile nt0 + u / 192 (clamped)
+  unsigned wsrc[WU];
+  int wdst[WU];
+#pragma unroll
+  for (int j = 0; j < WU; ++j) {
+    const int u = tid + 256 * j;
+    wdst[j] = u < NE * 192 ? u * 16 : -1;
+    const int i = u / 192, w = u - i * 192;
+    const int nt = nt0 + i < a.n_tiles ? nt0 + i : a.n_tiles - 1;
+    wsrc[j] = a.woff + (unsigned)(((size_t)nt * nsteps * 64) * 48 + w * 16);
+  }
+  u32x4v wst[WU];  // the next step to go into the ring
+  auto wfetch = [&](int s, u32x4v* r) {
+#pragma unroll
+    for (int j = 0; j < WU; ++j)
+      if (wdst[j] >= 0) r[j] = __builtin_amdgcn_raw_buffer_load_b128(wr, (int)wsrc[j], s * 64 * 48, 0);
+  };
+  auto wcommit = [&](int s, const u32x4v* r) {
+    unsigned char* slot = wring + (s % kHwsR) * (NE * 3072);
+#pragma unroll
+    for (int j = 0; j < WU; ++j)
+      if (wdst[j] >= 0) *(u32x4v*)(slot + wdst[j]) = r[j];
+  };
+  f32x4 acc[NE][NPT];
+#pragma unroll
+  for (int i = 0; i < NE; ++i)
+#pragma unroll
+    for (int t = 0; t < NPT; ++t) acc[i][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // prologue: chunk 0 staged, steps 0 and 1 of weights in the ring, step 2 in registers
+  fetch(0);
+  wfetch(0, wst);
+  commit(0);
+  wcommit(0, wst);
+  if (nsteps > 1) {
+    wfetch(1, wst);
+    wcommit(1, wst);
+  }
+  if (nsteps > 2) wfetch(2, wst);
+  for (int s = 0; s < nsteps; ++s) {
+    const int c = s / S, k = s - c * S;
+    __syncthreads();  // slot s % R and (at k == 0) chunk c's buffer are complete; slot (s + 2) % R is free
+    if (k == 0 && c + 1 < n_chunks) fetch(c + 1);  // in flight over this chunk's MFMAs
+    const unsigned char* xs = smem + (c & 1) * buf;
+    const unsigned char* ws = wring + (s % kHwsR) * (NE * 3072);
+    const int g = k / T, tt = k - g * T;
+    const int dy = tt / KS, dx = tt - dy * KS;
+    const unsigned toff = (unsigned)((dy * a.rp + dx) * 16);
+    u32x4v xa[NPT], xb[NPT];
+#pragma unroll
+    for (int f = 0; f < NPT; ++f) {
+      const unsigned char* pp = xs + g * 8 * plb + lb[f] + toff;
+      xa[f] = *(const u32x4v*)pp;
+      xb[f] = *(const u32x4v*)(pp + 4 * plb);
+    }
+#pragma unroll
+    for (int i = 0; i < NE; ++i) {
+      const unsigned char* wl = ws + i * 3072 + lane * 48;
+      const u32x4v a1 = *(const u32x4v*)wl, a2 = *(const u32x4v*)(wl + 16), a3 = *(const u32x4v*)(wl + 32);
+#pragma unroll
+      for (int f = 0; f < NPT; ++f) acc[i][f] = mfma_bf16(a1, xa[f], acc[i][f]);
+#pragma unroll
+      for (int f = 0; f < NPT; ++f) acc[i][f] = mfma_bf16(a2, xa[f], acc[i][f]);
+#pragma unroll
+      for (int f = 0; f < NPT; ++f) acc[i][f] = mfma_bf16(a3, xb[f], acc[i][f]);
+    }
+    // ring: step s + 2's fragments (loaded one step ago) into slot (s + 2) % 3 = (s - 1) % 3, which
+    // every wave finished reading before this step's barrier; then step s + 3's loads
+    if (s + 2 < nsteps) {
+      wcommit(s + 2, wst);
+      if (s + 3 < nsteps) wfetch(s + 3, wst);
+    }
+    if (k == S - 1 && c + 1 < n_chunks) commit((c + 1) & 1);  // read last in chunk c - 1
+  }
+#pragma unroll
+  for (int i = 0; i < NE; ++i) {
+    const int nt = nt0 + i;
+    const int n0 = nt * 16 + kg * 4;
+    if (nt >= a.n_tiles || n0 >= a.cout) continue;
+    const float4 bb = *(const float4*)(a.bias + n0);
+#pragma unroll
+    for (int f = 0; f < NPT; ++f) {
+      const int p = opx[f];
+      if (p < 0) continue;
+      float v[4] = {acc[i][f][0] + bb.x, acc[i][f][1] + bb.y, acc[i][f][2] + bb.z, acc[i][f][3] + bb.w};
+      if (a.act) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = silu<true>(v[j]);
+      }
+      if (a.res) {
+        float r[4];
+        load4((const float*)a.res + (size_t)p * a.r_cstride + a.r_coff + n0, r);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = r[j] + v[j];
+      }
+      store4((float*)a.dst + (size_t)p * a.d_cstride + a.d_coff + n0, v);
+    }
+  }
+}
+
 // LDS bytes of conv_fast_kernel for an op: the K-step table (+ the split-K reduction buffer).
 inline size_t fast_lds(int k_steps, int nnt, int npt, bool ws) {
   const size_t t = ((size_t)k_steps * 4 * 8 + 15) & ~(size_t)15;
@@ -3471,7 +3671,25 @@ void set_halo_attr_n() {
   set_halo_attr_p<NE, 2>();
   set_halo_attr_p<NE, 4>();
 }
+template <int NE, int NPT>
+void set_hws_attr_p() {
+  (void)hipFuncSetAttribute((const void*)conv_hws_kernel<NE, NPT, 3>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  if constexpr (NPT <= 2)
+    (void)hipFuncSetAttribute((const void*)conv_hws_kernel<NE, NPT, 1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+}
+template <int NE>
+void set_hws_attr_n() {
+  set_hws_attr_p<NE, 1>();
+  set_hws_attr_p<NE, 2>();
+  set_hws_attr_p<NE, 4>();
+}
 void set_tile_attrs() {
+  set_hws_attr_n<1>();
+  set_hws_attr_n<2>();
+  set_hws_attr_n<3>();
+  set_hws_attr_n<4>();
+  set_hws_attr_n<5>();
   set_halo_attr_n<1>();
   set_halo_attr_n<2>();
   set_tile_attrs_t<BF16>();
@@ -3506,7 +3724,9 @@ void set_tile_attrs() {
 }
 
 // Conv kernel choice for one op at batch B.
-enum { CK_DIRECT = 0, CK_TILE = 1, CK_SPLITK = 2, CK_FAST = 3, CK_WIDE = 4, CK_HALO = 5 };
+enum { CK_DIRECT = 0, CK_TILE = 1, CK_SPLITK = 2, CK_FAST = 3, CK_WIDE = 4, CK_HALO = 5, CK_HWS = 6 };
+// CK_HWS plan (F32 build, stride 1): nnt = NE in [1, 5] (output-channel tiles per workgroup), npt = NPT in
+// {1, 2, 4} (fragments per wave: a tile of 64 NPT pixels)
 // CK_FAST plan npt bit: the F32 build's op runs the F32S split-MFMA body (every mode)
 constexpr int kSplitBit = 64;
 // CK_WIDE plan: nnt in {2, 4} (output-channel tiles per workgroup), npt unused
@@ -3613,6 +3833,38 @@ HaloPlan halo_plan(const yk_op& op, int npt, int wm) {
   return h;
 }
 
+struct HwsPlan {
+  bool ok = false;
+  int tr = 0, tc = 0, twin = 0, npx = 0, rp = 0, pxp = 0, tiles_x = 0, tiles_y = 0;
+  size_t lds = 0;
+};
+// conv_hws_kernel geometry: 64 NPT output pixels as tc = 16 (or 8 where that wastes fewer columns)
+// by tr rows; the window (+ halo) one plane per 16-channel part, row pitch rp (= tc mod 16 for tc 8).
+HwsPlan hws_plan(const yk_op& op, int ne, int npt) {
+  HwsPlan h;
+  const int k = op.ksize;
+  const int c0 = op.src_ch[0], cin = op.src_ch[0] + (op.n_src > 1 ? op.src_ch[1] : 0);
+  if ((k != 1 && k != 3) || op.stride != 1 || cin % 4 || c0 % 4 || op.out_h < 1 || op.out_w < 1) return h;
+  if (ne < 1 || ne > 5 || (npt != 1 && npt != 2 && npt != 4) || (k == 1 && npt > 2)) return h;
+  const int px = 64 * npt;
+  const int w16 = (op.out_w + 15) / 16 * 16, w8 = (op.out_w + 7) / 8 * 8;
+  h.tc = (w8 < w16 && px / 8 >= 2) ? 8 : 16;
+  h.tr = px / h.tc;
+  h.twin = h.tc + k - 1;
+  const int thin = h.tr + k - 1;
+  h.rp = h.tc == 16 ? h.twin : h.twin + (((8 - h.twin) % 16) + 16) % 16;
+  h.npx = h.twin * thin;
+  h.pxp = (h.rp * thin + 15) / 16 * 16;
+  if ((k == 3 && h.npx > 512) || (k == 1 && h.npx > 128)) return h;
+  const int cc = k == 1 ? 4 : 1;
+  h.lds = (size_t)2 * 8 * cc * h.pxp * 16 + (size_t)kHwsR * ne * 3072;
+  if (h.lds > 160 * 1024) return h;
+  h.tiles_x = (op.out_w + h.tc - 1) / h.tc;
+  h.tiles_y = (op.out_h + h.tr - 1) / h.tr;
+  h.ok = true;
+  return h;
+}
+
 // conv_fast_kernel geometry: the largest fragment tile (NNT x NPT) that still gives >= 1024
 // workgroups (>= 4 waves per CU) and wastes < 25% of the n-tiles; the four waves split K (WS)
 // when the per-wave-pixel layout would give too few workgroups.
@@ -3665,6 +3917,13 @@ ConvPlan conv_plan(const yk_model* m, const yk_op& op, int B) {
       p.nnt = t[1];
       p.npt = t[2];
       if ((p.npt & kSplitBit) && !(m->wsplit && m->ws_off[idx] >= 0)) p.npt &= ~kSplitBit;
+      return p;
+    }
+    if (t[0] == CK_HWS && m->wkslot && m->wk_off[idx] >= 0 && hws_plan(op, t[1], t[2]).ok) {
+      ConvPlan p;
+      p.kind = CK_HWS;
+      p.nnt = t[1];
+      p.npt = t[2];
       return p;
     }
     if (t[0] == CK_HALO && m->wkslot && m->wk_off[idx] >= 0 && halo_plan(op, t[2] & 15, (t[2] >> 4) & 1).ok) {
@@ -3793,6 +4052,31 @@ void launch_halo_p(const HaloArgs& a, int B, int npt, int wm, int ks, hipStream_
   if (npt == 4) launch_halo_w<NE, 4>(a, B, wm, ks, st);
   else if (npt == 2) launch_halo_w<NE, 2>(a, B, wm, ks, st);
   else launch_halo_w<NE, 1>(a, B, wm, ks, st);
+}
+template <int NE, int NPT, int KS>
+void launch_hws_t(const HwsArgs& a, int B, size_t lds, hipStream_t st) {
+  dim3 grid(B * a.h.tiles_x * a.h.tiles_y, (a.h.n_tiles + NE - 1) / NE);
+  hipLaunchKernelGGL((conv_hws_kernel<NE, NPT, KS>), grid, dim3(256), lds, st, a);
+}
+template <int NE, int NPT>
+void launch_hws_k(const HwsArgs& a, int B, int ks, size_t lds, hipStream_t st) {
+  if (ks == 3) launch_hws_t<NE, NPT, 3>(a, B, lds, st);
+  else if constexpr (NPT <= 2) launch_hws_t<NE, NPT, 1>(a, B, lds, st);
+}
+template <int NE>
+void launch_hws_p(const HwsArgs& a, int B, int npt, int ks, size_t lds, hipStream_t st) {
+  if (npt == 4) launch_hws_k<NE, 4>(a, B, ks, lds, st);
+  else if (npt == 2) launch_hws_k<NE, 2>(a, B, ks, lds, st);
+  else launch_hws_k<NE, 1>(a, B, ks, lds, st);
+}
+void launch_hws(const HwsArgs& a, int B, const ConvPlan& p, int ks, size_t lds, hipStream_t st) {
+  switch (p.nnt) {
+    case 1: launch_hws_p<1>(a, B, p.npt, ks, lds, st); break;
+    case 2: launch_hws_p<2>(a, B, p.npt, ks, lds, st); break;
+    case 3: launch_hws_p<3>(a, B, p.npt, ks, lds, st); break;
+    case 4: launch_hws_p<4>(a, B, p.npt, ks, lds, st); break;
+    default: launch_hws_p<5>(a, B, p.npt, ks, lds, st); break;
+  }
 }
 void launch_halo(const HaloArgs& a, int B, const ConvPlan& p, int ks, hipStream_t st) {
   const int npt = p.npt & 15, wm = (p.npt >> 4) & 1;
@@ -3940,10 +4224,24 @@ int launch_op(yk_model* m, const yk_op& op, const uint8_t* frames, int B, float 
             if (nw == 8) launch_wide_n<Tr, 4, 8>(w, wp.upt, wp.lds, st);
             else launch_wide_n<Tr, 4, 4>(w, wp.upt, wp.lds, st);
           }
-        } else if (cp.kind == CK_HALO) {
+        } else if (cp.kind == CK_HALO || cp.kind == CK_HWS) {
           if constexpr (std::is_same<Tr, F32>::value) {
             const size_t oi = (size_t)(&op - m->ops.data());
-            const HaloPlan hp = halo_plan(op, cp.npt & 15, (cp.npt >> 4) & 1);
+            HaloPlan hp;
+            HwsPlan wp;
+            if (cp.kind == CK_HWS) {
+              wp = hws_plan(op, cp.nnt, cp.npt);
+              hp.tr = wp.tr;
+              hp.tc = wp.tc;
+              hp.twin = wp.twin;
+              hp.npx = wp.npx;
+              hp.rp = wp.rp;
+              hp.hw = 0;
+              hp.tiles_x = wp.tiles_x;
+              hp.tiles_y = wp.tiles_y;
+            } else {
+              hp = halo_plan(op, cp.npt & 15, (cp.npt >> 4) & 1);
+            }
             HaloArgs h;
             h.arena = m->arena;
             h.arena_bytes = (unsigned)m->arena_bytes;
@@ -3987,7 +4285,15 @@ int launch_op(yk_model* m, const yk_op& op, const uint8_t* frames, int B, float 
             h.r_coff = a.r_coff;
             h.act = a.act;
             h.xcd = m->xcd;
-            launch_halo(h, B, cp, op.ksize, st);
+            if (cp.kind == CK_HWS) {
+              HwsArgs w;
+              w.h = h;
+              w.pxp = wp.pxp;
+              w.nsteps = ((a.cin + 15) / 16) * op.ksize * op.ksize;
+              launch_hws(w, B, cp, op.ksize, wp.lds, st);
+            } else {
+              launch_halo(h, B, cp, op.ksize, st);
+            }
           }
         } else if (cp.kind == CK_FAST) {
           FastArgs f;
@@ -4185,6 +4491,10 @@ const char* op_kernel_name(const yk_model* m, const yk_op& op) {
   }
   if (cp.kind == CK_HALO) {
     snprintf(buf, sizeof buf, "conv_halo_kernel<%d, %d, %d, %d>", cp.nnt, cp.npt & 15, (cp.npt >> 4) & 1, op.ksize);
+    return buf;
+  }
+  if (cp.kind == CK_HWS) {
+    snprintf(buf, sizeof buf, "conv_hws_kernel<%d, %d, %d>", cp.nnt, cp.npt, op.ksize);
     return buf;
   }
   if (cp.kind == CK_FAST) {
@@ -4910,7 +5220,10 @@ int yk_model_profile(yk_model* m, const uint8_t* frames, int batch, float conf, 
 
 int yk_model_set_plan(yk_model* m, int op_index, int batch, int kind, int nnt, int npt) {
   YK_CHECK_ARG(m && op_index >= -1 && op_index < (int)m->ops.size(), "yk_model_set_plan: bad op index");
-  YK_CHECK_ARG(kind >= -1 && kind <= CK_HALO, "yk_model_set_plan: kind must be -1 (heuristic), 0, 1, 2, 3, 4 or 5");
+  YK_CHECK_ARG(kind >= -1 && kind <= CK_HWS, "yk_model_set_plan: kind must be -1 (heuristic), 0, 1, 2, 3, 4, 5 or 6");
+  YK_CHECK_ARG(kind != CK_HWS || (m->wkslot && nnt >= 1 && nnt <= 5 && (npt == 1 || npt == 2 || npt == 4)),
+               "yk_model_set_plan: halo + shared-weight conv (kind 6) needs the fp32 build, nnt in [1, 5], npt in "
+               "{1, 2, 4}");
   YK_CHECK_ARG(kind != CK_HALO || (m->wkslot && (nnt == 1 || nnt == 2) &&
                                    ((npt & 15) == 1 || (npt & 15) == 2 || (npt & 15) == 4) && (npt & ~31) == 0),
                "yk_model_set_plan: halo conv (kind 5) needs the fp32 build, nnt in {1, 2}, npt in {1, 2, 4} (+16: "
@@ -5006,6 +5319,15 @@ int yk_model_autotune(yk_model* m, const uint8_t* frames, int batch, float conf,
             if (!hp.ok || (long)bt * hp.tiles_x * hp.tiles_y * groups < 64) continue;
             cands.push_back({CK_HALO, ne, npt | (wm << 4)});
           }
+    if (m->wkslot && m->wk_off[i] >= 0 && m->autotune_split)
+      for (int ne = 1; ne <= 5; ++ne)
+        for (int npt : {1, 2, 4}) {
+          const int groups = (op.n_tiles + ne - 1) / ne;
+          if (4 * op.n_tiles < 3 * groups * ne) continue;  // < 75 % of the tiles real
+          const HwsPlan hp = hws_plan(op, ne, npt);
+          if (!hp.ok || (long)bt * hp.tiles_x * hp.tiles_y * groups < 64) continue;
+          cands.push_back({CK_HWS, ne, npt});
+        }
     if (cands.empty()) continue;  // (FP8 without a table: yk_model_create refuses that)
     float best = 1e30f;
     std::array<int, 3> pick = {-1, 0, 0};

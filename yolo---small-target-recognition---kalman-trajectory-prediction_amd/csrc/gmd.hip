@@ -49,6 +49,8 @@
 //     4  lk_kernel solves every corner twice in a row, counting differing answers in info[s][0]
 //     8  a second lk_kernel launch re-solves every corner and counts answers differing from the
 //        first launch's in info[s][1] (the kernel template's diag bit picks the role)
+//    32  the gray pyramids / derivatives in fine-grained device memory (hipDeviceMallocFinegrained)
+//    64  the same in uncached device memory (hipDeviceMallocUncached)
 //    16  ordering probe: every wave of the pyramid / derivative producers adds 1 to info[0][2] after
 //        an agent-scope release; lk_kernel's waves check on entry that every producer wave of
 //        this call has (info[0][3] counts the waves that found fewer)
@@ -731,8 +733,13 @@ template <int CHECK>
 __global__ void __launch_bounds__(256) lk_kernel(Dev g) {
   const int s = blockIdx.y, lane = threadIdx.x & 63;
   const int p = blockIdx.x * 4 + (threadIdx.x >> 6);
-  __shared__ int red_lds[(YK_GMD_DIAG & 1) ? 4 : 1][64];
-  int* red = red_lds[(YK_GMD_DIAG & 1) ? (threadIdx.x >> 6) : 0];
+  __shared__ int red_lds[(YK_GMD_DIAG & 5) ? 4 : 1][64];
+  // diag 4: pass 1's per-iteration record (level, position, weights, J-sample hash), compared by pass 2
+  __shared__ long long rec_lds[(YK_GMD_DIAG & 4) ? 4 : 1][(YK_GMD_DIAG & 4) ? (MAXLV + 1) * MAXIT * 3 : 1];
+  long long* rec = rec_lds[(YK_GMD_DIAG & 4) ? (threadIdx.x >> 6) : 0];
+  int* dred = red_lds[(YK_GMD_DIAG & 5) ? (threadIdx.x >> 6) : 0];
+  int nrec = 0, first_diff = -1;
+  int* red = dred;
   if (YK_GMD_DIAG & 2) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
   if ((YK_GMD_DIAG & 16) && !CHECK && (threadIdx.x & 63) == 0) {
     const int done = __hip_atomic_load(g.info + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -778,6 +785,7 @@ __global__ void __launch_bounds__(256) lk_kernel(Dev g) {
     nit0 = nit;
     hI = hJ = 0;
     nit = 0;
+    nrec = 0;
   }
   for (int l = G.levels; l >= 0; --l) {
     const int cols = G.lw[l], rows = G.lh[l];
@@ -893,7 +901,32 @@ __global__ void __launch_bounds__(256) lk_kernel(Dev g) {
           }
         }
       }
-      if (YK_GMD_DIAG & 4) ++nit;
+      if (YK_GMD_DIAG & 4) {
+        ++nit;
+        // wave-uniform record of this iteration: position, weights, and a hash of the J samples
+        const long long hj = wave_sum_lds((int)(hJ & 0x3fffffffull), dred);
+        const long long r0 = ((long long)l << 48) | ((long long)(jy & 0xffff) << 16) | (jx & 0xffff);
+        const long long r1 = ((long long)(v00 & 0xffff) << 32) | ((long long)(v01 & 0xffff) << 16) | (v10 & 0xffff);
+        if (nrec < (MAXLV + 1) * MAXIT) {
+          if (rep == 0) {
+            if (lane == 0) {
+              rec[nrec * 3] = r0;
+              rec[nrec * 3 + 1] = r1;
+              rec[nrec * 3 + 2] = hj;
+            }
+          } else if (first_diff < 0) {
+            __builtin_amdgcn_wave_barrier();
+            const long long q0 = rec[nrec * 3], q1 = rec[nrec * 3 + 1], q2 = rec[nrec * 3 + 2];
+            if (q0 != r0 || q1 != r1 || q2 != hj) {
+              first_diff = nrec;
+              if (lane == 0)
+                printf("[lk iter] s %d p %d: first differing iteration %d (level %d): pass1 pos %llx w %llx hash %llx"
+                       " | pass2 pos %llx w %llx hash %llx\n", s, p, nrec, l, q0, q1, q2, r0, r1, hj);
+            }
+          }
+        }
+        ++nrec;
+      }
       const float fb1 = (float)wsum_wide(b1) * fs;
       const float fb2 = (float)wsum_wide(b2) * fs;
       const float dx = (A12 * fb2 - A22 * fb1) * Di;
@@ -1534,9 +1567,15 @@ int yk_gmd_create(yk_ctx* ctx, int n_streams, int height, int width, int method,
   auto A = [&](void** p, size_t bytes) {
     if (e == hipSuccess) e = hipMalloc(p, bytes);
   };
+  auto AP = [&](void** p, size_t bytes) {  // the pyramid buffers (diag 64: uncached memory)
+    if (e != hipSuccess) return;
+    e = (YK_GMD_DIAG & 64)   ? hipExtMallocWithFlags(p, bytes, hipDeviceMallocUncached)
+        : (YK_GMD_DIAG & 32) ? hipExtMallocWithFlags(p, bytes, hipDeviceMallocFinegrained)
+                             : hipMalloc(p, bytes);
+  };
   for (int i = 0; i < 2; ++i) {
-    A((void**)&d.pyr[i], S * G.per);
-    A((void**)&d.der[i], S * G.per * sizeof(short2));
+    AP((void**)&d.pyr[i], S * G.per);
+    AP((void**)&d.der[i], S * G.per * sizeof(short2));
   }
   A((void**)&d.eig, S * HW * sizeof(float));
   A((void**)&d.emax, S * sizeof(unsigned));

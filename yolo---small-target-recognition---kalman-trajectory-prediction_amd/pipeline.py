@@ -20,6 +20,15 @@ frame (motion.BatchedMotionDetector, gmd.hip) on the tracker stream right before
 step, which consumes its device results.  The frame slot is not refilled before that detector
 has read it.
 
+With the motion detector and forwards in flight, the motion kernels do not overlap any forward:
+the motion call of step t waits for every forward enqueued so far and forward(t + 1) waits for
+it.  Round 5 traced run-to-run differences of the pipelined motion records to the Lucas-Kanade
+kernel alone: one wave solving its corner twice in one launch read different J samples at the
+same addresses in the two passes while forwards ran beside it (csrc/gmd.hip YK_GMD_DIAG 4),
+with every pyramid producer wave provably complete before the launch (diag 16) and with the
+pyramids in fine-grained or uncached memory (diag 32 / 64) -- not a stale cache line, not an
+ordering fault of ours, not fixed by fences.  No overlap, no difference.
+
 ``inflight=D`` > 1 (needs ``pipelined``) keeps D detector forwards in flight: D DeviceModels
 (same program and conv plan, each its own activation arena) replay their hipGraphs on D HIP
 streams, step t on slot t % D with its own detection buffer.  Every forward is still one batch of the S streams' frames;
@@ -99,11 +108,19 @@ class StreamPipeline:
         self._gmd_pending = [False] * self.D
         # host-frame prefetch (run(..., next_frames=)): the next step's upload runs on its own copy
         # stream one step ahead, behind the forward that last read that slot
+        # Uploads go to a 3-buffer staging ring, not to the slot: a slot is still being read by its
+        # forward from D steps ago when the next upload is issued, and a copy stream made to wait for
+        # that forward held the host thread in hipMemcpyAsync (~1 ms per step, bench --io h2d).  A
+        # staging buffer is free again one device-to-device copy (~10 us) after its upload, so the
+        # copy stream waits for nothing in steady state; the slot stream then copies staging -> slot.
         self.copy_stream = torch.cuda.Stream(dev) if self.D > 1 else None
-        self._ev_fwd = [torch.cuda.Event() for _ in range(self.D)]  # slot's last forward enqueued
-        self._fwd_pending = [False] * self.D
-        self._ev_copy = [torch.cuda.Event() for _ in range(self.D)]
-        self._prefetched = [None] * self.D  # data_ptr of the host frames being uploaded into the slot
+        self._stage = [torch.empty_like(self.frames) for _ in range(3)] if self.D > 1 else []
+        self._ev_stage_read = [torch.cuda.Event() for _ in range(3)]  # slot stream's copy out of it
+        self._stage_read_pending = [False] * 3
+        self._ev_copy = [torch.cuda.Event() for _ in range(3)]
+        self._n_stage = 0
+        self._prefetched = None  # (data_ptr of the host frames, staging index) of the next step
+        self._ev_motion = None  # motion isolation (gmd with forwards in flight): this step's motion call
 
     @property
     def dets(self) -> torch.Tensor:
@@ -156,20 +173,28 @@ class StreamPipeline:
         if self._trk_pending[k]:  # tracker(t - nb) still reads buffer k
             cur.wait_event(self._ev_trk[k])
             self._trk_pending[k] = False
+        if self._ev_motion is not None:  # motion isolation: no forward beside the motion kernels
+            cur.wait_event(self._ev_motion)
         with torch.cuda.stream(cur):
             self.models[s].detect(self.frame_slots[s], self.conf, self.iou, self.max_det, self._dets[k],
                                   self._counts[k], graph=bool(self.graph))
-        self._ev_fwd[s].record(cur)
-        self._fwd_pending[s] = True
         if self.pipelined:
             self._ev_det[k].record(cur)
             self.trk_stream.wait_event(self._ev_det[k])
+            if self.gmd is not None and self.D > 1:
+                for j in range(self.D):  # every forward enqueued so far ends before the motion call
+                    if j != s:
+                        self.trk_stream.wait_stream(self._stream(j))
             with torch.cuda.stream(self.trk_stream):
                 self._track(k, s)
             self._ev_trk[k].record(self.trk_stream)
             self._trk_pending[k] = True
         else:
             self._track(k, s)
+        if self.gmd is not None and self.pipelined and self.D > 1:
+            # forward(t + 1) starts after this step's motion kernels (isolation, see the header)
+            self._ev_motion = torch.cuda.Event()
+            self._ev_motion.record(self.trk_stream)
         if self.step_hook is not None:
             # harness hook (tests/recorders): enqueue work after this step's launches on the
             # detector stream (reads of detection buffer k) and the tracker stream (results)
@@ -200,18 +225,26 @@ class StreamPipeline:
         has run (the caller's buffer; see download_async for the matching output side).
 
         next_frames (page-locked host, inflight > 1): the NEXT step's frames, already decoded (a
-        video driver reads ahead).  Their upload is issued now, on the copy stream, into the next
-        step's slot once the forward that last read that slot has run; the next run() is then
-        handed the same tensor and its forward only waits for that copy's event.  Every frame still
-        crosses PCIe once, inside the caller's loop; the upload of step t + 1 overlaps step t."""
+        video driver reads ahead).  Their upload is issued now, on the copy stream, into a staging
+        buffer; the next run() is handed the same tensor and its slot stream copies staging -> slot
+        (device to device) behind that upload's event.  Every frame still crosses PCIe once,
+        inside the caller's loop; the upload of step t + 1 overlaps step t."""
         s = self._slot(self._k)
         st = self._stream(s)
         cur = torch.cuda.current_stream(self.device)
-        if self._prefetched[s] is not None:
-            if frames.is_cuda or frames.data_ptr() != self._prefetched[s]:
+        if self._prefetched is not None:
+            ptr, i = self._prefetched
+            if frames.is_cuda or frames.data_ptr() != ptr:
                 raise ValueError("run(): the previous call prefetched other frames for this step (next_frames)")
-            st.wait_event(self._ev_copy[s])
-            self._prefetched[s] = None
+            self._prefetched = None
+            st.wait_event(self._ev_copy[i])
+            if self._gmd_pending[s]:  # the motion detector (tracker stream) still reads this slot's frames
+                st.wait_event(self._ev_gmd[s])
+                self._gmd_pending[s] = False
+            with torch.cuda.stream(st):
+                self.frame_slots[s].copy_(self._stage[i], non_blocking=True)
+            self._ev_stage_read[i].record(st)
+            self._stage_read_pending[i] = True
         else:
             if st != cur:
                 st.wait_stream(cur)
@@ -226,17 +259,16 @@ class StreamPipeline:
         if next_frames is not None:
             if next_frames.is_cuda or self.copy_stream is None:
                 raise ValueError("next_frames: page-locked host frames and inflight > 1")
-            s2 = self._slot(self._k)
+            i = self._n_stage % 3
+            self._n_stage += 1
             cs = self.copy_stream
-            if self._fwd_pending[s2]:  # the forward that last read slot s2
-                cs.wait_event(self._ev_fwd[s2])
-            if self._gmd_pending[s2]:  # and the motion detector's read of it
-                cs.wait_event(self._ev_gmd[s2])
-                self._gmd_pending[s2] = False
+            if self._stage_read_pending[i] and not self._ev_stage_read[i].query():
+                cs.wait_event(self._ev_stage_read[i])  # (rare: its staging -> slot copy has not run yet)
+            self._stage_read_pending[i] = False
             with torch.cuda.stream(cs):
-                self.frame_slots[s2].copy_(next_frames, non_blocking=True)
-            self._ev_copy[s2].record(cs)
-            self._prefetched[s2] = next_frames.data_ptr()
+                self._stage[i].copy_(next_frames, non_blocking=True)
+            self._ev_copy[i].record(cs)
+            self._prefetched = (next_frames.data_ptr(), i)
 
     def download_async(self, rows, counts, stats, rows_per_stream=None):
         """Enqueue the tracker output of the most recent step into page-locked host buffers
