@@ -381,6 +381,13 @@ def run_leg(a, P, cfg, dtype, frames, dev, local, rank, ws, headline):
     host = torch.empty((n_host,) + tuple(frames.shape[1:]), dtype=torch.uint8, pin_memory=True)
     for j in range(n_host):
         host[j].copy_(frames[(t_first + j) % F])
+    # a video driver's decode buffers are long-lived and already DMA-mapped: one untimed upload of
+    # each host frame (the first DMA from a fresh page-locked page costs its mapping)
+    sink = torch.empty_like(frames[0])
+    for j in range(n_host):
+        sink.copy_(host[j], non_blocking=True)
+    torch.cuda.synchronize()
+    del sink
     n_rows = pipe.tracker.n_streams * pipe.tracker.max_tracks
     out_rows = torch.empty(n_rows * P._lib.TRACK_OUT_DTYPE.itemsize, dtype=torch.uint8, pin_memory=True)
     out_counts = torch.empty(S, dtype=torch.int32, pin_memory=True)

@@ -49,14 +49,16 @@ def _threads():
     return max(1, min(16, n))
 
 
-def build_chain(seeds, n_frames, targets):
+def build_chain(seeds, n_frames, targets, model="yolov8s-small.yaml"):
     """Frames (rendered once on the CPU, the same arrays for both sides) and the oracle chain's
-    per-frame detections and track dicts for every stream (scene seed per stream)."""
+    per-frame detections and track dicts for every stream (scene seed per stream); `model` names
+    the architecture and scale (yolov8s-small.yaml: the bench's; yolov8n-small.yaml: the scale the
+    reference's trained model resolves to)."""
     P = pkg()
     S, F = len(seeds), n_frames
     scenes = [P.synth.Scene(seed=sd, n_targets=targets, n_frames=F + 1) for sd in seeds]
     frames = torch.stack([sc.frames_torch(0, F, "cpu") for sc in scenes], 1)  # [F, S, H, W, 3]
-    ar = P.arch.parse_arch(P.arch.load_model_dict("yolov8s-small.yaml"))
+    ar = P.arch.parse_arch(P.arch.load_model_dict(model))
     sd = P.weights.synthetic_state_dict(ar, 0)
     ref = D.RefDetector(_layers(ar), sd, P.arch.detect_strides(ar))
     torch.set_num_threads(_threads())
@@ -73,7 +75,7 @@ def build_chain(seeds, n_frames, targets):
     return {"frames": frames, "dets": dets, "tracks": tracks, "nms_score_ties": ties, "near": near,
             "tie_frames": sum(tr.tie_frames for tr in trks),
             "terminated": sum(tr.stats["total_tracks_terminated"] for tr in trks),
-            "live": [len(tr.trackers) for tr in trks], "S": S, "F": F}
+            "live": [len(tr.trackers) for tr in trks], "S": S, "F": F, "model": model}
 
 
 @pytest.fixture(scope="module")
@@ -83,13 +85,13 @@ def chain():
     return build_chain([P.shard.stream_seed(s, S) for s in range(S)], F, TARGETS)
 
 
-def _run_gpu(dtype, frames, plan=None):
+def _run_gpu(dtype, frames, plan=None, model="yolov8s-small.yaml"):
     P = pkg()
     import importlib
 
     pipeline = importlib.import_module(P.__name__ + ".pipeline")
     F, S = frames.shape[:2]
-    pipe = pipeline.StreamPipeline("yolov8s-small.yaml", S, (512, 640), dtype, seed=0, max_tracks=512,
+    pipe = pipeline.StreamPipeline(model, S, (512, 640), dtype, seed=0, max_tracks=512,
                                    pipelined=True, inflight=4)
     pipe.set_schedule(1, 1)  # bench.py's schedule with 3 forwards in flight
     # the committed conv plan bench.py loads for this workload (so the kernels under test are the
@@ -151,7 +153,7 @@ def check_chain(chain, plan_path, parity_record=False):
     from test_tracker_gpu import compare_frame
 
     S, F = chain["S"], chain["F"]
-    dets, counts, rows, tcounts, stats = _run_gpu("fp32", chain["frames"], plan_path)
+    dets, counts, rows, tcounts, stats = _run_gpu("fp32", chain["frames"], plan_path, chain["model"])
     assert int(stats[-1]["overflow"].sum()) == 0
     conf_dev, conf_dev_well, box_rel, n_tracks, n_outputs, ill_conf = 0.0, 0.0, 0.0, 0, 0, []
     flips, flip_scores, order_ties = [], [], []
@@ -244,6 +246,30 @@ def test_config4_rank_leg_b1_fp32_plan_matches_oracle_chain():
     out = check_chain(ch, "plans/s_640x512_i640_b1_fp32.json", parity_record=True)
     assert min(out["live_tracks_end"]) >= 64, out["live_tracks_end"]
     assert ch["terminated"] > 0
+
+
+@pytest.mark.timeout(900)
+def test_scale_n_b8_fp32_plan_matches_oracle_chain():
+    """The reference's own model scale (its trained model resolves to yolov8-small.yaml at scale
+    n: small_target_detection/yolov8_small_aircraft/args.yaml:3, nn/tasks.py:1545-1549) on bench.py's
+    config-3 pipeline (8 streams, one batch-8 forward, 4 in flight) with the committed scale-n
+    plan (plans/n_640x512_i640_b8_fp32.json, bench.py --scale n): the same resynced chain bar as
+    the scale-s test, every frame of every stream, and the plan's recorded near-tie count."""
+    P = pkg()
+    ch = build_chain([P.shard.stream_seed(s, S) for s in range(S)], F, TARGETS, model="yolov8n-small.yaml")
+    out = check_chain(ch, "plans/n_640x512_i640_b8_fp32.json", parity_record=True)
+    assert out["near_tie_flips"] + out["order_ties"] <= 3
+    assert min(ch["live"]) >= 40, ch["live"]
+
+
+@pytest.mark.timeout(900)
+def test_scale_n_b1_fp32_plan_matches_oracle_chain():
+    """Scale n's batch-1 fp32 plan (plans/n_640x512_i640_b1_fp32.json: config 4's per-rank leg and
+    the drop-in YOLO("best.pt") path of the reference's trained scale) under the chain bar."""
+    P = pkg()
+    ch = build_chain([P.shard.stream_seed(5, 1)], F, TARGETS, model="yolov8n-small.yaml")
+    out = check_chain(ch, "plans/n_640x512_i640_b1_fp32.json", parity_record=True)
+    assert out["near_tie_flips"] + out["order_ties"] <= 3
 
 
 @pytest.mark.timeout(900)

@@ -135,3 +135,56 @@ def test_fp8_detections_close_to_fp32_oracle(geom):
         best = _box_iou(ref[:, :4], ours[:, :4]).max(1).values
         assert float((best > 0.5).float().mean()) >= 0.85
     assert total > 0
+
+
+def test_config5_committed_b8_fp8_plan():
+    """BASELINE config 5's committed conv plan (plans/s_1280x1024_i1280_b8_fp8.json, the one
+    bench.py --config 5 loads) on a batch-8 fp8 model: the planned kernels give the same
+    detections as the heuristic plan's (same e4m3 arithmetic, other tilings: counts equal and
+    every box within IoU > 0.9 of its counterpart, scores within 2e-3), and two of the eight
+    images against the fp32 oracle by the property bar above."""
+    import json
+    import os
+
+    P, A, W, M = _mods()
+    ar = A.parse_arch(A.load_model_dict("yolov8s-small.yaml"))
+    sd = W.synthetic_state_dict(ar, 0)
+    B, hw, imgsz = 8, (1024, 1280), 1280
+    sc = P.synth.Scene(seed=3, n_targets=48, n_frames=B + 1, height=hw[0], width=hw[1])
+    frames = [sc.frame(t) for t in range(B)]
+    ft = torch.from_numpy(np.stack(frames)).cuda()
+    prog = M.Program(ar, sd, hw[0], hw[1], imgsz, B, "fp8")
+    heur = M.DeviceModel(prog)
+    d0, c0 = heur.detect(ft, 0.25, 0.7, 300)
+    planned = M.DeviceModel(prog)
+    with open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                           "plans", "s_1280x1024_i1280_b8_fp8.json")) as f:
+        pl = json.load(f)
+    assert pl["batch"] == B and len(pl["plan"]) == len(prog.ops)
+    planned.load_plan(pl["batch"], pl["plan"])
+    d1, c1 = planned.detect(ft, 0.25, 0.7, 300)
+    torch.cuda.synchronize()
+    planned.check()
+    d0, c0, d1, c1 = d0.cpu(), c0.cpu(), d1.cpu(), c1.cpu()
+    assert int(c1.sum()) > 0
+    for b in range(B):
+        n0, n1 = int(c0[b]), int(c1[b])
+        assert abs(n0 - n1) <= max(2, n0 // 50), (b, n0, n1)
+        if n0 == 0 or n1 == 0:
+            continue
+        iou = _box_iou(d0[b, :n0, :4], d1[b, :n1, :4])
+        best, j = iou.max(1)
+        assert float((best > 0.9).float().mean()) >= 0.95, b
+        close = best > 0.9
+        assert float((d0[b, :n0, 4][close] - d1[b, :n1, 4][j[close]]).abs().max()) <= 2e-3
+    torch.set_num_threads(8)
+    im = D.preprocess(frames[:2], imgsz)
+    f = D.RefDetector(layer_list(ar), sd, A.detect_strides(ar))
+    yf, _ = f.forward(im)
+    res = [D.scale_clip(p, im.shape[2:], hw) for p in D.non_max_suppression(yf, 0.25, 0.7, 300)]
+    for b in range(2):
+        ref, n = res[b], int(c1[b])
+        assert abs(n - len(ref)) <= max(3, int(0.25 * len(ref))), (n, len(ref))
+        if len(ref):
+            best = _box_iou(ref[:, :4], d1[b, :n, :4]).max(1).values
+            assert float((best > 0.5).float().mean()) >= 0.85

@@ -43,11 +43,14 @@ print(f"ts buffer 0x{ptr.value or 0:x}: {(ts[:, 0] > 0).sum()} starts, {(ts[:, 1
 ts = ts[ts[:, 0] > 0]
 if not len(ts):
     sys.exit(f"op {op}: no workgroup timestamps (not a conv_fast / conv_fastw op under this plan?)")
-# the buffer keeps the last launch of every workgroup index: keep the last launch's cluster
+# the buffer keeps the last launch of every workgroup index (the detect() calls above run the op
+# back to back, so one launch's workgroups can follow the previous launch's within microseconds):
+# keep the starts within 60 us before the newest end
+newest = ts[:, 2].max()
+ts = ts[ts[:, 0] >= newest - 6000]
 order = np.sort(ts[:, 0])
-gaps = np.nonzero(np.diff(order) > 300)[0]  # > 3 us between consecutive workgroup starts
-cut = order[gaps[-1] + 1] if len(gaps) else order[0]
-ts = ts[ts[:, 0] >= cut]
+hist = np.histogram((order - order[0]) / 100.0, bins=12)
+print("  starts per time bin (us edges %s): %s" % (np.round(hist[1], 1).tolist(), hist[0].tolist()))
 t0 = ts[:, 0].min()
 st, mid, en = (ts[:, 0] - t0) / 100.0, (ts[:, 1] - t0) / 100.0, (ts[:, 2] - t0) / 100.0  # us
 prof = dm.profile(ft, reps=5)

@@ -40,6 +40,7 @@
 //     4  halo kernel: no weight loads                     8  halo kernel: no input staging
 //    32  F32S split with scalar remainders               64  fp32 SiLU on v_exp_f32 / v_rcp_f32
 //   128  two waves per SIMD for the table / halo kernels (amdgpu_waves_per_eu(2))
+//   512  F32S: operands used as if stored pre-split (no split VALU, overlapping register quads)
 #ifndef YK_DIAG
 #define YK_DIAG 0
 #endif
@@ -286,6 +287,21 @@ __device__ __forceinline__ XS3 split3(const uint4& x) {
 }
 template <int NE, int NPT>
 __device__ __forceinline__ void mma_split_step(const WS2* w, const uint4* xf, f32x4 (*acc)[NPT]) {
+  if constexpr ((YK_DIAG & 512) != 0) {  // diagnostic: operands as if stored pre-split (no split VALU)
+#pragma unroll
+    for (int t = 0; t < NPT; ++t) {
+      const u32x4v xa = u32x4v{xf[t].x, xf[t].y, xf[t].z, xf[t].w};
+      const u32x4v xb = u32x4v{xf[t].z, xf[t].w, xf[t].x, xf[t].y};
+#pragma unroll
+      for (int i = 0; i < NE; ++i) acc[i][t] = mfma_bf16(w[i].w01, xb, acc[i][t]);
+#pragma unroll
+      for (int i = 0; i < NE; ++i)
+        acc[i][t] = mfma_bf16(u32x4v{w[i].w01.z, w[i].w01.w, w[i].w02.x, w[i].w02.y}, xa, acc[i][t]);
+#pragma unroll
+      for (int i = 0; i < NE; ++i) acc[i][t] = mfma_bf16(w[i].w02, xa, acc[i][t]);
+    }
+    return;
+  }
 #pragma unroll
   for (int t = 0; t < NPT; ++t) {
     const XS3 x = split3(xf[t]);

@@ -108,16 +108,19 @@ class StreamPipeline:
         self._gmd_pending = [False] * self.D
         # host-frame prefetch (run(..., next_frames=)): the next step's upload runs on its own copy
         # stream one step ahead, behind the forward that last read that slot
-        # Uploads go to a 3-buffer staging ring, not to the slot: a slot is still being read by its
-        # forward from D steps ago when the next upload is issued, and a copy stream made to wait for
-        # that forward held the host thread in hipMemcpyAsync (~1 ms per step, bench --io h2d).  A
-        # staging buffer is free again one device-to-device copy (~10 us) after its upload, so the
-        # copy stream waits for nothing in steady state; the slot stream then copies staging -> slot.
+        # Uploads go to a staging ring, not to the slot: a slot is still being read by its forward
+        # from D steps ago when the next upload is issued, and a copy stream made to wait for that
+        # forward holds the host thread in hipMemcpyAsync (the runtime resolves an SDMA copy's
+        # cross-stream wait on the host: ~1 ms per step, bench --io h2d).  A staging buffer is read
+        # by the slot stream's staging -> slot copy in front of its forward; with D + 4 buffers the
+        # buffer an upload reuses was read D + 4 steps earlier, which the host never outruns while
+        # D forwards are in flight, so the copy stream waits for nothing in steady state.
         self.copy_stream = torch.cuda.Stream(dev) if self.D > 1 else None
-        self._stage = [torch.empty_like(self.frames) for _ in range(3)] if self.D > 1 else []
-        self._ev_stage_read = [torch.cuda.Event() for _ in range(3)]  # slot stream's copy out of it
-        self._stage_read_pending = [False] * 3
-        self._ev_copy = [torch.cuda.Event() for _ in range(3)]
+        self.n_stage = self.D + 4 if self.D > 1 else 0
+        self._stage = [torch.empty_like(self.frames) for _ in range(self.n_stage)]
+        self._ev_stage_read = [torch.cuda.Event() for _ in range(self.n_stage)]  # slot stream's copy out of it
+        self._stage_read_pending = [False] * self.n_stage
+        self._ev_copy = [torch.cuda.Event() for _ in range(self.n_stage)]
         self._n_stage = 0
         self._prefetched = None  # (data_ptr of the host frames, staging index) of the next step
         self._ev_motion = None  # motion isolation (gmd with forwards in flight): this step's motion call
@@ -259,7 +262,7 @@ class StreamPipeline:
         if next_frames is not None:
             if next_frames.is_cuda or self.copy_stream is None:
                 raise ValueError("next_frames: page-locked host frames and inflight > 1")
-            i = self._n_stage % 3
+            i = self._n_stage % self.n_stage
             self._n_stage += 1
             cs = self.copy_stream
             if self._stage_read_pending[i] and not self._ev_stage_read[i].query():
