@@ -65,7 +65,7 @@ TRACK_STEP_BYTES = 1216  # R+W of x (8 f64) and dense P (64 f64), z
 # targets and crossing targets churn IDs, so live tracks != targets (40 targets -> ~70-150 live).
 CONFIGS = {
     2: dict(S=1, H=512, W=640, imgsz=640, max_tracks=512, targets=12, dtype="bf16", secondary="", live_floor=16),
-    3: dict(S=8, H=512, W=640, imgsz=640, max_tracks=512, targets=40, dtype="fp32", secondary="bf16", live_floor=64),
+    3: dict(S=8, H=512, W=640, imgsz=640, max_tracks=512, targets=40, dtype="fp32", secondary="bf16,n:fp32", live_floor=64),
     4: dict(S=1, H=512, W=640, imgsz=640, max_tracks=512, targets=40, dtype="fp32", secondary="", live_floor=64),
     5: dict(S=8, H=1024, W=1280, imgsz=1280, max_tracks=2048, targets=96, dtype="fp8", secondary="bf16",
             live_floor=256),
@@ -476,10 +476,11 @@ def cpu_baseline_seconds(a, rank, ws):
     return a.cpu_seconds if ws == 1 else min(a.cpu_seconds, 10.0)
 
 
-def leg_argv(argv, dtype):
+def leg_argv(argv, dtype, scale=None):
     """bench.py's own arguments for a secondary leg: the same workload and protocol, `dtype` as
-    the only leg, no CPU baseline, no plan / op-dump outputs, one process (no --gpus)."""
-    skip = {"--dtype", "--secondary", "--dump-ops", "--plan-in", "--plan-out", "--gpus"}
+    the only leg (and `scale`, if given, as the model scale), no CPU baseline, no plan / op-dump
+    outputs, one process (no --gpus)."""
+    skip = {"--dtype", "--secondary", "--dump-ops", "--plan-in", "--plan-out", "--gpus"} | ({"--scale"} if scale else set())
     out, i = [], 0
     while i < len(argv):
         t = argv[i]
@@ -492,20 +493,22 @@ def leg_argv(argv, dtype):
             continue
         out.append(t)
         i += 1
-    return out + ["--dtype", dtype, "--secondary", "none", "--no-cpu-baseline"]
+    return out + ["--dtype", dtype, "--secondary", "none", "--no-cpu-baseline"] + (["--scale", scale] if scale else [])
 
 
-def run_leg_subprocess(dtype):
-    """One more leg (same workload and protocol, another conv dtype) as its own bench.py process;
+def run_leg_subprocess(spec):
+    """One more leg (same workload and protocol, another conv dtype -- "bf16" -- or another model
+    scale and dtype -- "n:fp32", the reference's trained scale) as its own bench.py process;
     returns its leg dict.  Only used at world size 1 (secondary legs)."""
-    cmd = [sys.executable, os.path.abspath(__file__)] + leg_argv(sys.argv[1:], dtype)
+    scale, dtype = spec.split(":") if ":" in spec else (None, spec)
+    cmd = [sys.executable, os.path.abspath(__file__)] + leg_argv(sys.argv[1:], dtype, scale)
     r = subprocess.run(cmd, capture_output=True, text=True)
     sys.stderr.write(r.stderr)
     if r.returncode != 0:
-        raise SystemExit(f"secondary leg {dtype} failed (exit {r.returncode})")
+        raise SystemExit(f"secondary leg {spec} failed (exit {r.returncode})")
     d = json.loads(r.stdout.strip().splitlines()[-1])
     c = d["config"]
-    leg = {"dtype": dtype, "value": d["value"], "ms_per_step": d["ms_per_step"],
+    leg = {"dtype": dtype, "workload": c["workload"], "value": d["value"], "ms_per_step": d["ms_per_step"],
            "network_mfma_frac": d["network_mfma_frac"], "live_tracks_per_stream": c["live_tracks_per_stream"],
            "live_tracks_per_stream_min_at_start": c["live_tracks_per_stream_min_at_start"],
            "overflow": c["tracker_overflow"], "tracks_created": c["tracks_created"], "conv_plan": c["conv_plan"],
@@ -539,7 +542,7 @@ def main():
         cfg["imgsz"] = a.imgsz
     dtype = a.dtype or cfg["dtype"]
     sec = cfg["secondary"] if a.secondary is None else ("" if a.secondary == "none" else a.secondary)
-    secondary = [d for d in sec.split(",") if d and d != dtype] if ws == 1 else []
+    secondary = [d for d in sec.split(",") if d and d != dtype and d != f"{a.scale}:{dtype}"] if ws == 1 else []
     S, H, W = cfg["S"], cfg["H"], cfg["W"]
     shard = P.shard
     my_streams = shard.stream_ids(rank, ws, S)  # this GPU's block of independent streams

@@ -22,6 +22,10 @@ def test_secondary_leg_argv_keeps_workload_drops_outputs():
     assert out == ["--steps", "20", "--warmup=5", "--config", "5", "--inflight", "3",
                    "--dtype", "bf16", "--secondary", "none", "--no-cpu-baseline"]
     assert B.leg_argv([], "fp32") == ["--dtype", "fp32", "--secondary", "none", "--no-cpu-baseline"]
+    # a scale leg ("n:fp32", config 3's second secondary leg) replaces --scale
+    assert B.leg_argv(["--scale", "s", "--steps", "20"], "fp32", "n") == \
+        ["--steps", "20", "--dtype", "fp32", "--secondary", "none", "--no-cpu-baseline", "--scale", "n"]
+    assert "n:fp32" in B.CONFIGS[3]["secondary"].split(",")
 
 
 @pytest.mark.parametrize("cfg", [2, 3, 4, 5])
