@@ -222,12 +222,13 @@ def test_dag_schedule_matches_sequential(dtype):
                                   (3, 2, 2 | 32), (3, 3, 1 | 32), (3, 4, 4 | 32),
                                   (3, 2, 4 | 64), (3, 4, 2 | 16 | 64), (3, 2, 2 | 32 | 64), (3, 4, 4 | 32 | 64),
                                   (5, 1, 1), (5, 2, 2), (5, 1, 4), (5, 2, 4), (5, 1, 1 | 16), (5, 2, 2 | 16),
-                                  (5, 1, 4 | 16), (5, 2, 4 | 16), (6, 1, 1), (6, 2, 2), (6, 3, 2), (6, 4, 1),
-                                  (6, 5, 2), (6, 3, 4), (6, 2, 4), "tuned"])
+                                  (5, 1, 4 | 16), (5, 2, 4 | 16), (3, 1, 1 | 48), (3, 3, 4 | 48), (3, 2, 2 | 48 | 64),
+                                  (3, 3, 4 | 48 | 64), (3, 4, 4 | 48 | 64), (3, 4, 1 | 48 | 64), "tuned"])
 def test_fp32_conv_variants_match_oracle(plan):
     """Every conv kernel variant (direct, LDS-tiled, split-K fragment tiles, table kernel with
-    and without LDS-shared weights and the split-bf16 body (+64), halo-tile split kernel (kind
-    5), halo tile with LDS-shared weights (kind 6), autotuned mix) forced onto every conv op reproduces the oracle's activations and
+    and without LDS-shared weights, the four waves or two wave pairs splitting K (+16 / +48) and
+    the split-bf16 body (+64), halo-tile split kernel (kind 5), autotuned mix) forced onto every
+    conv op reproduces the oracle's activations and
     detections (ops a variant does not cover run the direct kernel)."""
     s = setup()
     P, A, W, M = _mods()

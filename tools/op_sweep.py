@@ -44,7 +44,7 @@ def main():
     dm.load_plan(B, plan)
     base = dm.profile(frames, reps=a.reps)
     cands = []
-    for mode in range(3):
+    for mode in range(4):
         for nnt in (1, 2, 3, 4):
             for npt in (1, 2, 4):
                 for sp in (0, 64):
@@ -55,9 +55,6 @@ def main():
         for npt in (1, 2, 4):
             for wm in (0, 1):
                 cands.append((5, ne, npt | (wm << 4)))
-    for ne in (1, 2, 3, 4, 5):
-        for npt in (1, 2, 4):
-            cands.append((6, ne, npt))
     for op in (int(v) for v in a.ops.split(",")):
         res = []
         for kind, nnt, npt in cands:

@@ -928,8 +928,11 @@ __global__ void __launch_bounds__(256) conv_tile_kernel(TileArgs a) {
 // << 5} (model create, yk_model::ktab); the workgroup copies the op's table into LDS once.
 // Each lane computes its pixels' window-origin offsets in both sources and a 9-bit tap
 // validity mask once, so a K step costs one ds_read_b64, a mask test and an add per pixel
-// fragment.  WS: the four waves share one 16*NPT-pixel tile and split the K steps (partial
-// tiles summed in LDS); otherwise each wave owns its own 16*NPT pixels and the full K.
+// fragment.  KW (waves per K split) 4: the four waves share one 16*NPT-pixel tile and split the
+// K steps (partial tiles summed in LDS); 2: two pairs of waves, each pair one 16*NPT-pixel tile
+// and half the K steps (a short split-K wave pays its prologue and exposed load latency per
+// 1/4 of K, a pair per 1/2, and a launch of half as many workgroups fits the CUs in fewer
+// rounds); 1: each wave owns its own 16*NPT pixels and the full K.
 // SKD K steps of loads stay in flight per wave.
 struct FastArgs {
   const void* arena;             // every activation buffer lives in one allocation (< 2 GiB)
@@ -1004,11 +1007,12 @@ constexpr int fastw_skd(int nnt, int npt) { return nnt * npt >= 8 ? 2 : 4; }
 // NE = output-channel tiles this workgroup computes: NNT, or fewer for the last channel group of
 // an op whose n_tiles is not a multiple of NNT (its missing tiles cost no loads and no MFMAs;
 // each body is straight-line code, the dispatch is one scalar branch per workgroup).
-template <class Tr, int NE, int NPT, bool WS, int SKD>
+template <class Tr, int NE, int NPT, int KW, int SKD>
 __device__ __forceinline__ void conv_fast_body(const FastArgs& a, int2 blk, int nt0) {
   using T = typename Tr::T;
   constexpr int ESZ = (int)sizeof(T);
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr bool WS = KW > 1;
   int2* tab = (int2*)smem;  // [k_steps * 4]; WS: then the f32x4 reduction buffer
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1030,7 +1034,7 @@ __device__ __forceinline__ void conv_fast_body(const FastArgs& a, int2 blk, int 
   const __amdgpu_buffer_rsrc_t wr = make_srd(a.wblob, a.wbytes);
   const int hw = a.out_h * a.out_w;
   unsigned vo0[NPT], vo1[NPT], vm[NPT];
-  const int pbase = WS ? blk.x * (16 * NPT) : (blk.x * 4 + wave) * (16 * NPT);
+  const int pbase = (blk.x * (4 / KW) + wave / KW) * (16 * NPT);  // this wave's pixel tile
   // the lane's window origins in both sources and its 9-bit tap mask, per pixel fragment
   {
 #pragma unroll
@@ -1101,8 +1105,8 @@ __device__ __forceinline__ void conv_fast_body(const FastArgs& a, int2 blk, int 
   };
   int k0 = 0, k1 = nk;
   if (WS) {
-    const int kq = (nk + 3) >> 2;
-    k0 = wave * kq;
+    const int kq = (nk + KW - 1) / KW;
+    k0 = (wave % KW) * kq;
     k1 = k0 + kq < nk ? k0 + kq : nk;
   }
   WF wb[SKD][NE];
@@ -1193,20 +1197,22 @@ __device__ __forceinline__ void conv_fast_body(const FastArgs& a, int2 blk, int 
   }
   if (a.tstamp && tid == 0 && wg_lin < a.tstamp_cap) a.tstamp[3 * wg_lin + 1] = wall_clock64();
   if constexpr (WS) {
-    // partial tiles to LDS; each wave then finishes the (tile, fragment) slots q = 4 j + wave,
-    // with the slots' bias and residual loads in flight over the barrier (runtime slot
-    // indices: no acc registers live in the epilogue)
+    // partial tiles to LDS; each wave of a K-split group g (waves g KW .. g KW + KW - 1) then
+    // finishes the group's (tile, fragment) slots q = KW j + (wave % KW), with the slots' bias
+    // and residual loads in flight over the barrier (runtime slot indices: no acc registers
+    // live in the epilogue)
     f32x4* red = (f32x4*)(smem + (((size_t)nk * 4 * 8 + 15) & ~(size_t)15));
 #pragma unroll
     for (int i = 0; i < NE; ++i)
 #pragma unroll
       for (int t = 0; t < NPT; ++t) red[((wave * NE + i) * NPT + t) * 64 + lane] = acc[i][t];
-    constexpr int J = (NE * NPT + 3) / 4;
+    constexpr int J = (NE * NPT + KW - 1) / KW;
+    const int w0 = wave - wave % KW;  // the group's first wave
     float4 sb[J], ss[J];
     float rv[J][4];
 #pragma unroll
     for (int j = 0; j < J; ++j) {
-      const int q = j * 4 + wave, i = q / NPT, t = q - i * NPT;
+      const int q = j * KW + wave % KW, i = q / NPT, t = q - i * NPT;
       const int n0 = (nt0 + i) * 16 + kg * 4, p = pbase + t * 16 + col;
       const bool ok = q < NE * NPT && nt0 + i < a.n_tiles && n0 < a.cout && p < a.M;
       sb[j] = ok ? *(const float4*)(a.bias + n0) : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -1216,13 +1222,13 @@ __device__ __forceinline__ void conv_fast_body(const FastArgs& a, int2 blk, int 
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < J; ++j) {
-      const int q = j * 4 + wave, i = q / NPT, t = q - i * NPT;
+      const int q = j * KW + wave % KW, i = q / NPT, t = q - i * NPT;
       const int n0 = (nt0 + i) * 16 + kg * 4, p = pbase + t * 16 + col;
       if (!(q < NE * NPT && nt0 + i < a.n_tiles && n0 < a.cout && p < a.M)) continue;
-      f32x4 v4 = red[((0 * NE + i) * NPT + t) * 64 + lane];
+      f32x4 v4 = red[((w0 * NE + i) * NPT + t) * 64 + lane];
 #pragma unroll
-      for (int w = 1; w < 4; ++w) {
-        const f32x4 u = red[((w * NE + i) * NPT + t) * 64 + lane];
+      for (int w = 1; w < KW; ++w) {
+        const f32x4 u = red[(((w0 + w) * NE + i) * NPT + t) * 64 + lane];
         v4[0] += u[0];
         v4[1] += u[1];
         v4[2] += u[2];
@@ -1287,23 +1293,23 @@ __device__ __forceinline__ void conv_fast_body(const FastArgs& a, int2 blk, int 
 // Measured (round 3, fp32 headline): 2 lets the large split tiles drop their AGPR accumulators and
 // run two waves per SIMD without spills, but the headline does not move (5,279 vs 5,264 frames/s:
 // those kernels are bound by the split VALU work, not by occupancy); 3 spills (-32 %).
-template <class Tr, int NNT, int NPT, bool WS, int SKD>
+template <class Tr, int NNT, int NPT, int KW, int SKD>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(YK_FAST_WPE))) conv_fast_kernel(FastArgs a) {
   const int2 blk = xcd_block(a.xcd);
   const int nt0 = blk.y * NNT;
   const int rem = a.n_tiles - nt0;
   if constexpr (NNT == 1) {
-    conv_fast_body<Tr, 1, NPT, WS, SKD>(a, blk, nt0);
+    conv_fast_body<Tr, 1, NPT, KW, SKD>(a, blk, nt0);
   } else {
     if (rem >= NNT) {
-      conv_fast_body<Tr, NNT, NPT, WS, SKD>(a, blk, nt0);
+      conv_fast_body<Tr, NNT, NPT, KW, SKD>(a, blk, nt0);
     } else if (rem == 1) {
-      conv_fast_body<Tr, 1, NPT, WS, SKD>(a, blk, nt0);
+      conv_fast_body<Tr, 1, NPT, KW, SKD>(a, blk, nt0);
     } else if constexpr (NNT > 2) {
       if (rem == 2 || NNT == 3)
-        conv_fast_body<Tr, 2, NPT, WS, SKD>(a, blk, nt0);
+        conv_fast_body<Tr, 2, NPT, KW, SKD>(a, blk, nt0);
       else
-        conv_fast_body<Tr, (NNT > 3 ? 3 : 1), NPT, WS, SKD>(a, blk, nt0);
+        conv_fast_body<Tr, (NNT > 3 ? 3 : 1), NPT, KW, SKD>(a, blk, nt0);
     }
   }
 }
@@ -1999,210 +2005,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(YK_FAS
   }
 }
 
-// ---------------------------------------------------------------- halo tile + shared weights (F32 build)
-// conv_halo_kernel's waves each fetch their own weight fragments from global memory every K step:
-// with the four waves splitting the tile's pixels (WM 0) that is four copies of NE x 3 KB per step
-// through one CU's vector-memory path, which -- not the matrix cores -- paces it (two K steps of
-// weights per wave = 2 x 3 KB against 3 x NE x NPT MFMAs).  Here the workgroup loads each step's
-// NE x 3 KB of K-slot weight fragments ONCE, 16 bytes per thread, two steps ahead through
-// registers into a three-slot LDS ring, and every wave reads them from LDS (one barrier per K
-// step); the input window is staged split, as in conv_halo_kernel, one 16-channel group per chunk,
-// double-buffered.  Tiles are 16 output columns wide (a fragment = one tile row, consecutive in
-// LDS) or 8 (a fragment = two rows; row pitch = 8 mod 16 pixels keeps the 16 pixels on 16
-// different bank groups).  Stride 1, 3x3 or 1x1.  Same arithmetic and accumulation order per
-// output as conv_halo_kernel (K-slot weights, group-major / tap-minor K order).
-struct HwsArgs {
-  HaloArgs h;
-  int pxp;      // pixels per LDS plane (window rounded up to 16)
-  int nsteps;   // K steps (16-channel groups x taps)
-};
-constexpr int kHwsR = 3;  // weight ring slots
-
-template <int NE, int NPT, int KS>
-__global__ void __launch_bounds__(256) conv_hws_kernel(HwsArgs A) {
-  const HaloArgs& a = A.h;
-  constexpr int T = KS * KS;
-  constexpr int CC = KS == 1 ? 4 : 1;             // 16-channel groups per chunk
-  constexpr int S = CC * T;                        // K steps per chunk
-  constexpr int WU = (NE * 192 + 255) / 256;       // weight uint4s per thread per step
-  constexpr int UMAX = 8;                          // staging units per thread (3x3 window <= 512 px,
-                                                   // 1x1 tile <= 128 px)
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int kg = lane >> 4, col = lane & 15;
-  const int pxp = A.pxp, nsteps = A.nsteps;
-  const int plb = pxp * 16;                        // plane bytes
-  const int buf = 8 * CC * plb;                    // one chunk buffer
-  unsigned char* wring = smem + 2 * buf;           // kHwsR slots of NE x 3 KB
-  const int2 blk = xcd_block(a.xcd);
-  const int tpi = a.tiles_x * a.tiles_y;
-  const int b = blk.x / tpi, rr = blk.x - b * tpi;
-  const int tyi = rr / a.tiles_x, txi = rr - tyi * a.tiles_x;
-  const int oy0 = tyi * a.tr, ox0 = txi * a.tc;
-  const int iy0 = oy0 - a.pad, ix0 = ox0 - a.pad;
-  const int nt0 = blk.y * NE;
-  const int n_groups = (a.cin + 15) >> 4;
-  const int n_chunks = (n_groups + CC - 1) / CC;
-  const __amdgpu_buffer_rsrc_t xr = make_srd(a.arena, a.arena_bytes);
-  const __amdgpu_buffer_rsrc_t wr = make_srd(a.wblob, a.wbytes);
-  // the lane's pixel of each fragment: LDS byte offset of its window origin in plane XA(kg)
-  unsigned lb[NPT];
-  int opx[NPT];
-#pragma unroll
-  for (int t = 0; t < NPT; ++t) {
-    const int q = (wave * NPT + t) * 16 + col;
-    const int ty = q / a.tc, tx = q - ty * a.tc;
-    const bool v = ty < a.tr && oy0 + ty < a.out_h && ox0 + tx < a.out_w;
-    lb[t] = (unsigned)(kg * plb + (v ? (ty * a.rp + tx) * 16 : 0));
-    opx[t] = v ? (b * a.out_h + oy0 + ty) * a.out_w + ox0 + tx : -1;
-  }
-  // staging: unit j of a thread = channel group kgu, window pixel px = (tid & 15) + 16 (tid >> 6) + 64 j
-  // (3x3: one 16-channel group per chunk); 1x1: px = (tid & 15) + 16 (tid >> 6) + 64 (j >> 2), group j & 3
-  const int kgu = (tid >> 4) & 3;
-  unsigned sv0[UMAX], sv1[UMAX];
-  int sl[UMAX];
-#pragma unroll
-  for (int j = 0; j < UMAX; ++j) {
-    const int px = (tid & 15) + 16 * (tid >> 6) + (CC == 1 ? 64 * j : 64 * (j >> 2));
-    const int g = CC == 1 ? 0 : (j & 3);
-    sl[j] = -1;
-    sv0[j] = sv1[j] = kOOB;
-    if (px < a.npx) {
-      const int py = px / a.twin, pxx = px - py * a.twin;
-      const int iy = iy0 + py, ix = ix0 + pxx;
-      sl[j] = (g * 8 + kgu) * plb + (py * a.rp + pxx) * 16;
-      if (iy >= 0 && iy < a.in_h && ix >= 0 && ix < a.in_w) {
-        sv0[j] = a.soff0 + (unsigned)(((b * a.h0 + (iy >> a.up0)) * a.w0 + (ix >> a.up0)) * a.cs0 * 4);
-        sv1[j] = a.soff1 + (unsigned)(((b * a.h1 + (iy >> a.up1)) * a.w1 + (ix >> a.up1)) * a.cs1 * 4);
-      }
-    }
-  }
-  uint4 st[UMAX];
-  auto fetch = [&](int c) {
-#pragma unroll
-    for (int j = 0; j < UMAX; ++j) {
-      if (sl[j] < 0) continue;
-      const int ch = (c * CC + (CC == 1 ? 0 : (j & 3))) * 16 + kgu * 4;
-      const bool s1 = ch >= a.c0, cv = ch < a.cin;
-      const unsigned o = s1 ? sv1[j] : sv0[j];
-      st[j] = bload(xr, cv && o != kOOB ? o + (unsigned)((s1 ? ch - a.c0 : ch) * 4) : kOOB, 0);
-    }
-  };
-  auto commit = [&](int bi) {
-    unsigned char* base = smem + bi * buf;
-#pragma unroll
-    for (int j = 0; j < UMAX; ++j)
-      if (sl[j] >= 0) {
-        u32x4v xa, xb;
-        split_kslot(st[j], xa, xb);
-        *(u32x4v*)(base + sl[j]) = xa;
-        *(u32x4v*)(base + 4 * plb + sl[j]) = xb;
-      }
-  };
-  // weight staging: uint4 u = tid + 256 j of step s's NE x 192; tile nt0 + u / 192 (clamped)
-  unsigned wsrc[WU];
-  int wdst[WU];
-#pragma unroll
-  for (int j = 0; j < WU; ++j) {
-    const int u = tid + 256 * j;
-    wdst[j] = u < NE * 192 ? u * 16 : -1;
-    const int i = u / 192, w = u - i * 192;
-    const int nt = nt0 + i < a.n_tiles ? nt0 + i : a.n_tiles - 1;
-    wsrc[j] = a.woff + (unsigned)(((size_t)nt * nsteps * 64) * 48 + w * 16);
-  }
-  u32x4v wst[WU];  // the next step to go into the ring
-  auto wfetch = [&](int s, u32x4v* r) {
-#pragma unroll
-    for (int j = 0; j < WU; ++j)
-      if (wdst[j] >= 0) r[j] = __builtin_amdgcn_raw_buffer_load_b128(wr, (int)wsrc[j], s * 64 * 48, 0);
-  };
-  auto wcommit = [&](int s, const u32x4v* r) {
-    unsigned char* slot = wring + (s % kHwsR) * (NE * 3072);
-#pragma unroll
-    for (int j = 0; j < WU; ++j)
-      if (wdst[j] >= 0) *(u32x4v*)(slot + wdst[j]) = r[j];
-  };
-  f32x4 acc[NE][NPT];
-#pragma unroll
-  for (int i = 0; i < NE; ++i)
-#pragma unroll
-    for (int t = 0; t < NPT; ++t) acc[i][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // prologue: chunk 0 staged, steps 0 and 1 of weights in the ring, step 2 in registers
-  fetch(0);
-  wfetch(0, wst);
-  commit(0);
-  wcommit(0, wst);
-  if (nsteps > 1) {
-    wfetch(1, wst);
-    wcommit(1, wst);
-  }
-  if (nsteps > 2) wfetch(2, wst);
-  for (int s = 0; s < nsteps; ++s) {
-    const int c = s / S, k = s - c * S;
-    __syncthreads();  // slot s % R and (at k == 0) chunk c's buffer are complete; slot (s + 2) % R is free
-    if (k == 0 && c + 1 < n_chunks) fetch(c + 1);  // in flight over this chunk's MFMAs
-    const unsigned char* xs = smem + (c & 1) * buf;
-    const unsigned char* ws = wring + (s % kHwsR) * (NE * 3072);
-    const int g = k / T, tt = k - g * T;
-    const int dy = tt / KS, dx = tt - dy * KS;
-    const unsigned toff = (unsigned)((dy * a.rp + dx) * 16);
-    u32x4v xa[NPT], xb[NPT];
-#pragma unroll
-    for (int f = 0; f < NPT; ++f) {
-      const unsigned char* pp = xs + g * 8 * plb + lb[f] + toff;
-      xa[f] = *(const u32x4v*)pp;
-      xb[f] = *(const u32x4v*)(pp + 4 * plb);
-    }
-#pragma unroll
-    for (int i = 0; i < NE; ++i) {
-      const unsigned char* wl = ws + i * 3072 + lane * 48;
-      const u32x4v a1 = *(const u32x4v*)wl, a2 = *(const u32x4v*)(wl + 16), a3 = *(const u32x4v*)(wl + 32);
-#pragma unroll
-      for (int f = 0; f < NPT; ++f) acc[i][f] = mfma_bf16(a1, xa[f], acc[i][f]);
-#pragma unroll
-      for (int f = 0; f < NPT; ++f) acc[i][f] = mfma_bf16(a2, xa[f], acc[i][f]);
-#pragma unroll
-      for (int f = 0; f < NPT; ++f) acc[i][f] = mfma_bf16(a3, xb[f], acc[i][f]);
-    }
-    // ring: step s + 2's fragments (loaded one step ago) into slot (s + 2) % 3 = (s - 1) % 3, which
-    // every wave finished reading before this step's barrier; then step s + 3's loads
-    if (s + 2 < nsteps) {
-      wcommit(s + 2, wst);
-      if (s + 3 < nsteps) wfetch(s + 3, wst);
-    }
-    if (k == S - 1 && c + 1 < n_chunks) commit((c + 1) & 1);  // read last in chunk c - 1
-  }
-#pragma unroll
-  for (int i = 0; i < NE; ++i) {
-    const int nt = nt0 + i;
-    const int n0 = nt * 16 + kg * 4;
-    if (nt >= a.n_tiles || n0 >= a.cout) continue;
-    const float4 bb = *(const float4*)(a.bias + n0);
-#pragma unroll
-    for (int f = 0; f < NPT; ++f) {
-      const int p = opx[f];
-      if (p < 0) continue;
-      float v[4] = {acc[i][f][0] + bb.x, acc[i][f][1] + bb.y, acc[i][f][2] + bb.z, acc[i][f][3] + bb.w};
-      if (a.act) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] = silu<true>(v[j]);
-      }
-      if (a.res) {
-        float r[4];
-        load4((const float*)a.res + (size_t)p * a.r_cstride + a.r_coff + n0, r);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] = r[j] + v[j];
-      }
-      store4((float*)a.dst + (size_t)p * a.d_cstride + a.d_coff + n0, v);
-    }
-  }
-}
-
 // LDS bytes of conv_fast_kernel for an op: the K-step table (+ the split-K reduction buffer).
-inline size_t fast_lds(int k_steps, int nnt, int npt, bool ws) {
+inline size_t fast_lds(int k_steps, int nnt, int npt, int kw) {
   const size_t t = ((size_t)k_steps * 4 * 8 + 15) & ~(size_t)15;
-  return t + (ws ? (size_t)4 * nnt * npt * 64 * 16 : 0);
+  return t + (kw > 1 ? (size_t)4 * nnt * npt * 64 * 16 : 0);
 }
 
 // ---------------------------------------------------------------- LetterBox resize
@@ -3632,10 +3438,10 @@ void set_tile_attrs_t() {
   set_tile_attr_n<Tr, 1, true>();
   set_tile_attr_n<Tr, 2, true>();
 }
-template <class Tr, int NNT, int NPT, bool WS>
+template <class Tr, int NNT, int NPT, int KW>
 void set_fast_attr() {
   constexpr int SKD = fast_skd(NNT, NPT);
-  (void)hipFuncSetAttribute((const void*)conv_fast_kernel<Tr, NNT, NPT, WS, SKD>,
+  (void)hipFuncSetAttribute((const void*)conv_fast_kernel<Tr, NNT, NPT, KW, SKD>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
 }
 template <class Tr, int NNT, int NPT>
@@ -3644,23 +3450,23 @@ void set_fastw_attr() {
   (void)hipFuncSetAttribute((const void*)conv_fastw_kernel<Tr, NNT, NPT, SKD>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
 }
-template <class Tr, int NNT, bool WS>
+template <class Tr, int NNT, int KW>
 void set_fast_attr_n() {
-  set_fast_attr<Tr, NNT, 1, WS>();
-  set_fast_attr<Tr, NNT, 2, WS>();
-  set_fast_attr<Tr, NNT, 4, WS>();
-  if constexpr (!WS) {
+  set_fast_attr<Tr, NNT, 1, KW>();
+  set_fast_attr<Tr, NNT, 2, KW>();
+  set_fast_attr<Tr, NNT, 4, KW>();
+  if constexpr (KW == 1) {
     set_fastw_attr<Tr, NNT, 1>();
     set_fastw_attr<Tr, NNT, 2>();
     set_fastw_attr<Tr, NNT, 4>();
   }
 }
-template <class Tr, bool WS>
+template <class Tr, int KW>
 void set_fast_attr_w() {
-  set_fast_attr_n<Tr, 1, WS>();
-  set_fast_attr_n<Tr, 2, WS>();
-  set_fast_attr_n<Tr, 3, WS>();
-  set_fast_attr_n<Tr, 4, WS>();
+  set_fast_attr_n<Tr, 1, KW>();
+  set_fast_attr_n<Tr, 2, KW>();
+  set_fast_attr_n<Tr, 3, KW>();
+  set_fast_attr_n<Tr, 4, KW>();
 }
 template <class Tr, int NNT, int NW>
 void set_wide_attr_w() {
@@ -3687,25 +3493,7 @@ void set_halo_attr_n() {
   set_halo_attr_p<NE, 2>();
   set_halo_attr_p<NE, 4>();
 }
-template <int NE, int NPT>
-void set_hws_attr_p() {
-  (void)hipFuncSetAttribute((const void*)conv_hws_kernel<NE, NPT, 3>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  if constexpr (NPT <= 2)
-    (void)hipFuncSetAttribute((const void*)conv_hws_kernel<NE, NPT, 1>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
-}
-template <int NE>
-void set_hws_attr_n() {
-  set_hws_attr_p<NE, 1>();
-  set_hws_attr_p<NE, 2>();
-  set_hws_attr_p<NE, 4>();
-}
 void set_tile_attrs() {
-  set_hws_attr_n<1>();
-  set_hws_attr_n<2>();
-  set_hws_attr_n<3>();
-  set_hws_attr_n<4>();
-  set_hws_attr_n<5>();
   set_halo_attr_n<1>();
   set_halo_attr_n<2>();
   set_tile_attrs_t<BF16>();
@@ -3717,18 +3505,23 @@ void set_tile_attrs() {
   set_wide_attr_n<F16, 4>();
   set_wide_attr_n<F32, 2>();
   set_wide_attr_n<F32, 4>();
-  set_fast_attr_w<BF16, false>();
-  set_fast_attr_w<BF16, true>();
-  set_fast_attr_w<F16, false>();
-  set_fast_attr_w<F16, true>();
-  set_fast_attr_w<F32, false>();
-  set_fast_attr_w<F32, true>();
-  set_fast_attr_w<F32S, false>();
-  set_fast_attr_w<F32S, true>();
+  set_fast_attr_w<BF16, 1>();
+  set_fast_attr_w<BF16, 2>();
+  set_fast_attr_w<BF16, 4>();
+  set_fast_attr_w<F16, 1>();
+  set_fast_attr_w<F16, 2>();
+  set_fast_attr_w<F16, 4>();
+  set_fast_attr_w<F32, 1>();
+  set_fast_attr_w<F32, 2>();
+  set_fast_attr_w<F32, 4>();
+  set_fast_attr_w<F32S, 1>();
+  set_fast_attr_w<F32S, 2>();
+  set_fast_attr_w<F32S, 4>();
   set_wide_attr_n<FP8, 2>();
   set_wide_attr_n<FP8, 4>();
-  set_fast_attr_w<FP8, false>();
-  set_fast_attr_w<FP8, true>();
+  set_fast_attr_w<FP8, 1>();
+  set_fast_attr_w<FP8, 2>();
+  set_fast_attr_w<FP8, 4>();
   (void)hipFuncSetAttribute((const void*)sppf_lds_kernel<FP8, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, kSppfLdsBytes);
   (void)hipFuncSetAttribute((const void*)sppf_lds_kernel<BF16, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, kSppfLdsBytes);
   (void)hipFuncSetAttribute((const void*)sppf_lds_kernel<F16, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, kSppfLdsBytes);
@@ -3740,14 +3533,12 @@ void set_tile_attrs() {
 }
 
 // Conv kernel choice for one op at batch B.
-enum { CK_DIRECT = 0, CK_TILE = 1, CK_SPLITK = 2, CK_FAST = 3, CK_WIDE = 4, CK_HALO = 5, CK_HWS = 6 };
-// CK_HWS plan (F32 build, stride 1): nnt = NE in [1, 5] (output-channel tiles per workgroup), npt = NPT in
-// {1, 2, 4} (fragments per wave: a tile of 64 NPT pixels)
+enum { CK_DIRECT = 0, CK_TILE = 1, CK_SPLITK = 2, CK_FAST = 3, CK_WIDE = 4, CK_HALO = 5 };
 // CK_FAST plan npt bit: the F32 build's op runs the F32S split-MFMA body (every mode)
 constexpr int kSplitBit = 64;
 // CK_WIDE plan: nnt in {2, 4} (output-channel tiles per workgroup), npt unused
 // CK_HALO plan (F32 build): nnt = NE in {1, 2}, npt = NPT | WM << 4 with NPT in {1, 2, 4}
-// CK_FAST plan: nnt in {1, 2, 3, 4}, npt = NPT | (WS << 4) with NPT in {1, 2, 4}
+// CK_FAST plan: nnt in {1, 2, 3, 4}, npt = NPT | (mode << 4) with NPT in {1, 2, 4} (launch_fast)
 struct ConvPlan {
   int kind = CK_DIRECT, nnt = 0, npt = 0;
   TilePlan tp;
@@ -3849,38 +3640,6 @@ HaloPlan halo_plan(const yk_op& op, int npt, int wm) {
   return h;
 }
 
-struct HwsPlan {
-  bool ok = false;
-  int tr = 0, tc = 0, twin = 0, npx = 0, rp = 0, pxp = 0, tiles_x = 0, tiles_y = 0;
-  size_t lds = 0;
-};
-// conv_hws_kernel geometry: 64 NPT output pixels as tc = 16 (or 8 where that wastes fewer columns)
-// by tr rows; the window (+ halo) one plane per 16-channel part, row pitch rp (= tc mod 16 for tc 8).
-HwsPlan hws_plan(const yk_op& op, int ne, int npt) {
-  HwsPlan h;
-  const int k = op.ksize;
-  const int c0 = op.src_ch[0], cin = op.src_ch[0] + (op.n_src > 1 ? op.src_ch[1] : 0);
-  if ((k != 1 && k != 3) || op.stride != 1 || cin % 4 || c0 % 4 || op.out_h < 1 || op.out_w < 1) return h;
-  if (ne < 1 || ne > 5 || (npt != 1 && npt != 2 && npt != 4) || (k == 1 && npt > 2)) return h;
-  const int px = 64 * npt;
-  const int w16 = (op.out_w + 15) / 16 * 16, w8 = (op.out_w + 7) / 8 * 8;
-  h.tc = (w8 < w16 && px / 8 >= 2) ? 8 : 16;
-  h.tr = px / h.tc;
-  h.twin = h.tc + k - 1;
-  const int thin = h.tr + k - 1;
-  h.rp = h.tc == 16 ? h.twin : h.twin + (((8 - h.twin) % 16) + 16) % 16;
-  h.npx = h.twin * thin;
-  h.pxp = (h.rp * thin + 15) / 16 * 16;
-  if ((k == 3 && h.npx > 512) || (k == 1 && h.npx > 128)) return h;
-  const int cc = k == 1 ? 4 : 1;
-  h.lds = (size_t)2 * 8 * cc * h.pxp * 16 + (size_t)kHwsR * ne * 3072;
-  if (h.lds > 160 * 1024) return h;
-  h.tiles_x = (op.out_w + h.tc - 1) / h.tc;
-  h.tiles_y = (op.out_h + h.tr - 1) / h.tr;
-  h.ok = true;
-  return h;
-}
-
 // conv_fast_kernel geometry: the largest fragment tile (NNT x NPT) that still gives >= 1024
 // workgroups (>= 4 waves per CU) and wastes < 25% of the n-tiles; the four waves split K (WS)
 // when the per-wave-pixel layout would give too few workgroups.
@@ -3935,13 +3694,6 @@ ConvPlan conv_plan(const yk_model* m, const yk_op& op, int B) {
       if ((p.npt & kSplitBit) && !(m->wsplit && m->ws_off[idx] >= 0)) p.npt &= ~kSplitBit;
       return p;
     }
-    if (t[0] == CK_HWS && m->wkslot && m->wk_off[idx] >= 0 && hws_plan(op, t[1], t[2]).ok) {
-      ConvPlan p;
-      p.kind = CK_HWS;
-      p.nnt = t[1];
-      p.npt = t[2];
-      return p;
-    }
     if (t[0] == CK_HALO && m->wkslot && m->wk_off[idx] >= 0 && halo_plan(op, t[2] & 15, (t[2] >> 4) & 1).ok) {
       ConvPlan p;
       p.kind = CK_HALO;
@@ -3989,27 +3741,27 @@ void launch_splitk(const ConvArgs& a, const ConvPlan& p, hipStream_t st) {
   else launch_splitk_n<Tr, 1>(a, p.npt, st);
 }
 
-template <class Tr, int NNT, int NPT, bool WS>
+template <class Tr, int NNT, int NPT, int KW>
 void launch_fast_t(const FastArgs& a, hipStream_t st) {
   constexpr int SKD = fast_skd(NNT, NPT);
-  const int px = WS ? 16 * NPT : 64 * NPT;
+  const int px = (64 / KW) * NPT;
   dim3 grid((a.M + px - 1) / px, (a.n_tiles + NNT - 1) / NNT);
-  hipLaunchKernelGGL((conv_fast_kernel<Tr, NNT, NPT, WS, SKD>), grid, dim3(256), fast_lds(a.k_steps, NNT, NPT, WS), st,
+  hipLaunchKernelGGL((conv_fast_kernel<Tr, NNT, NPT, KW, SKD>), grid, dim3(256), fast_lds(a.k_steps, NNT, NPT, KW), st,
                      a);
 }
-template <class Tr, int NNT, bool WS>
+template <class Tr, int NNT, int KW>
 void launch_fast_n(const FastArgs& a, int npt, hipStream_t st) {
-  if (npt == 4) launch_fast_t<Tr, NNT, 4, WS>(a, st);
-  else if (npt == 2) launch_fast_t<Tr, NNT, 2, WS>(a, st);
-  else launch_fast_t<Tr, NNT, 1, WS>(a, st);
+  if (npt == 4) launch_fast_t<Tr, NNT, 4, KW>(a, st);
+  else if (npt == 2) launch_fast_t<Tr, NNT, 2, KW>(a, st);
+  else launch_fast_t<Tr, NNT, 1, KW>(a, st);
 }
-template <class Tr, bool WS>
+template <class Tr, int KW>
 void launch_fast_w(const FastArgs& a, int nnt, int npt, hipStream_t st) {
   switch (nnt) {
-    case 1: launch_fast_n<Tr, 1, WS>(a, npt, st); break;
-    case 2: launch_fast_n<Tr, 2, WS>(a, npt, st); break;
-    case 3: launch_fast_n<Tr, 3, WS>(a, npt, st); break;
-    default: launch_fast_n<Tr, 4, WS>(a, npt, st); break;
+    case 1: launch_fast_n<Tr, 1, KW>(a, npt, st); break;
+    case 2: launch_fast_n<Tr, 2, KW>(a, npt, st); break;
+    case 3: launch_fast_n<Tr, 3, KW>(a, npt, st); break;
+    default: launch_fast_n<Tr, 4, KW>(a, npt, st); break;
   }
 }
 template <class Tr, int NNT, int NPT>
@@ -4034,8 +3786,9 @@ void launch_fastw(const FastArgs& a, int nnt, int npt, hipStream_t st) {
     default: launch_fastw_n<Tr, 4>(a, npt, st); break;
   }
 }
-// plan.npt = NPT | mode << 4: mode 0 per-wave pixels, 1 = the four waves split K (WS),
-// 2 = per-wave pixels with the weight fragments shared through LDS (conv_fastw_kernel)
+// plan.npt = NPT | mode << 4: mode 0 per-wave pixels, 1 = the four waves split K (KW 4),
+// 2 = per-wave pixels with the weight fragments shared through LDS (conv_fastw_kernel),
+// 3 = two pairs of waves, each pair splitting K (KW 2)
 template <class Tr>
 void launch_fast(const FastArgs& a, const ConvPlan& p, hipStream_t st) {
   const int mode = (p.npt >> 4) & 3;
@@ -4043,8 +3796,9 @@ void launch_fast(const FastArgs& a, const ConvPlan& p, hipStream_t st) {
     launch_fastw<Tr>(a, p.nnt, p.npt & 15, st);
     return;
   }
-  if (mode == 1) launch_fast_w<Tr, true>(a, p.nnt, p.npt & 15, st);
-  else launch_fast_w<Tr, false>(a, p.nnt, p.npt & 15, st);
+  if (mode == 1) launch_fast_w<Tr, 4>(a, p.nnt, p.npt & 15, st);
+  else if (mode == 3) launch_fast_w<Tr, 2>(a, p.nnt, p.npt & 15, st);
+  else launch_fast_w<Tr, 1>(a, p.nnt, p.npt & 15, st);
 }
 
 template <int NE, int NPT, int WM, int KS>
@@ -4068,31 +3822,6 @@ void launch_halo_p(const HaloArgs& a, int B, int npt, int wm, int ks, hipStream_
   if (npt == 4) launch_halo_w<NE, 4>(a, B, wm, ks, st);
   else if (npt == 2) launch_halo_w<NE, 2>(a, B, wm, ks, st);
   else launch_halo_w<NE, 1>(a, B, wm, ks, st);
-}
-template <int NE, int NPT, int KS>
-void launch_hws_t(const HwsArgs& a, int B, size_t lds, hipStream_t st) {
-  dim3 grid(B * a.h.tiles_x * a.h.tiles_y, (a.h.n_tiles + NE - 1) / NE);
-  hipLaunchKernelGGL((conv_hws_kernel<NE, NPT, KS>), grid, dim3(256), lds, st, a);
-}
-template <int NE, int NPT>
-void launch_hws_k(const HwsArgs& a, int B, int ks, size_t lds, hipStream_t st) {
-  if (ks == 3) launch_hws_t<NE, NPT, 3>(a, B, lds, st);
-  else if constexpr (NPT <= 2) launch_hws_t<NE, NPT, 1>(a, B, lds, st);
-}
-template <int NE>
-void launch_hws_p(const HwsArgs& a, int B, int npt, int ks, size_t lds, hipStream_t st) {
-  if (npt == 4) launch_hws_k<NE, 4>(a, B, ks, lds, st);
-  else if (npt == 2) launch_hws_k<NE, 2>(a, B, ks, lds, st);
-  else launch_hws_k<NE, 1>(a, B, ks, lds, st);
-}
-void launch_hws(const HwsArgs& a, int B, const ConvPlan& p, int ks, size_t lds, hipStream_t st) {
-  switch (p.nnt) {
-    case 1: launch_hws_p<1>(a, B, p.npt, ks, lds, st); break;
-    case 2: launch_hws_p<2>(a, B, p.npt, ks, lds, st); break;
-    case 3: launch_hws_p<3>(a, B, p.npt, ks, lds, st); break;
-    case 4: launch_hws_p<4>(a, B, p.npt, ks, lds, st); break;
-    default: launch_hws_p<5>(a, B, p.npt, ks, lds, st); break;
-  }
 }
 void launch_halo(const HaloArgs& a, int B, const ConvPlan& p, int ks, hipStream_t st) {
   const int npt = p.npt & 15, wm = (p.npt >> 4) & 1;
@@ -4240,24 +3969,10 @@ int launch_op(yk_model* m, const yk_op& op, const uint8_t* frames, int B, float 
             if (nw == 8) launch_wide_n<Tr, 4, 8>(w, wp.upt, wp.lds, st);
             else launch_wide_n<Tr, 4, 4>(w, wp.upt, wp.lds, st);
           }
-        } else if (cp.kind == CK_HALO || cp.kind == CK_HWS) {
+        } else if (cp.kind == CK_HALO) {
           if constexpr (std::is_same<Tr, F32>::value) {
             const size_t oi = (size_t)(&op - m->ops.data());
-            HaloPlan hp;
-            HwsPlan wp;
-            if (cp.kind == CK_HWS) {
-              wp = hws_plan(op, cp.nnt, cp.npt);
-              hp.tr = wp.tr;
-              hp.tc = wp.tc;
-              hp.twin = wp.twin;
-              hp.npx = wp.npx;
-              hp.rp = wp.rp;
-              hp.hw = 0;
-              hp.tiles_x = wp.tiles_x;
-              hp.tiles_y = wp.tiles_y;
-            } else {
-              hp = halo_plan(op, cp.npt & 15, (cp.npt >> 4) & 1);
-            }
+            const HaloPlan hp = halo_plan(op, cp.npt & 15, (cp.npt >> 4) & 1);
             HaloArgs h;
             h.arena = m->arena;
             h.arena_bytes = (unsigned)m->arena_bytes;
@@ -4301,15 +4016,7 @@ int launch_op(yk_model* m, const yk_op& op, const uint8_t* frames, int B, float 
             h.r_coff = a.r_coff;
             h.act = a.act;
             h.xcd = m->xcd;
-            if (cp.kind == CK_HWS) {
-              HwsArgs w;
-              w.h = h;
-              w.pxp = wp.pxp;
-              w.nsteps = ((a.cin + 15) / 16) * op.ksize * op.ksize;
-              launch_hws(w, B, cp, op.ksize, wp.lds, st);
-            } else {
-              launch_halo(h, B, cp, op.ksize, st);
-            }
+            launch_halo(h, B, cp, op.ksize, st);
           }
         } else if (cp.kind == CK_FAST) {
           FastArgs f;
@@ -4509,10 +4216,6 @@ const char* op_kernel_name(const yk_model* m, const yk_op& op) {
     snprintf(buf, sizeof buf, "conv_halo_kernel<%d, %d, %d, %d>", cp.nnt, cp.npt & 15, (cp.npt >> 4) & 1, op.ksize);
     return buf;
   }
-  if (cp.kind == CK_HWS) {
-    snprintf(buf, sizeof buf, "conv_hws_kernel<%d, %d, %d>", cp.nnt, cp.npt, op.ksize);
-    return buf;
-  }
   if (cp.kind == CK_FAST) {
     const int npt = cp.npt & 15, mode = (cp.npt >> 4) & 3;
     const int skd = mode == 2 ? fastw_skd(cp.nnt, npt) : fast_skd(cp.nnt, npt);
@@ -4520,8 +4223,8 @@ const char* op_kernel_name(const yk_model* m, const yk_op& op) {
     if (mode == 2)
       snprintf(buf, sizeof buf, "conv_fastw_kernel<yk::det::%s, %d, %d, %d>", tn, cp.nnt, npt, skd);
     else
-      snprintf(buf, sizeof buf, "conv_fast_kernel<yk::det::%s, %d, %d, %s, %d>", tn, cp.nnt, npt,
-               mode ? "true" : "false", skd);
+      snprintf(buf, sizeof buf, "conv_fast_kernel<yk::det::%s, %d, %d, %d, %d>", tn, cp.nnt, npt,
+               mode == 1 ? 4 : mode == 3 ? 2 : 1, skd);
     return buf;
   }
   if (cp.kind == CK_SPLITK) {
@@ -5236,10 +4939,7 @@ int yk_model_profile(yk_model* m, const uint8_t* frames, int batch, float conf, 
 
 int yk_model_set_plan(yk_model* m, int op_index, int batch, int kind, int nnt, int npt) {
   YK_CHECK_ARG(m && op_index >= -1 && op_index < (int)m->ops.size(), "yk_model_set_plan: bad op index");
-  YK_CHECK_ARG(kind >= -1 && kind <= CK_HWS, "yk_model_set_plan: kind must be -1 (heuristic), 0, 1, 2, 3, 4, 5 or 6");
-  YK_CHECK_ARG(kind != CK_HWS || (m->wkslot && nnt >= 1 && nnt <= 5 && (npt == 1 || npt == 2 || npt == 4)),
-               "yk_model_set_plan: halo + shared-weight conv (kind 6) needs the fp32 build, nnt in [1, 5], npt in "
-               "{1, 2, 4}");
+  YK_CHECK_ARG(kind >= -1 && kind <= CK_HALO, "yk_model_set_plan: kind must be -1 (heuristic), 0, 1, 2, 3, 4 or 5");
   YK_CHECK_ARG(kind != CK_HALO || (m->wkslot && (nnt == 1 || nnt == 2) &&
                                    ((npt & 15) == 1 || (npt & 15) == 2 || (npt & 15) == 4) && (npt & ~31) == 0),
                "yk_model_set_plan: halo conv (kind 5) needs the fp32 build, nnt in {1, 2}, npt in {1, 2, 4} (+16: "
@@ -5247,9 +4947,9 @@ int yk_model_set_plan(yk_model* m, int op_index, int batch, int kind, int nnt, i
   YK_CHECK_ARG(kind != CK_WIDE || ((nnt == 2 || nnt == 4) && (npt == 0 || npt == 4 || npt == 8)),
                "yk_model_set_plan: wide conv nnt must be 2 or 4, npt (waves) 0, 4 or 8");
   YK_CHECK_ARG(kind != CK_FAST || (nnt >= 1 && nnt <= 4 && ((npt & 15) == 1 || (npt & 15) == 2 || (npt & 15) == 4) &&
-                                   ((npt >> 4) & 3) <= 2 && (npt & ~(kSplitBit | 63)) == 0),
+                                   (npt & ~(kSplitBit | 63)) == 0),
                "yk_model_set_plan: table conv needs nnt in [1, 4], npt in {1, 2, 4} (+16: waves split K, +32: LDS-shared "
-               "weights, +64: split-bf16 MFMA)");
+               "weights, +48: wave pairs split K, +64: split-bf16 MFMA)");
   YK_CHECK_ARG(kind != CK_FAST || !(npt & kSplitBit) || m->wsplit,
                "yk_model_set_plan: the split-bf16 MFMA variant (+64) needs the fp32 build");
   YK_CHECK_ARG(kind != CK_TILE || nnt == 0 || nnt == 1, "yk_model_set_plan: tiled conv nnt must be 0 or 1 (LDS-resident weights)");
@@ -5314,11 +5014,11 @@ int yk_model_autotune(yk_model* m, const uint8_t* frames, int batch, float conf,
           if (wide_plan(op, esz, nnt, nw).ok && (long)bt * op.out_h * op.out_w >= 4096) cands.push_back({CK_WIDE, nnt, nw});
       }
     if (m->ktab && m->ktab_off[i] >= 0 && (long)bt * op.out_h * op.out_w < (1L << 22))
-      for (int mode = 0; mode < 3; ++mode)  // per-wave pixels / waves split K / LDS-shared weights
+      for (int mode = 0; mode < 4; ++mode)  // per-wave pixels / waves split K / LDS-shared weights / pairs split K
         for (int nnt : {1, 2, 3, 4})
           for (int npt : {1, 2, 4}) {
             if (nnt > 1 && 4 * op.n_tiles < 3 * ((op.n_tiles + nnt - 1) / nnt) * nnt) continue;
-            const long px = mode == 1 ? 16 * npt : 64 * npt;
+            const long px = mode == 1 ? 16 * npt : mode == 3 ? 32 * npt : 64 * npt;
             const long wgs = ((long)bt * op.out_h * op.out_w + px - 1) / px * ((op.n_tiles + nnt - 1) / nnt);
             if (wgs < 64) continue;
             cands.push_back({CK_FAST, nnt, npt | (mode << 4)});
@@ -5335,15 +5035,6 @@ int yk_model_autotune(yk_model* m, const uint8_t* frames, int batch, float conf,
             if (!hp.ok || (long)bt * hp.tiles_x * hp.tiles_y * groups < 64) continue;
             cands.push_back({CK_HALO, ne, npt | (wm << 4)});
           }
-    if (m->wkslot && m->wk_off[i] >= 0 && m->autotune_split)
-      for (int ne = 1; ne <= 5; ++ne)
-        for (int npt : {1, 2, 4}) {
-          const int groups = (op.n_tiles + ne - 1) / ne;
-          if (4 * op.n_tiles < 3 * groups * ne) continue;  // < 75 % of the tiles real
-          const HwsPlan hp = hws_plan(op, ne, npt);
-          if (!hp.ok || (long)bt * hp.tiles_x * hp.tiles_y * groups < 64) continue;
-          cands.push_back({CK_HWS, ne, npt});
-        }
     if (cands.empty()) continue;  // (FP8 without a table: yk_model_create refuses that)
     float best = 1e30f;
     std::array<int, 3> pick = {-1, 0, 0};
