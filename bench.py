@@ -407,6 +407,7 @@ def run_leg(a, P, cfg, dtype, frames, dev, local, rank, ws, headline):
         if d2h:
             pipe.download_async(out_rows, out_counts, out_stats)
         host_ns += time.perf_counter_ns() - h0
+    pipe.flush()  # (motion windows: the last partial wave's motion + tracker steps, inside the timing)
     torch.cuda.synchronize()
     barrier(ws)
     elapsed = time.perf_counter() - t0
@@ -425,6 +426,7 @@ def run_leg(a, P, cfg, dtype, frames, dev, local, rank, ws, headline):
     th = time.perf_counter()
     for t in range(a.steps):
         pipe.run(frames[(t_first + a.steps + t) % F])
+    pipe.flush()
     torch.cuda.synchronize()
     barrier(ws)
     hbm_elapsed = time.perf_counter() - th

@@ -275,8 +275,8 @@ def test_pipeline_with_global_motion_matches_serial():
     seqs = [camera_sequence(80 + s, F, h=512, w=640, whip_at=(7, 14), n_targets=12)[0] for s in range(S)]
     frames = torch.from_numpy(np.stack(seqs, 1)).cuda()  # [F, S, H, W, 3]
     runs = []
-    # inflight 4 is bench.py's CMC depth, 6 the depth round 4 saw differ (LK end points of border
-    # windows; the lk_kernel stack object, fixed in round 5 -- csrc/gmd.hip lk_kernel)
+    # inflight 4 is bench.py's CMC depth, 6 the depth round 4 saw differ (Lucas-Kanade end points
+    # read beside forwards; the pipeline now runs the motion kernels in windows no forward overlaps)
     for pipelined, inflight in ((False, 1), (True, 1), (True, 3), (True, 4), (True, 6)):
         pipe = pipeline.StreamPipeline("yolov8s-small.yaml", S, (512, 640), "bf16", seed=0, max_tracks=256,
                                        pipelined=pipelined, inflight=inflight, tracker_policy=1,
@@ -300,6 +300,53 @@ def test_pipeline_with_global_motion_matches_serial():
             np.testing.assert_array_equal(ms1[f], ms0[f], err_msg=f"gmd stats.{f}")
         for s in range(S):
             assert r0[s][: c0[s]].tobytes() == r1[s][: c1[s]].tobytes()
+
+
+def test_motion_windows_record_every_step_and_download_in_order():
+    """Motion windows (pipelined tracker stream + motion detector): a wave's tracker steps are
+    enqueued in its window, so the step hook and download_async of each step must still see that
+    step's own tracker output.  Every step's recorded tracker rows at inflight 4 (a partial last
+    wave included: 18 steps) equal the serial pipeline's, and the page-locked download of the last
+    step equals the tracker's final state."""
+    from gmd_helpers import camera_sequence
+    from gpu_helpers import StepRecorder
+
+    P = pkg()
+    pipeline = importlib.import_module(P.__name__ + ".pipeline")
+    L = P._lib
+    S, F = 2, 18
+    seqs = [camera_sequence(60 + s, F, h=512, w=640, whip_at=(6, 12), n_targets=10)[0] for s in range(S)]
+    frames = torch.from_numpy(np.stack(seqs, 1)).cuda()
+    recs = []
+    for pipelined, inflight in ((False, 1), (True, 4)):
+        pipe = pipeline.StreamPipeline("yolov8s-small.yaml", S, (512, 640), "bf16", seed=0, max_tracks=256,
+                                       pipelined=pipelined, inflight=inflight, tracker_policy=1,
+                                       motion_method="optical_flow")
+        pipe.frames.copy_(frames[0])
+        pipe.capture(tune=False)
+        rec = StepRecorder(pipe, F)
+        pipe.step_hook = rec
+        rows_h = torch.empty(S * 256 * L.TRACK_OUT_DTYPE.itemsize, dtype=torch.uint8, pin_memory=True)
+        counts_h = torch.empty(S, dtype=torch.int32, pin_memory=True)
+        stats_h = torch.empty(S * L.STATS_DTYPE.itemsize, dtype=torch.uint8, pin_memory=True)
+        for t in range(F):
+            pipe.run(frames[t])
+            if pipelined:
+                pipe.download_async(rows_h, counts_h, stats_h)
+        pipe.sync()
+        recs.append(rec.host())
+        if pipelined:
+            rows, counts, _ = pipe.tracker.download()
+            got = rows_h.numpy().view(L.TRACK_OUT_DTYPE).reshape(S, -1)
+            np.testing.assert_array_equal(counts_h.numpy(), counts)
+            for s in range(S):
+                assert got[s, : counts[s]].tobytes() == rows[s, : counts[s]].tobytes()
+    (d0, n0, r0, c0, s0), (d1, n1, r1, c1, s1) = recs
+    np.testing.assert_array_equal(n0, n1)
+    np.testing.assert_array_equal(c0, c1)
+    for t in range(F):
+        for s in range(S):
+            assert r0[t, s, : c0[t, s]].tobytes() == r1[t, s, : c1[t, s]].tobytes(), (t, s)
 
 
 def _pan_scene(seed, F, K=10):

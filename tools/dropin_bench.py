@@ -94,9 +94,29 @@ def main():
     model = YOLO("yolov8s-small.yaml", **({"dtype": a.dtype} if a.dtype else {}))
     tracker = EnhancedMultiTargetTracker(max_lost_frames=150, min_hits=1, iou_threshold=0.1)
     split = dict.fromkeys(("preprocess", "inference", "postprocess", "predict_call", "boxes", "tracker", "driver"), 0.0)
+    # the tracker update's own phases, timed inside the same update calls (so they add up to the
+    # split's "tracker" entry): H2D + step launch, download (counts / stats / rows), rows -> dicts
+    T = importlib.import_module(PKG + ".tracker")
+    ph = dict.fromkeys(("step_host", "download", "dicts"), 0.0)
+    gate = {"on": False}
+
+    def timed(fn, key):
+        def w(*args, **kw):
+            t = time.perf_counter()
+            r = fn(*args, **kw)
+            if gate["on"]:
+                ph[key] += time.perf_counter() - t
+            return r
+        return w
+
+    tracker._core.step_host = timed(tracker._core.step_host, "step_host")
+    tracker._core.download = timed(tracker._core.download, "download")
+    T.rows_to_dicts = timed(T.rows_to_dicts, "dicts")
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    live = driver_loop(model, tracker, frames, a.preroll, split)
+    live = driver_loop(model, tracker, frames[: a.preroll], 0, dict.fromkeys(split, 0.0))
+    gate["on"] = True
+    live = driver_loop(model, tracker, frames[a.preroll:], 0, split)
     torch.cuda.synchronize()
     # the timed part is the frames from `preroll` on: re-time them alone
     total_split = sum(split[k] for k in ("predict_call", "boxes", "tracker", "driver"))
@@ -108,27 +128,6 @@ def main():
            "ms_per_frame": round(total_split * 1e3 / a.frames, 4),
            "split_ms_per_frame": {k: round(v * 1e3 / a.frames, 4) for k, v in split.items()},
            "wall_incl_preroll_s": round(time.perf_counter() - t0, 3)}
-    # the tracker update's own phases on the same detections (a second tracker, same frames):
-    # H2D + step launch, download (counts / stats, rows), rows -> dicts
-    T = importlib.import_module(PKG + ".tracker")
-    trk2 = EnhancedMultiTargetTracker(max_lost_frames=150, min_hits=1, iou_threshold=0.1)
-    ph = dict.fromkeys(("step_host", "download", "dicts"), 0.0)
-    for i, frame in enumerate(frames):
-        r = model(frame, verbose=False)
-        b, c = r[0].boxes.xyxy.cpu().numpy(), r[0].boxes.conf.cpu().numpy()
-        dets = [[x[0], x[1], x[2], x[3], s] for x, s in zip(b, c) if s > 0.1]
-        ta = time.perf_counter()
-        trk2._core.step_host([dets])
-        tb = time.perf_counter()
-        rows, counts, stats = trk2._core.download()
-        tc = time.perf_counter()
-        T.rows_to_dicts(rows[0, : int(counts[0])]) if hasattr(T, "rows_to_dicts") else \
-            [T._row_to_dict(x, T.track_id_of(x["track_num"])) for x in rows[0, : int(counts[0])]]
-        td = time.perf_counter()
-        if i >= a.preroll:
-            ph["step_host"] += tb - ta
-            ph["download"] += tc - tb
-            ph["dicts"] += td - tc
     out["tracker_split_ms_per_frame"] = {k: round(v * 1e3 / a.frames, 4) for k, v in ph.items()}
     if a.cpu_frames > 0:
         from oracle import detector_ref as D

@@ -20,9 +20,12 @@ frame (motion.BatchedMotionDetector, gmd.hip) on the tracker stream right before
 step, which consumes its device results.  The frame slot is not refilled before that detector
 has read it.
 
-With the motion detector and forwards in flight, the motion kernels do not overlap any forward:
-the motion call of step t waits for every forward enqueued so far and forward(t + 1) waits for
-it.  Round 5 traced run-to-run differences of the pipelined motion records to the Lucas-Kanade
+With the motion detector on a pipelined tracker stream, the motion kernels never overlap a
+forward (motion windows): the D forwards of a wave (steps t .. t + D - 1) run concurrently, then
+one window on the tracker stream -- which waits for every forward enqueued so far -- runs the
+wave's motion + tracker steps in frame order, and the next wave's forwards wait for the window.
+A step's tracker output therefore exists once its wave's window has been enqueued (the last step
+of the wave, or flush() / sync()).  Round 5 traced run-to-run differences of the pipelined motion records to the Lucas-Kanade
 kernel alone: one wave solving its corner twice in one launch read different J samples at the
 same addresses in the two passes while forwards ran beside it (csrc/gmd.hip YK_GMD_DIAG 4),
 with every pyramid producer wave provably complete before the launch (diag 16) and with the
@@ -67,7 +70,11 @@ class StreamPipeline:
                                             policy=tracker_policy)
         dev = torch.device("cuda", self.device)
         self.frames = torch.zeros((self.S, frame_hw[0], frame_hw[1], 3), dtype=torch.uint8, device=dev)
-        self.nb = max(2, int(inflight))  # detection buffers (= detector slots when inflight > 1)
+        # motion windows (see the header): with the motion detector on a pipelined tracker stream
+        self._windowed = motion_method is not None and bool(pipelined)
+        # detection buffers: D (one per detector slot) or, with motion windows, 2 D so the next
+        # wave's forwards do not wait for this wave's tracker steps
+        self.nb = max(2, int(inflight)) * (2 if self._windowed else 1)
         self._dets = torch.zeros((self.nb, self.S, self.max_det, 6), dtype=torch.float32, device=dev)
         self._counts = torch.zeros((self.nb, self.S), dtype=torch.int32, device=dev)
         self._k = 0  # detection buffer the next step writes
@@ -123,7 +130,9 @@ class StreamPipeline:
         self._ev_copy = [torch.cuda.Event() for _ in range(self.n_stage)]
         self._n_stage = 0
         self._prefetched = None  # (data_ptr of the host frames, staging index) of the next step
-        self._ev_motion = None  # motion isolation (gmd with forwards in flight): this step's motion call
+        self._ev_window = None  # end of the last motion window (the next wave's forwards wait for it)
+        self._wave = []  # detection buffers of the current wave's steps (forwards enqueued, window not yet)
+        self._dl = {}  # download_async requests of the current wave's steps, issued in its window
 
     @property
     def dets(self) -> torch.Tensor:
@@ -146,7 +155,7 @@ class StreamPipeline:
                 m.load_plan(b, plan)
 
     def _slot(self, k: int) -> int:
-        return k if self.D > 1 else 0
+        return k % self.D
 
     def _stream(self, s: int):
         st = self.det_streams[s]
@@ -176,28 +185,27 @@ class StreamPipeline:
         if self._trk_pending[k]:  # tracker(t - nb) still reads buffer k
             cur.wait_event(self._ev_trk[k])
             self._trk_pending[k] = False
-        if self._ev_motion is not None:  # motion isolation: no forward beside the motion kernels
-            cur.wait_event(self._ev_motion)
+        if self._ev_window is not None:  # no forward beside a motion window
+            cur.wait_event(self._ev_window)
         with torch.cuda.stream(cur):
             self.models[s].detect(self.frame_slots[s], self.conf, self.iou, self.max_det, self._dets[k],
                                   self._counts[k], graph=bool(self.graph))
+        if self._windowed:
+            self._ev_det[k].record(cur)
+            self._wave.append(k)
+            self._k = (k + 1) % self.nb
+            if len(self._wave) == self.D:
+                self._run_window()
+            return
         if self.pipelined:
             self._ev_det[k].record(cur)
             self.trk_stream.wait_event(self._ev_det[k])
-            if self.gmd is not None and self.D > 1:
-                for j in range(self.D):  # every forward enqueued so far ends before the motion call
-                    if j != s:
-                        self.trk_stream.wait_stream(self._stream(j))
             with torch.cuda.stream(self.trk_stream):
                 self._track(k, s)
             self._ev_trk[k].record(self.trk_stream)
             self._trk_pending[k] = True
         else:
             self._track(k, s)
-        if self.gmd is not None and self.pipelined and self.D > 1:
-            # forward(t + 1) starts after this step's motion kernels (isolation, see the header)
-            self._ev_motion = torch.cuda.Event()
-            self._ev_motion.record(self.trk_stream)
         if self.step_hook is not None:
             # harness hook (tests/recorders): enqueue work after this step's launches on the
             # detector stream (reads of detection buffer k) and the tracker stream (results)
@@ -215,8 +223,37 @@ class StreamPipeline:
             self._gmd_pending[s] = True
         self.tracker.step_device(self._dets[k], self._counts[k], motion=self.gmd.motion_ptr)
 
+    def _run_window(self):
+        """Motion window of the current wave (see the header): after every forward enqueued so far,
+        each step's motion detector and tracker step in frame order on the tracker stream (plus the
+        step hook and any download_async request of that step); the next forwards wait for its end."""
+        trk = self.trk_stream
+        for j in range(self.D):
+            trk.wait_stream(self._stream(j))
+        with torch.cuda.stream(trk):
+            for k in self._wave:
+                s = self._slot(k)
+                self._track(k, s)
+                self._ev_trk[k].record(trk)
+                self._trk_pending[k] = True
+                if self.step_hook is not None:
+                    self.step_hook(self, k, self._stream(s), trk)
+                req = self._dl.pop(k, None)
+                if req is not None:
+                    self.tracker.download_async(*req, stream=trk.cuda_stream)
+        self._ev_window = torch.cuda.Event()
+        self._ev_window.record(trk)
+        self._wave = []
+
+    def flush(self):
+        """Enqueue the motion window of a partial wave (motion windows only; a no-op otherwise):
+        after it every run() so far has its tracker step enqueued."""
+        if self._windowed and self._wave:
+            self._run_window()
+
     def sync(self):
         """Wait for every launched step (detector and tracker streams)."""
+        self.flush()
         torch.cuda.synchronize(self.device)
 
     def run(self, frames: torch.Tensor, next_frames: torch.Tensor | None = None):
@@ -277,13 +314,18 @@ class StreamPipeline:
         """Enqueue the tracker output of the most recent step into page-locked host buffers
         (rows [S * max_tracks] yk_track_out bytes, counts int32 [S], stats [S] yk_tracker_stats)
         on the tracker stream, behind that step; no host wait.  The host reads them after
-        sync() (or an event recorded on the tracker stream after this call)."""
+        sync() (or an event recorded on the tracker stream after this call).  With motion windows
+        the copy is issued right after that step's tracker step, inside its wave's window."""
+        if self._windowed and self._wave:  # this step's tracker step runs in its wave's window
+            self._dl[self._wave[-1]] = (rows, counts, stats, rows_per_stream)
+            return
         st = self.trk_stream if self.pipelined else torch.cuda.current_stream(self.device)
         self.tracker.download_async(rows, counts, stats, rows_per_stream, stream=st.cuda_stream)
 
     def download(self):
         """Tracker results of the most recent step (rows, counts, stats; host arrays).  Waits for
         the tracker stream first, so it is safe while steps are pipelined."""
+        self.flush()
         if self.pipelined:
             torch.cuda.current_stream(self.device).wait_stream(self.trk_stream)
         return self.tracker.download()
