@@ -113,6 +113,8 @@ def parse():
     ap.add_argument("--save-plans", action="store_true", help="write every leg's conv plan to plans/<workload>.json")
     ap.add_argument("--plan-in", default="", help="conv plan (json) of the headline leg (default: plans/<workload>.json)")
     ap.add_argument("--dump-ops", default="", help="write per-op device times (json) to this path")
+    ap.add_argument("--no-prefetch", action="store_true",
+                    help="upload each step's host frames on its slot stream instead of one step ahead on the copy stream")
     ap.add_argument("--io", default="both", choices=["both", "h2d", "d2h", "none"],
                     help="diagnostics: which host copies the timed loop makes (default both: the metric's definition)")
     a = ap.parse_args()
@@ -401,7 +403,8 @@ def run_leg(a, P, cfg, dtype, frames, dev, local, rank, ws, headline):
     for t in range(a.steps):
         h0 = time.perf_counter_ns()
         if h2d:  # the next step's frames are uploaded while this step runs (decode-ahead driver)
-            pipe.run(host[t % n_host], next_frames=host[(t + 1) % n_host] if t + 1 < a.steps and pipe.D > 1 else None)
+            nxt = host[(t + 1) % n_host] if t + 1 < a.steps and pipe.D > 1 and not a.no_prefetch else None
+            pipe.run(host[t % n_host], next_frames=nxt)
         else:
             pipe.run(frames[(t_first + t) % F])
         if d2h:

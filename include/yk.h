@@ -511,6 +511,15 @@ int yk_detect_graph(yk_model* m, const uint8_t* dev_frames, int batch, float con
 
 int yk_model_outputs(yk_model* m, float** dev_dets, int32_t** dev_counts);
 
+/* The driver's frame in host memory -> HBM (cv2.VideoCapture.read() then model(frame),
+ * kalman/aircraft_detection_tracking.py:96-100): copy `bytes` (a multiple of 16) of page-locked
+ * host memory (hipHostMalloc / torch pin_memory; checked) to device memory with a kernel that
+ * reads the host pages directly, on `stream`, without a host wait.  For frames below a few MiB:
+ * the runtime copies small page-locked H2D transfers through the CPU synchronously (one
+ * 640x512 frame held the host ~170 us), this call costs one launch; large transfers are as fast
+ * through hipMemcpyAsync's DMA engine. */
+int yk_upload_pinned_async(void* dev_dst, const void* host_src, size_t bytes, void* stream);
+
 /* Pre-NMS candidates of the last yk_detect: [max_batch][n_anchors] rows of
  * {x1, y1, x2, y2, score, anchor_index (int32 bits)} in network-input pixels, unordered,
  * counts per image (parity harnesses compare them to the oracle's Detect output). */

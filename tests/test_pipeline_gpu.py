@@ -416,3 +416,22 @@ def test_stream_pipeline_global_motion_fp32_matches_oracle_chain():
             n_rows += len(rb)
     assert n_rows > 200
     assert sum(r.stats["global_resets"] for r in refs) >= 2
+
+
+def test_upload_pinned_async_copies_host_frames_exactly():
+    """yk_upload_pinned_async (the pull kernel the pipeline uses for page-locked frames below
+    StreamPipeline.PULL_BYTES): bit-exact copies of one and of eight 640x512 frames, a ragged
+    16-byte multiple, and a refusal of pageable memory."""
+    P = pkg()
+    L = P._lib
+    g = torch.Generator().manual_seed(3)
+    for shape in ((1, 512, 640, 3), (8, 512, 640, 3), (7, 16)):
+        src = torch.randint(0, 256, shape, dtype=torch.uint8, generator=g).pin_memory()
+        dst = torch.zeros(shape, dtype=torch.uint8, device="cuda")
+        L.check(L.lib().yk_upload_pinned_async(L.ptr(dst), L.ptr(src), src.numel(), L.current_stream(0)), "upload")
+        torch.cuda.synchronize()
+        assert torch.equal(dst.cpu(), src)
+    pageable = torch.zeros(64, dtype=torch.uint8)
+    dst = torch.zeros(64, dtype=torch.uint8, device="cuda")
+    with pytest.raises(L.YKError):
+        L.check(L.lib().yk_upload_pinned_async(L.ptr(dst), L.ptr(pageable), 64, L.current_stream(0)), "upload")

@@ -148,6 +148,7 @@ _SIGS = {
     "yk_tracker_outputs": ([_vp, C.POINTER(_vp), C.POINTER(_vp), C.POINTER(_vp)], C.c_int),
     "yk_tracker_download": ([_vp, _vp, _vp, _vp, _vp], C.c_int),
     "yk_tracker_download_async": ([_vp, _vp, _vp, _vp, C.c_int, _vp], C.c_int),
+    "yk_upload_pinned_async": ([_vp, _vp, C.c_size_t, _vp], C.c_int),
     "yk_tracker_snapshot": ([_vp, C.c_int, _vp, C.POINTER(_i32), _vp], C.c_int),
     "yk_track_op": ([_vp, C.c_int, C.c_int, C.c_int, C.c_int, _vp, C.c_int, _vp, _vp, _vp], C.c_int),
     "yk_track_create": ([_vp, C.c_int, _vp, C.c_int, _i32, _i32, _vp], C.c_int),

@@ -4859,12 +4859,28 @@ int yk_detect_graph(yk_model* m, const uint8_t* frames, int batch, float conf, f
   auto key = std::make_tuple(batch, conf, iou, max_det, (const void*)frames, (void*)dets, (void*)counts);
   auto it = m->graphs.find(key);
   if (it == m->graphs.end()) {
-    // one capture stream per model, alive as long as the model and its graphs: round 4 created a
-    // stream per capture and destroyed it right after hipStreamEndCapture, and multi-lane graphs
-    // (forked onto m->aux) then crashed inside hipGraphLaunch once several models were alive
-    // (tools/graph_fork_repro.hip reproduces that pattern in pure HIP)
-    if (!m->cap) YK_HIP(hipStreamCreateWithFlags(&m->cap, hipStreamNonBlocking));
-    hipStream_t cap = m->cap;
+    // Capture stream: one per model, kept for the model's lifetime (round 4 created one per
+    // capture and destroyed it after hipStreamEndCapture, and multi-lane graphs then crashed in
+    // hipGraphLaunch once several models were alive; tools/graph_fork_repro.hip did not reproduce
+    // that in either form).  Which stream a graph is captured on moves the launch rate through
+    // the streams' hardware-queue mapping, not through the graph: capturing on the launch stream
+    // (YK_CAP_STREAM=launch) or on a temporary stream (=destroy) measured 4-11 % slower on the
+    // host-frame bench lines with one created stream per slot (gpurun_out/r6i: config 3
+    // 4,648-4,658 vs 5,181-5,231 frames/s) and faster only with slot 0 on the legacy null stream
+    // at batch 1 (r6e).  The variable is kept for A/B runs.
+    const char* cm = getenv("YK_CAP_STREAM");
+    const int cap_mode = cm && !strcmp(cm, "destroy") ? 1 : cm && !strcmp(cm, "launch") ? 2 : 0;
+    hipStream_t cap = nullptr;
+    bool cap_tmp = false;
+    if (cap_mode == 2 && stream) {
+      cap = (hipStream_t)stream;
+    } else if (cap_mode != 0) {
+      YK_HIP(hipStreamCreateWithFlags(&cap, hipStreamNonBlocking));
+      cap_tmp = true;
+    } else {
+      if (!m->cap) YK_HIP(hipStreamCreateWithFlags(&m->cap, hipStreamNonBlocking));
+      cap = m->cap;
+    }
     hipGraph_t g;
     const bool dbg = getenv("YK_DEBUG_GRAPH") != nullptr;
     YK_HIP(hipStreamBeginCapture(cap, hipStreamCaptureModeThreadLocal));
@@ -4873,6 +4889,7 @@ int yk_detect_graph(yk_model* m, const uint8_t* frames, int batch, float conf, f
     if (dbg) fprintf(stderr, "[yk] ops recorded rc=%d\n", rc);
     hipError_t ce = hipStreamEndCapture(cap, &g);
     if (dbg) fprintf(stderr, "[yk] capture ended: %s\n", hipGetErrorString(ce));
+    if (cap_tmp) (void)hipStreamDestroy(cap);
     if (rc != YK_OK) return rc;
     if (ce != hipSuccess) {
       yk::set_error(std::string("yk_detect_graph: capture failed: ") + hipGetErrorString(ce));
@@ -5072,6 +5089,36 @@ int yk_nms_candidates(yk_model* m, int batch, float iou, int max_det, float* det
   yk::DeviceGuard guard(m->ctx->device);
   return launch_nms(m, batch, iou, max_det, dets ? dets : m->dets, counts ? counts : m->counts, (hipStream_t)stream,
                     keep);
+}
+
+namespace yk {
+namespace det {
+// page-locked host -> device copy read by the device (yk_upload_pinned_async): 16 B per lane,
+// grid-stride, plain loads of the host pages through their device-mapped address
+__global__ void __launch_bounds__(256) pull_copy_kernel(uint4* __restrict__ dst, const uint4* __restrict__ src, size_t n16) {
+  const size_t stride = (size_t)gridDim.x * 256;
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += stride) dst[i] = src[i];
+}
+}  // namespace det
+}  // namespace yk
+
+int yk_upload_pinned_async(void* dev_dst, const void* host_src, size_t bytes, void* stream) {
+  YK_CHECK_ARG(dev_dst && host_src && bytes % 16 == 0 && ((size_t)dev_dst & 15) == 0 && ((size_t)host_src & 15) == 0,
+               "yk_upload_pinned_async: NULL pointer, or bytes / addresses not multiples of 16");
+  if (bytes == 0) return YK_OK;
+  hipPointerAttribute_t at;
+  const hipError_t e = hipPointerGetAttributes(&at, host_src);
+  if (e != hipSuccess || at.type != hipMemoryTypeHost || !at.devicePointer) {
+    (void)hipGetLastError();
+    yk::set_error("yk_upload_pinned_async: the source must be page-locked, device-mapped host memory");
+    return YK_ERR_ARG;
+  }
+  const size_t n16 = bytes / 16;
+  const unsigned blocks = (unsigned)std::min<size_t>((n16 + 255) / 256, 2048);
+  hipLaunchKernelGGL(yk::det::pull_copy_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (uint4*)dev_dst,
+                     (const uint4*)at.devicePointer, n16);
+  YK_HIP(hipGetLastError());
+  return YK_OK;
 }
 
 int yk_nms(yk_model* m, const float* dev_rows, int row_stride, int max_rows, const int32_t* dev_counts, int batch,

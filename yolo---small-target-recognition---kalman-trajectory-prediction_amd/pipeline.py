@@ -98,7 +98,9 @@ class StreamPipeline:
         # slot s: detector model, input frames and launch stream (None = the caller's stream)
         self.models = [self.model] + [M.DeviceModel(self.prog, self.device) for _ in range(self.D - 1)]
         self.frame_slots = [self.frames] + [torch.zeros_like(self.frames) for _ in range(self.D - 1)]
-        self.det_streams = [None] + [torch.cuda.Stream(dev) for _ in range(self.D - 1)]
+        # one created stream per slot with forwards in flight (the caller's stream with one: the
+        # serial order); slot 0 on the legacy null stream cost ~4 % of the host-frame rate
+        self.det_streams = [None] if self.D == 1 else [torch.cuda.Stream(dev) for _ in range(self.D)]
         if self.D > 1:
             # forwards in flight are the concurrency: one lane per graph (bench.py's default too).
             # Multi-lane (forked) graphs of several in-flight slots plus other live models were
@@ -268,7 +270,9 @@ class StreamPipeline:
         video driver reads ahead).  Their upload is issued now, on the copy stream, into a staging
         buffer; the next run() is handed the same tensor and its slot stream copies staging -> slot
         (device to device) behind that upload's event.  Every frame still crosses PCIe once,
-        inside the caller's loop; the upload of step t + 1 overlaps step t."""
+        inside the caller's loop; the upload of step t + 1 overlaps step t.  Frames smaller than
+        PULL_BYTES are not prefetched: the next run() pulls them onto the slot stream with a kernel
+        (yk_upload_pinned_async), which holds neither the host nor a copy stream."""
         s = self._slot(self._k)
         st = self._stream(s)
         cur = torch.cuda.current_stream(self.device)
@@ -294,9 +298,12 @@ class StreamPipeline:
                 st.wait_event(self._ev_gmd[s])
                 self._gmd_pending[s] = False
             with torch.cuda.stream(st):
-                self.frame_slots[s].copy_(frames, non_blocking=True)
+                self._upload(self.frame_slots[s], frames)
         self.step()
-        if next_frames is not None:
+        if next_frames is not None and next_frames.numel() * next_frames.element_size() >= self.PULL_BYTES:
+            # (frames below PULL_BYTES are pulled on the slot stream by the next run() instead: the
+            # pull kernel costs the host nothing, and a copy-stream hop measured 26 % slower at
+            # batch 1, bench.py --config 2 --no-prefetch)
             if next_frames.is_cuda or self.copy_stream is None:
                 raise ValueError("next_frames: page-locked host frames and inflight > 1")
             i = self._n_stage % self.n_stage
@@ -306,9 +313,26 @@ class StreamPipeline:
                 cs.wait_event(self._ev_stage_read[i])  # (rare: its staging -> slot copy has not run yet)
             self._stage_read_pending[i] = False
             with torch.cuda.stream(cs):
-                self._stage[i].copy_(next_frames, non_blocking=True)
+                self._upload(self._stage[i], next_frames)
             self._ev_copy[i].record(cs)
             self._prefetched = (next_frames.data_ptr(), i)
+
+    # page-locked host frames below this size are pulled by a kernel (yk_upload_pinned_async):
+    # the runtime copies small page-locked H2D transfers through the CPU, synchronously (one
+    # 640x512 frame held the host ~170 us per step, tools/host_split_probe.py); larger ones go to
+    # the DMA engine, which costs no CU time
+    PULL_BYTES = int(__import__("os").environ.get("YK_PULL_BYTES", 4 << 20))
+
+    def _upload(self, dst: torch.Tensor, src: torch.Tensor):
+        """dst (device) <- src (device, or page-locked host) on the current stream."""
+        n = src.numel() * src.element_size()
+        if not src.is_cuda and n < self.PULL_BYTES and src.is_pinned() and src.is_contiguous() and n % 16 == 0:
+            from . import _lib as L
+
+            L.check(L.lib().yk_upload_pinned_async(L.ptr(dst), L.ptr(src), n, L.current_stream(self.device)),
+                    "yk_upload_pinned_async")
+        else:
+            dst.copy_(src, non_blocking=True)
 
     def download_async(self, rows, counts, stats, rows_per_stream=None):
         """Enqueue the tracker output of the most recent step into page-locked host buffers
