@@ -116,7 +116,10 @@ def main():
 
         def hook(p, k, det_stream, trk_stream):
             t = step[0]
-            d2d_async(rec[t].data_ptr(), p.gmd.motion_ptr, nbytes, trk_stream)
+            # (motion windows: each step's record is its own buffer; the debug buffers below then
+            # hold the state after the wave's last motion call, so only the records are per step)
+            src = p._motion_out[k].data_ptr() if getattr(p, "_windowed", False) else p.gmd.motion_ptr
+            d2d_async(rec[t].data_ptr(), src, nbytes, trk_stream)
             d2d_async(cor[t].data_ptr(), ptrs[0].value, S * M * 8, trk_stream)
             d2d_async(nxt[t].data_ptr(), ptrs[1].value, S * M * 8, trk_stream)
             for j in range(2):

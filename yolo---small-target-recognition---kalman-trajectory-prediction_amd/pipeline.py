@@ -135,6 +135,7 @@ class StreamPipeline:
         self._ev_window = None  # end of the last motion window (the next wave's forwards wait for it)
         self._wave = []  # detection buffers of the current wave's steps (forwards enqueued, window not yet)
         self._dl = {}  # download_async requests of the current wave's steps, issued in its window
+        self._motion_out = None  # per detection buffer: its step's yk_motion[S] (motion windows)
 
     @property
     def dets(self) -> torch.Tensor:
@@ -227,15 +228,29 @@ class StreamPipeline:
 
     def _run_window(self):
         """Motion window of the current wave (see the header): after every forward enqueued so far,
-        each step's motion detector and tracker step in frame order on the tracker stream (plus the
-        step hook and any download_async request of that step); the next forwards wait for its end."""
+        each step's motion detector in frame order on the tracker stream, each into its own motion
+        record; the next forwards wait for the window's end.  Then the wave's tracker steps (plus
+        the step hook and any download_async request of each step), which may overlap them."""
         trk = self.trk_stream
         for j in range(self.D):
             trk.wait_stream(self._stream(j))
+        if self._motion_out is None:
+            from . import _lib as L
+
+            self._motion_out = torch.zeros((self.nb, self.S * L.MOTION_DTYPE.itemsize), dtype=torch.uint8,
+                                           device=self.frames.device)
+        with torch.cuda.stream(trk):
+            for k in self._wave:  # the exclusive part: the wave's motion detector calls, in order
+                s = self._slot(k)
+                self.gmd.detect_device(self.frame_slots[s], out=self._motion_out[k].data_ptr())
+                self._ev_gmd[s].record(trk)
+                self._gmd_pending[s] = True
+        self._ev_window = torch.cuda.Event()
+        self._ev_window.record(trk)  # the next wave's forwards may start: the tracker steps overlap them
         with torch.cuda.stream(trk):
             for k in self._wave:
                 s = self._slot(k)
-                self._track(k, s)
+                self.tracker.step_device(self._dets[k], self._counts[k], motion=self._motion_out[k].data_ptr())
                 self._ev_trk[k].record(trk)
                 self._trk_pending[k] = True
                 if self.step_hook is not None:
@@ -243,8 +258,6 @@ class StreamPipeline:
                 req = self._dl.pop(k, None)
                 if req is not None:
                     self.tracker.download_async(*req, stream=trk.cuda_stream)
-        self._ev_window = torch.cuda.Event()
-        self._ev_window.record(trk)
         self._wave = []
 
     def flush(self):
