@@ -41,6 +41,7 @@
 //    32  F32S split with scalar remainders               64  fp32 SiLU on v_exp_f32 / v_rcp_f32
 //   128  two waves per SIMD for the table / halo kernels (amdgpu_waves_per_eu(2))
 //   512  F32S: operands used as if stored pre-split (no split VALU, overlapping register quads)
+//  1024  conv_fast: one K step of loads in flight for the large tiles instead of two (registers)
 #ifndef YK_DIAG
 #define YK_DIAG 0
 #endif
@@ -1000,7 +1001,7 @@ __device__ __forceinline__ int fdiv(int n, int d, float inv) {
 
 // K steps of loads each conv_fast wave keeps in flight (2 for the large register tiles: register
 // budget).  8 steps for the 1- and 2-fragment tiles measured no faster than 4 (round 2).
-constexpr int fast_skd(int nnt, int npt) { return nnt * npt >= 8 ? 2 : 4; }
+constexpr int fast_skd(int nnt, int npt) { return nnt * npt >= 8 ? ((YK_DIAG & 1024) ? 1 : 2) : 4; }
 // conv_fastw's activation slots are indexed by the step within a 4-step weight chunk: SKD | 4
 constexpr int fastw_skd(int nnt, int npt) { return nnt * npt >= 8 ? 2 : 4; }
 
