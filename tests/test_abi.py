@@ -98,3 +98,21 @@ def test_c_host_abi_check_passes_against_this_library(tmp_path):
         assert r.returncode == 0, r.stderr
         out[tag] = int(r.stdout.strip())
     assert out == {"same": 0, "other": 4}, out
+
+
+def test_round5_entry_points_refuse_bad_arguments_without_a_device():
+    """yk_upload_pinned_async / yk_tracker_download_async check their arguments before any device
+    call: NULL pointers and sizes that are not multiples of 16 come back as YK_ERR_ARG with a
+    message (callable on this CPU-only host)."""
+    P = pkg()
+    L = P._lib
+    lib = L.lib()
+    buf = ctypes.create_string_buffer(64)
+    for args in ((None, None, 16, None), (ctypes.addressof(buf), None, 16, None),
+                 (ctypes.addressof(buf), ctypes.addressof(buf), 15, None)):
+        rc = lib.yk_upload_pinned_async(*args)
+        assert rc != 0
+        assert b"yk_upload_pinned_async" in ctypes.cast(lib.yk_last_error(), ctypes.c_char_p).value
+    rc = lib.yk_tracker_download_async(None, None, None, None, 0, None)
+    assert rc != 0
+    assert b"yk_tracker_download_async" in ctypes.cast(lib.yk_last_error(), ctypes.c_char_p).value
