@@ -260,6 +260,53 @@ def test_pipelined_tracker_stream_matches_serial():
             assert r0[s][: c0[s]].tobytes() == r1[s][: c1[s]].tobytes()
 
 
+def test_prefetched_host_frames_match_device_frames():
+    """Page-locked host frames through run(frames) (DMA on the slot stream), run(frames,
+    next_frames=...) and prefetch() 1 and 3 steps ahead (the copy stream's staging ring) give
+    exactly the tracker state of the same frames handed over in HBM; device frames prefetch too;
+    frames other than the prefetched ones, or a prefetch beyond the staging ring, are refused."""
+    P = pkg()
+    pipeline = importlib.import_module(P.__name__ + ".pipeline")
+    S, F = 8, 20
+    scenes = [P.synth.Scene(seed=60 + s, n_targets=16, n_frames=F) for s in range(S)]
+    frames = torch.stack([sc.frames_torch(0, F, "cuda") for sc in scenes], 1).contiguous()
+    host = frames.cpu().pin_memory()
+    assert host[0].numel() >= pipeline.StreamPipeline.PULL_BYTES  # the DMA / staging path, not the pull kernel
+    runs = []
+    for mode in ("device", "direct", "next", "ahead1", "ahead3", "device_ahead2"):
+        pipe = pipeline.StreamPipeline("yolov8s-small.yaml", S, (512, 640), "bf16", seed=0, max_tracks=256,
+                                       pipelined=True, inflight=4)
+        pipe.frames.copy_(frames[0])
+        pipe.capture(tune=False)
+        src = frames if mode.startswith("device") else host
+        depth = {"ahead1": 1, "ahead3": 3, "device_ahead2": 2}.get(mode, 0)
+        for t in range(F):
+            if mode == "next":
+                pipe.run(src[t], next_frames=src[t + 1] if t + 1 < F else None)
+            else:
+                pipe.run(src[t])
+            for u in range(t + 1 + len(pipe._prefetched), min(t + 1 + depth, F)):
+                pipe.prefetch(src[u])
+        pipe.sync()
+        rows, counts, stats = pipe.tracker.download()
+        runs.append((rows.copy(), counts.copy(), stats.copy()))
+        if mode == "ahead3":
+            pipe.prefetch(host[0])
+            with pytest.raises(ValueError):
+                pipe.run(host[1])  # host[0] was prefetched for this step
+            with pytest.raises(ValueError):
+                for _ in range(pipe.n_stage):
+                    pipe.prefetch(host[0])
+            pipe.sync()
+    r0, c0, s0 = runs[0]
+    assert c0.sum() > 0
+    for r1, c1, s1 in runs[1:]:
+        np.testing.assert_array_equal(c0, c1)
+        np.testing.assert_array_equal(s0, s1)
+        for s in range(S):
+            assert r0[s][: c0[s]].tobytes() == r1[s][: c1[s]].tobytes()
+
+
 def test_pipeline_with_global_motion_matches_serial():
     """StreamPipeline(tracker_policy=1, motion_method='optical_flow') -- the
     MotionCompensatedMultiTracker.update(dets, frame) loop with GlobalMotionDetector on the

@@ -5096,9 +5096,19 @@ namespace yk {
 namespace det {
 // page-locked host -> device copy read by the device (yk_upload_pinned_async): 16 B per lane,
 // grid-stride, plain loads of the host pages through their device-mapped address
+// four 16-B loads in flight per lane before their stores: a read across PCIe takes microseconds,
+// so a few workgroups with deep queues pull as fast as thousands with one load each
 __global__ void __launch_bounds__(256) pull_copy_kernel(uint4* __restrict__ dst, const uint4* __restrict__ src, size_t n16) {
   const size_t stride = (size_t)gridDim.x * 256;
-  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += stride) dst[i] = src[i];
+  size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  for (; i + 3 * stride < n16; i += 4 * stride) {
+    const uint4 a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
+    dst[i] = a;
+    dst[i + stride] = b;
+    dst[i + 2 * stride] = c;
+    dst[i + 3 * stride] = d;
+  }
+  for (; i < n16; i += stride) dst[i] = src[i];
 }
 }  // namespace det
 }  // namespace yk

@@ -72,9 +72,11 @@ class StreamPipeline:
         self.frames = torch.zeros((self.S, frame_hw[0], frame_hw[1], 3), dtype=torch.uint8, device=dev)
         # motion windows (see the header): with the motion detector on a pipelined tracker stream
         self._windowed = motion_method is not None and bool(pipelined)
-        # detection buffers: D (one per detector slot) or, with motion windows, 2 D so the next
-        # wave's forwards do not wait for this wave's tracker steps
-        self.nb = max(2, int(inflight)) * (2 if self._windowed else 1)
+        # detection buffers: 2 D when the tracker runs on its own stream, so the forward of step
+        # t + D does not wait for the tracker step of step t (HBM-resident rate +6.6 % fp32, +11.5 %
+        # bf16, profiles/r05_inflight_lanes_sweep.txt), and with motion windows the next wave's
+        # forwards do not wait for this wave's tracker steps; D (at least 2) otherwise
+        self.nb = max(2, int(inflight)) * (2 if pipelined else 1)
         self._dets = torch.zeros((self.nb, self.S, self.max_det, 6), dtype=torch.float32, device=dev)
         self._counts = torch.zeros((self.nb, self.S), dtype=torch.int32, device=dev)
         self._k = 0  # detection buffer the next step writes
@@ -131,7 +133,7 @@ class StreamPipeline:
         self._stage_read_pending = [False] * self.n_stage
         self._ev_copy = [torch.cuda.Event() for _ in range(self.n_stage)]
         self._n_stage = 0
-        self._prefetched = None  # (data_ptr of the host frames, staging index) of the next step
+        self._prefetched = __import__("collections").deque()  # (data_ptr of the host frames, staging index), one per upcoming step
         self._ev_window = None  # end of the last motion window (the next wave's forwards wait for it)
         self._wave = []  # detection buffers of the current wave's steps (forwards enqueued, window not yet)
         self._dl = {}  # download_async requests of the current wave's steps, issued in its window
@@ -289,11 +291,11 @@ class StreamPipeline:
         s = self._slot(self._k)
         st = self._stream(s)
         cur = torch.cuda.current_stream(self.device)
-        if self._prefetched is not None:
-            ptr, i = self._prefetched
-            if frames.is_cuda or frames.data_ptr() != ptr:
-                raise ValueError("run(): the previous call prefetched other frames for this step (next_frames)")
-            self._prefetched = None
+        if self._prefetched:
+            ptr, i = self._prefetched[0]
+            if frames.data_ptr() != ptr:
+                raise ValueError("run(): other frames were prefetched for this step (next_frames / prefetch)")
+            self._prefetched.popleft()
             st.wait_event(self._ev_copy[i])
             if self._gmd_pending[s]:  # the motion detector (tracker stream) still reads this slot's frames
                 st.wait_event(self._ev_gmd[s])
@@ -317,18 +319,29 @@ class StreamPipeline:
             # (frames below PULL_BYTES are pulled on the slot stream by the next run() instead: the
             # pull kernel costs the host nothing, and a copy-stream hop measured 26 % slower at
             # batch 1, bench.py --config 2 --no-prefetch)
-            if next_frames.is_cuda or self.copy_stream is None:
-                raise ValueError("next_frames: page-locked host frames and inflight > 1")
-            i = self._n_stage % self.n_stage
-            self._n_stage += 1
-            cs = self.copy_stream
-            if self._stage_read_pending[i] and not self._ev_stage_read[i].query():
-                cs.wait_event(self._ev_stage_read[i])  # (rare: its staging -> slot copy has not run yet)
-            self._stage_read_pending[i] = False
-            with torch.cuda.stream(cs):
-                self._upload(self._stage[i], next_frames)
-            self._ev_copy[i].record(cs)
-            self._prefetched = (next_frames.data_ptr(), i)
+            self.prefetch(next_frames)
+
+    def prefetch(self, frames: torch.Tensor):
+        """Issue the upload of a FUTURE step's page-locked host frames now, on the copy stream, into
+        a staging buffer.  Prefetches queue in step order: the run() calls that follow must be
+        handed the same tensors, in the same order.  At most n_stage - D may be outstanding."""
+        if self.copy_stream is None or not (frames.is_cuda or frames.is_pinned()):
+            raise ValueError("prefetch: page-locked host (or device) frames and inflight > 1")
+        if len(self._prefetched) >= self.n_stage - self.D:
+            raise ValueError(f"prefetch: at most {self.n_stage - self.D} steps ahead")
+        i = self._n_stage % self.n_stage
+        self._n_stage += 1
+        cs = self.copy_stream
+        if self._stage_read_pending[i] and not self._ev_stage_read[i].query():
+            cs.wait_event(self._ev_stage_read[i])  # (rare: its staging -> slot copy has not run yet)
+        self._stage_read_pending[i] = False
+        if frames.is_cuda:  # behind their producer; the allocator keeps them alive until the copy ran
+            cs.wait_stream(torch.cuda.current_stream(self.device))
+            frames.record_stream(cs)
+        with torch.cuda.stream(cs):
+            self._upload(self._stage[i], frames)
+        self._ev_copy[i].record(cs)
+        self._prefetched.append((frames.data_ptr(), i))
 
     # page-locked host frames below this size are pulled by a kernel (yk_upload_pinned_async):
     # the runtime copies small page-locked H2D transfers through the CPU, synchronously (one
