@@ -411,7 +411,7 @@ def run_leg(a, P, cfg, dtype, frames, dev, local, rank, ws, headline):
         h0 = time.perf_counter_ns()
         if h2d:  # the next steps' frames are uploaded while this step runs (decode-ahead driver)
             pipe.run(host[t % n_host])
-            for u in range(t + 1 + len(pipe._prefetched), min(t + 1 + ahead, a.steps)):
+            for u in range(t + 1 + pipe.n_prefetched, min(t + 1 + ahead, a.steps)):
                 pipe.prefetch(host[u % n_host])
         else:
             pipe.run(frames[(t_first + t) % F])

@@ -285,7 +285,7 @@ def test_prefetched_host_frames_match_device_frames():
                 pipe.run(src[t], next_frames=src[t + 1] if t + 1 < F else None)
             else:
                 pipe.run(src[t])
-            for u in range(t + 1 + len(pipe._prefetched), min(t + 1 + depth, F)):
+            for u in range(t + 1 + pipe.n_prefetched, min(t + 1 + depth, F)):
                 pipe.prefetch(src[u])
         pipe.sync()
         rows, counts, stats = pipe.tracker.download()

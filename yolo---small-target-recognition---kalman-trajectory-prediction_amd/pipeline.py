@@ -321,6 +321,11 @@ class StreamPipeline:
             # batch 1, bench.py --config 2 --no-prefetch)
             self.prefetch(next_frames)
 
+    @property
+    def n_prefetched(self) -> int:
+        """Uploads issued by prefetch() that no run() has consumed yet."""
+        return len(self._prefetched)
+
     def prefetch(self, frames: torch.Tensor):
         """Issue the upload of a FUTURE step's page-locked host frames now, on the copy stream, into
         a staging buffer.  Prefetches queue in step order: the run() calls that follow must be
