@@ -295,7 +295,7 @@ def test_prefetched_host_frames_match_device_frames():
             with pytest.raises(ValueError):
                 pipe.run(host[1])  # host[0] was prefetched for this step
             with pytest.raises(ValueError):
-                for _ in range(pipe.n_stage):
+                for _ in range(pipe.nb + 8):
                     pipe.prefetch(host[0])
             pipe.sync()
     r0, c0, s0 = runs[0]
