@@ -307,6 +307,35 @@ def test_prefetched_host_frames_match_device_frames():
             assert r0[s][: c0[s]].tobytes() == r1[s][: c1[s]].tobytes()
 
 
+def test_pulled_batch1_host_frames_match_device_frames():
+    """Batch-1 page-locked frames (below PULL_BYTES: pulled onto the slot stream by
+    yk_upload_pinned_async, four forwards in flight) give exactly the tracker state of the same
+    frames handed over in HBM."""
+    P = pkg()
+    pipeline = importlib.import_module(P.__name__ + ".pipeline")
+    F = 24
+    sc = P.synth.Scene(seed=71, n_targets=24, n_frames=F)
+    frames = sc.frames_torch(0, F, "cuda")[:, None].contiguous()  # [F, 1, H, W, 3]
+    host = frames.cpu().pin_memory()
+    assert host[0].numel() < pipeline.StreamPipeline.PULL_BYTES
+    runs = []
+    for src in (frames, host):
+        pipe = pipeline.StreamPipeline("yolov8s-small.yaml", 1, (512, 640), "fp32", seed=0, max_tracks=256,
+                                       pipelined=True, inflight=4)
+        pipe.frames.copy_(frames[0])
+        pipe.capture(tune=False)
+        for t in range(F):
+            pipe.run(src[t])
+        pipe.sync()
+        rows, counts, stats = pipe.tracker.download()
+        runs.append((rows.copy(), counts.copy(), stats.copy()))
+    (r0, c0, s0), (r1, c1, s1) = runs
+    assert c0.sum() > 0
+    np.testing.assert_array_equal(c0, c1)
+    np.testing.assert_array_equal(s0, s1)
+    assert r0[0][: c0[0]].tobytes() == r1[0][: c1[0]].tobytes()
+
+
 def test_pipeline_with_global_motion_matches_serial():
     """StreamPipeline(tracker_policy=1, motion_method='optical_flow') -- the
     MotionCompensatedMultiTracker.update(dets, frame) loop with GlobalMotionDetector on the
