@@ -49,7 +49,9 @@
 #define YK_HALO_DIAG ((YK_DIAG >> 2) & 3)
 #define YK_SPLIT_PK ((YK_DIAG & 32) == 0)
 #define YK_EXACT_SILU ((YK_DIAG & 64) == 0)
+#ifndef YK_FAST_WPE  // (a diagnostic build may set it: YK_DEFINES=-DYK_FAST_WPE=3)
 #define YK_FAST_WPE ((YK_DIAG & 128) ? 2 : 1)
+#endif
 
 namespace yk {
 namespace det {
