@@ -254,3 +254,43 @@ def test_tracker_event_messages_match_oracle(capsys, max_lost, min_hits, thr, fr
         assert kinds["delete"] > 0
     if frames_n >= 100:
         assert kinds["stats"] >= 1
+
+
+@pytest.mark.parametrize("max_tracks, offset", [(256, 0), (151, 0), (256, 8)])
+def test_download_async_pushes_the_rows_download_returns(max_tracks, offset):
+    """yk_tracker_download_async (the per-step output push of the host-frame loop): counts, stats and
+    every live row equal yk_tracker_download's, with 16-byte row stores (even max_tracks, aligned
+    buffer), the 8-byte path (odd max_tracks: every other stream's rows start 8 bytes off; a host
+    buffer 8 bytes off), and rows_per_stream cutting streams short."""
+    import torch
+
+    P = pkg()
+    L = P._lib
+    S = 4
+    trk = P.tracker.MultiStreamTracker(S, max_lost_frames=30, min_hits=1, iou_threshold=0.1, max_tracks=max_tracks,
+                                       max_dets=256)
+    rng = np.random.default_rng(max_tracks + offset)
+    for f in range(2):
+        dets = []
+        for s in range(S):
+            n = int(rng.integers(10, 30)) + 15 * s
+            xy = rng.uniform(0, 600, (n, 2))
+            dets.append(np.concatenate([xy, xy + rng.uniform(5, 20, (n, 2)), rng.uniform(0.2, 1, (n, 1))], 1))
+        trk.step_host(dets)
+    rows_ref, counts_ref, stats_ref = (x.copy() for x in trk.download())
+    assert (counts_ref > 0).all() and int(stats_ref["overflow"].sum()) == 0
+    nb = S * max_tracks * L.TRACK_OUT_DTYPE.itemsize
+    for rows_per_stream in (None, 17):
+        raw = torch.zeros(nb + 16, dtype=torch.uint8, pin_memory=True)
+        rows = raw[offset:offset + nb]
+        counts = torch.zeros(S, dtype=torch.int32, pin_memory=True)
+        stats = torch.zeros(S * L.STATS_DTYPE.itemsize, dtype=torch.uint8, pin_memory=True)
+        trk.download_async(rows, counts, stats, rows_per_stream)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(counts.numpy(), counts_ref)
+        assert stats.numpy().tobytes() == stats_ref.tobytes()
+        got = rows.numpy().view(L.TRACK_OUT_DTYPE).reshape(S, max_tracks)
+        for s in range(S):
+            n = int(counts_ref[s]) if rows_per_stream is None else min(int(counts_ref[s]), rows_per_stream)
+            assert got[s, :n].tobytes() == rows_ref[s, :n].tobytes()
+            assert not got[s, n:].tobytes().strip(b"\0")  # nothing past the live rows

@@ -2277,17 +2277,26 @@ __global__ void __launch_bounds__(256) push_out_kernel(Dev g, int S, int T, int 
   const int s = blockIdx.x;
   if (s >= S) return;
   const int c = g.counts[s];
-  if (threadIdx.x == 0) {
+  if (blockIdx.y == 0 && threadIdx.x == 0) {
     counts[s] = c;
     if (stats) stats[s] = g.stats[s];
   }
   if (!rows) return;
   const int n = c < rows_per_stream ? c : rows_per_stream;
+  // the live rows as one byte range spread over gridDim.y workgroups per stream: 16-byte stores when
+  // both bases are 16-byte aligned (the 8-byte tail of an odd row count last), 8-byte ones otherwise
   static_assert(sizeof(yk_track_out) % 8 == 0, "8-byte row copies");
-  constexpr int W = (int)(sizeof(yk_track_out) / 8);
-  const uint2* src = (const uint2*)(g.rows + (size_t)s * T);
-  uint2* dst = (uint2*)(rows + (size_t)s * T);
-  for (int i = threadIdx.x; i < n * W; i += blockDim.x) dst[i] = src[i];
+  const size_t bytes = (size_t)n * sizeof(yk_track_out);
+  const yk_track_out* src = g.rows + (size_t)s * T;
+  yk_track_out* dst = rows + (size_t)s * T;
+  const size_t i0 = (size_t)blockIdx.y * blockDim.x + threadIdx.x, step = (size_t)gridDim.y * blockDim.x;
+  if ((((size_t)src | (size_t)dst) & 15) == 0) {
+    const size_t n16 = bytes / 16;
+    for (size_t i = i0; i < n16; i += step) ((uint4*)dst)[i] = ((const uint4*)src)[i];
+    if (bytes % 16 && i0 == 0) ((uint2*)dst)[2 * n16] = ((const uint2*)src)[2 * n16];
+  } else {
+    for (size_t i = i0; i < bytes / 8; i += step) ((uint2*)dst)[i] = ((const uint2*)src)[i];
+  }
 }
 
 }  // namespace trk
@@ -2542,7 +2551,7 @@ int yk_tracker_download_async(yk_tracker* t, yk_track_out* host_rows, int32_t* h
     }
     dp[i] = at.devicePointer;
   }
-  hipLaunchKernelGGL(yk::trk::push_out_kernel, dim3(t->S), dim3(256), 0, st, t->dev, t->S, t->dev.T,
+  hipLaunchKernelGGL(yk::trk::push_out_kernel, dim3(t->S, 8), dim3(256), 0, st, t->dev, t->S, t->dev.T,
                      rows_per_stream, (yk_track_out*)dp[0], (int32_t*)dp[1], (yk_tracker_stats*)dp[2]);
   YK_HIP(hipGetLastError());
   return YK_OK;
