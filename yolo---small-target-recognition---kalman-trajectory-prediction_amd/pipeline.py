@@ -99,7 +99,17 @@ class StreamPipeline:
             raise ValueError("inflight > 1 needs pipelined=True (the tracker runs on its own stream)")
         # slot s: detector model, input frames and launch stream (None = the caller's stream)
         self.models = [self.model] + [M.DeviceModel(self.prog, self.device) for _ in range(self.D - 1)]
-        self.frame_slots = [self.frames] + [torch.zeros_like(self.frames) for _ in range(self.D - 1)]
+        # frame buffers: one per detector slot; or, with forwards in flight and no motion detector, a
+        # ring of 2 nb = 4 D that the step index walks (one graph per frame buffer), so a host-frame
+        # upload lands in the buffer its forward reads -- no staging hop -- and rewrites a buffer 4 D
+        # steps after its forward, which has long finished (bf16 +4-6 %, fp32 unchanged,
+        # profiles/r05_inflight_lanes_sweep.txt; a 2 D ring made the copies wait, -15 %)
+        self._ring = self.D > 1 and motion_method is None
+        nf = 2 * self.nb if self._ring else self.D
+        self.frame_slots = [self.frames] + [torch.zeros_like(self.frames) for _ in range(nf - 1)]
+        self._ev_fread = [torch.cuda.Event() for _ in range(nf)] if self._ring else []  # its forward
+        self._fread_pending = [False] * nf
+        self._kf = 0  # (ring) frame buffer of the next step
         # one created stream per slot with forwards in flight (the caller's stream with one: the
         # serial order); slot 0 on the legacy null stream cost ~4 % of the host-frame rate
         self.det_streams = [None] if self.D == 1 else [torch.cuda.Stream(dev) for _ in range(self.D)]
@@ -127,11 +137,11 @@ class StreamPipeline:
         # buffer an upload reuses was read D + 4 steps earlier, which the host never outruns while
         # D forwards are in flight, so the copy stream waits for nothing in steady state.
         self.copy_stream = torch.cuda.Stream(dev) if self.D > 1 else None
-        self.n_stage = self.D + 4 if self.D > 1 else 0
+        self.n_stage = self.D + 4 if self.D > 1 and not self._ring else 0
         self._stage = [torch.empty_like(self.frames) for _ in range(self.n_stage)]
         self._ev_stage_read = [torch.cuda.Event() for _ in range(self.n_stage)]  # slot stream's copy out of it
         self._stage_read_pending = [False] * self.n_stage
-        self._ev_copy = [torch.cuda.Event() for _ in range(self.n_stage)]
+        self._ev_copy = [torch.cuda.Event() for _ in range(nf if self._ring else self.n_stage)]
         self._n_stage = 0
         self._prefetched = __import__("collections").deque()  # (data_ptr of the host frames, staging index), one per upcoming step
         self._ev_window = None  # end of the last motion window (the next wave's forwards wait for it)
@@ -175,10 +185,15 @@ class StreamPipeline:
         for fs in self.frame_slots[1:]:
             fs.copy_(self.frames)
         self.graph = True
-        for k in range(self.nb):  # one graph per detection buffer
+        # one graph per (frame buffer, detection buffer) pair the steps use, in step order from the
+        # current step: the ring's frame index and the detection buffer index advance together
+        n = len(self.frame_slots) if self._ring else self.nb
+        for j in range(n):
+            k = (self._k + j) % self.nb
             s = self._slot(k)
+            f = (self._kf + j) % len(self.frame_slots) if self._ring else s
             with torch.cuda.stream(self._stream(s)):
-                self.models[s].detect(self.frame_slots[s], self.conf, self.iou, self.max_det, self._dets[k],
+                self.models[s].detect(self.frame_slots[f], self.conf, self.iou, self.max_det, self._dets[k],
                                       self._counts[k], graph=True)
         torch.cuda.synchronize(self.device)
         return self.graph
@@ -192,9 +207,14 @@ class StreamPipeline:
             self._trk_pending[k] = False
         if self._ev_window is not None:  # no forward beside a motion window
             cur.wait_event(self._ev_window)
+        f = self._kf if self._ring else s
         with torch.cuda.stream(cur):
-            self.models[s].detect(self.frame_slots[s], self.conf, self.iou, self.max_det, self._dets[k],
+            self.models[s].detect(self.frame_slots[f], self.conf, self.iou, self.max_det, self._dets[k],
                                   self._counts[k], graph=bool(self.graph))
+        if self._ring:
+            self._ev_fread[f].record(cur)
+            self._fread_pending[f] = True
+            self._kf = (f + 1) % len(self.frame_slots)
         if self._windowed:
             self._ev_det[k].record(cur)
             self._wave.append(k)
@@ -282,16 +302,35 @@ class StreamPipeline:
         has run (the caller's buffer; see download_async for the matching output side).
 
         next_frames (page-locked host, inflight > 1): the NEXT step's frames, already decoded (a
-        video driver reads ahead).  Their upload is issued now, on the copy stream, into a staging
-        buffer; the next run() is handed the same tensor and its slot stream copies staging -> slot
-        (device to device) behind that upload's event.  Every frame still crosses PCIe once,
+        video driver reads ahead).  Their upload is issued now, on the copy stream, into that step's
+        frame buffer of the ring (with a motion detector: into a staging buffer that the slot
+        stream copies to the slot); the next run() is handed the same tensor and its forward waits
+        for that upload's event.  Every frame still crosses PCIe once,
         inside the caller's loop; the upload of step t + 1 overlaps step t.  Frames smaller than
         PULL_BYTES are not prefetched: the next run() pulls them onto the slot stream with a kernel
         (yk_upload_pinned_async), which holds neither the host nor a copy stream."""
         s = self._slot(self._k)
         st = self._stream(s)
         cur = torch.cuda.current_stream(self.device)
-        if self._prefetched:
+        if self._ring:
+            f = self._kf
+            if self._prefetched:  # uploaded straight into this step's frame buffer
+                ptr, i = self._prefetched[0]
+                if frames.data_ptr() != ptr:
+                    raise ValueError("run(): other frames were prefetched for this step (next_frames / prefetch)")
+                self._prefetched.popleft()
+                st.wait_event(self._ev_copy[i])
+            else:
+                if st != cur:
+                    st.wait_stream(cur)
+                    if frames.is_cuda:
+                        frames.record_stream(st)  # the allocator keeps `frames` alive until the copy ran
+                if self._fread_pending[f]:  # its last forward ran on another slot stream
+                    st.wait_event(self._ev_fread[f])
+                    self._fread_pending[f] = False
+                with torch.cuda.stream(st):
+                    self._upload(self.frame_slots[f], frames)
+        elif self._prefetched:
             ptr, i = self._prefetched[0]
             if frames.data_ptr() != ptr:
                 raise ValueError("run(): other frames were prefetched for this step (next_frames / prefetch)")
@@ -328,15 +367,33 @@ class StreamPipeline:
 
     def prefetch(self, frames: torch.Tensor):
         """Issue the upload of a FUTURE step's page-locked host frames now, on the copy stream, into
-        a staging buffer.  Prefetches queue in step order: the run() calls that follow must be
-        handed the same tensors, in the same order.  At most n_stage - D may be outstanding."""
+        that step's frame buffer (a staging buffer with a motion detector).  Prefetches queue in step order: the run() calls that follow must be
+        handed the same tensors, in the same order.  At most 4 may be outstanding."""
         if self.copy_stream is None or not (frames.is_cuda or frames.is_pinned()):
             raise ValueError("prefetch: page-locked host (or device) frames and inflight > 1")
+        cs = self.copy_stream
+        if self._ring:
+            nf = len(self.frame_slots)
+            if len(self._prefetched) >= 4:
+                raise ValueError("prefetch: at most 4 steps ahead")
+            f = (self._kf + len(self._prefetched)) % nf  # that step's frame buffer
+            # its previous reader: the forward of 4 D steps earlier (done in steady state; waiting for
+            # it here would hold the host inside the copy call)
+            if self._fread_pending[f] and not self._ev_fread[f].query():
+                cs.wait_event(self._ev_fread[f])
+            self._fread_pending[f] = False
+            if frames.is_cuda:  # behind their producer; the allocator keeps them alive until the copy ran
+                cs.wait_stream(torch.cuda.current_stream(self.device))
+                frames.record_stream(cs)
+            with torch.cuda.stream(cs):
+                self._upload(self.frame_slots[f], frames)
+            self._ev_copy[f].record(cs)
+            self._prefetched.append((frames.data_ptr(), f))
+            return
         if len(self._prefetched) >= self.n_stage - self.D:
             raise ValueError(f"prefetch: at most {self.n_stage - self.D} steps ahead")
         i = self._n_stage % self.n_stage
         self._n_stage += 1
-        cs = self.copy_stream
         if self._stage_read_pending[i] and not self._ev_stage_read[i].query():
             cs.wait_event(self._ev_stage_read[i])  # (rare: its staging -> slot copy has not run yet)
         self._stage_read_pending[i] = False
