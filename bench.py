@@ -65,7 +65,10 @@ TRACK_STEP_BYTES = 1216  # R+W of x (8 f64) and dense P (64 f64), z
 # targets and crossing targets churn IDs, so live tracks != targets (40 targets -> ~70-150 live).
 CONFIGS = {
     2: dict(S=1, H=512, W=640, imgsz=640, max_tracks=512, targets=12, dtype="bf16", secondary="", live_floor=16),
-    3: dict(S=8, H=512, W=640, imgsz=640, max_tracks=512, targets=40, dtype="fp32", secondary="bf16,n:fp32", live_floor=64),
+    # tbatch (frames per stream per forward, --tbatch): 2 is +4 % at 100 steps but -1.3 % at the
+    # driver's 20 (the batch-16 forward's longer fill / drain, gpurun_out/r6a, r6b), so 1 here
+    3: dict(S=8, H=512, W=640, imgsz=640, max_tracks=512, targets=40, dtype="fp32", secondary="bf16,n:fp32", live_floor=64,
+            tbatch=1),
     4: dict(S=1, H=512, W=640, imgsz=640, max_tracks=512, targets=40, dtype="fp32", secondary="", live_floor=64),
     5: dict(S=8, H=1024, W=1280, imgsz=1280, max_tracks=2048, targets=96, dtype="fp8", secondary="bf16",
             live_floor=256),
@@ -102,6 +105,10 @@ def parse():
                     help="with --tracker motion_reset: also run GlobalMotionDetector('optical_flow') on every frame "
                          "(MotionCompensatedMultiTracker.update(dets, frame)); no CPU baseline (the oracle's numpy "
                          "restatement of cv2's optical flow is not a stand-in for cv2's speed)")
+    ap.add_argument("--tbatch", type=int, default=None, choices=range(1, 9),
+                    help="frames per stream in one forward (temporal batching: one batch-(tbatch x streams) forward "
+                         "covers tbatch consecutive steps; the tracker still steps once per frame); default: the "
+                         "config's")
     ap.add_argument("--inflight", type=int, default=None, choices=range(1, 9),
                     help="detector forwards in flight (each a batch of all streams, own graph + HIP stream); "
                          "default 4")
@@ -205,6 +212,47 @@ def roofline(pipe, frames, dtype, B):
     }, by, prof, [t0, t1]
 
 
+def decode_nms_rooflines(pipe, prof, dtype, B):
+    """HBM rooflines of the decode and NMS kernels (north_star: "Kalman/NMS HBM-GB/s fractions of
+    peak"), from the same per-op hipEvent pass as the conv roofline.  Algorithmic bytes per SURVEY
+    §8(d): decode reads the Detect head's 65 fp32 logits per anchor (64 DFL box bins + 1 class),
+    65 * A * 4 B per image, summed over the four detect_kernel launches of a forward (one per
+    stride; detect_kernel fuses the head's last 1x1 convs, so its real input is the (64 + c3)
+    features per anchor: `traffic` from the PMC passes); NMS reads the candidate rows that passed
+    the confidence threshold (6 f32 each) and writes the kept rows (<= 300 x 6 x 4 B per image),
+    counted from this forward's own candidate and detection counts."""
+    det = [(name, ms) for (i, kind, name, ms) in prof if "detect_kernel" in name]
+    nms = [(name, ms) for (i, kind, name, ms) in prof if name.startswith("nms_kernel")]
+    A = int(pipe.prog.n_anchors)
+    _, cand_n = pipe.model.candidates(B)
+    kept = np.zeros(pipe.prog.max_batch, np.int32)
+    P = importlib.import_module(PKG)
+    P.model._memcpy_d2h(kept, pipe.model.counts_ptr)
+    out = {}
+    if det:
+        ms = sum(m for _, m in det)
+        by = 65 * A * 4 * B
+        gbps = by / (ms * 1e-3) / 1e9
+        out["detect_roofline"] = {
+            "kernel": det[0][0], "bound": "hbm", "achieved": round(gbps, 2), "peak": HBM_PEAK, "unit": "GB/s",
+            "frac": round(gbps / HBM_PEAK, 5), "algorithmic_bytes_per_forward": by, "launches_per_step": len(det),
+            "avg_launch_us": round(ms / len(det) * 1e3, 2), "us_per_forward": round(ms * 1e3, 2),
+            "traffic": pmc_traffic(det[0][0], dtype), "traffic_unit": "bytes/launch (PMC, mean over the 4 strides)",
+            "bytes_basis": "SURVEY §8(d): 65 logits x A anchors x 4 B per image, A = %d, batch %d" % (A, B)}
+    if nms:
+        ms = sum(m for _, m in nms)
+        n_in, n_out = int(cand_n[:B].sum()), int(kept[:B].sum())
+        by = (n_in + n_out) * 6 * 4
+        gbps = by / (ms * 1e-3) / 1e9
+        out["nms_roofline"] = {
+            "kernel": nms[0][0], "bound": "hbm", "achieved": round(gbps, 3), "peak": HBM_PEAK, "unit": "GB/s",
+            "frac": round(gbps / HBM_PEAK, 6), "algorithmic_bytes_per_launch": by, "launches_per_step": len(nms),
+            "avg_launch_us": round(ms / len(nms) * 1e3, 2), "candidates_in": n_in, "detections_out": n_out,
+            "traffic": pmc_traffic(nms[0][0], dtype), "traffic_unit": "bytes/launch",
+            "bytes_basis": "SURVEY §8(d): candidate rows read + kept rows written, 6 x f32 each, batch %d" % B}
+    return out
+
+
 def pmc_traffic(kernel, dtype):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
     (tools/pmc_summary.py: FETCH_SIZE + WRITE_SIZE, separate passes), or None."""
@@ -240,6 +288,15 @@ def tracker_roofline(pipe, reps=20):
     gbps = by / (us * 1e-6) / 1e9 if us > 0 else 0.0
     return {"kernel": "assoc_kernel + tracks_kernel", "bound": "hbm", "avg_launch_us": round(us, 2), "live_tracks": live,
             "achieved": round(gbps, 3), "peak": HBM_PEAK, "unit": "GB/s", "frac": round(gbps / HBM_PEAK, 6)}
+
+
+def tbatch_of(a, cfg) -> int:
+    """Frames per stream in one forward (temporal batching); 1 with the motion detector (its
+    motion windows order each frame's forward) or without forwards in flight."""
+    tb = a.tbatch if a.tbatch is not None else cfg.get("tbatch", 1)
+    if a.gmd or a.no_pipeline or a.inflight < 2:
+        tb = 1
+    return tb
 
 
 def plan_path(a, dtype, S, W, H, imgsz):
@@ -331,16 +388,17 @@ def run_leg(a, P, cfg, dtype, frames, dev, local, rank, ws, headline):
     pipeline = importlib.import_module(PKG + ".pipeline")
     S, H, W, imgsz = cfg["S"], cfg["H"], cfg["W"], cfg["imgsz"]
     F = frames.shape[0]
-    lanes = a.lanes if a.lanes is not None else (1 if a.inflight > 1 and not a.no_pipeline else 3)
+    lanes = a.lanes if a.lanes is not None else 1  # (the model's default schedule: one lane)
+    tb = tbatch_of(a, cfg)
     pipe = pipeline.StreamPipeline(f"yolov8{a.scale}-small.yaml", S, (H, W), dtype, seed=0, device=local,
                                    pipelined=not a.no_pipeline, imgsz=imgsz, max_tracks=cfg["max_tracks"],
                                    inflight=1 if a.no_pipeline else a.inflight,
                                    tracker_policy=1 if a.tracker == "motion_reset" else 0,
-                                   motion_method="optical_flow" if a.gmd else None)
+                                   motion_method="optical_flow" if a.gmd else None, frames_per_forward=tb)
     pipe.set_schedule(a.groups, lanes)
     pipe.frames.copy_(frames[0])
     plan_src, parity = "heuristic", None
-    pth = (a.plan_in if (headline and a.plan_in) else plan_path(a, dtype, (S + a.groups - 1) // a.groups, W, H, imgsz))
+    pth = (a.plan_in if (headline and a.plan_in) else plan_path(a, dtype, (tb * S + a.groups - 1) // a.groups, W, H, imgsz))
     tune = a.autotune
     if not tune and os.path.exists(pth):
         with open(pth) as f:
@@ -362,7 +420,7 @@ def run_leg(a, P, cfg, dtype, frames, dev, local, rank, ws, headline):
     if not a.no_graph:
         pipe.capture(tune=tune)
     elif tune:
-        pipe.model.autotune(pipe.frames, pipe.conf)
+        pipe.model.autotune(pipe.forward_frames, pipe.conf)
         pipe.sync_plan()
     for out_path in ([a.plan_out] if headline and a.plan_out else []) + ([pth] if a.save_plans else []):
         if rank == 0:
@@ -459,14 +517,16 @@ def run_leg(a, P, cfg, dtype, frames, dev, local, rank, ws, headline):
            "live_tracks_per_stream_min_at_start": int(live_start.min()),
            "overflow": int(run["overflow"]), "tracks_created": int(run["total_tracks_created"]),
            "conv_plan": plan_src, "conv_plan_parity": parity, "window_monotonic_ns": [w0, w1],
+           "frames_per_forward": tb,
            "rank_devices": devices}
     if overflow:
         log(f"tracker overflow on this rank: {overflow} detections/tracks dropped")
     if rank == 0 and not a.no_profile:
-        bg = (S + a.groups - 1) // a.groups
-        rl, by_kernel, prof, win = roofline(pipe, frames[0][:bg], dtype, bg)
+        bg = (tb * S + a.groups - 1) // a.groups  # images per forward (per batch group)
+        rl, by_kernel, prof, win = roofline(pipe, frames[0].repeat(tb, 1, 1, 1)[:bg].contiguous(), dtype, bg)
         rl["window_monotonic_ns"] = win
         leg["roofline"] = rl
+        leg.update(decode_nms_rooflines(pipe, prof, dtype, bg))
         leg["tracker_roofline"] = tracker_roofline(pipe)
         if headline and a.dump_ops:
             flops = pipe.prog.op_flops(bg)
@@ -525,8 +585,9 @@ def run_leg_subprocess(spec):
            "network_mfma_frac": d["network_mfma_frac"], "live_tracks_per_stream": c["live_tracks_per_stream"],
            "live_tracks_per_stream_min_at_start": c["live_tracks_per_stream_min_at_start"],
            "overflow": c["tracker_overflow"], "tracks_created": c["tracks_created"], "conv_plan": c["conv_plan"],
-           "process": "own", "gflop_per_frame": c["gflop_per_frame"], "hbm_resident_fps": d.get("hbm_resident_fps")}
-    for k in ("roofline", "tracker_roofline"):
+           "process": "own", "gflop_per_frame": c["gflop_per_frame"], "hbm_resident_fps": d.get("hbm_resident_fps"),
+           "frames_per_forward": c.get("frames_per_forward", 1)}
+    for k in ("roofline", "detect_roofline", "nms_roofline", "tracker_roofline"):
         if d.get(k) is not None:
             leg[k] = d[k]
     return leg
@@ -595,8 +656,11 @@ def main():
             "scaling": "weak", "vs_baseline": None, "dtype": dtype,
             "data": f"synthetic: seeded {W}x{H} IR-like scenes ({cfg['targets']} targets/stream, occlusion bursts) "
                     "rendered into HBM before timing; seeded planted weights (no trained best.pt in the reference)",
-            "config": {"workload": f"YOLOv8{a.scale}+P2 {W}x{H} (imgsz {cfg['imgsz']}), {S} stream(s)/GPU as batch {S}, "
-                                   f"{a.tracker} tracker(150, 1, 0.1), BASELINE config {a.config}",
+            "config": {"workload": f"YOLOv8{a.scale}+P2 {W}x{H} (imgsz {cfg['imgsz']}), {S} stream(s)/GPU as batch {S}"
+                                   + (f" ({head['frames_per_forward']} consecutive steps per forward: batch "
+                                      f"{head['frames_per_forward'] * S})" if head["frames_per_forward"] > 1 else "")
+                                   + f", {a.tracker} tracker(150, 1, 0.1), BASELINE config {a.config}",
+                       "frames_per_forward": head["frames_per_forward"],
                        "baseline_config": a.config, "streams_per_gpu": S, "global_batch": S * ws,
                        "parallelism": f"streams sharded over {ws} GPU(s), no data-path collective",
                        "targets_per_stream": cfg["targets"], "tracker_preroll_frames": a.preroll,
@@ -614,7 +678,8 @@ def main():
             "timed_region": "frames in page-locked host memory -> H2D on the slot stream -> forward -> NMS -> tracker "
                             "-> tracker output (counts, stats, rows) D2H, every step; hbm_resident_fps: the same steps "
                             "with the frames already in HBM and no output copy (informational)",
-            "roofline": head.get("roofline"), "tracker_roofline": head.get("tracker_roofline"),
+            "roofline": head.get("roofline"), "detect_roofline": head.get("detect_roofline"),
+            "nms_roofline": head.get("nms_roofline"), "tracker_roofline": head.get("tracker_roofline"),
             "cpu_baseline": cpu,
             "secondary": [{k: v for k, v in leg.items() if k != "window_monotonic_ns"} for leg in legs],
             "timed_window_monotonic_ns": head["window_monotonic_ns"],

@@ -21,6 +21,12 @@ int yk_gmd_debug_buffers(yk_gmd* g, void** dev_corners, void** dev_next, void** 
 /* Diagnostics: the two gray-pyramid buffers (uint8 [S][per]) and Scharr-derivative buffers (int16 x, y
  * [S][per]) the calls alternate between; per = pixels of every level of one stream. */
 int yk_gmd_debug_pyramids(yk_gmd* g, void** dev_pyr0, void** dev_pyr1, void** dev_der0, void** dev_der1, int64_t* per);
+/* Diagnostics: captured forwards yk_detect_graph currently caches for this model, and the LRU
+ * bound of that cache (tests/test_detector_gpu.py). */
+int yk_model_graph_count(yk_model* m, int32_t* n_graphs, int32_t* cap);
+/* Diagnostics: detector stores found outside every detector allocation so far (store-check build,
+ * csrc/build.py YK_DEFINES=-DYK_STORE_CHECK=1); -1 from the product library. */
+int yk_store_check_count(int64_t* out);
 #ifdef __cplusplus
 }
 #endif

@@ -49,9 +49,10 @@ class StepRecorder:
     def __call__(self, pipe, k, det_stream, trk_stream):
         t = self.t
         assert t < self.n, "more steps than the recorder holds"
+        dets, counts = pipe.step_outputs(k)
         with torch.cuda.stream(det_stream):
-            self.dets[t].copy_(pipe._dets[k])
-            self.counts[t].copy_(pipe._counts[k])
+            self.dets[t].copy_(dets)
+            self.counts[t].copy_(counts)
         rows, counts, stats = pipe.tracker.device_outputs()
         d2d_async(self.rows[t].data_ptr(), rows, self.row_bytes, trk_stream)
         d2d_async(self.tcounts[t].data_ptr(), counts, self.S * 4, trk_stream)

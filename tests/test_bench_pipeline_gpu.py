@@ -32,8 +32,11 @@ S, F, TARGETS = 8, 160, 40  # bench.py config 3's streams and targets
 # (layer activations ~3e-6 apart, max-normalised; tools/split_ab.py)
 TIE_REL = 1e-5
 CONF_TOL = 1e-4  # north_star: floats within 1e-4 (confidences are in [0, 1])
-PLANS = {"exact_r2": "plans/exp/s_640x512_i640_b8_fp32_exact_r2.json",  # round-2 exact-f32 MFMA plan
-         "committed": "plans/s_640x512_i640_b8_fp32.json"}              # bench.py's plan (split-bf16 / halo)
+# (plan, frames per forward): the round-2 exact-f32 MFMA plan; the split-bf16 / halo plan at one
+# step per forward; bench.py's headline: the same variants at the batch-16 forward of two steps
+PLANS = {"exact_r2": ("plans/exp/s_640x512_i640_b8_fp32_exact_r2.json", 1),
+         "committed": ("plans/s_640x512_i640_b8_fp32.json", 1),
+         "committed_t2": ("plans/s_640x512_i640_b16_fp32.json", 2)}
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
@@ -85,20 +88,20 @@ def chain():
     return build_chain([P.shard.stream_seed(s, S) for s in range(S)], F, TARGETS)
 
 
-def _run_gpu(dtype, frames, plan=None, model="yolov8s-small.yaml"):
+def _run_gpu(dtype, frames, plan=None, model="yolov8s-small.yaml", tbatch=1):
     P = pkg()
     import importlib
 
     pipeline = importlib.import_module(P.__name__ + ".pipeline")
     F, S = frames.shape[:2]
     pipe = pipeline.StreamPipeline(model, S, (512, 640), dtype, seed=0, max_tracks=512,
-                                   pipelined=True, inflight=4)
+                                   pipelined=True, inflight=4, frames_per_forward=tbatch)
     pipe.set_schedule(1, 1)  # bench.py's schedule with 3 forwards in flight
     # the committed conv plan bench.py loads for this workload (so the kernels under test are the
     # bench's own: split-bf16 / halo-tile variants included)
     with open(os.path.join(REPO, plan or f"plans/s_640x512_i640_b{S}_{dtype}.json")) as f:
         pl = json.load(f)
-    assert len(pl["plan"]) == len(pipe.prog.ops)
+    assert len(pl["plan"]) == len(pipe.prog.ops) and pl["batch"] == tbatch * S
     pipe.model.load_plan(pl["batch"], pl["plan"])
     fd = frames.cuda()
     pipe.frames.copy_(fd[0])
@@ -140,20 +143,20 @@ def test_bench_pipeline_fp32_matches_oracle_chain_every_frame(chain, plan):
     deviation is reported and bounded (1e-2).  Tracker bar on identical input: the oracle tracker
     fed the GPU's own detections matches the GPU tracker to 1e-9 on every output float
     (test_tracker_gpu.compare_frame)."""
-    out = check_chain(chain, PLANS[plan], parity_record=plan == "committed")
+    out = check_chain(chain, *PLANS[plan], parity_record=plan.startswith("committed"))
     assert min(chain["live"]) >= 40, chain["live"]  # the bench's >= 64-track load (see bench.py CONFIGS)
     assert chain["terminated"] > 0  # the deletion path ran inside the chain
     assert out["near_tie_flips"] + out["order_ties"] <= 3
 
 
-def check_chain(chain, plan_path, parity_record=False):
+def check_chain(chain, plan_path, tbatch=1, parity_record=False):
     """The resynced chain comparison of test_bench_pipeline_fp32_matches_oracle_chain_every_frame
     for any stream count (chain from build_chain); returns the summary it prints."""
     from gpu_helpers import resync_rows
     from test_tracker_gpu import compare_frame
 
     S, F = chain["S"], chain["F"]
-    dets, counts, rows, tcounts, stats = _run_gpu("fp32", chain["frames"], plan_path, chain["model"])
+    dets, counts, rows, tcounts, stats = _run_gpu("fp32", chain["frames"], plan_path, chain["model"], tbatch)
     assert int(stats[-1]["overflow"].sum()) == 0
     conf_dev, conf_dev_well, box_rel, n_tracks, n_outputs, ill_conf = 0.0, 0.0, 0.0, 0, 0, []
     flips, flip_scores, order_ties = [], [], []
@@ -212,7 +215,7 @@ def check_chain(chain, plan_path, parity_record=False):
     live = [int(tcounts[-1, s]) for s in range(S)]
     for fs in flip_scores:
         print("NEAR_TIE_FLIP", json.dumps(fs))
-    summary = {"plan": plan_path, "frames": F, "streams": S, "stream_frames_compared": F * S,
+    summary = {"plan": plan_path, "frames_per_forward": tbatch, "frames": F, "streams": S, "stream_frames_compared": F * S,
                "track_outputs_compared": n_tracks, "live_tracks_end": live, "near_tie_flips": len(flips),
                "near_tie_flip_frames": flips, "order_ties": len(order_ties), "order_tie_frames": order_ties,
                "oracle_near_tie_boxes": int(sum(len(b) for fr in chain["near"] for b in fr)),
@@ -248,16 +251,22 @@ def test_config4_rank_leg_b1_fp32_plan_matches_oracle_chain():
     assert ch["terminated"] > 0
 
 
+@__import__("functools").lru_cache(maxsize=1)
+def _chain_n():
+    P = pkg()
+    return build_chain([P.shard.stream_seed(s, S) for s in range(S)], F, TARGETS, model="yolov8n-small.yaml")
+
+
 @pytest.mark.timeout(900)
-def test_scale_n_b8_fp32_plan_matches_oracle_chain():
+@pytest.mark.parametrize("tb", [1, 2], ids=["t1", "t2"])
+def test_scale_n_b8_fp32_plan_matches_oracle_chain(tb):
     """The reference's own model scale (its trained model resolves to yolov8-small.yaml at scale
     n: small_target_detection/yolov8_small_aircraft/args.yaml:3, nn/tasks.py:1545-1549) on bench.py's
     config-3 pipeline (8 streams, one batch-8 forward, 4 in flight) with the committed scale-n
     plan (plans/n_640x512_i640_b8_fp32.json, bench.py --scale n): the same resynced chain bar as
     the scale-s test, every frame of every stream, and the plan's recorded near-tie count."""
-    P = pkg()
-    ch = build_chain([P.shard.stream_seed(s, S) for s in range(S)], F, TARGETS, model="yolov8n-small.yaml")
-    out = check_chain(ch, "plans/n_640x512_i640_b8_fp32.json", parity_record=True)
+    ch = _chain_n()
+    out = check_chain(ch, f"plans/n_640x512_i640_b{8 * tb}_fp32.json", tb, parity_record=True)
     assert out["near_tie_flips"] + out["order_ties"] <= 3
     assert min(ch["live"]) >= 40, ch["live"]
 

@@ -192,6 +192,9 @@ def test_dag_schedule_matches_sequential(dtype):
     ft = torch.from_numpy(np.stack([sc.frame(t) for t in range(B)])).cuda()
     dm = M.DeviceModel(M.Program(ar, sd, 512, 640, 640, B, dtype))
     lane, waits = dm.schedule()
+    assert set(lane.tolist()) == {0} and waits.sum() == 0  # the default: one lane, no forked capture
+    dm.set_schedule(1, 3)
+    lane, waits = dm.schedule()
     assert len(set(lane.tolist())) >= 2 and waits.sum() > 0
     runs, grouped = [], []
     for groups, lanes in ((1, 3), (1, 4), (2, 1), (3, 1)):
@@ -342,3 +345,42 @@ def test_fp32_nms_max_nms_cap_at_1280():
     n = int(counts[0])
     assert n == len(ref) == 300
     np.testing.assert_array_equal(dets[0, :n].cpu().numpy(), ref.numpy())
+
+
+def test_graph_cache_is_lru_bounded_and_replays_match():
+    """yk_detect_graph keys its captured forwards by the call's pointers; a caller handing new
+    output buffers every call must not grow the cache without bound: past the
+    bound the least recently used graph is evicted, and every replay still equals the eager
+    forward.  Also covers a forked (3-lane) schedule's per-capture events: captures of the forked
+    schedule interleaved with eager forked forwards give the sequential result."""
+    import ctypes as C
+
+    P, A, W, M = _mods()
+    L = P._lib
+    ar = A.parse_arch(A.load_model_dict("yolov8-small.yaml"))
+    sd = W.synthetic_state_dict(ar, 0)
+    sc = P.synth.Scene(seed=3, n_targets=12, n_frames=2)
+    ft = torch.from_numpy(np.stack([sc.frame(0)])).cuda()
+    dm = M.DeviceModel(M.Program(ar, sd, 512, 640, 640, 1, "fp32"))
+    d0, c0 = dm.detect(ft)
+    torch.cuda.synchronize()
+    want = _sorted_dets(d0.cpu(), c0.cpu())
+    n, cap = C.c_int32(), C.c_int32()
+    for lanes in (1, 3):
+        dm.set_schedule(1, lanes)
+        outs = []
+        for i in range(70):
+            dets = torch.zeros((1, 300, 6), dtype=torch.float32, device="cuda")
+            cnt = torch.zeros(1, dtype=torch.int32, device="cuda")
+            dm.detect(ft, dets=dets, counts=cnt, graph=True)
+            if lanes > 1 and i % 10 == 0:
+                dm.detect(ft)  # eager forked forward between captures (m->ev, not a capture's events)
+            outs.append((dets, cnt))
+            L.check(L.lib().yk_model_graph_count(dm.handle, C.byref(n), C.byref(cap)), "yk_model_graph_count")
+            assert n.value <= cap.value
+        torch.cuda.synchronize()
+        assert cap.value < 70 and n.value == cap.value
+        for dets, cnt in outs:
+            got = _sorted_dets(dets.cpu(), cnt.cpu())
+            for a, b in zip(want, got):
+                np.testing.assert_array_equal(a, b)

@@ -2,6 +2,7 @@
 against the oracle chain (torch-CPU detector -> numpy tracker) per stream, plus the
 reference driver's loop through the compat ``ultralytics`` / ``kalman`` packages."""
 import importlib
+import json
 import os
 import sys
 
@@ -232,6 +233,16 @@ def test_reference_driver_loop_ill_conditioned_scene_counted_ties(tmp_path):
     assert len(out["assoc_near_tie_flips"]) <= 3, out["assoc_near_tie_flips"]
 
 
+def _plan_at_forward_batch(pipe, path="plans/s_640x512_i640_b8_bf16.json"):
+    """Load a committed conv plan for the pipeline's forward batch (frames_per_forward x streams):
+    the per-op kernel variants then do not depend on the batch, so pipelines with other forward
+    batches compute bit-identical detections (the heuristic plan picks tiles by batch)."""
+    with open(os.path.join(REPO, path)) as f:
+        plan = json.load(f)["plan"]
+    for m in pipe.models:
+        m.load_plan(pipe.T * pipe.S, plan)
+
+
 def test_pipelined_tracker_stream_matches_serial():
     """pipelined=True (tracker(t) on its own stream, overlapping detector(t+1), double-buffered
     detections) and inflight=2/3/4 (detector graphs in flight on their own streams) give exactly the
@@ -240,9 +251,13 @@ def test_pipelined_tracker_stream_matches_serial():
     pipeline = importlib.import_module(P.__name__ + ".pipeline")
     S, F = 4, 24
     runs = []
-    for pipelined, inflight in ((False, 1), (True, 1), (True, 2), (True, 3), (True, 4)):
+    # (pipelined, inflight, frames per forward): T > 1 is temporal batching (one forward of T
+    # steps' frames); T = 5 leaves a partial forward for flush() at the end (24 = 4 x 5 + 4)
+    for pipelined, inflight, tb in ((False, 1, 1), (True, 1, 1), (True, 2, 1), (True, 3, 1), (True, 4, 1),
+                                    (True, 4, 2), (True, 2, 3), (True, 3, 5)):
         pipe = pipeline.StreamPipeline("yolov8s-small.yaml", S, (512, 640), "bf16", seed=0, max_tracks=256,
-                                       pipelined=pipelined, inflight=inflight)
+                                       pipelined=pipelined, inflight=inflight, frames_per_forward=tb)
+        _plan_at_forward_batch(pipe)
         scenes = [P.synth.Scene(seed=40 + s, n_targets=16, n_frames=F) for s in range(S)]
         frames = torch.stack([sc.frames_torch(0, F, "cuda") for sc in scenes], 1)
         pipe.frames.copy_(frames[0])
@@ -273,15 +288,16 @@ def test_prefetched_host_frames_match_device_frames():
     host = frames.cpu().pin_memory()
     assert host[0].numel() >= pipeline.StreamPipeline.PULL_BYTES  # the DMA / staging path, not the pull kernel
     runs = []
-    for mode in ("device", "direct", "next", "ahead1", "ahead3", "device_ahead2"):
+    for mode in ("device", "direct", "next", "ahead1", "ahead3", "device_ahead2", "t2_ahead2", "t2_next"):
         pipe = pipeline.StreamPipeline("yolov8s-small.yaml", S, (512, 640), "bf16", seed=0, max_tracks=256,
-                                       pipelined=True, inflight=4)
+                                       pipelined=True, inflight=4, frames_per_forward=2 if mode.startswith("t2") else 1)
+        _plan_at_forward_batch(pipe)
         pipe.frames.copy_(frames[0])
         pipe.capture(tune=False)
         src = frames if mode.startswith("device") else host
-        depth = {"ahead1": 1, "ahead3": 3, "device_ahead2": 2}.get(mode, 0)
+        depth = {"ahead1": 1, "ahead3": 3, "device_ahead2": 2, "t2_ahead2": 2}.get(mode, 0)
         for t in range(F):
-            if mode == "next":
+            if mode in ("next", "t2_next"):
                 pipe.run(src[t], next_frames=src[t + 1] if t + 1 < F else None)
             else:
                 pipe.run(src[t])

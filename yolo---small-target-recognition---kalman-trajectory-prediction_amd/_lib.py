@@ -170,6 +170,8 @@ _SIGS = {
     "yk_model_set_plan": ([_vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int], C.c_int),
     "yk_model_autotune": ([_vp, _vp, C.c_int, C.c_float, C.c_int, _vp], C.c_int),
     "yk_model_get_schedule": ([_vp, _vp, _vp], C.c_int),
+    "yk_model_graph_count": ([_vp, C.POINTER(_i32), C.POINTER(_i32)], C.c_int),
+    "yk_store_check_count": ([_vp], C.c_int),
     "yk_model_get_plan": ([_vp, _vp, _vp], C.c_int),
     "yk_model_load": ([_vp, C.c_char_p, C.POINTER(_vp)], C.c_int),
     "yk_program_build": ([C.POINTER(Weights), C.c_char, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,

@@ -32,6 +32,7 @@
 #include <vector>
 
 #include "yk_internal.h"
+#include "yk_diag.h"
 
 // Diagnostic builds.  csrc/build.py YK_DEFINES="-DYK_DIAG=<mask>" builds libyk_diag.so with its
 // own objects; the product library is always built with YK_DIAG = 0, where every bit below is off
@@ -52,9 +53,37 @@
 #ifndef YK_FAST_WPE  // (a diagnostic build may set it: YK_DEFINES=-DYK_FAST_WPE=3)
 #define YK_FAST_WPE ((YK_DIAG & 128) ? 2 : 1)
 #endif
+// YK_STORE_CHECK=1 (diagnostic build): every detector-kernel store -- the conv
+// epilogues (store4), detect_kernel's candidate rows, nms_kernel's outputs and global scratch --
+// checks that its bytes lie inside one of the detector's own allocations (every model's arena,
+// candidate / NMS buffers, letterbox canvas, and the detection buffers handed to yk_detect); a
+// store outside them prints its site and address and is counted (yk_store_check_count).
+#ifndef YK_STORE_CHECK
+#define YK_STORE_CHECK 0
+#endif
 
 namespace yk {
 namespace det {
+
+#if YK_STORE_CHECK
+constexpr int kScMax = 256;
+__device__ unsigned long long sc_lo[kScMax], sc_hi[kScMax];
+__device__ int sc_n;
+__device__ unsigned long long sc_bad;
+__device__ __noinline__ void sc_fail(const void* p, int bytes, int site) {
+  const unsigned long long c = atomicAdd(&sc_bad, 1ull);
+  if (c < 16) printf("[yk store check] site %d: %d bytes at %p outside every detector allocation\n", site, bytes, p);
+}
+__device__ __forceinline__ void sc_check(const void* p, int bytes, int site) {
+  const unsigned long long a = (unsigned long long)p;
+  bool ok = false;
+  for (int i = 0; i < sc_n; ++i) ok = ok || (a >= sc_lo[i] && a + (unsigned long long)bytes <= sc_hi[i]);
+  if (!ok) sc_fail(p, bytes, site);
+}
+#define YK_SC(p, bytes, site) sc_check((const void*)(p), (bytes), (site))
+#else
+#define YK_SC(p, bytes, site) ((void)0)
+#endif
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
@@ -319,15 +348,20 @@ __device__ __forceinline__ void mma_split_step(const WS2* w, const uint4* xf, f3
 
 
 __device__ __forceinline__ void store4(unsigned short* p, const float v[4]) {
+  YK_SC(p, 8, 1);
   uint2 o;
   o.x = pack_bf16x2(v[0], v[1]);
   o.y = pack_bf16x2(v[2], v[3]);
   *(uint2*)p = o;
 }
-__device__ __forceinline__ void store4(float* p, const float v[4]) { *(float4*)p = make_float4(v[0], v[1], v[2], v[3]); }
+__device__ __forceinline__ void store4(float* p, const float v[4]) {
+  YK_SC(p, 16, 2);
+  *(float4*)p = make_float4(v[0], v[1], v[2], v[3]);
+}
 typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 // f32 -> f16 round-to-nearest-even (v_cvt_f16_f32), overflow to +-inf like torch's .half()
 __device__ __forceinline__ void store4(_Float16* p, const float v[4]) {
+  YK_SC(p, 8, 3);
   *(f16x4*)p = f16x4{(_Float16)v[0], (_Float16)v[1], (_Float16)v[2], (_Float16)v[3]};
 }
 __device__ __forceinline__ void load4(const _Float16* p, float v[4]) {
@@ -340,6 +374,7 @@ __device__ __forceinline__ void load4(const _Float16* p, float v[4]) {
 // f32 -> e4m3 with round-to-nearest-even (v_cvt_pk_fp8_f32), saturated to the finite range
 __device__ __forceinline__ float sat448(float v) { return __builtin_amdgcn_fmed3f(v, -448.f, 448.f); }
 __device__ __forceinline__ void store4(unsigned char* p, const float v[4]) {
+  YK_SC(p, 4, 4);
   int w = __builtin_amdgcn_cvt_pk_fp8_f32(sat448(v[0]), sat448(v[1]), 0, false);
   w = __builtin_amdgcn_cvt_pk_fp8_f32(sat448(v[2]), sat448(v[3]), w, true);
   *(int*)p = w;
@@ -2550,9 +2585,11 @@ __global__ void __launch_bounds__(256) detect_kernel(DetArgs a) {
   const float cx = ((x1 + x2) / 2.0f) * st, cy = ((y1 + y2) / 2.0f) * st;
   const float w = (x2 - x1) * st, h = (y2 - y1) * st;
   const float hw2 = w / 2.0f, hh2 = h / 2.0f;
+  YK_SC(&a.cand_count[b], 4, 10);
   const int slot = atomicAdd(&a.cand_count[b], 1);
   if (slot >= a.cap) return;
   float* c = a.cand + ((size_t)b * a.cap + slot) * 6;
+  YK_SC(c, 24, 11);
   c[0] = cx - hw2;
   c[1] = cy - hh2;
   c[2] = cx + hw2;
@@ -2978,9 +3015,13 @@ __device__ void nms_small(const NmsArgs& a, int b, int n, unsigned char* smem) {
   if (misc[13]) k = 0;  // corrupt candidate rows: no detections, error flagged below
   // outputs: x[i] rows, then scale_boxes (x - pad) / gain and clip (ops.py:105-184)
   for (int r = tid; r < k; r += NMS_NT) {
-    if (a.keep_out) a.keep_out[(size_t)b * a.max_det + r] = (int)(keys[pay[NMS_MASK_N + keep[r]]] & 0xffffffffu);
+    if (a.keep_out) {
+      YK_SC(&a.keep_out[(size_t)b * a.max_det + r], 4, 20);
+      a.keep_out[(size_t)b * a.max_det + r] = (int)(keys[pay[NMS_MASK_N + keep[r]]] & 0xffffffffu);
+    }
     const float* c = stg + pay[NMS_MASK_N + keep[r]] * 5;
     float* o = a.dets + ((size_t)b * a.max_det + r) * 6;
+    YK_SC(o, 24, 21);
     const float x1 = (c[0] - a.pad_x) / a.gain, y1 = (c[1] - a.pad_y) / a.gain;
     const float x2 = (c[2] - a.pad_x) / a.gain, y2 = (c[3] - a.pad_y) / a.gain;
     o[0] = fminf(fmaxf(x1, 0.f), a.clip_w);
@@ -2991,6 +3032,7 @@ __device__ void nms_small(const NmsArgs& a, int b, int n, unsigned char* smem) {
     o[5] = 0.f;
   }
   if (tid == 0) {
+    YK_SC(&a.counts[b], 4, 22);
     a.counts[b] = k;
     if (misc[13]) nms_flag_error(a.err);
     if (a.stat) {
@@ -3040,10 +3082,12 @@ __global__ void __launch_bounds__(NMS_NT) nms_kernel(NmsArgs a) {
         misc[13] = 1;                        // never index outside slot_of; flag it
         anc = 0;
       } else {
+        YK_SC(&slot_of[anc], 4, 30);
         slot_of[anc] = i;
       }
       k = nms_key(cand[i * 6 + 4], anc);
     }
+    if (!in_lds) YK_SC(&keys[i], 8, 31);
     keys[i] = k;
   }
   __syncthreads();
@@ -3060,6 +3104,10 @@ __global__ void __launch_bounds__(NMS_NT) nms_kernel(NmsArgs a) {
     const int s = slot_of[(int)(keys[i] & 0xffffffffu)];
     const float* c = cand + (size_t)s * 6;
     const float x1 = c[0], y1 = c[1], x2 = c[2], y2 = c[3];
+    if (!in_lds) {
+      YK_SC(&box[i * 5], 20, 32);
+      YK_SC(&removed[i], 1, 33);
+    }
     box[i * 5 + 0] = x1;
     box[i * 5 + 1] = y1;
     box[i * 5 + 2] = x2;
@@ -3118,7 +3166,10 @@ __global__ void __launch_bounds__(NMS_NT) nms_kernel(NmsArgs a) {
         const float h = fmaxf(fminf(by2, box[j * 5 + 3]) - fmaxf(by1, box[j * 5 + 1]), 0.f);
         const float inter = w * h;
         const float iou = inter / (ba + box[j * 5 + 4] - inter);
-        if (!(iou <= thr)) removed[j] = 1;
+        if (!(iou <= thr)) {
+          if (!in_lds) YK_SC(&removed[j], 1, 34);
+          removed[j] = 1;
+        }
       }
       __syncthreads();
     }
@@ -3127,10 +3178,14 @@ __global__ void __launch_bounds__(NMS_NT) nms_kernel(NmsArgs a) {
   // outputs: x[i] rows, then scale_boxes (x - pad) / gain and clip (ops.py:105-184)
   for (int r = tid; r < k; r += NMS_NT) {
     const int i = keep[r];
-    if (a.keep_out) a.keep_out[(size_t)b * a.max_det + r] = (int)(keys[i] & 0xffffffffu);
+    if (a.keep_out) {
+      YK_SC(&a.keep_out[(size_t)b * a.max_det + r], 4, 35);
+      a.keep_out[(size_t)b * a.max_det + r] = (int)(keys[i] & 0xffffffffu);
+    }
     const int s = slot_of[(int)(keys[i] & 0xffffffffu)];
     const float* c = cand + (size_t)s * 6;
     float* o = a.dets + ((size_t)b * a.max_det + r) * 6;
+    YK_SC(o, 24, 36);
     float x1 = (c[0] - a.pad_x) / a.gain, y1 = (c[1] - a.pad_y) / a.gain;
     float x2 = (c[2] - a.pad_x) / a.gain, y2 = (c[3] - a.pad_y) / a.gain;
     o[0] = fminf(fmaxf(x1, 0.f), a.clip_w);
@@ -3141,6 +3196,7 @@ __global__ void __launch_bounds__(NMS_NT) nms_kernel(NmsArgs a) {
     o[5] = 0.f;
   }
   if (tid == 0) {
+    YK_SC(&a.counts[b], 4, 37);
     a.counts[b] = k;
     if (a.stat) {
       atomicAdd(&a.stat[0], misc[14] && k > 0 ? 1 : 0);
@@ -3184,6 +3240,10 @@ __global__ void __launch_bounds__(64) zero_i32_kernel(int* p, int n) {
 
 using namespace yk::det;
 
+// captured forwards kept per model (yk_detect_graph's LRU cache): the pipeline needs one per
+// (frame buffer, detection buffer) pair, <= 2 x 4 D = 64 at D = 8
+constexpr int kGraphCap = 64;
+
 struct yk_model {
   yk_ctx* ctx = nullptr;
   yk_model_desc desc{};
@@ -3203,7 +3263,18 @@ struct yk_model {
   int* nms_stat = nullptr;          // [2] device: NMS early exits, images (yk_model_nms_stats)
   volatile int* err_host = nullptr;  // host-mapped error word the kernels flag (nms_flag_error)
   int* err_dev = nullptr;
-  std::map<std::tuple<int, float, float, int, const void*, void*, void*>, hipGraphExec_t> graphs;
+  // Captured forwards, keyed by the call's arguments (raw pointers: a caller that keeps handing
+  // new buffers would grow the cache without bound, so it is LRU-bounded at kGraphCap entries).
+  // A multi-lane graph owns the fork / join events its capture recorded (`evs`): no event is ever
+  // recorded by two captures, or by a capture and an uncaptured forward.
+  struct GraphEntry {
+    hipGraphExec_t exec = nullptr;
+    std::vector<hipEvent_t> evs;
+    unsigned long long last_use = 0;
+  };
+  std::map<std::tuple<int, float, float, int, const void*, void*, void*>, GraphEntry> graphs;
+  unsigned long long graph_clock = 0;
+  const hipEvent_t* run_ev = nullptr;  // events run_dag records into (a capture's own set), or m->ev
   int plan_batch = 1;  // batch the kernel names of yk_model_op_kernel are reported for
   bool tiled = true;  // LDS-tiled conv kernel where its tile fits (YK_CONV_DIRECT=1 forces the direct kernel)
   // DAG schedule: ops run on `lanes` streams (lane 0 = the caller's stream) with event edges
@@ -3211,7 +3282,7 @@ struct yk_model {
   // With `groups` > 1 the batch is cut into that many sub-batches, each an independent copy of
   // the DAG on its own `lanes` streams: the detector's kernels are latency-bound, so
   // independent chains overlap on the chip.
-  int lanes = 3, groups = 1;
+  int lanes = 1, groups = 1;
   struct Task {
     int op, grp, lane;
     std::vector<int> waits;  // producer tasks on other lanes (latest per lane)
@@ -3255,6 +3326,35 @@ struct yk_model {
 };
 
 namespace {
+
+#if YK_STORE_CHECK
+// (diagnostic build) the legal store ranges the kernels check against: a host copy, uploaded to
+// the device table whenever it grows (never while a stream captures: callers register first)
+std::vector<std::pair<unsigned long long, unsigned long long>> g_sc;
+void sc_register(const void* p, size_t bytes) {
+  if (!p || !bytes) return;
+  const unsigned long long lo = (unsigned long long)p, hi = lo + bytes;
+  for (auto& r : g_sc)
+    if (r.first <= lo && hi <= r.second) return;
+  if (g_sc.size() >= (size_t)kScMax) {
+    fprintf(stderr, "[yk store check] range table full\n");
+    return;
+  }
+  g_sc.push_back({lo, hi});
+  std::vector<unsigned long long> l, h;
+  for (auto& r : g_sc) {
+    l.push_back(r.first);
+    h.push_back(r.second);
+  }
+  const int n = (int)g_sc.size();
+  (void)hipDeviceSynchronize();
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(sc_lo), l.data(), n * 8);
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(sc_hi), h.data(), n * 8);
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(sc_n), &n, 4);
+}
+#else
+inline void sc_register(const void*, size_t) {}
+#endif
 
 int esz_of(int dtype) { return dtype == YK_ACT_F32 ? 4 : dtype == YK_ACT_FP8 ? 1 : 2; }  // BF16 / F16: 2
 size_t act_bytes(const yk_model* m) { return (size_t)esz_of(m->desc.act_dtype); }
@@ -3471,12 +3571,22 @@ void set_fast_attr_w() {
   set_fast_attr_n<Tr, 3, KW>();
   set_fast_attr_n<Tr, 4, KW>();
 }
+// conv_wide_kernel instantiations that compile without spilling: with 8 waves (two per SIMD, 256
+// registers each) the staging units of UPT > 12 (2 tiles) or UPT > 4 (4 tiles) spilled 12-209
+// VGPRs to scratch, so those are neither built nor offered to the autotuner
+constexpr bool wide_ok(int nnt, int upt, int nw) { return nw == 4 || (nnt == 2 ? upt <= 12 : upt <= 4); }
+template <class Tr, int NNT, int UPT, int NW>
+void set_wide_attr_u() {
+  if constexpr (wide_ok(NNT, UPT, NW))
+    (void)hipFuncSetAttribute((const void*)conv_wide_kernel<Tr, NNT, UPT, NW>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+}
 template <class Tr, int NNT, int NW>
 void set_wide_attr_w() {
-  (void)hipFuncSetAttribute((const void*)conv_wide_kernel<Tr, NNT, 4, NW>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  (void)hipFuncSetAttribute((const void*)conv_wide_kernel<Tr, NNT, 8, NW>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  (void)hipFuncSetAttribute((const void*)conv_wide_kernel<Tr, NNT, 12, NW>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  (void)hipFuncSetAttribute((const void*)conv_wide_kernel<Tr, NNT, 16, NW>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  set_wide_attr_u<Tr, NNT, 4, NW>();
+  set_wide_attr_u<Tr, NNT, 8, NW>();
+  set_wide_attr_u<Tr, NNT, 12, NW>();
+  set_wide_attr_u<Tr, NNT, 16, NW>();
 }
 template <class Tr, int NNT>
 void set_wide_attr_n() {
@@ -3599,7 +3709,8 @@ WidePlan wide_plan(const yk_op& op, int esz, int nnt, int nw = 4) {
   const int total = w.tih * w.tiw * units;
   w.upt = (total + 64 * nw - 1) / (64 * nw);
   w.lds = wide_lds(nnt, op.k_steps, w.tih, w.tiw, w.ps, esz);
-  w.ok = w.upt <= 16 && w.lds <= 160 * 1024 && w.tih < 128;
+  const int ub = w.upt <= 4 ? 4 : w.upt <= 8 ? 8 : w.upt <= 12 ? 12 : 16;  // the instantiation launch_wide_n takes
+  w.ok = w.upt <= 16 && w.lds <= 160 * 1024 && w.tih < 128 && wide_ok(nnt, ub, nw);
   for (int sidx = 0; sidx < op.n_src; ++sidx) w.ok = w.ok && (op.ksize == 1 || op.src[sidx].up == 0);
   return w;
 }
@@ -3834,6 +3945,9 @@ void launch_halo(const HaloArgs& a, int B, const ConvPlan& p, int ks, hipStream_
 
 template <class Tr, int NNT, int UPT, int NW>
 void launch_wide_t(const WideArgs& a, size_t lds, hipStream_t st) {
+  if constexpr (!wide_ok(NNT, UPT, NW)) {
+    return;  // (wide_plan never selects it)
+  } else {
   const int groups = (a.n_tiles + NNT - 1) / NNT;
   const int nsp = a.B * a.tiles_y * a.tiles_x;
   int per_cu = (int)((160 * 1024) / lds);
@@ -3842,6 +3956,7 @@ void launch_wide_t(const WideArgs& a, size_t lds, hipStream_t st) {
   if (gx < 1) gx = 1;
   if (gx > nsp) gx = nsp;
   hipLaunchKernelGGL((conv_wide_kernel<Tr, NNT, UPT, NW>), dim3(gx, groups), dim3(64 * NW), lds, st, a);
+  }
 }
 template <class Tr, int NNT, int NW>
 void launch_wide_n(const WideArgs& a, int upt, size_t lds, hipStream_t st) {
@@ -4340,24 +4455,25 @@ int run_dag(yk_model* m, const uint8_t* frames, int B, float conf, hipStream_t s
     b0 += gbn[g];
   }
   auto lane_stream = [&](int l) { return l == 0 ? st : m->aux[l - 1]; };
-  hipEvent_t fork = m->ev[nt];
+  const hipEvent_t* ev = m->run_ev ? m->run_ev : m->ev.data();
+  hipEvent_t fork = ev[nt];
   YK_HIP(hipEventRecord(fork, st));
   for (int l = 1; l < L; ++l)
     if (m->lane_used[l]) YK_HIP(hipStreamWaitEvent(m->aux[l - 1], fork, 0));
   for (int t = 0; t < nt; ++t) {
     const yk_model::Task& task = m->tasks[t];
     hipStream_t s = lane_stream(task.lane);
-    for (int d : task.waits) YK_HIP(hipStreamWaitEvent(s, m->ev[d], 0));
+    for (int d : task.waits) YK_HIP(hipStreamWaitEvent(s, ev[d], 0));
     if (gbn[task.grp] > 0) {
       const int rc = launch_op<Tr>(m, m->ops[task.op], frames, gbn[task.grp], conf, s, gb0[task.grp]);
       if (rc != YK_OK) return rc;
     }
-    if (task.ev) YK_HIP(hipEventRecord(m->ev[t], s));
+    if (task.ev) YK_HIP(hipEventRecord(ev[t], s));
   }
   for (int l = 1; l < L; ++l) {
     if (!m->lane_used[l]) continue;
-    YK_HIP(hipEventRecord(m->ev[nt + l], m->aux[l - 1]));
-    YK_HIP(hipStreamWaitEvent(st, m->ev[nt + l], 0));
+    YK_HIP(hipEventRecord(ev[nt + l], m->aux[l - 1]));
+    YK_HIP(hipStreamWaitEvent(st, ev[nt + l], 0));
   }
   return YK_OK;
 }
@@ -4642,9 +4758,24 @@ int take_device_error(yk_model* m) {
   return YK_ERR_STATE;
 }
 
-hipError_t set_schedule(yk_model* m, int groups, int lanes) {
-  for (auto& kv : m->graphs) (void)hipGraphExecDestroy(kv.second);
+void destroy_graph(yk_model::GraphEntry& g) {
+  if (g.exec) (void)hipGraphExecDestroy(g.exec);
+  for (hipEvent_t v : g.evs) (void)hipEventDestroy(v);
+  g.exec = nullptr;
+  g.evs.clear();
+}
+
+// Drop every captured forward.  A graph may still be executing (the caller's streams), so the
+// device is synchronised first: hipGraphExecDestroy of a graph in flight is not defined here.
+void clear_graphs(yk_model* m) {
+  if (m->graphs.empty()) return;
+  (void)hipDeviceSynchronize();
+  for (auto& kv : m->graphs) destroy_graph(kv.second);
   m->graphs.clear();
+}
+
+hipError_t set_schedule(yk_model* m, int groups, int lanes) {
+  clear_graphs(m);
   for (hipStream_t s : m->aux) (void)hipStreamDestroy(s);
   if (m->cap) (void)hipStreamDestroy(m->cap);
   m->cap = nullptr;
@@ -4792,7 +4923,26 @@ int yk_model_create(yk_ctx* ctx, const yk_model_desc* desc, const void* host_blo
         yk_model_destroy(m);
         return YK_ERR_ARG;
       }
-  if (e == hipSuccess) e = set_schedule(m, 1, 3);
+  if (e == hipSuccess && YK_STORE_CHECK) {
+    sc_register(m->arena, m->arena_bytes);
+    sc_register(m->cand, B * A * 6 * sizeof(float));
+    sc_register(m->cand_count, B * sizeof(int));
+    sc_register(m->slot_of, B * A * sizeof(int));
+    sc_register(m->gkeys, B * (size_t)kc * sizeof(unsigned long long));
+    sc_register(m->gbox, B * A * 5 * sizeof(float));
+    sc_register(m->gflag, B * A);
+    sc_register(m->dets, B * desc->max_det * 6 * sizeof(float));
+    sc_register(m->counts, B * sizeof(int));
+    sc_register(m->nms_stat, 2 * sizeof(int));
+    if (m->lbox) sc_register(m->lbox, B * (size_t)desc->in_h * desc->in_w * 3);
+  }
+  // Default schedule: one lane (the reference's sequential op order on the caller's stream).  A
+  // captured graph's parallel branches ran one after another, and the forked capture
+  // is the pattern that crashed hipGraphLaunch / a capture in rounds 4-5;
+  // YK_LANES=<n> selects a forked schedule for A/B runs, yk_model_set_schedule at run time.
+  int lanes0 = 1;
+  if (const char* env = getenv("YK_LANES")) lanes0 = atoi(env) >= 1 && atoi(env) <= 8 ? atoi(env) : 1;
+  if (e == hipSuccess) e = set_schedule(m, 1, lanes0);
   if (e != hipSuccess) {
     yk::set_error(std::string("yk_model_create: ") + hipGetErrorString(e));
     yk_model_destroy(m);
@@ -4831,7 +4981,7 @@ int yk_model_get_schedule(yk_model* m, int32_t* lane_of, int32_t* n_waits) {
 int yk_model_destroy(yk_model* m) {
   if (!m) return YK_OK;
   yk::DeviceGuard guard(m->ctx->device);
-  for (auto& kv : m->graphs) (void)hipGraphExecDestroy(kv.second);
+  clear_graphs(m);
   for (hipStream_t s : m->aux) (void)hipStreamDestroy(s);
   if (m->cap) (void)hipStreamDestroy(m->cap);
   for (hipEvent_t v : m->ev) (void)hipEventDestroy(v);
@@ -4850,6 +5000,10 @@ int yk_detect(yk_model* m, const uint8_t* frames, int batch, float conf, float i
   YK_CHECK_ARG(m, "yk_detect: NULL model");
   if (const int rc = take_device_error(m)) return rc;
   yk::DeviceGuard guard(m->ctx->device);
+  if (YK_STORE_CHECK && batch >= 1) {
+    sc_register(dets, (size_t)batch * max_det * 6 * sizeof(float));
+    sc_register(counts, (size_t)batch * sizeof(int));
+  }
   return detect_impl(m, frames, batch, conf, iou, max_det, dets, counts, (hipStream_t)stream);
 }
 
@@ -4858,10 +5012,38 @@ int yk_detect_graph(yk_model* m, const uint8_t* frames, int batch, float conf, f
   YK_CHECK_ARG(m, "yk_detect_graph: NULL model");
   if (const int rc = take_device_error(m)) return rc;
   yk::DeviceGuard guard(m->ctx->device);
+  if (YK_STORE_CHECK && batch >= 1) {  // (before any capture begins)
+    sc_register(dets, (size_t)batch * max_det * 6 * sizeof(float));
+    sc_register(counts, (size_t)batch * sizeof(int));
+  }
   hipStream_t st = (hipStream_t)stream;
   auto key = std::make_tuple(batch, conf, iou, max_det, (const void*)frames, (void*)dets, (void*)counts);
   auto it = m->graphs.find(key);
   if (it == m->graphs.end()) {
+    if (m->graphs.size() >= (size_t)kGraphCap) {  // LRU eviction (after a device sync: clear_graphs)
+      auto lru = m->graphs.begin();
+      for (auto j = m->graphs.begin(); j != m->graphs.end(); ++j)
+        if (j->second.last_use < lru->second.last_use) lru = j;
+      YK_HIP(hipDeviceSynchronize());
+      destroy_graph(lru->second);
+      m->graphs.erase(lru);
+    }
+    // a forked schedule records its fork / join events into this capture only: a fresh set, owned
+    // by the graph entry (destroyed with it), never shared with another capture or with the
+    // uncaptured forwards' m->ev
+    yk_model::GraphEntry ent;
+    if (m->groups * m->lanes > 1) {
+      for (size_t i = 0; i < m->ev.size(); ++i) {
+        hipEvent_t v;
+        const hipError_t ee = hipEventCreateWithFlags(&v, hipEventDisableTiming);
+        if (ee != hipSuccess) {
+          destroy_graph(ent);
+          yk::set_error(std::string("yk_detect_graph: ") + hipGetErrorString(ee));
+          return YK_ERR_HIP;
+        }
+        ent.evs.push_back(v);
+      }
+    }
     // Capture stream: one per model, kept for the model's lifetime (round 4 created one per
     // capture and destroyed it after hipStreamEndCapture, and multi-lane graphs then crashed in
     // hipGraphLaunch once several models were alive; tools/graph_fork_repro.hip did not reproduce
@@ -4886,15 +5068,25 @@ int yk_detect_graph(yk_model* m, const uint8_t* frames, int batch, float conf, f
     }
     hipGraph_t g;
     const bool dbg = getenv("YK_DEBUG_GRAPH") != nullptr;
-    YK_HIP(hipStreamBeginCapture(cap, hipStreamCaptureModeThreadLocal));
+    const hipError_t be = hipStreamBeginCapture(cap, hipStreamCaptureModeThreadLocal);
+    if (be != hipSuccess) {
+      destroy_graph(ent);
+      if (cap_tmp) (void)hipStreamDestroy(cap);
+      yk::set_error(std::string("yk_detect_graph: begin capture: ") + hipGetErrorString(be));
+      return YK_ERR_HIP;
+    }
     if (dbg) fprintf(stderr, "[yk] capture begun\n");
+    m->run_ev = ent.evs.empty() ? nullptr : ent.evs.data();
     int rc = detect_impl(m, frames, batch, conf, iou, max_det, dets, counts, cap);
+    m->run_ev = nullptr;
     if (dbg) fprintf(stderr, "[yk] ops recorded rc=%d\n", rc);
     hipError_t ce = hipStreamEndCapture(cap, &g);
     if (dbg) fprintf(stderr, "[yk] capture ended: %s\n", hipGetErrorString(ce));
     if (cap_tmp) (void)hipStreamDestroy(cap);
-    if (rc != YK_OK) return rc;
-    if (ce != hipSuccess) {
+    if (rc != YK_OK || ce != hipSuccess) {
+      if (ce == hipSuccess) (void)hipGraphDestroy(g);
+      destroy_graph(ent);
+      if (rc != YK_OK) return rc;
       yk::set_error(std::string("yk_detect_graph: capture failed: ") + hipGetErrorString(ce));
       return YK_ERR_HIP;
     }
@@ -4908,12 +5100,35 @@ int yk_detect_graph(yk_model* m, const uint8_t* frames, int batch, float conf, f
     if (dbg) fprintf(stderr, "[yk] instantiated: %s\n", hipGetErrorString(ie));
     (void)hipGraphDestroy(g);
     if (ie != hipSuccess) {
+      destroy_graph(ent);
       yk::set_error(std::string("yk_detect_graph: instantiate failed: ") + hipGetErrorString(ie));
       return YK_ERR_HIP;
     }
-    it = m->graphs.emplace(key, ge).first;
+    ent.exec = ge;
+    it = m->graphs.emplace(key, std::move(ent)).first;
   }
-  YK_HIP(hipGraphLaunch(it->second, st));
+  it->second.last_use = ++m->graph_clock;
+  YK_HIP(hipGraphLaunch(it->second.exec, st));
+  return YK_OK;
+}
+
+int yk_store_check_count(int64_t* out) {
+  YK_CHECK_ARG(out, "yk_store_check_count: NULL argument");
+#if YK_STORE_CHECK
+  unsigned long long v = 0;
+  YK_HIP(hipDeviceSynchronize());
+  YK_HIP(hipMemcpyFromSymbol(&v, HIP_SYMBOL(sc_bad), 8));
+  *out = (int64_t)v;
+#else
+  *out = -1;  // not a store-check build
+#endif
+  return YK_OK;
+}
+
+int yk_model_graph_count(yk_model* m, int32_t* n_graphs, int32_t* cap) {
+  YK_CHECK_ARG(m && n_graphs && cap, "yk_model_graph_count: NULL argument");
+  *n_graphs = (int32_t)m->graphs.size();
+  *cap = kGraphCap;
   return YK_OK;
 }
 
@@ -4980,8 +5195,7 @@ int yk_model_set_plan(yk_model* m, int op_index, int batch, int kind, int nnt, i
   m->tuned_batch = batch;
   for (int i = 0; i < (int)m->ops.size(); ++i)
     if ((op_index < 0 || i == op_index) && m->ops[i].kind == YK_K_CONV) m->tuned[i] = {kind, nnt, npt};
-  for (auto& kv : m->graphs) (void)hipGraphExecDestroy(kv.second);
-  m->graphs.clear();
+  clear_graphs(m);
   return YK_OK;
 }
 
@@ -5003,8 +5217,7 @@ int yk_model_autotune(yk_model* m, const uint8_t* frames, int batch, float conf,
   const int bt = (batch + m->groups - 1) / m->groups;  // the batch each group's kernels run at
   m->tuned.assign(n, {-1, 0, 0});
   m->tuned_batch = bt;
-  for (auto& kv : m->graphs) (void)hipGraphExecDestroy(kv.second);
-  m->graphs.clear();
+  clear_graphs(m);
   int rc = detect_impl(m, frames, batch, conf, 0.7f, 1, nullptr, nullptr, st);  // valid activations
   if (rc != YK_OK) return rc;
   hipEvent_t e0, e1;
@@ -5090,6 +5303,11 @@ int yk_nms_candidates(yk_model* m, int batch, float iou, int max_det, float* det
   YK_CHECK_ARG(max_det >= 0 && max_det <= m->desc.max_det, "yk_nms_candidates: max_det exceeds the model's capacity");
   if (const int rc = take_device_error(m)) return rc;
   yk::DeviceGuard guard(m->ctx->device);
+  if (YK_STORE_CHECK) {
+    sc_register(dets, (size_t)batch * max_det * 6 * sizeof(float));
+    sc_register(counts, (size_t)batch * sizeof(int));
+    sc_register(keep, (size_t)batch * max_det * sizeof(int));
+  }
   return launch_nms(m, batch, iou, max_det, dets ? dets : m->dets, counts ? counts : m->counts, (hipStream_t)stream,
                     keep);
 }

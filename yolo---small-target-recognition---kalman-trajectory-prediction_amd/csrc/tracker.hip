@@ -389,41 +389,55 @@ __device__ __forceinline__ void ph_push(Slot& s, double a, double b, bool f32) {
   s.ph32[p] = f32 ? 1 : 0;
 }
 
-// np.add.reduce of a 1-D contiguous array of n <= 16: identity 0 + numpy's pairwise sum
-// (8 accumulators from n = 8), in float32 when f32 (verified against numpy 2.2 add.reduce)
-template <typename F>
-__device__ F np_sum_t(const double* a, int n) {
-  F res;
-  if (n < 8) {
-    res = F(0);
-    for (int i = 0; i < n; ++i) res = res + (F)a[i];
-  } else {
+// np.add.reduce of a 1-D contiguous array a[0..n), n <= NMAX: identity 0 + numpy's pairwise sum
+// (8 accumulators from n = 8), in float32 when F = float (verified against numpy 2.2 add.reduce).
+// Every loop runs to the static bound NMAX with the n-dependent part as a predicate, so after
+// unrolling no private array is indexed by a run-time value (no scratch).
+template <typename F, int NMAX>
+__device__ __forceinline__ F np_sum_t(const double (&a)[NMAX], int n) {
+  F res = F(0);
+  if (NMAX < 8 || n < 8) {
+#pragma unroll
+    for (int i = 0; i < (NMAX < 8 ? NMAX : 7); ++i)
+      if (i < n) res = res + (F)a[i];
+  } else if constexpr (NMAX >= 8) {
     F r[8];
+#pragma unroll
     for (int j = 0; j < 8; ++j) r[j] = (F)a[j];
-    int i = 8;
-    for (; i < n - (n % 8); i += 8)
-      for (int j = 0; j < 8; ++j) r[j] = r[j] + (F)a[i + j];
+    const int nb = n - (n % 8);  // end of the 8-wide blocks
+#pragma unroll
+    for (int i = 8; i + 8 <= NMAX; i += 8)
+      if (i < nb) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) r[j] = r[j] + (F)a[i + j];
+      }
     res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
-    for (; i < n; ++i) res = res + (F)a[i];
+#pragma unroll
+    for (int i = 8; i < NMAX; ++i)
+      if (i >= nb && i < n) res = res + (F)a[i];
   }
   return F(0) + res;
 }
 
 // np.mean / np.var of a python list of numpy scalars / python floats (np.asarray dtype rule)
-__device__ Num np_mean_list(const Num* a, int n) {
+template <int NMAX>
+__device__ __forceinline__ Num np_mean_list(const Num (&a)[NMAX], int n) {
   bool f32 = true;
-  double v[10];
-  for (int i = 0; i < n; ++i) {
-    f32 = f32 && a[i].k == K32;
+  double v[NMAX];
+#pragma unroll
+  for (int i = 0; i < NMAX; ++i) {
+    if (i < n) f32 = f32 && a[i].k == K32;
     v[i] = a[i].v;
   }
   if (f32) return Num{(double)(np_sum_t<float>(v, n) / (float)n), K32};
   return Num{np_sum_t<double>(v, n) / (double)n, K64};
 }
-__device__ Num np_var_list(const Num* a, int n) {
+template <int NMAX>
+__device__ __forceinline__ Num np_var_list(const Num (&a)[NMAX], int n) {
   const Num m = np_mean_list(a, n);
-  double d[10];
-  for (int i = 0; i < n; ++i) {
+  double d[NMAX];
+#pragma unroll
+  for (int i = 0; i < NMAX; ++i) {
     if (m.k == K32) {
       const float x = (float)a[i].v - (float)m.v;
       d[i] = (double)(x * x);
@@ -485,9 +499,10 @@ __device__ Num cmc_consistency(const Slot& s) {
   const int n = s.ms_len;
   if (n < 3) return Num{0.0, KPY};
   Num sc[10];
-  for (int k = 0; k < n; ++k) {
-    const int i = ring_at<10>(s.ms_head, k);
-    sc[k] = Num{s.ms[i], (int)s.mk[i]};
+#pragma unroll
+  for (int k = 0; k < 10; ++k) {
+    const int i = ring_at<10>(s.ms_head, k < n ? k : 0);
+    sc[k] = k < n ? Num{s.ms[i], (int)s.mk[i]} : Num{0.0, KPY};
   }
   const Num m = np_mean_list(sc, n);
   if (!(m.v > 0.0)) return Num{1.0, KPY};
@@ -501,33 +516,39 @@ __device__ Num cmc_consistency(const Slot& s) {
 // _should_reset_kalman (:174-214) with the three detectors (:86-157).  val / why: the
 // reasons' values and bits (1 position jump, 2 velocity change, 4 size change).
 template <typename DT>
-__device__ __noinline__ bool cmc_decide(Slot& s, const DT* b, double* val, int& why, Num& conf) {
+__device__ __forceinline__ bool cmc_decide(Slot& s, const DT* b, double* val, int& why, Num& conf) {
   why = 0;
   const int since = s.age - s.last_reset;
   if (since < 15) return false;  // reset cooldown
   constexpr bool c32 = sizeof(DT) == 4;
   const DT cxd = (b[0] + b[2]) / DT(2), cyd = (b[1] + b[3]) / DT(2);
   const double cx = (double)cxd, cy = (double)cyd;
-  Num fac[3];
-  int nf = 0;
+  Num f1{0.0, KPY}, f2{0.0, KPY}, f3{0.0, KPY};  // the reasons' confidence factors, appended in order
+  bool b1 = false, b2 = false, b3 = false;
   // 1. position jump: the centre against the mean of the last <= 3 history entries
   if (s.ph_len >= 2) {
     const int m = s.ph_len < 3 ? s.ph_len : 3;
     int id[3];
     bool all32 = true;
-    for (int k = 0; k < m; ++k) {
-      id[k] = ring_at<8>(s.ph_head, s.ph_len - m + k);
-      all32 = all32 && s.ph32[id[k]];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      id[k] = ring_at<8>(s.ph_head, k < m ? s.ph_len - m + k : s.ph_len - 1);
+      if (k < m) all32 = all32 && s.ph32[id[k]];
     }
     double avg[2];
+#pragma unroll
     for (int j = 0; j < 2; ++j) {  // np.mean(axis=0): rows accumulated in order
       if (all32) {
         float acc = (float)s.ph[id[0]][j];
-        for (int k = 1; k < m; ++k) acc = acc + (float)s.ph[id[k]][j];
+#pragma unroll
+        for (int k = 1; k < 3; ++k)
+          if (k < m) acc = acc + (float)s.ph[id[k]][j];
         avg[j] = (double)(acc / (float)m);
       } else {
         double acc = s.ph[id[0]][j];
-        for (int k = 1; k < m; ++k) acc = acc + s.ph[id[k]][j];
+#pragma unroll
+        for (int k = 1; k < 3; ++k)
+          if (k < m) acc = acc + s.ph[id[k]][j];
         avg[j] = acc / (double)m;
       }
     }
@@ -540,7 +561,8 @@ __device__ __noinline__ bool cmc_decide(Slot& s, const DT* b, double* val, int& 
     if (gt_c(dist, 40.0)) {
       why |= 1;
       val[0] = dist.v;
-      fac[nf++] = pymin_c(div_c(dist, 40.0), 2.0);
+      f1 = pymin_c(div_c(dist, 40.0), 2.0);
+      b1 = true;
     }
   }
   // 2. velocity change: the newest step length against the mean of the two before it
@@ -567,7 +589,8 @@ __device__ __noinline__ bool cmc_decide(Slot& s, const DT* b, double* val, int& 
     if (gt_c(ch, 60.0)) {
       why |= 2;
       val[1] = ch.v;
-      fac[nf++] = pymin_c(div_c(ch, 60.0), 2.0);
+      f2 = pymin_c(div_c(ch, 60.0), 2.0);
+      b2 = true;
     }
   }
   // 3. size change against the previous detection box (the detection's dtype throughout)
@@ -584,10 +607,14 @@ __device__ __noinline__ bool cmc_decide(Slot& s, const DT* b, double* val, int& 
     if (gt_c(rn, 0.3)) {
       why |= 4;
       val[2] = rn.v;
-      fac[nf++] = div_c(rn, 0.3);
+      f3 = div_c(rn, 0.3);
+      b3 = true;
     }
   }
+  const int nf = (int)b1 + (int)b2 + (int)b3;
   if (nf == 0) return false;
+  // the list [f_i for i in 1..3 if b_i], by selects (static indices)
+  const Num fac[3] = {b1 ? f1 : (b2 ? f2 : f3), b1 ? (b2 ? f2 : f3) : f3, f3};
   conf = np_mean_list(fac, nf);
   const Num cons = cmc_consistency(s);
   s.consistency = cons.v;
@@ -2216,7 +2243,7 @@ __global__ void track_op_kernel(Dev g, int s, int pos, int op, int arg, const do
     case YK_OP_UPDATE: {
       DT b[4];
       for (int k = 0; k < 4; ++k) b[k] = (DT)in_box[k];
-      double st[3 * VS];
+      __shared__ double st[3 * VS];  // (one thread; LDS rather than a scratch array)
       stage_chrono(sl, st);
       double val[3] = {0.0, 0.0, 0.0};
       int why = 0;

@@ -39,6 +39,15 @@ the tracker consumes the detections in frame order.  The detector's ~90 launches
 bound by their own latency, not by the chip (op time is nearly flat in the batch), and the
 parallel branches inside one captured graph execute one after the other, so a second
 independent graph on another stream is what fills the idle CUs (tools/inflight.py: 1.45x).
+
+``frames_per_forward=T`` > 1 (temporal batching; forwards in flight, no motion detector) makes
+one forward of T consecutive steps' frames: run() t uploads step t's S frames into sub-batch
+t % T of the forward's frame buffer, and the T-th run() launches one batch-(T S) forward and then
+the T tracker steps in frame order.  Detections of one image do not depend on the other images
+of the batch (same kernels, same plan), and the tracker still sees every stream's frames in
+order, so the results are the T = 1 pipeline's; a step's tracker output exists once its forward
+has been launched (its T-th run(), or flush()).  Measured: fp32 +4 %, bf16 +18 % at T = 2
+(gpurun_out/r6a, BASELINE config 3).
 """
 from __future__ import annotations
 
@@ -56,30 +65,46 @@ class StreamPipeline:
                  dtype: str = "fp32", weights=None, seed: int = 0, conf: float = 0.25, iou: float = 0.7,
                  max_det: int = 300, max_lost_frames: int = 150, min_hits: int = 1, iou_threshold: float = 0.1,
                  max_tracks: int = 512, device: int = 0, pipelined: bool = False, imgsz=640, inflight: int = 1,
-                 tracker_policy: int = 0, motion_method: str | None = None):
+                 tracker_policy: int = 0, motion_method: str | None = None, frames_per_forward: int = 1):
         if conf < 0.1:
             raise ValueError("conf < 0.1 would need the driver's score > 0.1 filter on the device path")
         self.S, self.device = int(n_streams), int(device)
+        self.T = int(frames_per_forward)
+        if not 1 <= self.T <= 8:
+            raise ValueError("frames_per_forward must be in [1, 8]")
+        if self.T > 1 and (int(inflight) < 2 or not pipelined or motion_method is not None):
+            raise ValueError("frames_per_forward > 1 needs inflight > 1 (pipelined) and no motion detector")
         self.conf, self.iou, self.max_det = float(conf), float(iou), int(max_det)
         ar = A.parse_arch(A.load_model_dict(model_cfg))
         sd = weights if weights is not None else Wt.synthetic_state_dict(ar, seed)
-        self.prog = M.Program(ar, sd, frame_hw[0], frame_hw[1], imgsz, self.S, dtype, self.max_det)
+        self.prog = M.Program(ar, sd, frame_hw[0], frame_hw[1], imgsz, self.T * self.S, dtype, self.max_det)
         self.model = M.DeviceModel(self.prog, self.device)
         self.tracker = T.MultiStreamTracker(self.S, max_lost_frames, min_hits, iou_threshold, max_tracks,
                                             self.max_det, self.device,
                                             policy=tracker_policy)
         dev = torch.device("cuda", self.device)
-        self.frames = torch.zeros((self.S, frame_hw[0], frame_hw[1], 3), dtype=torch.uint8, device=dev)
+        BF = self.T * self.S  # images per forward
+        # slot 0's frame buffer; `frames` is its first step's S images (the capture / autotune input)
+        self.forward_frames = torch.zeros((BF, frame_hw[0], frame_hw[1], 3), dtype=torch.uint8, device=dev)
+        self.frames = self.forward_frames[:self.S]
         # motion windows (see the header): with the motion detector on a pipelined tracker stream
-        self._windowed = motion_method is not None and bool(pipelined)
+        # (YK_MOTION_OVERLAP=1, diagnostics only: the round-4 schedule, motion kernels on the tracker
+        # stream beside the forwards -- tools/gmd_step_diff.py --overlap)
+        self._windowed = motion_method is not None and bool(pipelined) and \
+            __import__("os").environ.get("YK_MOTION_OVERLAP") != "1"
         # detection buffers: 2 D when the tracker runs on its own stream, so the forward of step
         # t + D does not wait for the tracker step of step t (HBM-resident rate +6.6 % fp32, +11.5 %
         # bf16, profiles/r05_inflight_lanes_sweep.txt), and with motion windows the next wave's
         # forwards do not wait for this wave's tracker steps; D (at least 2) otherwise
         self.nb = max(2, int(inflight)) * (2 if pipelined else 1)
-        self._dets = torch.zeros((self.nb, self.S, self.max_det, 6), dtype=torch.float32, device=dev)
-        self._counts = torch.zeros((self.nb, self.S), dtype=torch.int32, device=dev)
+        self._dets = torch.zeros((self.nb, BF, self.max_det, 6), dtype=torch.float32, device=dev)
+        self._counts = torch.zeros((self.nb, BF), dtype=torch.int32, device=dev)
         self._k = 0  # detection buffer the next step writes
+        self._j = 0  # (frames_per_forward > 1) steps uploaded into the next forward's frame buffer
+        self._last = (0, 0)  # (detection buffer, sub-batch) of the most recent tracker step
+        self._hook_j = 0  # sub-batch of the step the step hook is called for
+        self._dl_t = {}  # (frames_per_forward > 1) download_async requests by sub-batch, issued after its tracker step
+        self._n_sub = self.T  # sub-batches the next step() tracks (fewer in a partial flush)
         self.pipelined = bool(pipelined)
         # default stream priorities: a high-priority tracker / motion stream halved the bf16 line
         # (12,301 -> 5,974 frames/s, profiles/r04_cmc_ab.txt).  The motion detector stays on the
@@ -106,7 +131,7 @@ class StreamPipeline:
         # profiles/r05_inflight_lanes_sweep.txt; a 2 D ring made the copies wait, -15 %)
         self._ring = self.D > 1 and motion_method is None
         nf = 2 * self.nb if self._ring else self.D
-        self.frame_slots = [self.frames] + [torch.zeros_like(self.frames) for _ in range(nf - 1)]
+        self.frame_slots = [self.forward_frames] + [torch.zeros_like(self.forward_frames) for _ in range(nf - 1)]
         self._ev_fread = [torch.cuda.Event() for _ in range(nf)] if self._ring else []  # its forward
         self._fread_pending = [False] * nf
         self._kf = 0  # (ring) frame buffer of the next step
@@ -141,7 +166,7 @@ class StreamPipeline:
         self._stage = [torch.empty_like(self.frames) for _ in range(self.n_stage)]
         self._ev_stage_read = [torch.cuda.Event() for _ in range(self.n_stage)]  # slot stream's copy out of it
         self._stage_read_pending = [False] * self.n_stage
-        self._ev_copy = [torch.cuda.Event() for _ in range(nf if self._ring else self.n_stage)]
+        self._ev_copy = [torch.cuda.Event() for _ in range(nf * self.T if self._ring else self.n_stage)]
         self._n_stage = 0
         self._prefetched = __import__("collections").deque()  # (data_ptr of the host frames, staging index), one per upcoming step
         self._ev_window = None  # end of the last motion window (the next wave's forwards wait for it)
@@ -149,14 +174,21 @@ class StreamPipeline:
         self._dl = {}  # download_async requests of the current wave's steps, issued in its window
         self._motion_out = None  # per detection buffer: its step's yk_motion[S] (motion windows)
 
+    def step_outputs(self, k: int, j: int | None = None):
+        """(detections [S, max_det, 6], counts [S]) of detection buffer k's sub-batch j (the step
+        the step hook is being called for when j is None)."""
+        j = self._hook_j if j is None else j
+        S = self.S
+        return self._dets[k][j * S:(j + 1) * S], self._counts[k][j * S:(j + 1) * S]
+
     @property
     def dets(self) -> torch.Tensor:
-        """Detections [S, max_det, 6] of the most recent step."""
-        return self._dets[(self._k - 1) % self.nb]
+        """Detections [S, max_det, 6] of the most recent tracker step."""
+        return self.step_outputs(*self._last)[0]
 
     @property
     def counts(self) -> torch.Tensor:
-        return self._counts[(self._k - 1) % self.nb]
+        return self.step_outputs(*self._last)[1]
 
     def set_schedule(self, groups: int, lanes: int):
         for m in self.models:
@@ -179,11 +211,13 @@ class StreamPipeline:
     def capture(self, tune: bool = True):
         """Autotune the conv kernels for this batch (on the current frames), then build and warm
         the detector's native hipGraph(s); later steps replay them."""
+        for j in range(1, self.T):  # every sub-batch of the forward holds the current frames
+            self.forward_frames[j * self.S:(j + 1) * self.S].copy_(self.frames)
         if tune:
-            self.model.autotune(self.frames, self.conf)
+            self.model.autotune(self.forward_frames, self.conf)
         self.sync_plan()
         for fs in self.frame_slots[1:]:
-            fs.copy_(self.frames)
+            fs.copy_(self.forward_frames)
         self.graph = True
         # one graph per (frame buffer, detection buffer) pair the steps use, in step order from the
         # current step: the ring's frame index and the detection buffer index advance together
@@ -225,22 +259,34 @@ class StreamPipeline:
         if self.pipelined:
             self._ev_det[k].record(cur)
             self.trk_stream.wait_event(self._ev_det[k])
-            with torch.cuda.stream(self.trk_stream):
-                self._track(k, s)
+            for j in range(self._n_sub):  # the forward's steps, in frame order
+                with torch.cuda.stream(self.trk_stream):
+                    self._track(k, s, j)
+                self._after_track(k, j, cur)
             self._ev_trk[k].record(self.trk_stream)
             self._trk_pending[k] = True
         else:
             self._track(k, s)
+            self._after_track(k, 0, cur)
+        self._k = (k + 1) % self.nb
+
+    def _after_track(self, k: int, j: int, cur):
+        """After the tracker step of detection buffer k's sub-batch j: the step hook and (T > 1)
+        a download_async request of that step."""
+        self._last = (k, j)
         if self.step_hook is not None:
             # harness hook (tests/recorders): enqueue work after this step's launches on the
             # detector stream (reads of detection buffer k) and the tracker stream (results)
+            self._hook_j = j
             self.step_hook(self, k, cur, self.trk_stream if self.pipelined else cur)
-        self._k = (k + 1) % self.nb
+        req = self._dl_t.pop(j, None)
+        if req is not None:
+            self.tracker.download_async(*req, stream=self.trk_stream.cuda_stream)
 
-    def _track(self, k: int, s: int):
-        """Tracker step of detection buffer k (frames of slot s) on the current stream."""
+    def _track(self, k: int, s: int, j: int = 0):
+        """Tracker step of detection buffer k's sub-batch j (frames of slot s) on the current stream."""
         if self.gmd is None:
-            self.tracker.step_device(self._dets[k], self._counts[k])
+            self.tracker.step_device(*self.step_outputs(k, j))
             return
         self.gmd.detect_device(self.frame_slots[s])
         if self.pipelined:
@@ -283,10 +329,19 @@ class StreamPipeline:
         self._wave = []
 
     def flush(self):
-        """Enqueue the motion window of a partial wave (motion windows only; a no-op otherwise):
-        after it every run() so far has its tracker step enqueued."""
+        """Enqueue what run() has held back, so that after it every run() so far has its tracker
+        step enqueued: the motion window of a partial wave, or (frames_per_forward > 1) the
+        forward of a partly filled frame buffer.  A partial forward runs the whole batch (the
+        same graph; the sub-batches not refilled hold older frames) and steps the tracker on the
+        filled sub-batches only.  A no-op otherwise."""
         if self._windowed and self._wave:
             self._run_window()
+        if self.T > 1 and self._j:
+            if self._prefetched:
+                raise ValueError("flush(): prefetched frames wait for steps not yet run")
+            self._n_sub, self._j = self._j, 0
+            self.step()
+            self._n_sub = self.T
 
     def sync(self):
         """Wait for every launched step (detector and tracker streams)."""
@@ -313,7 +368,7 @@ class StreamPipeline:
         st = self._stream(s)
         cur = torch.cuda.current_stream(self.device)
         if self._ring:
-            f = self._kf
+            f, j = self._kf, self._j
             if self._prefetched:  # uploaded straight into this step's frame buffer
                 ptr, i = self._prefetched[0]
                 if frames.data_ptr() != ptr:
@@ -329,13 +384,22 @@ class StreamPipeline:
                     st.wait_event(self._ev_fread[f])
                     self._fread_pending[f] = False
                 with torch.cuda.stream(st):
-                    self._upload(self.frame_slots[f], frames)
+                    self._upload(self.frame_slots[f][j * self.S:(j + 1) * self.S], frames)
+            if self.T > 1:
+                self._j = j + 1
+                if self._j < self.T:  # the forward waits for its last step's frames
+                    if next_frames is not None and next_frames.numel() * next_frames.element_size() >= self.PULL_BYTES:
+                        self.prefetch(next_frames)
+                    return
+                self._j = 0
         elif self._prefetched:
             ptr, i = self._prefetched[0]
             if frames.data_ptr() != ptr:
                 raise ValueError("run(): other frames were prefetched for this step (next_frames / prefetch)")
             self._prefetched.popleft()
             st.wait_event(self._ev_copy[i])
+            if self._ev_window is not None:  # the staging -> slot copy is a kernel: not beside a motion window
+                st.wait_event(self._ev_window)
             if self._gmd_pending[s]:  # the motion detector (tracker stream) still reads this slot's frames
                 st.wait_event(self._ev_gmd[s])
                 self._gmd_pending[s] = False
@@ -351,6 +415,8 @@ class StreamPipeline:
             if self._gmd_pending[s]:  # the motion detector (tracker stream) still reads this slot's frames
                 st.wait_event(self._ev_gmd[s])
                 self._gmd_pending[s] = False
+            if self._ev_window is not None:  # (device copies and pull kernels: not beside a motion window)
+                st.wait_event(self._ev_window)
             with torch.cuda.stream(st):
                 self._upload(self.frame_slots[s], frames)
         self.step()
@@ -376,7 +442,8 @@ class StreamPipeline:
             nf = len(self.frame_slots)
             if len(self._prefetched) >= 4:
                 raise ValueError("prefetch: at most 4 steps ahead")
-            f = (self._kf + len(self._prefetched)) % nf  # that step's frame buffer
+            q = self._kf * self.T + self._j + len(self._prefetched)  # that step's (frame buffer, sub-batch)
+            f, j = (q // self.T) % nf, q % self.T
             # its previous reader: the forward of 4 D steps earlier (done in steady state; waiting for
             # it here would hold the host inside the copy call)
             if self._fread_pending[f] and not self._ev_fread[f].query():
@@ -386,9 +453,9 @@ class StreamPipeline:
                 cs.wait_stream(torch.cuda.current_stream(self.device))
                 frames.record_stream(cs)
             with torch.cuda.stream(cs):
-                self._upload(self.frame_slots[f], frames)
-            self._ev_copy[f].record(cs)
-            self._prefetched.append((frames.data_ptr(), f))
+                self._upload(self.frame_slots[f][j * self.S:(j + 1) * self.S], frames)
+            self._ev_copy[f * self.T + j].record(cs)
+            self._prefetched.append((frames.data_ptr(), f * self.T + j))
             return
         if len(self._prefetched) >= self.n_stage - self.D:
             raise ValueError(f"prefetch: at most {self.n_stage - self.D} steps ahead")
@@ -430,6 +497,9 @@ class StreamPipeline:
         the copy is issued right after that step's tracker step, inside its wave's window."""
         if self._windowed and self._wave:  # this step's tracker step runs in its wave's window
             self._dl[self._wave[-1]] = (rows, counts, stats, rows_per_stream)
+            return
+        if self.T > 1 and self._j:  # this step's forward (and tracker step) has not been launched yet
+            self._dl_t[self._j - 1] = (rows, counts, stats, rows_per_stream)
             return
         st = self.trk_stream if self.pipelined else torch.cuda.current_stream(self.device)
         self.tracker.download_async(rows, counts, stats, rows_per_stream, stream=st.cuda_stream)
