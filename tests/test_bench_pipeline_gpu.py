@@ -77,6 +77,7 @@ def build_chain(seeds, n_frames, targets, model="yolov8s-small.yaml"):
                        for s in range(S)])
     return {"frames": frames, "dets": dets, "tracks": tracks, "nms_score_ties": ties, "near": near,
             "tie_frames": sum(tr.tie_frames for tr in trks),
+            "tie_divergent_frames": sum(tr.tie_divergent_frames for tr in trks),
             "terminated": sum(tr.stats["total_tracks_terminated"] for tr in trks),
             "live": [len(tr.trackers) for tr in trks], "S": S, "F": F, "model": model}
 
@@ -206,8 +207,11 @@ def check_chain(chain, plan_path, tbatch=1, parity_record=False):
                     spread = lost_conf_spread(tr, max(dv, 1e-7))
                     assert r["status"] == "predicted" and spread >= 0.5 * dc, \
                         (t, s, r["track_id"], o["confidence"], r["confidence"], dv, spread)
+                    sp = [float(np.hypot(*v)) for v in tr.velocity_history]
                     ill_conf.append({"frame": t, "stream": s, "track": str(r["track_id"]), "dev": dc,
-                                     "velocity_history_dev": dv, "spread": spread})
+                                     "velocity_history_dev": dv, "spread": spread,
+                                     "mean_speed": float(np.mean(sp)) if sp else 0.0,
+                                     "min_speed": float(np.min(sp)) if sp else 0.0})
                 else:
                     conf_dev_well = max(conf_dev_well, dc)
                 n_tracks += 1
@@ -221,7 +225,17 @@ def check_chain(chain, plan_path, tbatch=1, parity_record=False):
                "oracle_near_tie_boxes": int(sum(len(b) for fr in chain["near"] for b in fr)),
                "max_box_rel_dev": box_rel, "max_confidence_abs_dev": conf_dev,
                "max_confidence_abs_dev_well_conditioned": conf_dev_well, "ill_conditioned_confidences": len(ill_conf),
-               "oracle_tie_frames": chain["tie_frames"], "nms_early_exit": _run_gpu.nms,
+               # of those: the velocity history's mean speed below 1 px / frame, where the direction
+               # statistics' arctan2 (kf.py:165-182) turns ~1e-6 velocity differences into large angle changes
+               "ill_conditioned_near_zero_speed": sum(1 for c in ill_conf if c["mean_speed"] < 1.0),
+               "ill_conditioned_mean_speed_max": max((c["mean_speed"] for c in ill_conf), default=0.0),
+               "ill_conditioned_spread_from": "oracle RefTrack.get_lost_prediction (kf.py:205-247, 319-333) on "
+                                              "perturbed copies of the oracle track's own velocity history",
+               "oracle_tie_frames": chain["tie_frames"],
+               "oracle_tie_frames_stable_vs_default_argsort_differ": chain["tie_divergent_frames"],
+               "compared_chain_tie_frames": sum(tr.tie_frames for tr in ctrk),
+               "compared_chain_stable_vs_default_argsort_differ": sum(tr.tie_divergent_frames for tr in ctrk),
+               "nms_early_exit": _run_gpu.nms,
                "nms_score_ties": chain["nms_score_ties"], "terminated": chain["terminated"]}
     print("BENCH_PIPELINE_FP32", json.dumps(summary))
     assert n_tracks == n_outputs  # every track output of every stream-frame compared

@@ -84,13 +84,21 @@ def main():
     ap.add_argument("--isolate", action="store_true", help="no forward overlaps the motion kernels")
     ap.add_argument("--private", action="store_true", help="motion reads a tracker-stream copy of the frames")
     ap.add_argument("--serial", action="store_true", help="repetitions run the serial pipeline too (baseline noise)")
+    ap.add_argument("--overlap", action="store_true",
+                    help="the round-4 schedule: motion kernels beside the forwards (YK_MOTION_OVERLAP=1, no windows)")
+    ap.add_argument("--beside", type=int, default=0,
+                    help="MiB: a host thread keeps device-to-device torch copies of this size running on a stream of "
+                         "its own during every run (no detector code beside the motion kernels: use with the serial "
+                         "pipeline, --serial)")
     a = ap.parse_args()
+    if a.overlap:
+        os.environ["YK_MOTION_OVERLAP"] = "1"
     S, F = 3, 20
     seqs = [camera_sequence(80 + s, F, h=512, w=640, whip_at=(7, 14), n_targets=12)[0] for s in range(S)]
     frames = torch.from_numpy(np.stack(seqs, 1)).cuda()
     nbytes = S * L.MOTION_DTYPE.itemsize
 
-    def run(pipelined, inflight):
+    def run(pipelined, inflight, churn=False):
         cls = pipeline.StreamPipeline
         if pipelined and a.isolate:
             cls = IsolatedMotionPipeline
@@ -130,9 +138,36 @@ def main():
         pipe.frames.copy_(frames[0])
         pipe.capture(tune=False)
         pipe.step_hook = hook
+        side = None
+        if a.beside and churn:
+            import threading
+
+            stop = threading.Event()
+            sbuf = [torch.empty(a.beside << 18, dtype=torch.float32, device="cuda") for _ in range(2)]
+            sst = torch.cuda.Stream()
+
+            def spin():
+                n = 0
+                while not stop.is_set():
+                    with torch.cuda.stream(sst):
+                        sbuf[n & 1].copy_(sbuf[(n + 1) & 1])
+                        sbuf[n & 1].add_(1.0)
+                    n += 1
+                    if n % 8 == 0:
+                        sst.synchronize()
+                spin.n = n
+
+            spin.n = 0
+            side = threading.Thread(target=spin)
+            side.start()
         for t in range(F):
             pipe.run(frames[t])
         pipe.sync()
+        if side is not None:
+            stop.set()
+            side.join()
+            torch.cuda.synchronize()
+            print(f"    beside: {spin.n} copy + add pairs of {a.beside} MiB ran on another stream", flush=True)
         info = np.zeros((S, 5), np.int32)  # diag builds (YK_GMD_DIAG 4 / 8): LK self-consistency counters
         L.check(L.lib().yk_gmc_info(pipe.gmd._h, L.ptr(info), L.current_stream(0)), "yk_gmc_info")
         if info[:, :2].any():
@@ -154,7 +189,7 @@ def main():
     ref, rcor, rnxt, rpyr, rder = run(False, 1)
     bad = 0
     for r in range(a.reps):
-        got, gcor, gnxt, gpyr, gder = run(False, 1) if a.serial else run(True, a.inflight)
+        got, gcor, gnxt, gpyr, gder = run(False, 1, True) if a.serial else run(True, a.inflight, True)
         for t in range(1, F):  # first step whose pyramid / derivative buffers differ (both written)
             bp = [int((rpyr[t, j] != gpyr[t, j]).sum()) for j in range(2)]
             bd = [int((rder[t, j] != gder[t, j]).sum()) for j in range(2)]
@@ -191,7 +226,12 @@ def main():
                 print(f"    {name:9s} serial {ref[t][name].tolist()}  pipelined {got[t][name].tolist()}", flush=True)
         else:
             print(f"rep {r}: identical", flush=True)
-    print(f"inflight={a.inflight}{' isolated' if a.isolate else ''}{' private' if a.private else ''}{' serial' if a.serial else ''}: {bad} of {a.reps} runs differ", flush=True)
+    print(f"inflight={a.inflight}{' isolated' if a.isolate else ''}{' private' if a.private else ''}{' serial' if a.serial else ''}"
+          f"{' overlap' if a.overlap else ''}: {bad} of {a.reps} runs differ", flush=True)
+    n = np.zeros(1, np.int64)
+    L.check(L.lib().yk_store_check_count(L.ptr(n)), "yk_store_check_count")
+    print("detector stores outside the detector's allocations:",
+          "n/a (product library)" if n[0] < 0 else int(n[0]), flush=True)
 
 
 if __name__ == "__main__":

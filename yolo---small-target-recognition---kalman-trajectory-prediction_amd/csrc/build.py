@@ -32,6 +32,7 @@ ARCH = os.environ.get("YK_OFFLOAD_ARCH", "gfx950")
 # (source, extra flags).  The tracker must not contract a*b+c into FMA: it reproduces
 # numpy's separately rounded float64 arithmetic (see tracker.hip header).
 SOURCES = [
+    ("yk_host.cpp", []),
     ("yk_capi.cpp", []),
     ("program.cpp", []),
     ("tracker.hip", ["-ffp-contract=off"]),
@@ -39,7 +40,7 @@ SOURCES = [
     ("bytetrack.hip", ["-ffp-contract=off"]),
     ("gmd.hip", ["-ffp-contract=off"]),
 ]
-HEADERS = ["yk_internal.h", os.path.join("..", "..", "include", "yk.h"), os.path.join("..", "..", "include", "yk_diag.h")]
+HEADERS = ["yk_internal.h", "yk_host.h", os.path.join("..", "..", "include", "yk.h"), os.path.join("..", "..", "include", "yk_diag.h")]
 
 
 def _hipcc() -> str:

@@ -53,6 +53,17 @@
 #ifndef YK_FAST_WPE  // (a diagnostic build may set it: YK_DEFINES=-DYK_FAST_WPE=3)
 #define YK_FAST_WPE ((YK_DIAG & 128) ? 2 : 1)
 #endif
+// The table-kernel tiles of at most YK_WPE_TILE fragments (NNT x NPT) with two K steps of loads in
+// flight are compiled for 3 waves per SIMD (<= 168 registers) -- except the 12-fragment tile
+// without a K split, which spills there, and FP8 -- the others as YK_FAST_WPE.  12 (round 6): the
+// dominant <F32S, 3, 4, 4, 2> 200 -> 166 registers, 22.0 -> 21.0 us per launch, fp32 line +1 %
+// (A/B x3, gpurun_out/r6d); 0 restores the round-5 allocation
+#ifndef YK_WPE_TILE
+#define YK_WPE_TILE 12
+#endif
+constexpr int fast_wpe(int nnt, int npt, int kw, int skd, bool fp8) {
+  return !fp8 && nnt * npt <= YK_WPE_TILE && skd == 2 && !(kw == 1 && nnt * npt >= 12) ? 3 : YK_FAST_WPE;
+}
 // YK_STORE_CHECK=1 (diagnostic build): every detector-kernel store -- the conv
 // epilogues (store4), detect_kernel's candidate rows, nms_kernel's outputs and global scratch --
 // checks that its bytes lie inside one of the detector's own allocations (every model's arena,
@@ -450,7 +461,6 @@ __device__ __forceinline__ View pick_view(const View& v0, const View& v1, bool s
 }
 
 // ---------------------------------------------------------------- implicit-GEMM conv
-constexpr int kTabMax = 1024;
 constexpr int kTsCap = 65536;  // YK_FAST_TS diagnostics: workgroups with timestamps
 
 // Table entry of K chunk q computed arithmetically (model.py Program.pack: tap, ch =
@@ -1332,7 +1342,7 @@ __device__ __forceinline__ void conv_fast_body(const FastArgs& a, int2 blk, int 
 // run two waves per SIMD without spills, but the headline does not move (5,279 vs 5,264 frames/s:
 // those kernels are bound by the split VALU work, not by occupancy); 3 spills (-32 %).
 template <class Tr, int NNT, int NPT, int KW, int SKD>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(YK_FAST_WPE))) conv_fast_kernel(FastArgs a) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(fast_wpe(NNT, NPT, KW, SKD, Tr::kScaled)))) conv_fast_kernel(FastArgs a) {
   const int2 blk = xcd_block(a.xcd);
   const int nt0 = blk.y * NNT;
   const int rem = a.n_tiles - nt0;
@@ -2109,7 +2119,6 @@ __global__ void __launch_bounds__(256) letterbox_kernel(LboxArgs a, int B) {
 }
 
 // ---------------------------------------------------------------- first conv from uint8 frames
-constexpr int kInputCoutMax = 64;
 
 struct InputArgs {
   const unsigned char* frames;  // [B][fh][fw][3] BGR
@@ -4806,41 +4815,7 @@ extern "C" {
 int yk_model_create(yk_ctx* ctx, const yk_model_desc* desc, const void* host_blob, int64_t blob_bytes,
                     yk_model** out) {
   YK_CHECK_ARG(ctx && desc && host_blob && out, "yk_model_create: NULL argument");
-  YK_CHECK_ARG(desc->n_ops > 0 && desc->ops && desc->n_bufs > 0 && desc->buf_elems, "yk_model_create: empty program");
-  YK_CHECK_ARG(desc->max_batch >= 1 && desc->n_anchors > 0 && desc->max_det >= 1, "yk_model_create: bad sizes");
-  YK_CHECK_ARG(desc->nc == 1, "yk_model_create: only single-class detection heads are supported");
-  YK_CHECK_ARG(desc->max_det <= 2048, "yk_model_create: max_det must be <= 2048");
-  YK_CHECK_ARG(desc->act_dtype == YK_ACT_BF16 || desc->act_dtype == YK_ACT_F32 || desc->act_dtype == YK_ACT_FP8 ||
-                   desc->act_dtype == YK_ACT_F16,
-               "yk_model_create: bad act dtype");
-  for (int i = 0; i < desc->n_ops; ++i) {
-    const yk_op& op = desc->ops[i];
-    YK_CHECK_ARG(op.kind >= YK_K_CONV_INPUT && op.kind <= YK_K_DETECT, "yk_model_create: bad op kind");
-    YK_CHECK_ARG(op.dst.buf >= 0 && op.dst.buf < desc->n_bufs, "yk_model_create: dst buffer index out of range");
-    for (int s = 0; s < op.n_src; ++s)
-      YK_CHECK_ARG(op.src[s].buf >= 0 && op.src[s].buf < desc->n_bufs, "yk_model_create: src buffer out of range");
-    YK_CHECK_ARG(op.n_src >= (op.kind == YK_K_CONV_INPUT ? 0 : 1) && op.n_src <= 2, "yk_model_create: n_src");
-    YK_CHECK_ARG(op.w_off >= 0 && op.w_off < blob_bytes && op.b_off >= 0 && op.b_off < blob_bytes,
-                 "yk_model_create: weight offsets outside the blob");
-    YK_CHECK_ARG(op.kind != YK_K_CONV || (op.cout % 4 == 0 && op.k_steps > 0 && op.n_tiles > 0),
-                 "yk_model_create: conv geometry");
-    YK_CHECK_ARG(op.kind != YK_K_CONV || op.ksize == 1 || op.ksize == 3, "yk_model_create: ksize must be 1 or 3");
-    YK_CHECK_ARG(op.kind != YK_K_CONV ||
-                     op.ksize * op.ksize * (op.src_ch[0] + (op.n_src > 1 ? op.src_ch[1] : 0)) / 8 <= kTabMax,
-                 "yk_model_create: conv input too wide (K-chunk table > 1024 entries)");
-    YK_CHECK_ARG(op.kind != YK_K_CONV_INPUT || (op.ksize == 3 && op.stride <= 2),
-                 "yk_model_create: the input conv must be 3x3 with stride <= 2");
-    YK_CHECK_ARG(op.kind != YK_K_CONV_INPUT || op.cout <= kInputCoutMax,
-                 "yk_model_create: the input conv must have <= 64 (padded) output channels");
-  }
-  YK_CHECK_ARG(desc->rs_mode >= 0 && desc->rs_mode <= 2, "yk_model_create: bad resize mode");
-  YK_CHECK_ARG(desc->rs_mode == 0 ||
-                   (desc->rs_w >= 1 && desc->rs_h >= 1 && desc->pad_left + desc->rs_w <= desc->in_w &&
-                    desc->pad_top + desc->rs_h <= desc->in_h && desc->rs_tab_off >= 0 &&
-                    desc->rs_tab_off + (int64_t)(2 * desc->rs_w + 2 * desc->rs_h) * 4 <= blob_bytes &&
-                    (desc->rs_mode != 2 || (2 * desc->rs_w <= desc->frame_w && 2 * desc->rs_h <= desc->frame_h))),
-               "yk_model_create: inconsistent LetterBox resize geometry");
-  YK_CHECK_ARG(desc->box_gain > 0.f, "yk_model_create: box_gain must be > 0");
+  if (const int rc = yk::validate_model_desc(desc, blob_bytes)) return rc;  // (yk_host.cpp, host only)
   yk::DeviceGuard guard(ctx->device);
   auto* m = new yk_model();
   m->ctx = ctx;

@@ -827,9 +827,12 @@ __global__ void __launch_bounds__(256) lk_kernel(Dev g) {
         // (dx, dy) as one packed int32 load, 0 outside the level.  Round 4 wrote `cond ? D[i] : z`
         // with a local short2 z: the compiler turned that into a select between &D[i] and the
         // address of a stack copy of z, i.e. FLAT loads through a private-aperture pointer (8 bytes
-        // of scratch) -- the one scratch user of the motion chain, and the only place its results
-        // depended on what ran beside it (LK end points of border windows differing from the
-        // serial run while forwards with spilling conv kernels ran concurrently).  No scratch now.
+        // of scratch).  Removing that scratch did NOT remove the run-to-run LK differences seen
+        // while other kernels ran beside this one ("The camera-motion path with
+        // forwards in flight": a wave re-reading the same J addresses within one launch got other
+        // bytes; round 6 found no detector store outside the detector's own allocations in that
+        // schedule, profiles/r06_lk_store_check_overlap.txt).  The cause is not known; the product
+        // never runs these kernels beside a forward (motion windows, pipeline.py).
         const int* Dw = (const int*)D;
         const int e00 = (iy0 && ix0) ? Dw[(long long)Y * cols + X] : 0;
         const int e01 = (iy0 && ix1) ? Dw[(long long)Y * cols + X + 1] : 0;

@@ -22,7 +22,7 @@
 #include <string>
 #include <vector>
 
-#include "yk_internal.h"
+#include "yk_host.h"
 
 namespace {
 
@@ -629,8 +629,8 @@ std::vector<int32_t> lb_table(const LbPlan& p) {
   t.insert(t.end(), p.yofs.begin(), p.yofs.end());
   const size_t nx = p.xw.size() / 2, ny = p.yw.size() / 2;
   std::vector<int32_t> x(nx), y(ny);
-  memcpy(x.data(), p.xw.data(), nx * 4);
-  memcpy(y.data(), p.yw.data(), ny * 4);
+  if (nx) memcpy(x.data(), p.xw.data(), nx * 4);
+  if (ny) memcpy(y.data(), p.yw.data(), ny * 4);
   t.insert(t.end(), x.begin(), x.end());
   t.insert(t.end(), y.begin(), y.end());
   return t;
@@ -812,6 +812,12 @@ int yk_program_build(const yk_weights* weights, char scale, int act_dtype, int f
   d.box_pad_y = lb.pad_y;
   d.box_gain = (float)lb.gain;
   d.rs_tab_off = rs_tab_off;
+  // a program yk_model_create would refuse (sizes beyond the kernels' limits, e.g. max_det > 2048)
+  // is refused here already, with the same message
+  if (const int rc = yk::validate_model_desc(&d, (int64_t)p->blob.size())) {
+    delete p;
+    return rc;
+  }
   *out = p;
   return YK_OK;
 }
@@ -827,17 +833,6 @@ int yk_program_get(const yk_program* p, const yk_model_desc** desc, const void**
 int yk_program_destroy(yk_program* p) {
   delete p;
   return YK_OK;
-}
-
-int yk_model_load_weights(yk_ctx* ctx, const yk_weights* weights, char scale, int act_dtype, int frame_h, int frame_w,
-                          int imgsz, int max_batch, yk_model** out) {
-  YK_CHECK_ARG(ctx && out, "yk_model_load_weights: NULL argument");
-  yk_program* p = nullptr;
-  int rc = yk_program_build(weights, scale, act_dtype, frame_h, frame_w, imgsz, max_batch, 300, &p);
-  if (rc != YK_OK) return rc;
-  rc = yk_model_create(ctx, &p->desc, p->blob.data(), (int64_t)p->blob.size(), out);
-  yk_program_destroy(p);
-  return rc;
 }
 
 }  // extern "C"

@@ -5,24 +5,11 @@
 
 #include <cstdlib>
 #include <cstring>
-#include <fstream>
 #include <vector>
 
 #include "yk_internal.h"
 
-namespace yk {
-namespace {
-thread_local std::string g_last_error;
-}
-void set_error(const std::string& msg) { g_last_error = msg; }
-void clear_error() { g_last_error.clear(); }
-}  // namespace yk
-
 extern "C" {
-
-int yk_abi_version(void) { return YK_ABI_VERSION; }
-
-const char* yk_last_error(void) { return yk::g_last_error.c_str(); }
 
 namespace {
 // Diagnostics (YK_SEGV_TRACE=1 at context creation): a SIGSEGV prints the native stack to stderr,
@@ -96,44 +83,18 @@ int yk_ctx_destroy(yk_ctx* ctx) {
   return YK_OK;
 }
 
-// Engine file (yk.h, yk_model_load): a program packed once by model.Program.export_engine.
+// Engine file (yk.h, yk_model_load): a program packed once by model.Program.export_engine, read
+// and validated on the host (yk_host.cpp read_engine) before anything touches the device.
 int yk_model_load(yk_ctx* ctx, const char* path, yk_model** out) {
   YK_CHECK_ARG(ctx && path && out, "yk_model_load: NULL argument");
-  std::ifstream f(path, std::ios::binary);
-  YK_CHECK_ARG(f.good(), std::string("yk_model_load: cannot open ") + path);
-  struct Head {
-    char magic[8];
-    int32_t version, sizeof_desc, sizeof_op, n_bufs, n_ops, plan_batch, n_plan, pad;
-    int64_t blob_bytes;
-  } h{};
-  f.read((char*)&h, sizeof h);
-  YK_CHECK_ARG(f.good() && std::memcmp(h.magic, "YKENGINE", 8) == 0, "yk_model_load: not a YKENGINE file");
-  YK_CHECK_ARG(h.version == 1, "yk_model_load: unsupported engine version");
-  YK_CHECK_ARG(h.sizeof_desc == (int32_t)sizeof(yk_model_desc) && h.sizeof_op == (int32_t)sizeof(yk_op),
-               "yk_model_load: engine written for another ABI (struct sizes differ)");
-  YK_CHECK_ARG(h.n_bufs > 0 && h.n_bufs < (1 << 16) && h.n_ops > 0 && h.n_ops < (1 << 16) && h.blob_bytes > 0 &&
-                   h.n_plan >= 0 && h.n_plan <= h.n_ops,
-               "yk_model_load: corrupt engine header");
-  yk_model_desc d{};
-  f.read((char*)&d, sizeof d);
-  std::vector<int64_t> bufs(h.n_bufs);
-  std::vector<yk_op> ops(h.n_ops);
-  std::vector<char> blob((size_t)h.blob_bytes);
-  std::vector<int32_t> plan((size_t)h.n_plan * 4);
-  f.read((char*)bufs.data(), (std::streamsize)(bufs.size() * sizeof(int64_t)));
-  f.read((char*)ops.data(), (std::streamsize)(ops.size() * sizeof(yk_op)));
-  f.read(blob.data(), (std::streamsize)blob.size());
-  if (h.n_plan) f.read((char*)plan.data(), (std::streamsize)(plan.size() * sizeof(int32_t)));
-  YK_CHECK_ARG(f.good(), "yk_model_load: truncated engine file");
-  YK_CHECK_ARG(d.n_bufs == h.n_bufs && d.n_ops == h.n_ops, "yk_model_load: header / descriptor mismatch");
-  d.buf_elems = bufs.data();
-  d.ops = ops.data();
+  yk::EngineImage e;
+  if (const int rc = yk::read_engine(path, e)) return rc;
   yk_model* m = nullptr;
-  const int rc = yk_model_create(ctx, &d, blob.data(), h.blob_bytes, &m);
+  const int rc = yk_model_create(ctx, &e.desc, e.blob.data(), (int64_t)e.blob.size(), &m);
   if (rc != YK_OK) return rc;
-  for (int32_t i = 0; i < h.n_plan; ++i) {
-    const int32_t* p = &plan[(size_t)i * 4];
-    const int r = yk_model_set_plan(m, p[0], h.plan_batch, p[1], p[2], p[3]);
+  for (size_t i = 0; i < e.plan.size() / 4; ++i) {
+    const int32_t* p = &e.plan[i * 4];
+    const int r = yk_model_set_plan(m, p[0], e.plan_batch, p[1], p[2], p[3]);
     if (r != YK_OK) {
       yk_model_destroy(m);
       return r;
@@ -141,6 +102,22 @@ int yk_model_load(yk_ctx* ctx, const char* path, yk_model** out) {
   }
   *out = m;
   return YK_OK;
+}
+
+// The program built by the library (program.cpp, host only), then the model on the device.
+int yk_model_load_weights(yk_ctx* ctx, const yk_weights* weights, char scale, int act_dtype, int frame_h, int frame_w,
+                          int imgsz, int max_batch, yk_model** out) {
+  YK_CHECK_ARG(ctx && out, "yk_model_load_weights: NULL argument");
+  yk_program* p = nullptr;
+  int rc = yk_program_build(weights, scale, act_dtype, frame_h, frame_w, imgsz, max_batch, 300, &p);
+  if (rc != YK_OK) return rc;
+  const yk_model_desc* d = nullptr;
+  const void* blob = nullptr;
+  int64_t bytes = 0;
+  rc = yk_program_get(p, &d, &blob, &bytes);
+  if (rc == YK_OK) rc = yk_model_create(ctx, d, blob, bytes, out);
+  yk_program_destroy(p);
+  return rc;
 }
 
 }  // extern "C"

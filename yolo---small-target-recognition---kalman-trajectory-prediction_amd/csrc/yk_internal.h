@@ -6,15 +6,13 @@
 #include <string>
 
 #include "../../include/yk.h"
+#include "yk_host.h"
 
 struct yk_ctx {
   int device;
 };
 
 namespace yk {
-
-void set_error(const std::string& msg);
-void clear_error();
 
 // Evaluate a HIP call; on failure record the message and return YK_ERR_HIP from the caller.
 #define YK_HIP(expr)                                                                   \
@@ -25,14 +23,6 @@ void clear_error();
                       __FILE__ + ":" + std::to_string(__LINE__) + ")");                \
       return YK_ERR_HIP;                                                               \
     }                                                                                  \
-  } while (0)
-
-#define YK_CHECK_ARG(cond, msg)      \
-  do {                               \
-    if (!(cond)) {                   \
-      ::yk::set_error(msg);          \
-      return YK_ERR_ARG;             \
-    }                                \
   } while (0)
 
 // Bind the calling thread to the handle's device for the duration of a call.
