@@ -65,10 +65,12 @@ TRACK_STEP_BYTES = 1216  # R+W of x (8 f64) and dense P (64 f64), z
 # targets and crossing targets churn IDs, so live tracks != targets (40 targets -> ~70-150 live).
 CONFIGS = {
     2: dict(S=1, H=512, W=640, imgsz=640, max_tracks=512, targets=12, dtype="bf16", secondary="", live_floor=16),
-    # tbatch (frames per stream per forward, --tbatch): 2 is +4 % at 100 steps but -1.3 % at the
-    # driver's 20 (the batch-16 forward's longer fill / drain, gpurun_out/r6a, r6b), so 1 here
+    # tbatch (frames per stream per forward, --tbatch) x inflight (forwards in flight) x prefetch depth,
+    # swept at the driver's 20 steps (gpurun_out/r6f, two runs each): fp32 T1 D4 4,914-4,938, T2 D3
+    # (prefetch 4) 5,131-5,183, T2 D2 5,035-5,044, T2 D4 4,839-4,874; bf16 T1 D4 11,090-11,104, T2 D3
+    # 12,384-12,527, T4 D2 11,644-11,662 frames/s
     3: dict(S=8, H=512, W=640, imgsz=640, max_tracks=512, targets=40, dtype="fp32", secondary="bf16,n:fp32", live_floor=64,
-            tbatch=1),
+            tbatch=2, inflight=3),
     4: dict(S=1, H=512, W=640, imgsz=640, max_tracks=512, targets=40, dtype="fp32", secondary="", live_floor=64),
     5: dict(S=8, H=1024, W=1280, imgsz=1280, max_tracks=2048, targets=96, dtype="fp8", secondary="bf16",
             live_floor=256),
@@ -122,17 +124,19 @@ def parse():
     ap.add_argument("--dump-ops", default="", help="write per-op device times (json) to this path")
     ap.add_argument("--no-prefetch", action="store_true",
                     help="upload each step's host frames on its slot stream instead of one step ahead on the copy stream")
-    ap.add_argument("--prefetch-depth", type=int, default=2,
+    ap.add_argument("--prefetch-depth", type=int, default=None,
                     help="how many steps ahead the host frames are uploaded (page-locked frames >= PULL_BYTES; "
-                         "2 measured +1.5-4.4 %% over 1 at fp32, profiles/r05_inflight_lanes_sweep.txt)")
+                         "default 2, 4 with --tbatch > 1: one forward's steps ahead; 2 measured +1.5-4.4 %% over 1 "
+                         "at fp32, profiles/r05_inflight_lanes_sweep.txt)")
     ap.add_argument("--io", default="both", choices=["both", "h2d", "d2h", "none", "stage-dev"],
                     help="diagnostics: which host copies the timed loop makes (default both: the metric's definition)")
     a = ap.parse_args()
     if a.inflight is None:
-        # 4 for every line: six forwards in flight lift the CMC lines (bf16 8,883 -> 10,115 frames/s)
-        # but the motion records then differ from the serial pipeline's in float rounding
-        # (profiles/r04_inflight_sweep.txt), so the CMC line is not measured there
-        a.inflight = 4
+        # the config's (config 3: 3 with two frames per forward), else 4: six forwards in flight lift
+        # the CMC lines (bf16 8,883 -> 10,115 frames/s) but the motion records then differ from the
+        # serial pipeline's in float rounding (profiles/r04_inflight_sweep.txt), so the CMC line is
+        # not measured there
+        a.inflight = 4 if a.gmd or a.no_pipeline else CONFIGS[a.config].get("inflight", 4)
     return a
 
 
@@ -464,7 +468,8 @@ def run_leg(a, P, cfg, dtype, frames, dev, local, rank, ws, headline):
         host = frames[t_first:t_first + n_host].clone() if t_first + n_host <= F else host.to(dev)
     host_ns = 0
     big = host[0].numel() >= pipe.PULL_BYTES or a.io == "stage-dev"
-    ahead = a.prefetch_depth if pipe.D > 1 and big and not a.no_prefetch else 0
+    depth = a.prefetch_depth if a.prefetch_depth is not None else (4 if tb > 1 else 2)
+    ahead = depth if pipe.D > 1 and big and not a.no_prefetch else 0
     for t in range(a.steps):
         h0 = time.perf_counter_ns()
         if h2d:  # the next steps' frames are uploaded while this step runs (decode-ahead driver)
@@ -489,13 +494,18 @@ def run_leg(a, P, cfg, dtype, frames, dev, local, rank, ws, headline):
     if d2h and not np.array_equal(out_counts.numpy(), counts) or d2h and any(
             rows_host[s, :counts[s]].tobytes() != rows_dev[s, :counts[s]].tobytes() for s in range(S)):
         raise SystemExit("bench: the per-step tracker output copied to the host differs from the tracker's")
-    # informational: the same steps with the frames already resident in HBM and no output copy
+    # informational: the same steps with the frames already resident in HBM and no output copy.
+    # Issued from a created stream: run() orders a device source behind the caller's current stream,
+    # and on the legacy null stream that wait would also order it behind every other blocking stream
+    # (the forwards in flight), serialising the steps
     torch.cuda.synchronize()
     barrier(ws)
+    side = torch.cuda.Stream(dev)
     th = time.perf_counter()
-    for t in range(a.steps):
-        pipe.run(frames[(t_first + a.steps + t) % F])
-    pipe.flush()
+    with torch.cuda.stream(side):
+        for t in range(a.steps):
+            pipe.run(frames[(t_first + a.steps + t) % F])
+        pipe.flush()
     torch.cuda.synchronize()
     barrier(ws)
     hbm_elapsed = time.perf_counter() - th

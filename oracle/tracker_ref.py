@@ -293,9 +293,12 @@ class RefMultiTracker:
         self.stats = {"total_tracks_created": 0, "total_tracks_terminated": 0,
                       "current_active_tracks": 0, "long_term_predictions": 0,
                       "successful_recoveries": 0}
-        # diagnostics for parity harnesses: exact IoU ties among candidate pairs
+        # diagnostics for parity harnesses: exact IoU ties among candidate pairs, and the frames on
+        # which the stable order (the HIP kernel's) and numpy's default argsort (the reference's,
+        # enhanced_multi_target_tracker.py:259) pick different pairs
         self.last_iou = None
         self.tie_frames = 0
+        self.tie_divergent_frames = 0
         if verbose:  # enhanced_multi_target_tracker.py:40
             print(f"增强版多目标跟踪器初始化完成 - 最大丢失容忍: {max_lost_frames}帧 ({max_lost_frames/30:.1f}秒)")
 
@@ -309,9 +312,12 @@ class RefMultiTracker:
                     iou[d, t] = ref_iou(det[:4], tb)
         self.last_iou = iou
         cand = iou[iou >= self.iou_threshold]
+        pairs = ref_greedy_assign(iou, self.iou_threshold, stable=self.stable_ties)
         if cand.size != np.unique(cand).size:
             self.tie_frames += 1
-        pairs = ref_greedy_assign(iou, self.iou_threshold, stable=self.stable_ties)
+            other = ref_greedy_assign(iou, self.iou_threshold, stable=not self.stable_ties)
+            if sorted((int(d), int(t)) for d, t in other) != sorted((int(d), int(t)) for d, t in pairs):
+                self.tie_divergent_frames += 1
         md = {p[0] for p in pairs}
         mt = {p[1] for p in pairs}
         un_d = [d for d in range(len(dets)) if d not in md]

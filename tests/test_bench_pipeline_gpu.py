@@ -95,8 +95,9 @@ def _run_gpu(dtype, frames, plan=None, model="yolov8s-small.yaml", tbatch=1):
 
     pipeline = importlib.import_module(P.__name__ + ".pipeline")
     F, S = frames.shape[:2]
+    # bench.py config 3's schedule: 4 forwards in flight, or 3 with two frames per forward
     pipe = pipeline.StreamPipeline(model, S, (512, 640), dtype, seed=0, max_tracks=512,
-                                   pipelined=True, inflight=4, frames_per_forward=tbatch)
+                                   pipelined=True, inflight=3 if tbatch > 1 else 4, frames_per_forward=tbatch)
     pipe.set_schedule(1, 1)  # bench.py's schedule with 3 forwards in flight
     # the committed conv plan bench.py loads for this workload (so the kernels under test are the
     # bench's own: split-bf16 / halo-tile variants included)

@@ -110,6 +110,19 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 // block's channel groups on one XCD: its activations are fetched into one L2).  (Round 4: a
 // channel-group-major order for the weight-heavy P5 convs cut their PMC bytes 3.73x -> 3.18x of
 // algorithmic but not their time, 25.3 vs 25.8 µs; not kept.)
+// The same placement for a persistent launch's item q of n (gy channel groups): item q runs on the
+// workgroup q % gridDim.x, whose XCD is q % 8 when gridDim.x is a multiple of 8.
+__device__ __forceinline__ int2 xcd_item(int q, int n, int gy, int on) {
+  if (!on) {
+    const int gx = n / gy, y = q / gx;
+    return make_int2(q - y * gx, y);
+  }
+  const int k = q & 7, i = q >> 3, qq = n >> 3, r = n & 7;
+  const int item = k * qq + (k < r ? k : r) + i;
+  const int px = item / gy;
+  return make_int2(px, item - px * gy);
+}
+
 __device__ __forceinline__ int2 xcd_block(int on) {
   if (!on) return make_int2(blockIdx.x, blockIdx.y);
   const int gx = gridDim.x, gy = gridDim.y, n = gx * gy;
@@ -1002,6 +1015,9 @@ struct FastArgs {
   int xcd;
   unsigned long long* tstamp;  // diagnostics (YK_FAST_TS): per-workgroup [start, end] wall clock
   int tstamp_cap;              // workgroups the tstamp buffer holds (3 entries each)
+  // persistent form (ipw > 1): a grid of ceil(n_items / ipw) workgroups, each looping over the
+  // (pixel block, channel group) items q = blockIdx.x, + gridDim.x, ... (n_cg channel groups)
+  int ipw, n_items, n_cg;
 };
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
@@ -1068,16 +1084,6 @@ __device__ __forceinline__ void conv_fast_body(const FastArgs& a, int2 blk, int 
   const int nk = a.k_steps;
   const int wg_lin = blockIdx.y * gridDim.x + blockIdx.x;
   if (a.tstamp && tid == 0 && wg_lin < a.tstamp_cap) a.tstamp[3 * wg_lin] = wall_clock64();
-  {
-    int2 tv[2];  // <= 512 entries (nk <= 128) in one round trip
-#pragma unroll
-    for (int u = 0; u < 2; ++u)
-      if (tid + u * 256 < nk * 4) tv[u] = a.ktab[tid + u * 256];
-#pragma unroll
-    for (int u = 0; u < 2; ++u)
-      if (tid + u * 256 < nk * 4) tab[tid + u * 256] = tv[u];
-    for (int i = tid + 512; i < nk * 4; i += 256) tab[i] = a.ktab[i];
-  }
   const __amdgpu_buffer_rsrc_t xr = make_srd(a.arena, a.arena_bytes);
   const __amdgpu_buffer_rsrc_t wr = make_srd(a.wblob, a.wbytes);
   const int hw = a.out_h * a.out_w;
@@ -1341,9 +1347,23 @@ __device__ __forceinline__ void conv_fast_body(const FastArgs& a, int2 blk, int 
 // Measured (round 3, fp32 headline): 2 lets the large split tiles drop their AGPR accumulators and
 // run two waves per SIMD without spills, but the headline does not move (5,279 vs 5,264 frames/s:
 // those kernels are bound by the split VALU work, not by occupancy); 3 spills (-32 %).
+// The op's K-step table into LDS (once per workgroup; conv_fast_body's first barrier publishes it)
+__device__ __forceinline__ void fast_table_lds(const FastArgs& a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  int2* tab = (int2*)smem;
+  const int tid = threadIdx.x, nk = a.k_steps;
+  int2 tv[2];  // <= 512 entries (nk <= 128) in one round trip
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+    if (tid + u * 256 < nk * 4) tv[u] = a.ktab[tid + u * 256];
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+    if (tid + u * 256 < nk * 4) tab[tid + u * 256] = tv[u];
+  for (int i = tid + 512; i < nk * 4; i += 256) tab[i] = a.ktab[i];
+}
+
 template <class Tr, int NNT, int NPT, int KW, int SKD>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(fast_wpe(NNT, NPT, KW, SKD, Tr::kScaled)))) conv_fast_kernel(FastArgs a) {
-  const int2 blk = xcd_block(a.xcd);
+__device__ __forceinline__ void conv_fast_item(const FastArgs& a, int2 blk) {
   const int nt0 = blk.y * NNT;
   const int rem = a.n_tiles - nt0;
   if constexpr (NNT == 1) {
@@ -1359,6 +1379,29 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(fast_w
       else
         conv_fast_body<Tr, (NNT > 3 ? 3 : 1), NPT, KW, SKD>(a, blk, nt0);
     }
+  }
+}
+
+// One launch = every (pixel block, channel group) item of the op.  ipw = 1: one item per
+// workgroup.  ipw > 1 (persistent form): ceil(items / ipw) workgroups, each
+// loads the K-step table once and loops over its items; a barrier between items keeps the next
+// item's LDS reduction behind this one's epilogue.
+// The loop costs registers in every instantiation (the 3-waves-per-SIMD tiles spilled 28-32 B), so
+// the persistent form is a build option (YK_DEFINES=-DYK_FAST_PERSIST=1, then YK_FAST_IPW=n at run
+// time) for A/B runs; the product kernel is the one-item form.
+#ifndef YK_FAST_PERSIST
+#define YK_FAST_PERSIST 0
+#endif
+template <class Tr, int NNT, int NPT, int KW, int SKD>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(fast_wpe(NNT, NPT, KW, SKD, Tr::kScaled)))) conv_fast_kernel(FastArgs a) {
+  fast_table_lds(a);
+  if (!YK_FAST_PERSIST || a.ipw <= 1) {
+    conv_fast_item<Tr, NNT, NPT, KW, SKD>(a, xcd_block(a.xcd));
+    return;
+  }
+  for (int q = blockIdx.x; q < a.n_items; q += gridDim.x) {
+    conv_fast_item<Tr, NNT, NPT, KW, SKD>(a, xcd_item(q, a.n_items, a.n_cg, a.xcd));
+    __syncthreads();
   }
 }
 
@@ -3315,6 +3358,7 @@ struct yk_model {
   int wide_dbg = 0;                   // YK_WIDE_DBG: conv_wide_kernel diagnostics (never in production)
   bool no_wide = false;               // YK_NO_WIDE=1: autotune without the LDS-resident wide kernel
   int ts_op = -1;                     // YK_FAST_TS=<op>: per-workgroup timestamps of that conv_fast op
+  int fast_ipw = 1;                   // YK_FAST_IPW=<n>: conv_fast in its persistent form, n items per workgroup
   unsigned long long* ts = nullptr;   // [3 * kTsCap] start, after K loop, end (wall_clock64, 100 MHz)
   std::vector<int64_t> ltab_off;
   unsigned char* lbox = nullptr;  // letterboxed frames [max_batch][in_h][in_w][3] (resize only)
@@ -3865,10 +3909,20 @@ void launch_splitk(const ConvArgs& a, const ConvPlan& p, hipStream_t st) {
 }
 
 template <class Tr, int NNT, int NPT, int KW>
-void launch_fast_t(const FastArgs& a, hipStream_t st) {
+void launch_fast_t(const FastArgs& a0, hipStream_t st) {
   constexpr int SKD = fast_skd(NNT, NPT);
   const int px = (64 / KW) * NPT;
-  dim3 grid((a.M + px - 1) / px, (a.n_tiles + NNT - 1) / NNT);
+  dim3 grid((a0.M + px - 1) / px, (a0.n_tiles + NNT - 1) / NNT);
+  FastArgs a = a0;
+  a.n_items = (int)(grid.x * grid.y);
+  a.n_cg = (int)grid.y;
+  if (YK_FAST_PERSIST && a.ipw > 1 && a.n_items > 8) {  // persistent form: a multiple of 8 workgroups (XCD placement)
+    int g = (a.n_items + a.ipw - 1) / a.ipw;
+    g = (g + 7) / 8 * 8;
+    grid = dim3(g < a.n_items ? g : a.n_items, 1);
+  } else {
+    a.ipw = 1;
+  }
   hipLaunchKernelGGL((conv_fast_kernel<Tr, NNT, NPT, KW, SKD>), grid, dim3(256), fast_lds(a.k_steps, NNT, NPT, KW), st,
                      a);
 }
@@ -4187,6 +4241,7 @@ int launch_op(yk_model* m, const yk_op& op, const uint8_t* frames, int B, float 
           f.xcd = m->xcd;
           f.tstamp = (m->ts && (int)(&op - m->ops.data()) == m->ts_op) ? m->ts : nullptr;
           f.tstamp_cap = kTsCap;
+          f.ipw = m->fast_ipw;
           if constexpr (std::is_same<Tr, F32>::value) {
             if (cp.npt & kSplitBit) {  // split-MFMA body on the bf16-split weights
               f.wblob = m->wsplit;
@@ -4878,6 +4933,7 @@ int yk_model_create(yk_ctx* ctx, const yk_model_desc* desc, const void* host_blo
   if (const char* env = getenv("YK_WIDE_DBG")) m->wide_dbg = atoi(env);
   if (const char* env = getenv("YK_NMS_DBG")) m->nms_dbg = atoi(env);
   if (const char* env = getenv("YK_NO_WIDE")) m->no_wide = env[0] == '1';
+  if (const char* env = getenv("YK_FAST_IPW")) m->fast_ipw = atoi(env) >= 1 ? atoi(env) : 1;
   if (const char* env = getenv("YK_FAST_TS")) {
     m->ts_op = atoi(env);
     if (e == hipSuccess) e = hipMalloc((void**)&m->ts, 3 * (size_t)kTsCap * sizeof(unsigned long long));
