@@ -527,3 +527,30 @@ def test_upload_pinned_async_copies_host_frames_exactly():
     dst = torch.zeros(64, dtype=torch.uint8, device="cuda")
     with pytest.raises(L.YKError):
         L.check(L.lib().yk_upload_pinned_async(L.ptr(dst), L.ptr(pageable), 64, L.current_stream(0)), "upload")
+
+
+def test_run_refuses_next_frames_before_enqueuing_the_step():
+    """run(frames, next_frames=...) that prefetch() would refuse -- no copy stream (inflight 1), or
+    pageable (not page-locked) host frames -- raises before this step is enqueued: the
+    step counter is unchanged and the same step then runs normally."""
+    P = pkg()
+    pipeline = importlib.import_module(P.__name__ + ".pipeline")
+    S = 8
+    sc = [P.synth.Scene(seed=90 + s, n_targets=8, n_frames=3) for s in range(S)]
+    frames = torch.stack([x.frames_torch(0, 3, "cuda") for x in sc], 1).contiguous()
+    pinned = frames.cpu().pin_memory()
+    pageable = frames.cpu()
+    assert pinned[0].numel() >= pipeline.StreamPipeline.PULL_BYTES
+    for inflight, bad in ((1, pinned[2]), (4, pageable[2])):
+        pipe = pipeline.StreamPipeline("yolov8n-small.yaml", S, (512, 640), "bf16", seed=0, max_tracks=128,
+                                       pipelined=True, inflight=inflight)
+        pipe.frames.copy_(frames[0])
+        pipe.capture(tune=False)
+        pipe.run(frames[0])
+        k0 = pipe._k
+        with pytest.raises(ValueError):
+            pipe.run(frames[1], next_frames=bad)
+        assert pipe._k == k0
+        pipe.run(frames[1])
+        pipe.sync()
+        assert pipe._k == (k0 + 1) % pipe.nb

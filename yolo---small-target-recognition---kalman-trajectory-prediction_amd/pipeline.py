@@ -364,6 +364,9 @@ class StreamPipeline:
         inside the caller's loop; the upload of step t + 1 overlaps step t.  Frames smaller than
         PULL_BYTES are not prefetched: the next run() pulls them onto the slot stream with a kernel
         (yk_upload_pinned_async), which holds neither the host nor a copy stream."""
+        pre = next_frames is not None and next_frames.numel() * next_frames.element_size() >= self.PULL_BYTES
+        if pre:  # refuse before anything of this step is enqueued (ADVICE r5)
+            self._check_prefetch(next_frames, extra=1 if self._prefetched else 0)
         s = self._slot(self._k)
         st = self._stream(s)
         cur = torch.cuda.current_stream(self.device)
@@ -388,7 +391,7 @@ class StreamPipeline:
             if self.T > 1:
                 self._j = j + 1
                 if self._j < self.T:  # the forward waits for its last step's frames
-                    if next_frames is not None and next_frames.numel() * next_frames.element_size() >= self.PULL_BYTES:
+                    if pre:
                         self.prefetch(next_frames)
                     return
                 self._j = 0
@@ -420,7 +423,7 @@ class StreamPipeline:
             with torch.cuda.stream(st):
                 self._upload(self.frame_slots[s], frames)
         self.step()
-        if next_frames is not None and next_frames.numel() * next_frames.element_size() >= self.PULL_BYTES:
+        if pre:
             # (frames below PULL_BYTES are pulled on the slot stream by the next run() instead: the
             # pull kernel costs the host nothing, and a copy-stream hop measured 26 % slower at
             # batch 1, bench.py --config 2 --no-prefetch)
@@ -435,13 +438,10 @@ class StreamPipeline:
         """Issue the upload of a FUTURE step's page-locked host frames now, on the copy stream, into
         that step's frame buffer (a staging buffer with a motion detector).  Prefetches queue in step order: the run() calls that follow must be
         handed the same tensors, in the same order.  At most 4 may be outstanding."""
-        if self.copy_stream is None or not (frames.is_cuda or frames.is_pinned()):
-            raise ValueError("prefetch: page-locked host (or device) frames and inflight > 1")
+        self._check_prefetch(frames)
         cs = self.copy_stream
         if self._ring:
             nf = len(self.frame_slots)
-            if len(self._prefetched) >= 4:
-                raise ValueError("prefetch: at most 4 steps ahead")
             q = self._kf * self.T + self._j + len(self._prefetched)  # that step's (frame buffer, sub-batch)
             f, j = (q // self.T) % nf, q % self.T
             # its previous reader: the forward of 4 D steps earlier (done in steady state; waiting for
@@ -457,8 +457,6 @@ class StreamPipeline:
             self._ev_copy[f * self.T + j].record(cs)
             self._prefetched.append((frames.data_ptr(), f * self.T + j))
             return
-        if len(self._prefetched) >= self.n_stage - self.D:
-            raise ValueError(f"prefetch: at most {self.n_stage - self.D} steps ahead")
         i = self._n_stage % self.n_stage
         self._n_stage += 1
         if self._stage_read_pending[i] and not self._ev_stage_read[i].query():
@@ -471,6 +469,16 @@ class StreamPipeline:
             self._upload(self._stage[i], frames)
         self._ev_copy[i].record(cs)
         self._prefetched.append((frames.data_ptr(), i))
+
+    def _check_prefetch(self, frames: torch.Tensor, extra: int = 0):
+        """Raise ValueError if prefetch(frames) would be refused (after `extra` more steps have
+        consumed theirs): no copy stream (inflight 1), frames neither page-locked nor on the
+        device, or the prefetch queue full."""
+        if self.copy_stream is None or not (frames.is_cuda or frames.is_pinned()):
+            raise ValueError("prefetch: page-locked host (or device) frames and inflight > 1")
+        cap = 4 if self._ring else self.n_stage - self.D
+        if len(self._prefetched) - extra >= cap:
+            raise ValueError(f"prefetch: at most {cap} steps ahead")
 
     # page-locked host frames below this size are pulled by a kernel (yk_upload_pinned_async):
     # the runtime copies small page-locked H2D transfers through the CPU, synchronously (one
