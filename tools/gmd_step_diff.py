@@ -153,9 +153,11 @@ def main():
                         sbuf[n & 1].copy_(sbuf[(n + 1) & 1])
                         sbuf[n & 1].add_(1.0)
                     n += 1
-                    if n % 8 == 0:
+                    if n % 32 == 0:  # bound the queue (~32 x 2 kernels of a few tens of us each)
                         sst.synchronize()
                 spin.n = n
+
+            sys.setswitchinterval(1e-4)  # the side thread gets the GIL between the pipeline's calls
 
             spin.n = 0
             side = threading.Thread(target=spin)
