@@ -1,11 +1,11 @@
 #!/usr/bin/env python3
 """Per-op kernel sweep: every table / halo conv variant on the chosen ops, at the tuner's batch.
 
-Starts from the committed fp32 plan and, for each op in --ops, sets each candidate variant in
+Starts from a committed plan (fp32 by default) and, for each op in --ops, sets each candidate variant in
 turn (invalid ones are rejected by yk_model_set_plan and skipped) and records that op's device
 time from yk_model_profile.  Prints one JSON line per op with the candidates sorted by time.
 
-usage: op_sweep.py [--ops 3,10,22] [--batch 16] [--plan plans/s_640x512_i640_b8_fp32.json]
+usage: op_sweep.py [--ops 3,10,22] [--batch 16] [--plan plans/s_640x512_i640_b8_fp32.json] [--dtype bf16]
 """
 from __future__ import annotations
 
@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--batch", type=int, default=16)
     ap.add_argument("--plan", default=os.path.join(REPO, "plans", "s_640x512_i640_b8_fp32.json"))
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--dtype", default="fp32", choices=("fp32", "bf16", "fp16", "fp8"))
     a = ap.parse_args()
     P = importlib.import_module(PKG)
     M = importlib.import_module(PKG + ".model")
@@ -35,7 +36,7 @@ def main():
     ar = P.arch.parse_arch(P.arch.load_model_dict("yolov8s-small.yaml"))
     sd = P.weights.synthetic_state_dict(ar, 0)
     B = a.batch
-    prog = M.Program(ar, sd, 512, 640, 640, B, "fp32")
+    prog = M.Program(ar, sd, 512, 640, 640, B, a.dtype)
     dm = M.DeviceModel(prog)
     dm.set_schedule(1, 1)
     frames = torch.stack([P.synth.Scene(seed=s, n_targets=40, n_frames=2, width=640, height=512)

@@ -8,7 +8,7 @@
 //   scharr_kernel   Scharr derivatives of every level of the new frame (kept for the next call,
 //                   when this frame is the "previous" one, like the stored prev_gray :93-94)
 //   -- from the second frame on --
-//   eig_kernel      cornerMinEigenVal(prev, blockSize 7, Sobel 3) on 16x16 tiles: Sobel
+//   eig_kernel      cornerMinEigenVal(prev, blockSize 7, Sobel 3) on 32x32 tiles: Sobel
 //                   responses and 7x7 box sums in exact integers through LDS, one float rounding
 //                   per covariance entry, per-stream max by an ordered-bits atomicMax
 //   cand_kernel     TOZERO threshold at 0.01 * max, 3x3 dilate test, interior local maxima
@@ -264,23 +264,27 @@ __global__ void clear_kernel(Dev g) {
   }
 }
 
-// cornerMinEigenVal on a 16x16 output tile: the (16 + BS - 1)^2 Sobel-product halo (box radius
-// BS / 2; the products outside the image are those of the reflected pixel, like boxFilter's
+// cornerMinEigenVal on an ETS x ETS output tile: the (ETS + BS - 1)^2 Sobel-product halo (box
+// radius BS / 2; the products outside the image are those of the reflected pixel, like boxFilter's
 // reflect-101 border over the product image), BS-wide horizontal then vertical integer sums.  The
-// gray pixels the Sobel taps of those products read -- rows / columns [o - 1, o + 16 + BS) of the
+// gray pixels the Sobel taps of those products read -- rows / columns [o - 1, o + ETS + BS) of the
 // image, each product at its reflected position with Sobel's own reflect-101 neighbours -- are
 // staged in LDS once (coalesced rows), so a product costs LDS reads instead of eight global byte
 // loads.  BS = 7: GlobalMotionDetector (global_motion_detector.py:49-55); 3: GMC (gmc.py:78-80).
+// ETS 32 (4 outputs a thread): a quarter of the 16 x 16 tiles' workgroups, each paying the same
+// load latency and barriers, and 1.4x fewer halo products per output (8 streams of 640x512 on the
+// CMC line, rocprofv3: 48.8 -> 34.5 µs; results bit-identical).
+constexpr int ETS = 32;
 template <int BS>
 __global__ void __launch_bounds__(256) eig_kernel(Dev g) {
-  constexpr int R = BS / 2, PN = 16 + 2 * R, GN = PN + 2;
+  constexpr int R = BS / 2, PN = ETS + 2 * R, GN = PN + 2;
   __shared__ int gt[GN][GN + 1];
   __shared__ int pxx[PN][PN + 1], pxy[PN][PN + 1], pyy[PN][PN + 1];
-  __shared__ int hxx[PN][17], hxy[PN][17], hyy[PN][17];
+  __shared__ int hxx[PN][ETS + 1], hxy[PN][ETS + 1], hyy[PN][ETS + 1];
   __shared__ unsigned wmax[4];
   const int s = blockIdx.z, W = g.geo.W, H = g.geo.H, tid = threadIdx.x;
   const unsigned char* img = g.pyr[g.sel[s]] + (long long)s * g.geo.per;
-  const int ox = blockIdx.x * 16 - R, oy = blockIdx.y * 16 - R;
+  const int ox = blockIdx.x * ETS - R, oy = blockIdx.y * ETS - R;
   const int gy0 = oy - 1, gx0 = ox - 1;  // LDS tile origin (image coordinates)
   for (int i = tid; i < GN * GN; i += 256) {
     const int ry = i / GN, rx = i - ry * GN;
@@ -301,8 +305,8 @@ __global__ void __launch_bounds__(256) eig_kernel(Dev g) {
     pyy[ry][rx] = iy * iy;
   }
   __syncthreads();
-  for (int i = tid; i < PN * 16; i += 256) {
-    const int ry = i >> 4, cx = i & 15;
+  for (int i = tid; i < PN * ETS; i += 256) {
+    const int ry = i / ETS, cx = i - ry * ETS;
     int a = 0, b = 0, c = 0;
 #pragma unroll
     for (int k = 0; k < BS; ++k) {
@@ -315,24 +319,29 @@ __global__ void __launch_bounds__(256) eig_kernel(Dev g) {
     hyy[ry][cx] = c;
   }
   __syncthreads();
-  const int tx = tid & 15, ty = tid >> 4;
-  int sxx = 0, sxy = 0, syy = 0;
-#pragma unroll
-  for (int k = 0; k < BS; ++k) {
-    sxx += hxx[ty + k][tx];
-    sxy += hxy[ty + k][tx];
-    syy += hyy[ty + k][tx];
-  }
-  const int x = blockIdx.x * 16 + tx, y = blockIdx.y * 16 + ty;
+  const int tx = tid % ETS, ty0 = tid / ETS;
   unsigned m = 0u;
-  if (x < W && y < H) {
-    constexpr double sc = 4.0 * BS * 255.0;
-    const double s2 = 1.0 / (sc * sc);  // (1 / (4 * blockSize * 255))^2
-    const float cxx = (float)((double)sxx * s2), cxy = (float)((double)sxy * s2), cyy = (float)((double)syy * s2);
-    const float a = cxx * 0.5f, c = cyy * 0.5f, d = a - c;
-    const float e = (a + c) - sqrtf(d * d + cxy * cxy);
-    g.eig[(long long)s * W * H + (long long)y * W + x] = e;
-    m = ord_bits(e);
+#pragma unroll
+  for (int q = 0; q < ETS * ETS / 256; ++q) {
+    const int ty = ty0 + q * (256 / ETS);
+    int sxx = 0, sxy = 0, syy = 0;
+#pragma unroll
+    for (int k = 0; k < BS; ++k) {
+      sxx += hxx[ty + k][tx];
+      sxy += hxy[ty + k][tx];
+      syy += hyy[ty + k][tx];
+    }
+    const int x = blockIdx.x * ETS + tx, y = blockIdx.y * ETS + ty;
+    if (x < W && y < H) {
+      constexpr double sc = 4.0 * BS * 255.0;
+      const double s2 = 1.0 / (sc * sc);  // (1 / (4 * blockSize * 255))^2
+      const float cxx = (float)((double)sxx * s2), cxy = (float)((double)sxy * s2), cyy = (float)((double)syy * s2);
+      const float a = cxx * 0.5f, c = cyy * 0.5f, d = a - c;
+      const float e = (a + c) - sqrtf(d * d + cxy * cxy);
+      g.eig[(long long)s * W * H + (long long)y * W + x] = e;
+      const unsigned o = ord_bits(e);
+      m = o > m ? o : m;
+    }
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
@@ -345,7 +354,7 @@ __global__ void __launch_bounds__(256) eig_kernel(Dev g) {
     unsigned b = wmax[0];
     for (int i = 1; i < 4; ++i) b = wmax[i] > b ? wmax[i] : b;
     // the per-stream maximum only grows: a workgroup whose maximum does not exceed a value
-    // already there skips the atomic (1,280 same-address atomics per stream serialised at L2)
+    // already there skips the atomic (same-address atomics per stream serialised at L2)
     if (b > __hip_atomic_load(&g.emax[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(&g.emax[s], b);
   }
 }
@@ -729,6 +738,8 @@ __device__ __forceinline__ void lk_weights(float a, float b, int& w00, int& w01,
 
 // One wavefront per corner (4 corners per workgroup); all control flow is wave-uniform.
 // (Staging each level's search region in LDS was measured slower: 111 -> 159 µs for 8 streams.)
+// (So was a per-wave LDS copy of the 24 x 24 J pixels around the window, restaged when its integer
+// position leaves the copy: 70.1 -> 87.9 µs on the CMC line, round 6.)
 template <int CHECK>
 __global__ void __launch_bounds__(256) lk_kernel(Dev g) {
   const int s = blockIdx.y, lane = threadIdx.x & 63;
@@ -1676,9 +1687,11 @@ static void gmd_front(yk_gmd* g, const uint8_t* frames, hipStream_t st) {
   if (g->frames > 0) {
     hipLaunchKernelGGL(yk::gmd::clear_kernel, dim3((S + 255) / 256), dim3(256), 0, st, d);
     if (d.mode)
-      hipLaunchKernelGGL(yk::gmd::eig_kernel<3>, dim3((G.W + 15) / 16, (G.H + 15) / 16, S), dim3(256), 0, st, d);
+      hipLaunchKernelGGL(yk::gmd::eig_kernel<3>, dim3((G.W + yk::gmd::ETS - 1) / yk::gmd::ETS, (G.H + yk::gmd::ETS - 1) / yk::gmd::ETS, S),
+                         dim3(256), 0, st, d);
     else
-      hipLaunchKernelGGL(yk::gmd::eig_kernel<7>, dim3((G.W + 15) / 16, (G.H + 15) / 16, S), dim3(256), 0, st, d);
+      hipLaunchKernelGGL(yk::gmd::eig_kernel<7>, dim3((G.W + yk::gmd::ETS - 1) / yk::gmd::ETS, (G.H + yk::gmd::ETS - 1) / yk::gmd::ETS, S),
+                         dim3(256), 0, st, d);
     hipLaunchKernelGGL(yk::gmd::cand_kernel, dim3((unsigned)((HW + 256 * yk::gmd::CPX - 1) / (256 * yk::gmd::CPX)), S),
                        dim3(256), 0, st, d);
     if (d.mode)
