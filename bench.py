@@ -463,7 +463,10 @@ def run_leg(a, P, cfg, dtype, frames, dev, local, rank, ws, headline):
     out_rows = torch.empty(n_rows * P._lib.TRACK_OUT_DTYPE.itemsize, dtype=torch.uint8, pin_memory=True)
     out_counts = torch.empty(S, dtype=torch.int32, pin_memory=True)
     out_stats = torch.empty(S * P._lib.STATS_DTYPE.itemsize, dtype=torch.uint8, pin_memory=True)
-    # untimed pre-roll (steady-state track load, independent of --steps/--warmup), then warm-up
+    # untimed pre-roll (steady-state track load, independent of --steps/--warmup), then warm-up.
+    # The ranks line up first, so they finish the warm-up together and none idles long at the
+    # barrier before the timed steps (the same clock drop as above)
+    barrier(ws)
     for t in range(n_pre + a.warmup):
         pipe.run(frames[t % F])
     _, st0 = pipe.stats()
