@@ -132,11 +132,10 @@ def parse():
                     help="diagnostics: which host copies the timed loop makes (default both: the metric's definition)")
     a = ap.parse_args()
     if a.inflight is None:
-        # the config's (config 3: 3 with two frames per forward), else 4: six forwards in flight lift
-        # the CMC lines (bf16 8,883 -> 10,115 frames/s) but the motion records then differ from the
-        # serial pipeline's in float rounding (profiles/r04_inflight_sweep.txt), so the CMC line is
-        # not measured there
-        a.inflight = 4 if a.gmd or a.no_pipeline else CONFIGS[a.config].get("inflight", 4)
+        # the config's (config 3: 3 with two frames per forward, the CMC lines too: motion windows of
+        # three batch-16 forwards, bf16 9,004 vs 8,208 frames/s for four forwards of one step, fp32
+        # 4,420 vs 4,429, profiles/r06_sweeps.txt r6aa), else 4
+        a.inflight = 4 if a.no_pipeline else CONFIGS[a.config].get("inflight", 4)
     return a
 
 
@@ -300,10 +299,9 @@ def tracker_roofline(pipe, reps=20):
 
 
 def tbatch_of(a, cfg) -> int:
-    """Frames per stream in one forward (temporal batching); 1 with the motion detector (its
-    motion windows order each frame's forward) or without forwards in flight."""
+    """Frames per stream in one forward (temporal batching); 1 without forwards in flight."""
     tb = a.tbatch if a.tbatch is not None else cfg.get("tbatch", 1)
-    if a.gmd or a.no_pipeline or a.inflight < 2:
+    if a.no_pipeline or a.inflight < 2:
         tb = 1
     return tb
 

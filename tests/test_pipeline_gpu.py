@@ -441,6 +441,73 @@ def test_motion_windows_record_every_step_and_download_in_order():
             assert r0[t, s, : c0[t, s]].tobytes() == r1[t, s, : c1[t, s]].tobytes(), (t, s)
 
 
+def test_motion_windows_with_temporal_batching_match_serial():
+    """Temporal batching inside motion windows (frames_per_forward T > 1 with the motion
+    detector): a forward carries T steps' frames, the window runs the motion detector on each
+    step's sub-batch in frame order, then the tracker steps.  The serial pipeline's tracker rows
+    (every step, through the step hook), motion records and detector statistics are reproduced at
+    T = 2 with 2 / 3 forwards in flight and at T = 3 (20 steps: a partial last forward), device
+    frames and page-locked host frames prefetched ahead; download_async of each step hands back
+    that step's output.  One committed plan at every forward batch (the per-op variants fix the
+    detections' rounding)."""
+    from gmd_helpers import camera_sequence
+    from gpu_helpers import StepRecorder
+
+    P = pkg()
+    pipeline = importlib.import_module(P.__name__ + ".pipeline")
+    L = P._lib
+    S, F = 3, 20
+    seqs = [camera_sequence(70 + s, F, h=512, w=640, whip_at=(7, 14), n_targets=12)[0] for s in range(S)]
+    frames = torch.from_numpy(np.stack(seqs, 1)).cuda()  # [F, S, H, W, 3]
+    host = frames.cpu().pin_memory()
+    runs = []
+    for pipelined, inflight, T, pinned in ((False, 1, 1, False), (True, 2, 2, False), (True, 3, 2, True),
+                                           (True, 3, 3, False)):
+        pipe = pipeline.StreamPipeline("yolov8s-small.yaml", S, (512, 640), "bf16", seed=0, max_tracks=256,
+                                       pipelined=pipelined, inflight=inflight, tracker_policy=1,
+                                       motion_method="optical_flow", frames_per_forward=T)
+        _plan_at_forward_batch(pipe)
+        pipe.frames.copy_(frames[0])
+        pipe.capture(tune=False)
+        rec = StepRecorder(pipe, F)
+        pipe.step_hook = rec
+        rows_h = torch.empty(S * 256 * L.TRACK_OUT_DTYPE.itemsize, dtype=torch.uint8, pin_memory=True)
+        counts_h = torch.empty(S, dtype=torch.int32, pin_memory=True)
+        stats_h = torch.empty(S * L.STATS_DTYPE.itemsize, dtype=torch.uint8, pin_memory=True)
+        for t in range(F):
+            if pinned:  # this step's host frames, the next two steps' uploads issued ahead
+                pipe.run(host[t])
+                for u in range(t + 1 + pipe.n_prefetched, min(t + 3, F)):
+                    pipe.prefetch(host[u])
+            else:
+                pipe.run(frames[t])
+            if pipelined:
+                pipe.download_async(rows_h, counts_h, stats_h)
+        pipe.sync()
+        rows, counts, stats = pipe.tracker.download()
+        if pipelined:  # the last step's page-locked copy is the tracker's final state
+            got = rows_h.numpy().view(L.TRACK_OUT_DTYPE).reshape(S, -1)
+            np.testing.assert_array_equal(counts_h.numpy(), counts)
+            for s in range(S):
+                assert got[s, : counts[s]].tobytes() == rows[s, : counts[s]].tobytes()
+        motion, mstats = pipe.gmd.download()
+        runs.append((rec.host(), stats.copy(), motion.copy(), mstats.copy(), (inflight, T)))
+        del pipe
+    (d0, n0, r0, c0, s0), st0, m0, ms0, _ = runs[0]
+    assert int(ms0["reset_triggers"].sum()) > 0  # the whip pans reached the global reset branch
+    for ((d1, n1, r1, c1, s1), st1, m1, ms1, cfg) in runs[1:]:
+        np.testing.assert_array_equal(n0, n1, err_msg=str(cfg))
+        np.testing.assert_array_equal(c0, c1, err_msg=str(cfg))
+        np.testing.assert_array_equal(st0, st1, err_msg=str(cfg))
+        for f in m0.dtype.names:
+            np.testing.assert_array_equal(m1[f], m0[f], err_msg=f"motion.{f} {cfg}")
+        for f in ms0.dtype.names:
+            np.testing.assert_array_equal(ms1[f], ms0[f], err_msg=f"gmd stats.{f} {cfg}")
+        for t in range(F):
+            for s in range(S):
+                assert r0[t, s, : c0[t, s]].tobytes() == r1[t, s, : c1[t, s]].tobytes(), (t, s, cfg)
+
+
 def _pan_scene(seed, F, K=10):
     """A camera pan (tests/gmd_helpers.py, texture at 0.6 contrast) over K bright 18-px targets
     that move with the world plus their own drift: the planted detector sees ~2 boxes per

@@ -40,14 +40,16 @@ bound by their own latency, not by the chip (op time is nearly flat in the batch
 parallel branches inside one captured graph execute one after the other, so a second
 independent graph on another stream is what fills the idle CUs (tools/inflight.py: 1.45x).
 
-``frames_per_forward=T`` > 1 (temporal batching; forwards in flight, no motion detector) makes
+``frames_per_forward=T`` > 1 (temporal batching; forwards in flight) makes
 one forward of T consecutive steps' frames: run() t uploads step t's S frames into sub-batch
 t % T of the forward's frame buffer, and the T-th run() launches one batch-(T S) forward and then
 the T tracker steps in frame order.  Detections of one image do not depend on the other images
 of the batch (same kernels, same plan), and the tracker still sees every stream's frames in
 order, so the results are the T = 1 pipeline's; a step's tracker output exists once its forward
 has been launched (its T-th run(), or flush()).  Measured: fp32 +4 %, bf16 +18 % at T = 2
-(gpurun_out/r6a, BASELINE config 3).
+(gpurun_out/r6a, BASELINE config 3).  With the motion detector the window runs each forward's T
+steps (the motion detector on each step's sub-batch of the slot's frames, in frame order, then
+the tracker steps), so a wave of D forwards covers D T steps.
 """
 from __future__ import annotations
 
@@ -72,8 +74,10 @@ class StreamPipeline:
         self.T = int(frames_per_forward)
         if not 1 <= self.T <= 8:
             raise ValueError("frames_per_forward must be in [1, 8]")
-        if self.T > 1 and (int(inflight) < 2 or not pipelined or motion_method is not None):
-            raise ValueError("frames_per_forward > 1 needs inflight > 1 (pipelined) and no motion detector")
+        if self.T > 1 and (int(inflight) < 2 or not pipelined):
+            raise ValueError("frames_per_forward > 1 needs inflight > 1 (pipelined)")
+        if self.T > 1 and motion_method is not None and __import__("os").environ.get("YK_MOTION_OVERLAP") == "1":
+            raise ValueError("frames_per_forward > 1 with a motion detector needs the motion windows")
         self.conf, self.iou, self.max_det = float(conf), float(iou), int(max_det)
         ar = A.parse_arch(A.load_model_dict(model_cfg))
         sd = weights if weights is not None else Wt.synthetic_state_dict(ar, seed)
@@ -251,7 +255,10 @@ class StreamPipeline:
             self._kf = (f + 1) % len(self.frame_slots)
         if self._windowed:
             self._ev_det[k].record(cur)
-            self._wave.append(k)
+            self._wave.append((k, self._n_sub))
+            for j, req in self._dl_t.items():  # (T > 1) requests of this forward's steps, issued in the window
+                self._dl[(k, j)] = req
+            self._dl_t = {}
             self._k = (k + 1) % self.nb
             if len(self._wave) == self.D:
                 self._run_window()
@@ -288,11 +295,11 @@ class StreamPipeline:
         if self.gmd is None:
             self.tracker.step_device(*self.step_outputs(k, j))
             return
-        self.gmd.detect_device(self.frame_slots[s])
+        self.gmd.detect_device(self.frame_slots[s][j * self.S:(j + 1) * self.S])
         if self.pipelined:
             self._ev_gmd[s].record(torch.cuda.current_stream(self.device))
             self._gmd_pending[s] = True
-        self.tracker.step_device(self._dets[k], self._counts[k], motion=self.gmd.motion_ptr)
+        self.tracker.step_device(*self.step_outputs(k, j), motion=self.gmd.motion_ptr)
 
     def _run_window(self):
         """Motion window of the current wave (see the header): after every forward enqueued so far,
@@ -305,27 +312,32 @@ class StreamPipeline:
         if self._motion_out is None:
             from . import _lib as L
 
-            self._motion_out = torch.zeros((self.nb, self.S * L.MOTION_DTYPE.itemsize), dtype=torch.uint8,
+            self._motion_out = torch.zeros((self.nb, self.T, self.S * L.MOTION_DTYPE.itemsize), dtype=torch.uint8,
                                            device=self.frames.device)
+        S = self.S
         with torch.cuda.stream(trk):
-            for k in self._wave:  # the exclusive part: the wave's motion detector calls, in order
+            for k, n in self._wave:  # the exclusive part: the wave's motion detector calls, in order
                 s = self._slot(k)
-                self.gmd.detect_device(self.frame_slots[s], out=self._motion_out[k].data_ptr())
+                for j in range(n):
+                    self.gmd.detect_device(self.frame_slots[s][j * S:(j + 1) * S], out=self._motion_out[k, j].data_ptr())
                 self._ev_gmd[s].record(trk)
                 self._gmd_pending[s] = True
         self._ev_window = torch.cuda.Event()
         self._ev_window.record(trk)  # the next wave's forwards may start: the tracker steps overlap them
         with torch.cuda.stream(trk):
-            for k in self._wave:
+            for k, n in self._wave:
                 s = self._slot(k)
-                self.tracker.step_device(self._dets[k], self._counts[k], motion=self._motion_out[k].data_ptr())
+                for j in range(n):
+                    self.tracker.step_device(*self.step_outputs(k, j), motion=self._motion_out[k, j].data_ptr())
+                    self._last = (k, j)
+                    if self.step_hook is not None:
+                        self._hook_j = j
+                        self.step_hook(self, k, self._stream(s), trk)
+                    req = self._dl.pop((k, j), None)
+                    if req is not None:
+                        self.tracker.download_async(*req, stream=trk.cuda_stream)
                 self._ev_trk[k].record(trk)
                 self._trk_pending[k] = True
-                if self.step_hook is not None:
-                    self.step_hook(self, k, self._stream(s), trk)
-                req = self._dl.pop(k, None)
-                if req is not None:
-                    self.tracker.download_async(*req, stream=trk.cuda_stream)
         self._wave = []
 
     def flush(self):
@@ -334,14 +346,14 @@ class StreamPipeline:
         forward of a partly filled frame buffer.  A partial forward runs the whole batch (the
         same graph; the sub-batches not refilled hold older frames) and steps the tracker on the
         filled sub-batches only.  A no-op otherwise."""
-        if self._windowed and self._wave:
-            self._run_window()
         if self.T > 1 and self._j:
             if self._prefetched:
                 raise ValueError("flush(): prefetched frames wait for steps not yet run")
             self._n_sub, self._j = self._j, 0
             self.step()
             self._n_sub = self.T
+        if self._windowed and self._wave:
+            self._run_window()
 
     def sync(self):
         """Wait for every launched step (detector and tracker streams)."""
@@ -395,33 +407,42 @@ class StreamPipeline:
                         self.prefetch(next_frames)
                     return
                 self._j = 0
-        elif self._prefetched:
-            ptr, i = self._prefetched[0]
-            if frames.data_ptr() != ptr:
-                raise ValueError("run(): other frames were prefetched for this step (next_frames / prefetch)")
-            self._prefetched.popleft()
-            st.wait_event(self._ev_copy[i])
-            if self._ev_window is not None:  # the staging -> slot copy is a kernel: not beside a motion window
-                st.wait_event(self._ev_window)
-            if self._gmd_pending[s]:  # the motion detector (tracker stream) still reads this slot's frames
-                st.wait_event(self._ev_gmd[s])
-                self._gmd_pending[s] = False
-            with torch.cuda.stream(st):
-                self.frame_slots[s].copy_(self._stage[i], non_blocking=True)
-            self._ev_stage_read[i].record(st)
-            self._stage_read_pending[i] = True
         else:
-            if st != cur:
+            # the slot's frame buffer: sub-batch j of its forward (T > 1), the whole buffer otherwise
+            j = self._j
+            dst = self.frame_slots[s][j * self.S:(j + 1) * self.S]
+            staged = None
+            if self._prefetched:
+                ptr, i = self._prefetched[0]
+                if frames.data_ptr() != ptr:
+                    raise ValueError("run(): other frames were prefetched for this step (next_frames / prefetch)")
+                self._prefetched.popleft()
+                st.wait_event(self._ev_copy[i])
+                staged = i
+            elif st != cur:
                 st.wait_stream(cur)
                 if frames.is_cuda:
                     frames.record_stream(st)  # the allocator keeps `frames` alive until the copy ran
             if self._gmd_pending[s]:  # the motion detector (tracker stream) still reads this slot's frames
                 st.wait_event(self._ev_gmd[s])
                 self._gmd_pending[s] = False
-            if self._ev_window is not None:  # (device copies and pull kernels: not beside a motion window)
+            if self._ev_window is not None:  # (staging copies, device copies, pull kernels: not beside a motion window)
                 st.wait_event(self._ev_window)
             with torch.cuda.stream(st):
-                self._upload(self.frame_slots[s], frames)
+                if staged is not None:
+                    dst.copy_(self._stage[staged], non_blocking=True)
+                else:
+                    self._upload(dst, frames)
+            if staged is not None:
+                self._ev_stage_read[staged].record(st)
+                self._stage_read_pending[staged] = True
+            if self.T > 1:
+                self._j = j + 1
+                if self._j < self.T:  # the forward waits for its last step's frames
+                    if pre:
+                        self.prefetch(next_frames)
+                    return
+                self._j = 0
         self.step()
         if pre:
             # (frames below PULL_BYTES are pulled on the slot stream by the next run() instead: the
@@ -503,11 +524,12 @@ class StreamPipeline:
         on the tracker stream, behind that step; no host wait.  The host reads them after
         sync() (or an event recorded on the tracker stream after this call).  With motion windows
         the copy is issued right after that step's tracker step, inside its wave's window."""
-        if self._windowed and self._wave:  # this step's tracker step runs in its wave's window
-            self._dl[self._wave[-1]] = (rows, counts, stats, rows_per_stream)
-            return
         if self.T > 1 and self._j:  # this step's forward (and tracker step) has not been launched yet
             self._dl_t[self._j - 1] = (rows, counts, stats, rows_per_stream)
+            return
+        if self._windowed and self._wave:  # this step's tracker step runs in its wave's window
+            k, n = self._wave[-1]
+            self._dl[(k, n - 1)] = (rows, counts, stats, rows_per_stream)
             return
         st = self.trk_stream if self.pipelined else torch.cuda.current_stream(self.device)
         self.tracker.download_async(rows, counts, stats, rows_per_stream, stream=st.cuda_stream)
