@@ -305,6 +305,14 @@ int yk_gmd_set_thresholds(yk_gmd* g, double global_motion_threshold, double rese
  * see yk_gmd_outputs, which holds the last call's results either way).  Asynchronous on
  * `stream`. */
 int yk_gmd_detect(yk_gmd* g, const uint8_t* dev_frames, yk_motion* dev_motion, void* stream);
+/* n consecutive detect_motion() calls in one launch sequence: dev_frames[i] (host array of n
+ * device pointers, each [n_streams][height][width][3] uint8) is step i's frame of every stream;
+ * dev_motion[n][n_streams] receives the n records in frame order (NULL: a buffer of the
+ * detector's own), bit for bit the n yk_gmd_detect calls' (the n frame pairs' corners and flow
+ * run as n * n_streams independent problems, the post-processing steps each stream's state in
+ * order).  A detector keeps its previous frame in one of two layouts: once either entry point has
+ * run, the other refuses until yk_gmd_reset.  Asynchronous on `stream`. */
+int yk_gmd_detect_window(yk_gmd* g, const uint8_t* const* dev_frames, int n, yk_motion* dev_motion, void* stream);
 int yk_gmd_outputs(yk_gmd* g, yk_motion** dev_motion);
 /* Copy the last results (and stats when host_stats != NULL) to the host; synchronous. */
 int yk_gmd_download(yk_gmd* g, yk_motion* host_motion, yk_gmd_stats* host_stats, void* stream);

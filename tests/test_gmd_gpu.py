@@ -203,3 +203,45 @@ def test_many_candidates_take_the_windowed_selection():
     _, info = G.good_features(G.bgr_to_gray(frames[0]), return_info=True)
     assert info["n_candidates"] > 16384
     run([frames])
+
+
+def test_window_mode_matches_per_call_and_oracle():
+    """yk_gmd_detect_window (n consecutive steps as n x S independent frame pairs in one launch
+    sequence, chunks of 8, the post-processing stepping each stream's state in order) gives the
+    per-call records bit for bit and the oracle's results: windows of 1, 3, 8 and 11 steps (a
+    chunked one), odd frame size included; the two layouts refuse each other until reset."""
+    M = _motion()
+    L = pkg()._lib
+    for h, w, seed in ((512, 640, 21), (251, 333, 22)):
+        S, F = 3, 23
+        seqs = [camera_sequence(seed + s, F, h=h, w=w, whip_at=(6 + s, 15))[0] for s in range(S)]
+        frames = torch.from_numpy(np.stack(seqs, 1)).cuda()  # [F, S, H, W, 3]
+        rec = L.MOTION_DTYPE.itemsize * S
+        single = M.BatchedMotionDetector(S, h, w)
+        out1 = torch.zeros((F, rec), dtype=torch.uint8, device="cuda")
+        for f in range(F):
+            single.detect_device(frames[f], out=out1[f].data_ptr())
+        win = M.BatchedMotionDetector(S, h, w)
+        out2 = torch.zeros((F, rec), dtype=torch.uint8, device="cuda")
+        t = 0
+        for n in (1, 3, 8, 11):
+            win.detect_window([frames[f] for f in range(t, t + n)], out=out2[t].data_ptr())
+            t += n
+        assert t == F
+        torch.cuda.synchronize()
+        a, b = out1.cpu().numpy(), out2.cpu().numpy()
+        assert a.tobytes() == b.tobytes(), [f for f in range(F) if a[f].tobytes() != b[f].tobytes()]
+        m1, st1 = single.download()
+        m2, st2 = win.download()
+        assert m1.tobytes() == m2.tobytes() and st1.tobytes() == st2.tobytes()
+        refs = [RefGlobalMotionDetector() for _ in range(S)]
+        recs = a.view(L.MOTION_DTYPE).reshape(F, S)
+        for f in range(F):
+            for s in range(S):
+                check_result(recs[f, s], refs[s].detect_motion(seqs[s][f]), refs[s], f"window mode frame {f} stream {s}")
+        with pytest.raises(L.YKError):
+            win.detect_device(frames[0])
+        with pytest.raises(L.YKError):
+            single.detect_window([frames[0]])
+        win.reset()
+        win.detect_device(frames[0])  # a reset detector takes either layout

@@ -193,6 +193,7 @@ _SIGS = {
     "yk_gmd_reset_stats": ([_vp, _vp], C.c_int),
     "yk_gmd_set_thresholds": ([_vp, C.c_double, C.c_double], C.c_int),
     "yk_gmd_detect": ([_vp, _vp, _vp, _vp], C.c_int),
+    "yk_gmd_detect_window": ([_vp, C.POINTER(_vp), C.c_int, _vp, _vp], C.c_int),
     "yk_gmd_outputs": ([_vp, C.POINTER(_vp)], C.c_int),
     "yk_gmd_debug_buffers": ([_vp, C.POINTER(_vp), C.POINTER(_vp), C.POINTER(_vp), C.POINTER(_vp), C.POINTER(_i32)],
                              C.c_int),

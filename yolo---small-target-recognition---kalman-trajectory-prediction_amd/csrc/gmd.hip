@@ -990,15 +990,17 @@ __device__ __forceinline__ int rank_of(const float* v, int n, int i) {
   return r;
 }
 
-__global__ void __launch_bounds__(256) finish_kernel(Dev g, yk_motion* __restrict__ out) {
+// The reference's post-processing of one detect_motion call: LK results of (virtual) stream v,
+// the detector state S of its stream, the record to *o.  Called by every thread of a workgroup
+// (barriers inside); flip: toggle sel[v] (the per-call layout's previous-frame buffer).
+__device__ void finish_one(const Dev& g, int v, State& S, yk_motion* __restrict__ o, bool flip) {
   __shared__ float vx[MAXC], vy[MAXC], sx[MAXC], sy[MAXC], dist[MAXC], sd[MAXC];
   __shared__ int wcnt[4];
   __shared__ int hv[2];
-  const int s = blockIdx.x, tid = threadIdx.x;
-  State& S = g.st[s];
+  const int tid = threadIdx.x;
   if (tid == 0) {  // read once before thread 0 sets has_prev below: every wave takes the same branch
     hv[0] = S.has_prev;
-    hv[1] = g.ncorners[s];
+    hv[1] = g.ncorners[v];
   }
   __syncthreads();
   if (!hv[0]) {  // first frame: only stored (:77-80)
@@ -1007,19 +1009,20 @@ __global__ void __launch_bounds__(256) finish_kernel(Dev g, yk_motion* __restric
       r.valid = 1;
       r.first_frame = 1;
       r.consistency = -1.0f;
-      out[s] = r;
+      *o = r;
       S.has_prev = 1;
-      g.sel[s] ^= 1;  // this frame is the next call's previous one
+      if (flip) g.sel[v] ^= 1;  // this frame is the next call's previous one
     }
+    __syncthreads();
     return;
   }
   const int n = hv[1];
   // status == 1 compaction in corner order (n <= 200 < 256 threads)
   int flag = 0;
   float mvx = 0.0f, mvy = 0.0f;
-  if (tid < n && n >= 20 && g.status[s * g.maxc + tid]) {
+  if (tid < n && n >= 20 && g.status[v * g.maxc + tid]) {
     flag = 1;
-    const float2 a = g.corners[s * g.maxc + tid], b = g.next[s * g.maxc + tid];
+    const float2 a = g.corners[v * g.maxc + tid], b = g.next[v * g.maxc + tid];
     mvx = b.x - a.x;  // next_points - prev_points (:140)
     mvy = b.y - a.y;
   }
@@ -1060,84 +1063,99 @@ __global__ void __launch_bounds__(256) finish_kernel(Dev g, yk_motion* __restric
     if (tid < ng) sd[rank_of(dist, ng, tid)] = dist[tid];
     __syncthreads();
   }
-  if (tid != 0) return;  // (tid 0 flips sel at the end)
-  yk_motion r{};
-  r.valid = 1;
-  r.consistency = -1.0f;
-  r.n_corners = n;
-  r.n_tracked = n >= 20 ? ng : 0;
-  if (est) {
-    // np.percentile(distances, 75), linear: lerp in float32 at virtual index 0.75 * (ng - 1)
-    const double vi = 0.75 * (double)(ng - 1);
-    const int lo = (int)floor(vi);
-    const int hi = lo + 1 < ng ? lo + 1 : ng - 1;
-    const float t = (float)(vi - (double)lo);
-    const float a = sd[lo], b = sd[hi], df = b - a;
-    const float p75 = t >= 0.5f ? b - df * (1.0f - t) : a + df * t;
-    int ni = 0;
-    float gx = 0.0f, gy = 0.0f;
-    for (int i = 0; i < ng; ++i)
-      if (dist[i] < p75) {  // np.mean(motion_vectors[inliers], axis=0): float32, in order
-        if (ni == 0) {
-          gx = vx[i];
-          gy = vy[i];
+  if (tid == 0) {
+    yk_motion r{};
+    r.valid = 1;
+    r.consistency = -1.0f;
+    r.n_corners = n;
+    r.n_tracked = n >= 20 ? ng : 0;
+    if (est) {
+      // np.percentile(distances, 75), linear: lerp in float32 at virtual index 0.75 * (ng - 1)
+      const double vi = 0.75 * (double)(ng - 1);
+      const int lo = (int)floor(vi);
+      const int hi = lo + 1 < ng ? lo + 1 : ng - 1;
+      const float t = (float)(vi - (double)lo);
+      const float a = sd[lo], b = sd[hi], df = b - a;
+      const float p75 = t >= 0.5f ? b - df * (1.0f - t) : a + df * t;
+      int ni = 0;
+      float gx = 0.0f, gy = 0.0f;
+      for (int i = 0; i < ng; ++i)
+        if (dist[i] < p75) {  // np.mean(motion_vectors[inliers], axis=0): float32, in order
+          if (ni == 0) {
+            gx = vx[i];
+            gy = vy[i];
+          } else {
+            gx += vx[i];
+            gy += vy[i];
+          }
+          ++ni;
+        }
+      r.n_inliers = ni;
+      if (ni > 5) {
+        gx = gx / (float)ni;
+        gy = gy / (float)ni;
+        const float mag = sqrtf(gx * gx + gy * gy);
+        int pos2;  // motion_vectors.append (deque maxlen 5)
+        if (S.mv_len < MVQ) {
+          pos2 = S.mv_head + S.mv_len;
+          if (pos2 >= MVQ) pos2 -= MVQ;
+          ++S.mv_len;
         } else {
-          gx += vx[i];
-          gy += vy[i];
+          pos2 = S.mv_head;
+          S.mv_head = S.mv_head + 1 == MVQ ? 0 : S.mv_head + 1;
         }
-        ++ni;
-      }
-    r.n_inliers = ni;
-    if (ni > 5) {
-      gx = gx / (float)ni;
-      gy = gy / (float)ni;
-      const float mag = sqrtf(gx * gx + gy * gy);
-      int pos2;  // motion_vectors.append (deque maxlen 5)
-      if (S.mv_len < MVQ) {
-        pos2 = S.mv_head + S.mv_len;
-        if (pos2 >= MVQ) pos2 -= MVQ;
-        ++S.mv_len;
-      } else {
-        pos2 = S.mv_head;
-        S.mv_head = S.mv_head + 1 == MVQ ? 0 : S.mv_head + 1;
-      }
-      S.mv[pos2][0] = gx;
-      S.mv[pos2][1] = gy;
-      bool is_motion = mag > g.thr_motion;
-      bool should_reset = mag > g.thr_reset;
-      if (S.mv_len >= 3) {  // _calculate_motion_consistency(last 3) (:241-261)
-        float ang[3];
-        for (int k = 0; k < 3; ++k) {
-          int q = S.mv_head + S.mv_len - 3 + k;
-          if (q >= MVQ) q -= MVQ;
-          ang[k] = (float)atan2((double)S.mv[q][1], (double)S.mv[q][0]);
+        S.mv[pos2][0] = gx;
+        S.mv[pos2][1] = gy;
+        bool is_motion = mag > g.thr_motion;
+        bool should_reset = mag > g.thr_reset;
+        if (S.mv_len >= 3) {  // _calculate_motion_consistency(last 3) (:241-261)
+          float ang[3];
+          for (int k = 0; k < 3; ++k) {
+            int q = S.mv_head + S.mv_len - 3 + k;
+            if (q >= MVQ) q -= MVQ;
+            ang[k] = (float)atan2((double)S.mv[q][1], (double)S.mv[q][0]);
+          }
+          float dsum = 0.0f;
+          for (int k = 1; k < 3; ++k) {
+            float d = fabsf(ang[k] - ang[k - 1]);
+            if (d > F_PI) d = F_2PI - d;
+            dsum = k == 1 ? d : dsum + d;
+          }
+          const float c = 1.0f - (dsum / 2.0f) / F_PI;
+          const float cons = c > 0.0f ? c : 0.0f;
+          r.consistency = cons;
+          if (cons > 0.7f && is_motion) should_reset = should_reset || mag > g.thr_reset_cons;
         }
-        float dsum = 0.0f;
-        for (int k = 1; k < 3; ++k) {
-          float d = fabsf(ang[k] - ang[k - 1]);
-          if (d > F_PI) d = F_2PI - d;
-          dsum = k == 1 ? d : dsum + d;
-        }
-        const float c = 1.0f - (dsum / 2.0f) / F_PI;
-        const float cons = c > 0.0f ? c : 0.0f;
-        r.consistency = cons;
-        if (cons > 0.7f && is_motion) should_reset = should_reset || mag > g.thr_reset_cons;
+        r.is_motion = is_motion;
+        r.should_reset = should_reset;
+        r.magnitude_kind = 1;
+        r.magnitude = mag;
+        r.vector[0] = gx;
+        r.vector[1] = gy;
       }
-      r.is_motion = is_motion;
-      r.should_reset = should_reset;
-      r.magnitude_kind = 1;
-      r.magnitude = mag;
-      r.vector[0] = gx;
-      r.vector[1] = gy;
     }
+    // GlobalMotionDetector.stats (:96-109)
+    S.total += 1;
+    S.motion_events += r.is_motion;
+    S.reset_triggers += r.should_reset;
+    S.avg = (S.avg * (float)(S.total - 1) + r.magnitude) / (float)S.total;
+    *o = r;
+    if (flip) g.sel[v] ^= 1;
   }
-  // GlobalMotionDetector.stats (:96-109)
-  S.total += 1;
-  S.motion_events += r.is_motion;
-  S.reset_triggers += r.should_reset;
-  S.avg = (S.avg * (float)(S.total - 1) + r.magnitude) / (float)S.total;
-  out[s] = r;
-  g.sel[s] ^= 1;
+  __syncthreads();  // the shared arrays and S are reused by the caller's next call
+}
+
+__global__ void __launch_bounds__(256) finish_kernel(Dev g, yk_motion* __restrict__ out) {
+  const int s = blockIdx.x;
+  finish_one(g, s, g.st[s], out + s, true);
+}
+
+// Window mode (yk_gmd_detect_window): n steps of S streams as n * S virtual streams v = w S + s,
+// each a (previous, new) frame pair; the post-processing steps every stream's state through its
+// n records in frame order.
+__global__ void __launch_bounds__(256) finish_window_kernel(Dev g, int n, int S_real, yk_motion* __restrict__ out) {
+  const int s = blockIdx.x;
+  for (int w = 0; w < n; ++w) finish_one(g, w * S_real + s, g.st[s], out + w * S_real + s, false);
 }
 
 // ---------------------------------------------------------------- GMC: estimateAffinePartial2D
@@ -1520,10 +1538,31 @@ __global__ void state_reset_kernel(Dev g, int stats_only) {
 
 using yk::gmd::Dev;
 
+// Window mode (yk_gmd_detect_window): up to kWindow steps per launch sequence, as kWindow * S
+// virtual streams v = w S + s.  Pyramids / derivatives of the previous frame (slot 0) and of the
+// window's frames (slots 1 .. n) are laid out [slot][S][per], so the per-call kernels, run with
+// pyr[0] / der[0] at slot 0 and pyr[1] / der[1] at slot 1 and every sel[v] = 0, read virtual stream
+// v's previous frame from slot w and write its new one to slot w + 1; the last new frame is copied
+// back to slot 0 for the next window.
+constexpr int kWindow = 8;
+struct GmdWindow {
+  unsigned char* pyr = nullptr;  // [kWindow + 1][S][per]
+  short2* der = nullptr;         // [kWindow + 1][S][per]
+  float* eig = nullptr;
+  unsigned* emax = nullptr;
+  unsigned long long* cand = nullptr;
+  int *ncand = nullptr, *ncorners = nullptr, *sel = nullptr, *info = nullptr;
+  float2 *corners = nullptr, *next = nullptr;
+  unsigned char* status = nullptr;
+  yk_motion* out = nullptr;  // [kWindow][S]
+};
+
 struct yk_gmd {
   yk_ctx* ctx;
   Dev dev;
   long long frames;
+  int calls_single = 0, calls_window = 0;  // the two layouts keep the previous frame differently
+  GmdWindow win;
 };
 
 extern "C" {
@@ -1630,8 +1669,11 @@ int yk_gmd_destroy(yk_gmd* g) {
   if (!g) return YK_OK;
   yk::DeviceGuard guard(g->ctx->device);
   Dev& d = g->dev;
+  GmdWindow& w = g->win;
   void* ptrs[] = {d.pyr[0], d.pyr[1], d.der[0], d.der[1], d.eig, d.emax, d.cand, d.ncand, d.corners,
-                  d.ncorners, d.next, d.status, d.st, d.out, d.sel, d.warp, d.info};
+                  d.ncorners, d.next, d.status, d.st, d.out, d.sel, d.warp, d.info,
+                  w.pyr, w.der, w.eig, w.emax, w.cand, w.ncand, w.ncorners, w.sel, w.info, w.corners,
+                  w.next, w.status, w.out};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   delete g;
@@ -1645,6 +1687,7 @@ int yk_gmd_reset(yk_gmd* g, void* stream) {
                      g->dev, 0);
   YK_HIP(hipGetLastError());
   g->frames = 0;
+  g->calls_single = g->calls_window = 0;
   return YK_OK;
 }
 
@@ -1706,6 +1749,10 @@ static void gmd_front(yk_gmd* g, const uint8_t* frames, hipStream_t st) {
 int yk_gmd_detect(yk_gmd* g, const uint8_t* frames, yk_motion* out, void* stream) {
   YK_CHECK_ARG(g && frames, "yk_gmd_detect: NULL argument");
   YK_CHECK_ARG(g->dev.mode == 0, "yk_gmd_detect: a YK_GMD_SPARSE_OPTFLOW detector computes warps (yk_gmc_apply)");
+  YK_CHECK_ARG(g->calls_window == 0,
+               "yk_gmd_detect: this detector's previous frame is in the window layout (yk_gmd_detect_window); "
+               "yk_gmd_reset first");
+  g->calls_single += 1;
   yk::DeviceGuard guard(g->ctx->device);
   const Dev& d = g->dev;
   hipStream_t st = (hipStream_t)stream;
@@ -1714,6 +1761,115 @@ int yk_gmd_detect(yk_gmd* g, const uint8_t* frames, yk_motion* out, void* stream
   if (out) YK_HIP(hipMemcpyAsync(d.out, out, d.S * sizeof(yk_motion), hipMemcpyDeviceToDevice, st));
   YK_HIP(hipGetLastError());
   g->frames += 1;
+  return YK_OK;
+}
+
+static hipError_t gmd_window_alloc(yk_gmd* g) {
+  Dev& d = g->dev;
+  GmdWindow& w = g->win;
+  if (w.pyr) return hipSuccess;
+  const size_t S = d.S, V = S * kWindow, HW = (size_t)d.geo.W * d.geo.H, per = (size_t)d.geo.per;
+  hipError_t e = hipSuccess;
+  auto A = [&](void** p, size_t bytes) {
+    if (e == hipSuccess) e = hipMalloc(p, bytes);
+  };
+  A((void**)&w.pyr, (kWindow + 1) * S * per);
+  A((void**)&w.der, (kWindow + 1) * S * per * sizeof(short2));
+  A((void**)&w.eig, V * HW * sizeof(float));
+  A((void**)&w.emax, V * sizeof(unsigned));
+  A((void**)&w.cand, V * HW * sizeof(unsigned long long));
+  A((void**)&w.ncand, V * sizeof(int));
+  A((void**)&w.corners, V * d.maxc * sizeof(float2));
+  A((void**)&w.ncorners, V * sizeof(int));
+  A((void**)&w.next, V * d.maxc * sizeof(float2));
+  A((void**)&w.status, V * d.maxc);
+  A((void**)&w.sel, V * sizeof(int));
+  A((void**)&w.info, V * 5 * sizeof(int));
+  A((void**)&w.out, V * sizeof(yk_motion));
+  if (e == hipSuccess) e = hipMemset(w.pyr, 0, (kWindow + 1) * S * per);  // (slot 0 before any frame: read, unused)
+  if (e == hipSuccess) e = hipMemset(w.der, 0, (kWindow + 1) * S * per * sizeof(short2));
+  if (e == hipSuccess) e = hipMemset(w.sel, 0, V * sizeof(int));
+  if (e == hipSuccess) e = hipMemset(w.ncorners, 0, V * sizeof(int));
+  if (e == hipSuccess) e = hipMemset(w.info, 0, V * 5 * sizeof(int));
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  return e;
+}
+
+// The window's device view: n steps as n * S virtual streams (see GmdWindow)
+static Dev gmd_window_dev(const yk_gmd* g, int n) {
+  const Dev& d = g->dev;
+  const GmdWindow& w = g->win;
+  const long long sp = (long long)d.S * d.geo.per;  // one slot
+  Dev v = d;
+  v.S = d.S * n;
+  v.pyr[0] = w.pyr;
+  v.pyr[1] = w.pyr + sp;
+  v.der[0] = w.der;
+  v.der[1] = w.der + sp;
+  v.eig = w.eig;
+  v.emax = w.emax;
+  v.cand = w.cand;
+  v.ncand = w.ncand;
+  v.corners = w.corners;
+  v.ncorners = w.ncorners;
+  v.next = w.next;
+  v.status = w.status;
+  v.sel = w.sel;
+  v.info = w.info;
+  v.out = w.out;
+  return v;  // st: the real streams' detector state (finish_window_kernel)
+}
+
+int yk_gmd_detect_window(yk_gmd* g, const uint8_t* const* frames, int n, yk_motion* out, void* stream) {
+  YK_CHECK_ARG(g && frames && n >= 1, "yk_gmd_detect_window: NULL argument or n < 1");
+  YK_CHECK_ARG(g->dev.mode == 0, "yk_gmd_detect_window: a YK_GMD_SPARSE_OPTFLOW detector computes warps (yk_gmc_apply)");
+  YK_CHECK_ARG(g->calls_single == 0,
+               "yk_gmd_detect_window: this detector's previous frame is in the per-call layout (yk_gmd_detect); "
+               "yk_gmd_reset first");
+  for (int i = 0; i < n; ++i) YK_CHECK_ARG(frames[i], "yk_gmd_detect_window: NULL frame pointer");
+  yk::DeviceGuard guard(g->ctx->device);
+  hipError_t e = gmd_window_alloc(g);
+  if (e != hipSuccess) {
+    yk::set_error(std::string("yk_gmd_detect_window: hipMalloc failed: ") + hipGetErrorString(e));
+    return YK_ERR_HIP;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  const Dev& d = g->dev;
+  const yk::gmd::Geo& G = d.geo;
+  const int S = d.S;
+  const long long HW = (long long)G.W * G.H, sp = (long long)S * G.per;
+  for (int c0 = 0; c0 < n; c0 += kWindow) {  // chunks of at most kWindow steps, in frame order
+    const int m = n - c0 < kWindow ? n - c0 : kWindow;
+    const Dev v = gmd_window_dev(g, m);
+    for (int w = 0; w < m; ++w) {  // each step's gray image into slot w + 1
+      Dev vw = v;
+      vw.S = S;
+      vw.pyr[1] = g->win.pyr + (w + 1) * sp;
+      hipLaunchKernelGGL(yk::gmd::gray_kernel, dim3((unsigned)((HW + 255) / 256), S), dim3(256), 0, st, vw, frames[c0 + w]);
+    }
+    for (int l = 1; l <= G.levels; ++l)
+      hipLaunchKernelGGL(yk::gmd::pyrdown_kernel, dim3((G.lw[l] + 15) / 16, (G.lh[l] + 15) / 16, v.S), dim3(256), 0, st,
+                         v, l);
+    hipLaunchKernelGGL(yk::gmd::scharr_kernel, dim3((G.lw[0] + 15) / 16, (G.lh[0] + 15) / 16, v.S * (G.levels + 1)),
+                       dim3(256), 0, st, v);
+    hipLaunchKernelGGL(yk::gmd::clear_kernel, dim3((v.S + 255) / 256), dim3(256), 0, st, v);
+    hipLaunchKernelGGL(yk::gmd::eig_kernel<7>, dim3((G.W + yk::gmd::ETS - 1) / yk::gmd::ETS, (G.H + yk::gmd::ETS - 1) / yk::gmd::ETS, v.S),
+                       dim3(256), 0, st, v);
+    hipLaunchKernelGGL(yk::gmd::cand_kernel, dim3((unsigned)((HW + 256 * yk::gmd::CPX - 1) / (256 * yk::gmd::CPX)), v.S),
+                       dim3(256), 0, st, v);
+    hipLaunchKernelGGL(yk::gmd::select_kernel, dim3(v.S), dim3(yk::gmd::NTS), yk::gmd::SEL_LDS, st, v);
+    hipLaunchKernelGGL(yk::gmd::lk_kernel<0>, dim3(d.maxc / 4, v.S), dim3(256), 0, st, v);
+    yk_motion* o = out ? out + (size_t)c0 * S : g->win.out;
+    hipLaunchKernelGGL(yk::gmd::finish_window_kernel, dim3(S), dim3(256), 0, st, v, m, S, o);
+    // the chunk's last frame is the next chunk's (or call's) previous one
+    YK_HIP(hipMemcpyAsync(g->win.pyr, g->win.pyr + m * sp, (size_t)sp, hipMemcpyDeviceToDevice, st));
+    YK_HIP(hipMemcpyAsync(g->win.der, g->win.der + m * sp, (size_t)sp * sizeof(short2), hipMemcpyDeviceToDevice, st));
+    // the last record of every stream is yk_gmd_outputs' "last call"
+    YK_HIP(hipMemcpyAsync(d.out, o + (size_t)(m - 1) * S, S * sizeof(yk_motion), hipMemcpyDeviceToDevice, st));
+  }
+  YK_HIP(hipGetLastError());
+  g->frames += n;
+  g->calls_window += 1;
   return YK_OK;
 }
 

@@ -72,6 +72,19 @@ class BatchedMotionDetector:
         L.check(L.lib().yk_gmd_detect(self._h, L.ptr(f), C.c_void_p(out), L.current_stream(self.device)),
                 "yk_gmd_detect")
 
+    def detect_window(self, frames, out: int = 0):
+        """detect_device on each of `frames` (a list of n device uint8 [S, H, W, 3] tensors: n
+        consecutive steps) in one launch sequence (yk_gmd_detect_window): the same n records, in
+        frame order, at `out` (device address of yk_motion[n][S]; 0: the detector's own buffer).
+        A detector uses either this or detect_device until reset()."""
+        shp = (self.S, self.H, self.W, 3)
+        for f in frames:
+            if f.dtype != torch.uint8 or tuple(f.shape) != shp or not f.is_contiguous():
+                raise ValueError(f"frames must be contiguous uint8 tensors of shape {shp}")
+        ptrs = (C.c_void_p * len(frames))(*[f.data_ptr() for f in frames])
+        L.check(L.lib().yk_gmd_detect_window(self._h, ptrs, len(frames), C.c_void_p(out), L.current_stream(self.device)),
+                "yk_gmd_detect_window")
+
     def detect_host(self, frames):
         """Host frames (one [H, W, 3] uint8 BGR array per stream)."""
         if len(frames) != self.S:

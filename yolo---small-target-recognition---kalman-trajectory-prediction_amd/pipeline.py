@@ -174,6 +174,9 @@ class StreamPipeline:
         self._n_stage = 0
         self._prefetched = __import__("collections").deque()  # (data_ptr of the host frames, staging index), one per upcoming step
         self._ev_window = None  # end of the last motion window (the next wave's forwards wait for it)
+        # a window's motion calls as one launch sequence (yk_gmd_detect_window); YK_GMD_WINDOW=0: one
+        # yk_gmd_detect per step (the A/B of profiles/r06_sweeps.txt r6ac)
+        self._gmd_window = __import__("os").environ.get("YK_GMD_WINDOW", "1") != "0"
         self._wave = []  # detection buffers of the current wave's steps (forwards enqueued, window not yet)
         self._dl = {}  # download_async requests of the current wave's steps, issued in its window
         self._motion_out = None  # per detection buffer: its step's yk_motion[S] (motion windows)
@@ -309,26 +312,34 @@ class StreamPipeline:
         trk = self.trk_stream
         for j in range(self.D):
             trk.wait_stream(self._stream(j))
-        if self._motion_out is None:
+        if self._motion_out is None:  # the window's records, one row per step (yk_motion[S] each)
             from . import _lib as L
 
-            self._motion_out = torch.zeros((self.nb, self.T, self.S * L.MOTION_DTYPE.itemsize), dtype=torch.uint8,
+            self._motion_out = torch.zeros((self.D * self.T, self.S * L.MOTION_DTYPE.itemsize), dtype=torch.uint8,
                                            device=self.frames.device)
         S = self.S
-        with torch.cuda.stream(trk):
-            for k, n in self._wave:  # the exclusive part: the wave's motion detector calls, in order
+        steps = [(k, j) for k, n in self._wave for j in range(n)]
+        with torch.cuda.stream(trk):  # the exclusive part: the wave's motion detector calls, in frame order,
+            # as one launch sequence (yk_gmd_detect_window: the steps' frame pairs side by side)
+            fr = [self.frame_slots[self._slot(k)][j * S:(j + 1) * S] for k, j in steps]
+            if self._gmd_window:
+                self.gmd.detect_window(fr, out=self._motion_out.data_ptr())
+            else:  # (diagnostics, YK_GMD_WINDOW=0: one call per step)
+                for i, f in enumerate(fr):
+                    self.gmd.detect_device(f, out=self._motion_out[i].data_ptr())
+            for k, _ in self._wave:
                 s = self._slot(k)
-                for j in range(n):
-                    self.gmd.detect_device(self.frame_slots[s][j * S:(j + 1) * S], out=self._motion_out[k, j].data_ptr())
                 self._ev_gmd[s].record(trk)
                 self._gmd_pending[s] = True
         self._ev_window = torch.cuda.Event()
         self._ev_window.record(trk)  # the next wave's forwards may start: the tracker steps overlap them
         with torch.cuda.stream(trk):
+            i = 0
             for k, n in self._wave:
                 s = self._slot(k)
                 for j in range(n):
-                    self.tracker.step_device(*self.step_outputs(k, j), motion=self._motion_out[k, j].data_ptr())
+                    self.tracker.step_device(*self.step_outputs(k, j), motion=self._motion_out[i].data_ptr())
+                    i += 1
                     self._last = (k, j)
                     if self.step_hook is not None:
                         self._hook_j = j
