@@ -25,7 +25,9 @@ forward (motion windows): the D forwards of a wave (steps t .. t + D - 1) run co
 one window on the tracker stream -- which waits for every forward enqueued so far -- runs the
 wave's motion + tracker steps in frame order, and the next wave's forwards wait for the window.
 A step's tracker output therefore exists once its wave's window has been enqueued (the last step
-of the wave, or flush() / sync()).  Round 5 traced run-to-run differences of the pipelined motion records to the Lucas-Kanade
+of the wave, or flush() / sync()).  The window's motion calls run as one launch sequence
+(yk_gmd_detect_window: its steps' frame pairs side by side, each stream's detector state stepped
+in frame order; the per-call records bit for bit).  Round 5 traced run-to-run differences of the pipelined motion records to the Lucas-Kanade
 kernel alone: one wave solving its corner twice in one launch read different J samples at the
 same addresses in the two passes while forwards ran beside it (csrc/gmd.hip YK_GMD_DIAG 4),
 with every pyramid producer wave provably complete before the launch (diag 16) and with the
