@@ -477,6 +477,7 @@ def run_leg(a, P, cfg, dtype, frames, dev, local, rank, ws, headline):
     if a.io == "stage-dev":  # diagnostics: the host path's copy-stream structure, frames from HBM
         host = frames[t_first:t_first + n_host].clone() if t_first + n_host <= F else host.to(dev)
     host_ns = 0
+    io_side = torch.cuda.Stream(dev)
     big = host[0].numel() >= pipe.PULL_BYTES or a.io == "stage-dev"
     depth = a.prefetch_depth if a.prefetch_depth is not None else (4 if tb > 1 else 2)
     ahead = depth if pipe.D > 1 and big and not a.no_prefetch else 0
@@ -486,8 +487,9 @@ def run_leg(a, P, cfg, dtype, frames, dev, local, rank, ws, headline):
             pipe.run(host[t % n_host])
             for u in range(t + 1 + pipe.n_prefetched, min(t + 1 + ahead, a.steps)):
                 pipe.prefetch(host[u % n_host])
-        else:
-            pipe.run(frames[(t_first + t) % F])
+        else:  # (frames from HBM: issued from a created stream, see the HBM-resident pass below)
+            with torch.cuda.stream(io_side):
+                pipe.run(frames[(t_first + t) % F])
         if d2h:
             pipe.download_async(out_rows, out_counts, out_stats)
         host_ns += time.perf_counter_ns() - h0
