@@ -469,15 +469,15 @@ def run_leg(a, P, cfg, dtype, frames, dev, local, rank, ws, headline):
         pipe.run(frames[t % F])
     _, st0 = pipe.stats()
     live_start = st0["current_active_tracks"].astype(np.float64)
+    h2d, d2h = a.io in ("both", "h2d", "stage-dev"), a.io in ("both", "d2h")
+    if a.io == "stage-dev":  # diagnostics: the host path's copy-stream structure, frames from HBM
+        host = frames[t_first:t_first + n_host].clone() if t_first + n_host <= F else host.to(dev)
+    io_side = None if h2d else torch.cuda.Stream(dev)
     barrier(ws)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     w0 = time.clock_gettime_ns(time.CLOCK_MONOTONIC)
-    h2d, d2h = a.io in ("both", "h2d", "stage-dev"), a.io in ("both", "d2h")
-    if a.io == "stage-dev":  # diagnostics: the host path's copy-stream structure, frames from HBM
-        host = frames[t_first:t_first + n_host].clone() if t_first + n_host <= F else host.to(dev)
     host_ns = 0
-    io_side = None if h2d else torch.cuda.Stream(dev)
     big = host[0].numel() >= pipe.PULL_BYTES or a.io == "stage-dev"
     depth = a.prefetch_depth if a.prefetch_depth is not None else (4 if tb > 1 else 2)
     ahead = depth if pipe.D > 1 and big and not a.no_prefetch else 0
