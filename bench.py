@@ -16,7 +16,8 @@ Workloads (BASELINE.json configs; the default is config 3, the metric's workload
 Protocol: frames are rendered into HBM before anything is timed; the committed conv plan
 (plans/*.json) is loaded instead of autotuning; an untimed tracker pre-roll of --preroll frames
 (independent of --steps/--warmup) brings every stream to its steady-state track load; then
---warmup untimed steps and exactly --steps timed steps between barrier + synchronize.  The run
+--warmup untimed steps through the timed loop's body (page-locked frames in, tracker output out)
+and exactly --steps timed steps between barrier + synchronize.  The run
 fails if the tracker dropped anything (stats.overflow != 0).
 
 Multi-GPU: `torchrun --nproc-per-node N bench.py --gpus N`, or `bench.py --gpus N` alone, which
@@ -128,6 +129,9 @@ def parse():
                     help="how many steps ahead the host frames are uploaded (page-locked frames >= PULL_BYTES; "
                          "default 2, 4 with --tbatch > 1: one forward's steps ahead; 2 measured +1.5-4.4 %% over 1 "
                          "at fp32, profiles/r05_inflight_lanes_sweep.txt)")
+    ap.add_argument("--fw-times", action="store_true",
+                    help="diagnostics: each timed forward's start / end (ms from the start of the timed region, "
+                         "timing events on its stream) in the line's fw_times")
     ap.add_argument("--io", default="both", choices=["both", "h2d", "d2h", "none", "stage-dev"],
                     help="diagnostics: which host copies the timed loop makes (default both: the metric's definition)")
     a = ap.parse_args()
@@ -450,53 +454,82 @@ def run_leg(a, P, cfg, dtype, frames, dev, local, rank, ws, headline):
     host = torch.empty((n_host,) + tuple(frames.shape[1:]), dtype=torch.uint8, pin_memory=True)
     for j in range(n_host):
         host[j].copy_(frames[(t_first + j) % F])
+    # the warm-up steps' own frames, also in page-locked memory: the warm-up runs the timed loop's
+    # body (host frames uploaded ahead, tracker output pushed back), so the copy engines and their
+    # page mappings are in use right before the timed steps (a warm-up from HBM frames left the
+    # first timed forward waiting 2.4 ms for its uploads at bf16, r6ai)
+    n_warm = min(a.warmup, F)
+    host_w = torch.empty((max(n_warm, 1),) + tuple(frames.shape[1:]), dtype=torch.uint8, pin_memory=True)
+    for j in range(n_warm):
+        host_w[j].copy_(frames[(n_pre + j) % F])
     # a video driver's decode buffers are long-lived and already DMA-mapped: one untimed upload of
     # each host frame (the first DMA from a fresh page-locked page costs its mapping)
     sink = torch.empty_like(frames[0])
     for j in range(n_host):
         sink.copy_(host[j], non_blocking=True)
+    for j in range(n_warm):
+        sink.copy_(host_w[j], non_blocking=True)
     torch.cuda.synchronize()
     del sink
     n_rows = pipe.tracker.n_streams * pipe.tracker.max_tracks
     out_rows = torch.empty(n_rows * P._lib.TRACK_OUT_DTYPE.itemsize, dtype=torch.uint8, pin_memory=True)
     out_counts = torch.empty(S, dtype=torch.int32, pin_memory=True)
     out_stats = torch.empty(S * P._lib.STATS_DTYPE.itemsize, dtype=torch.uint8, pin_memory=True)
-    # untimed pre-roll (steady-state track load, independent of --steps/--warmup), then warm-up.
-    # The ranks line up first, so they finish the warm-up together and none idles long at the
-    # barrier before the timed steps (the same clock drop as above)
-    barrier(ws)
-    for t in range(n_pre + a.warmup):
-        pipe.run(frames[t % F])
-    _, st0 = pipe.stats()
-    live_start = st0["current_active_tracks"].astype(np.float64)
     h2d, d2h = a.io in ("both", "h2d", "stage-dev"), a.io in ("both", "d2h")
     if a.io == "stage-dev":  # diagnostics: the host path's copy-stream structure, frames from HBM
         host = frames[t_first:t_first + n_host].clone() if t_first + n_host <= F else host.to(dev)
+        host_w = frames[n_pre:n_pre + n_warm].clone() if n_pre + n_warm <= F else host_w.to(dev)
     io_side = None if h2d else torch.cuda.Stream(dev)
+    big = host[0].numel() >= pipe.PULL_BYTES or a.io == "stage-dev"
+    depth = a.prefetch_depth if a.prefetch_depth is not None else (4 if tb > 1 else 2)
+    ahead = depth if pipe.D > 1 and big and not a.no_prefetch else 0
+
+    def steps(hbuf, n, t_dev):
+        """n steps of the timed loop's body on page-locked frames hbuf[t % len] (from HBM, frame
+        t_dev + t, without --io h2d); returns the host time spent enqueueing."""
+        ns = 0
+        for t in range(n):
+            h0 = time.perf_counter_ns()
+            if h2d:  # the next steps' frames are uploaded while this step runs (decode-ahead driver)
+                pipe.run(hbuf[t % len(hbuf)])
+                for u in range(t + 1 + pipe.n_prefetched, min(t + 1 + ahead, n)):
+                    pipe.prefetch(hbuf[u % len(hbuf)])
+            else:  # (frames from HBM: issued from a created stream, see the HBM-resident pass below)
+                with torch.cuda.stream(io_side):
+                    pipe.run(frames[(t_dev + t) % F])
+            if d2h:
+                pipe.download_async(out_rows, out_counts, out_stats)
+            ns += time.perf_counter_ns() - h0
+        return ns
+
+    # untimed pre-roll (steady-state track load, independent of --steps/--warmup), then the
+    # warm-up through the timed loop's body.  The ranks line up first, so they finish the warm-up
+    # together and none idles long at the barrier before the timed steps (the same clock drop as
+    # above)
+    barrier(ws)
+    for t in range(n_pre):
+        pipe.run(frames[t % F])
+    steps(host_w[:n_warm], n_warm, n_pre)
+    pipe.flush()
+    _, st0 = pipe.stats()
+    live_start = st0["current_active_tracks"].astype(np.float64)
     barrier(ws)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     w0 = time.clock_gettime_ns(time.CLOCK_MONOTONIC)
-    host_ns = 0
-    big = host[0].numel() >= pipe.PULL_BYTES or a.io == "stage-dev"
-    depth = a.prefetch_depth if a.prefetch_depth is not None else (4 if tb > 1 else 2)
-    ahead = depth if pipe.D > 1 and big and not a.no_prefetch else 0
-    for t in range(a.steps):
-        h0 = time.perf_counter_ns()
-        if h2d:  # the next steps' frames are uploaded while this step runs (decode-ahead driver)
-            pipe.run(host[t % n_host])
-            for u in range(t + 1 + pipe.n_prefetched, min(t + 1 + ahead, a.steps)):
-                pipe.prefetch(host[u % n_host])
-        else:  # (frames from HBM: issued from a created stream, see the HBM-resident pass below)
-            with torch.cuda.stream(io_side):
-                pipe.run(frames[(t_first + t) % F])
-        if d2h:
-            pipe.download_async(out_rows, out_counts, out_stats)
-        host_ns += time.perf_counter_ns() - h0
+    if a.fw_times:
+        ev_t0 = torch.cuda.Event(enable_timing=True)
+        ev_t0.record()
+        pipe.fw_events = []
+    host_ns = steps(host, a.steps, t_first)
     pipe.flush()  # (motion windows: the last partial wave's motion + tracker steps, inside the timing)
     torch.cuda.synchronize()
     barrier(ws)
     elapsed = time.perf_counter() - t0
+    fw_times = None
+    if a.fw_times:
+        fw_times = [[round(ev_t0.elapsed_time(e0), 3), round(ev_t0.elapsed_time(e1), 3)] for e0, e1 in pipe.fw_events]
+        pipe.fw_events = None
     w1 = time.clock_gettime_ns(time.CLOCK_MONOTONIC)
     log(f"{dtype}: timed {a.steps} steps (host frames in, tracker output out) in {elapsed:.4f}s")
     counts, stats = pipe.stats()
@@ -541,6 +574,8 @@ def run_leg(a, P, cfg, dtype, frames, dev, local, rank, ws, headline):
            "conv_plan": plan_src, "conv_plan_parity": parity, "window_monotonic_ns": [w0, w1],
            "frames_per_forward": tb,
            "rank_devices": devices}
+    if fw_times is not None:
+        leg["fw_times"] = fw_times
     if overflow:
         log(f"tracker overflow on this rank: {overflow} detections/tracks dropped")
     if rank == 0 and not a.no_profile:
@@ -706,6 +741,8 @@ def main():
             "secondary": [{k: v for k, v in leg.items() if k != "window_monotonic_ns"} for leg in legs],
             "timed_window_monotonic_ns": head["window_monotonic_ns"],
         }
+        if "fw_times" in head:
+            out["fw_times"] = head["fw_times"]
         print(json.dumps(out), flush=True)
     bad = head["overflow"] or any(leg["overflow"] for leg in legs)
     if ws > 1:

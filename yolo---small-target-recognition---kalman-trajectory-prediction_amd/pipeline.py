@@ -179,6 +179,7 @@ class StreamPipeline:
         # a window's motion calls as one launch sequence (yk_gmd_detect_window); YK_GMD_WINDOW=0: one
         # yk_gmd_detect per step (the A/B of profiles/r06_sweeps.txt r6ac)
         self._gmd_window = __import__("os").environ.get("YK_GMD_WINDOW", "1") != "0"
+        self.fw_events = None  # a list: step() appends (start, end) timing events of each forward
         self._wave = []  # detection buffers of the current wave's steps (forwards enqueued, window not yet)
         self._dl = {}  # download_async requests of the current wave's steps, issued in its window
         self._motion_out = None  # per detection buffer: its step's yk_motion[S] (motion windows)
@@ -251,9 +252,15 @@ class StreamPipeline:
         if self._ev_window is not None:  # no forward beside a motion window
             cur.wait_event(self._ev_window)
         f = self._kf if self._ring else s
+        if self.fw_events is not None:  # (diagnostics: each forward's start / end on its stream)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(cur)
         with torch.cuda.stream(cur):
             self.models[s].detect(self.frame_slots[f], self.conf, self.iou, self.max_det, self._dets[k],
                                   self._counts[k], graph=bool(self.graph))
+        if self.fw_events is not None:
+            e1.record(cur)
+            self.fw_events.append((e0, e1))
         if self._ring:
             self._ev_fread[f].record(cur)
             self._fread_pending[f] = True
