@@ -130,8 +130,8 @@ def parse():
                          "default 2, 4 with --tbatch > 1: one forward's steps ahead; 2 measured +1.5-4.4 %% over 1 "
                          "at fp32, profiles/r05_inflight_lanes_sweep.txt)")
     ap.add_argument("--fw-times", action="store_true",
-                    help="diagnostics: each timed forward's start / end (ms from the start of the timed region, "
-                         "timing events on its stream) in the line's fw_times")
+                    help="diagnostics: each timed forward's start / end and its tracker steps' start / end (ms from "
+                         "the start of the timed region, timing events on the streams) in the line's fw_times")
     ap.add_argument("--io", default="both", choices=["both", "h2d", "d2h", "none", "stage-dev"],
                     help="diagnostics: which host copies the timed loop makes (default both: the metric's definition)")
     a = ap.parse_args()
@@ -528,7 +528,7 @@ def run_leg(a, P, cfg, dtype, frames, dev, local, rank, ws, headline):
     elapsed = time.perf_counter() - t0
     fw_times = None
     if a.fw_times:
-        fw_times = [[round(ev_t0.elapsed_time(e0), 3), round(ev_t0.elapsed_time(e1), 3)] for e0, e1 in pipe.fw_events]
+        fw_times = [[round(ev_t0.elapsed_time(e), 3) if e is not None else None for e in evs] for evs in pipe.fw_events]
         pipe.fw_events = None
     w1 = time.clock_gettime_ns(time.CLOCK_MONOTONIC)
     log(f"{dtype}: timed {a.steps} steps (host frames in, tracker output out) in {elapsed:.4f}s")

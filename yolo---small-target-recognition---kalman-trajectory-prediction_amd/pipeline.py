@@ -179,7 +179,7 @@ class StreamPipeline:
         # a window's motion calls as one launch sequence (yk_gmd_detect_window); YK_GMD_WINDOW=0: one
         # yk_gmd_detect per step (the A/B of profiles/r06_sweeps.txt r6ac)
         self._gmd_window = __import__("os").environ.get("YK_GMD_WINDOW", "1") != "0"
-        self.fw_events = None  # a list: step() appends (start, end) timing events of each forward
+        self.fw_events = None  # a list: step() appends (start, end, tracker start, tracker end) timing events of each forward
         self._wave = []  # detection buffers of the current wave's steps (forwards enqueued, window not yet)
         self._dl = {}  # download_async requests of the current wave's steps, issued in its window
         self._motion_out = None  # per detection buffer: its step's yk_motion[S] (motion windows)
@@ -260,7 +260,7 @@ class StreamPipeline:
                                   self._counts[k], graph=bool(self.graph))
         if self.fw_events is not None:
             e1.record(cur)
-            self.fw_events.append((e0, e1))
+            self.fw_events.append([e0, e1, None, None])
         if self._ring:
             self._ev_fread[f].record(cur)
             self._fread_pending[f] = True
@@ -278,10 +278,16 @@ class StreamPipeline:
         if self.pipelined:
             self._ev_det[k].record(cur)
             self.trk_stream.wait_event(self._ev_det[k])
+            if self.fw_events is not None:  # (diagnostics: its tracker steps' start / end)
+                self.fw_events[-1][2] = torch.cuda.Event(enable_timing=True)
+                self.fw_events[-1][2].record(self.trk_stream)
             for j in range(self._n_sub):  # the forward's steps, in frame order
                 with torch.cuda.stream(self.trk_stream):
                     self._track(k, s, j)
                 self._after_track(k, j, cur)
+            if self.fw_events is not None:
+                self.fw_events[-1][3] = torch.cuda.Event(enable_timing=True)
+                self.fw_events[-1][3].record(self.trk_stream)
             self._ev_trk[k].record(self.trk_stream)
             self._trk_pending[k] = True
         else:
