@@ -72,7 +72,10 @@ CONFIGS = {
     # 12,384-12,527, T4 D2 11,644-11,662 frames/s
     3: dict(S=8, H=512, W=640, imgsz=640, max_tracks=512, targets=40, dtype="fp32", secondary="bf16,n:fp32", live_floor=64,
             tbatch=2, inflight=3),
-    4: dict(S=1, H=512, W=640, imgsz=640, max_tracks=512, targets=40, dtype="fp32", secondary="", live_floor=64),
+    # config 4: four consecutive steps of the rank's stream per forward, four forwards in flight (20 steps:
+    # 2,738-2,770 frames/s vs 2,194-2,326 at one step per forward, profiles/r06_sweeps.txt r6at)
+    4: dict(S=1, H=512, W=640, imgsz=640, max_tracks=512, targets=40, dtype="fp32", secondary="", live_floor=64,
+            tbatch=4, inflight=4),
     5: dict(S=8, H=1024, W=1280, imgsz=1280, max_tracks=2048, targets=96, dtype="fp8", secondary="bf16",
             live_floor=256),
 }

@@ -89,15 +89,17 @@ def chain():
     return build_chain([P.shard.stream_seed(s, S) for s in range(S)], F, TARGETS)
 
 
-def _run_gpu(dtype, frames, plan=None, model="yolov8s-small.yaml", tbatch=1):
+def _run_gpu(dtype, frames, plan=None, model="yolov8s-small.yaml", tbatch=1, inflight=None):
     P = pkg()
     import importlib
 
     pipeline = importlib.import_module(P.__name__ + ".pipeline")
     F, S = frames.shape[:2]
-    # bench.py config 3's schedule: 4 forwards in flight, or 3 with two frames per forward
+    # bench.py config 3's schedule: 4 forwards in flight, or 3 with two frames per forward (config
+    # 4's: four frames per forward, 4 in flight)
+    D = inflight if inflight is not None else (3 if tbatch > 1 else 4)
     pipe = pipeline.StreamPipeline(model, S, (512, 640), dtype, seed=0, max_tracks=512,
-                                   pipelined=True, inflight=3 if tbatch > 1 else 4, frames_per_forward=tbatch)
+                                   pipelined=True, inflight=D, frames_per_forward=tbatch)
     pipe.set_schedule(1, 1)  # bench.py's schedule with 3 forwards in flight
     # the committed conv plan bench.py loads for this workload (so the kernels under test are the
     # bench's own: split-bf16 / halo-tile variants included)
@@ -151,14 +153,14 @@ def test_bench_pipeline_fp32_matches_oracle_chain_every_frame(chain, plan):
     assert out["near_tie_flips"] + out["order_ties"] <= 3
 
 
-def check_chain(chain, plan_path, tbatch=1, parity_record=False):
+def check_chain(chain, plan_path, tbatch=1, parity_record=False, inflight=None):
     """The resynced chain comparison of test_bench_pipeline_fp32_matches_oracle_chain_every_frame
     for any stream count (chain from build_chain); returns the summary it prints."""
     from gpu_helpers import resync_rows
     from test_tracker_gpu import compare_frame
 
     S, F = chain["S"], chain["F"]
-    dets, counts, rows, tcounts, stats = _run_gpu("fp32", chain["frames"], plan_path, chain["model"], tbatch)
+    dets, counts, rows, tcounts, stats = _run_gpu("fp32", chain["frames"], plan_path, chain["model"], tbatch, inflight)
     assert int(stats[-1]["overflow"].sum()) == 0
     conf_dev, conf_dev_well, box_rel, n_tracks, n_outputs, ill_conf = 0.0, 0.0, 0.0, 0, 0, []
     flips, flip_scores, order_ties = [], [], []
@@ -253,15 +255,23 @@ def check_chain(chain, plan_path, tbatch=1, parity_record=False):
     return summary
 
 
+@pytest.fixture(scope="module")
+def chain_c4():
+    """Config 4's rank-5 stream (scene seed shard.stream_seed(5, 1) = 5000, 40 targets)."""
+    P = pkg()
+    return build_chain([P.shard.stream_seed(5, 1)], F, TARGETS)
+
+
 @pytest.mark.timeout(900)
-def test_config4_rank_leg_b1_fp32_plan_matches_oracle_chain():
+@pytest.mark.parametrize("tb", [1, 4], ids=["t1", "t4"])
+def test_config4_rank_leg_b1_fp32_plan_matches_oracle_chain(chain_c4, tb):
     """BASELINE config 4's per-rank leg (one stream per GPU, bench.py --config 4): the committed
     batch-1 fp32 plan (plans/s_640x512_i640_b1_fp32.json) under the same resynced chain bar as
-    config 3, on rank 5's stream (scene seed shard.stream_seed(5, 1) = 5000, 40 targets), 160
-    frames with >= 64 live tracks at the end."""
-    P = pkg()
-    ch = build_chain([P.shard.stream_seed(5, 1)], F, TARGETS)
-    out = check_chain(ch, "plans/s_640x512_i640_b1_fp32.json", parity_record=True)
+    config 3, on rank 5's stream, 160 frames with >= 64 live tracks at the end; t4: bench.py's
+    config-4 schedule, the same variants at the batch-4 forward of four consecutive steps
+    (plans/s_640x512_i640_b4_fp32.json), four forwards in flight."""
+    ch = chain_c4
+    out = check_chain(ch, f"plans/s_640x512_i640_b{tb}_fp32.json", tb, parity_record=True, inflight=4)
     assert min(out["live_tracks_end"]) >= 64, out["live_tracks_end"]
     assert ch["terminated"] > 0
 
