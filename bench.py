@@ -76,8 +76,11 @@ CONFIGS = {
     # 2,738-2,770 frames/s vs 2,194-2,326 at one step per forward, profiles/r06_sweeps.txt r6at)
     4: dict(S=1, H=512, W=640, imgsz=640, max_tracks=512, targets=40, dtype="fp32", secondary="", live_floor=64,
             tbatch=4, inflight=4),
+    # config 5: the fp8 leg runs two steps per forward, three in flight (20 steps: 4,811-4,830 vs 4,418-4,502
+    # frames/s at one step, r6av); the bf16 leg keeps one step (its batch-16 arena passes the 2 GiB the table
+    # kernels address: 2,612-2,623 vs 3,700-3,746)
     5: dict(S=8, H=1024, W=1280, imgsz=1280, max_tracks=2048, targets=96, dtype="fp8", secondary="bf16",
-            live_floor=256),
+            live_floor=256, tbatch={"fp8": 2}, inflight={"fp8": 3}),
 }
 
 
@@ -142,8 +145,14 @@ def parse():
         # the config's (config 3: 3 with two frames per forward, the CMC lines too: motion windows of
         # three batch-16 forwards, bf16 9,004 vs 8,208 frames/s for four forwards of one step, fp32
         # 4,420 vs 4,429, profiles/r06_sweeps.txt r6aa), else 4
-        a.inflight = 4 if a.no_pipeline else CONFIGS[a.config].get("inflight", 4)
+        cfg = CONFIGS[a.config]
+        a.inflight = 4 if a.no_pipeline else by_dtype(cfg.get("inflight", 4), a.dtype or cfg["dtype"], 4)
     return a
+
+
+def by_dtype(v, dtype, default):
+    """A CONFIGS schedule entry: one value, or a {dtype: value} map (default for other dtypes)."""
+    return v.get(dtype, default) if isinstance(v, dict) else v
 
 
 # ---------------------------------------------------------------------------- ranks
@@ -305,9 +314,9 @@ def tracker_roofline(pipe, reps=20):
             "achieved": round(gbps, 3), "peak": HBM_PEAK, "unit": "GB/s", "frac": round(gbps / HBM_PEAK, 6)}
 
 
-def tbatch_of(a, cfg) -> int:
+def tbatch_of(a, cfg, dtype) -> int:
     """Frames per stream in one forward (temporal batching); 1 without forwards in flight."""
-    tb = a.tbatch if a.tbatch is not None else cfg.get("tbatch", 1)
+    tb = a.tbatch if a.tbatch is not None else by_dtype(cfg.get("tbatch", 1), dtype, 1)
     if a.no_pipeline or a.inflight < 2:
         tb = 1
     return tb
@@ -403,7 +412,7 @@ def run_leg(a, P, cfg, dtype, frames, dev, local, rank, ws, headline):
     S, H, W, imgsz = cfg["S"], cfg["H"], cfg["W"], cfg["imgsz"]
     F = frames.shape[0]
     lanes = a.lanes if a.lanes is not None else 1  # (the model's default schedule: one lane)
-    tb = tbatch_of(a, cfg)
+    tb = tbatch_of(a, cfg, dtype)
     pipe = pipeline.StreamPipeline(f"yolov8{a.scale}-small.yaml", S, (H, W), dtype, seed=0, device=local,
                                    pipelined=not a.no_pipeline, imgsz=imgsz, max_tracks=cfg["max_tracks"],
                                    inflight=1 if a.no_pipeline else a.inflight,

@@ -188,3 +188,38 @@ def test_config5_committed_b8_fp8_plan():
         if len(ref):
             best = _box_iou(ref[:, :4], d1[b, :n, :4]).max(1).values
             assert float((best > 0.5).float().mean()) >= 0.85
+
+
+def test_config5_b16_fp8_plan_equals_b8_per_image():
+    """bench.py --config 5's fp8 leg runs two steps per forward: the batch-8 plan's variants at
+    the batch-16 forward (plans/s_1280x1024_i1280_b16_fp8.json).  Every image's detections equal
+    the batch-8 plan's on the same image bit for bit (a conv output pixel's arithmetic does not
+    depend on the batch), so the b8 plan's checks above carry over."""
+    import json
+    import os
+
+    P, A, W, M = _mods()
+    ar = A.parse_arch(A.load_model_dict("yolov8s-small.yaml"))
+    sd = W.synthetic_state_dict(ar, 0)
+    hw, imgsz = (1024, 1280), 1280
+    sc = P.synth.Scene(seed=3, n_targets=48, n_frames=17, height=hw[0], width=hw[1])
+    ft = torch.from_numpy(np.stack([sc.frame(t) for t in range(16)])).cuda()
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = {}
+    for B in (8, 16):
+        with open(os.path.join(root, "plans", f"s_1280x1024_i1280_b{B}_fp8.json")) as f:
+            pl = json.load(f)
+        prog = M.Program(ar, sd, hw[0], hw[1], imgsz, B, "fp8")
+        assert pl["batch"] == B and len(pl["plan"]) == len(prog.ops)
+        dm = M.DeviceModel(prog)
+        dm.load_plan(pl["batch"], pl["plan"])
+        parts = [dm.detect(ft[i:i + B].contiguous(), 0.25, 0.7, 300) for i in range(0, 16, B)]
+        torch.cuda.synchronize()
+        dm.check()
+        out[B] = (torch.cat([d for d, _ in parts]).cpu(), torch.cat([c for _, c in parts]).cpu())
+        del dm
+    assert int(out[8][1].sum()) > 0
+    assert torch.equal(out[8][1], out[16][1])
+    for b in range(16):
+        n = int(out[8][1][b])
+        assert out[8][0][b, :n].numpy().tobytes() == out[16][0][b, :n].numpy().tobytes(), b
