@@ -77,8 +77,8 @@ CONFIGS = {
     4: dict(S=1, H=512, W=640, imgsz=640, max_tracks=512, targets=40, dtype="fp32", secondary="", live_floor=64,
             tbatch=4, inflight=4),
     # config 5: the fp8 leg runs two steps per forward, three in flight (20 steps: 4,811-4,830 vs 4,418-4,502
-    # frames/s at one step, r6av); the bf16 leg keeps one step (its batch-16 arena passes the 2 GiB the table
-    # kernels address: 2,612-2,623 vs 3,700-3,746)
+    # frames/s at one step, r6av); the bf16 leg keeps one step (two steps: 3,783-3,831 vs 3,653-3,756 once its
+    # 2.9 GiB batch-16 arena runs on the table kernels, r6az -- within the spread)
     5: dict(S=8, H=1024, W=1280, imgsz=1280, max_tracks=2048, targets=96, dtype="fp8", secondary="bf16",
             live_floor=256, tbatch={"fp8": 2}, inflight={"fp8": 3}),
 }

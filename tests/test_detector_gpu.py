@@ -384,3 +384,40 @@ def test_graph_cache_is_lru_bounded_and_replays_match():
             got = _sorted_dets(dets.cpu(), cnt.cpu())
             for a, b in zip(want, got):
                 np.testing.assert_array_equal(a, b)
+
+
+def test_arena_above_2gib_table_kernels_match_per_image():
+    """The table / wide / halo kernels address the activation arena with 32-bit unsigned buffer
+    offsets up to 4 GiB (kArenaMax; the masked-tap sentinel kOOB past it).  A batch-24 fp32
+    forward (arena 2.0 GiB) on the batch-8 plan's variants runs the same kernels as the batch-8
+    forward and gives every image the batch-8 forward's detections bit for bit."""
+    import json
+    import os
+
+    P, A, W, M = _mods()
+    ar = A.parse_arch(A.load_model_dict("yolov8s-small.yaml"))
+    sd = W.synthetic_state_dict(ar, 0)
+    fr = torch.stack([P.synth.Scene(seed=s, n_targets=40, n_frames=2).frames_torch(0, 1, "cuda")[0]
+                      for s in range(24)]).contiguous()
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with open(os.path.join(root, "plans", "s_640x512_i640_b8_fp32.json")) as f:
+        plan = json.load(f)["plan"]
+    res = {}
+    for B in (8, 24):
+        prog = M.Program(ar, sd, 512, 640, 640, B, "fp32")
+        if B == 24:
+            assert 4 * sum(prog.desc().buf_elems[i] for i in range(prog.desc().n_bufs)) * B > 2 ** 31
+        dm = M.DeviceModel(prog)
+        dm.load_plan(B, plan)
+        outs = [dm.detect(fr[i:i + B].contiguous()) for i in range(0, 24, B)]
+        torch.cuda.synchronize()
+        dm.check()
+        kinds = sorted({k for (_, _, k, _) in dm.profile(fr[:B].contiguous(), reps=1) if "conv" in k})
+        res[B] = (torch.cat([d for d, _ in outs]).cpu().numpy(), torch.cat([c for _, c in outs]).cpu().numpy(), kinds)
+        del dm
+        torch.cuda.empty_cache()
+    (d8, c8, k8), (d24, c24, k24) = res[8], res[24]
+    assert any("F32S" in k for k in k24) and k8 == k24  # the split table kernels, as at batch 8
+    assert int(c8.sum()) > 0 and np.array_equal(c8, c24)
+    for i in range(24):
+        assert d8[i, :c8[i]].tobytes() == d24[i, :c24[i]].tobytes(), i

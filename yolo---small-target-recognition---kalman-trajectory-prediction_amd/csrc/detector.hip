@@ -996,7 +996,7 @@ __global__ void __launch_bounds__(256) conv_tile_kernel(TileArgs a) {
 // rounds); 1: each wave owns its own 16*NPT pixels and the full K.
 // SKD K steps of loads stay in flight per wave.
 struct FastArgs {
-  const void* arena;             // every activation buffer lives in one allocation (< 2 GiB)
+  const void* arena;             // every activation buffer lives in one allocation (< kArenaMax)
   unsigned arena_bytes;
   unsigned soff0, soff1;         // byte offsets of the two source views (image b0, channel coff)
   int h0, w0, cs0, up0, h1, w1, cs1, up1;
@@ -1021,7 +1021,12 @@ struct FastArgs {
 };
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-constexpr unsigned kOOB = 0x80000000u;  // buffer offset past every num_records: the load returns 0
+// Activation-arena loads use 32-bit unsigned buffer offsets (SRD num_records = the arena's bytes):
+// the table / wide / halo kernels serve arenas below kArenaMax (4 GiB less 64 KiB), e.g. the
+// 2.7 GiB fp32 arena of a batch-32 forward; kOOB lies past every such arena, so a masked tap's
+// load returns 0 (and kOOB + 16 does not wrap)
+constexpr unsigned long long kArenaMax = 0xFFFF0000ull;
+constexpr unsigned kOOB = 0xFFFFFF00u;  // buffer offset past every num_records: the load returns 0
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_srd(const void* base, unsigned bytes) {
   const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)(size_t)base);
@@ -3845,7 +3850,7 @@ ConvPlan conv_plan(const yk_model* m, const yk_op& op, int B) {
   if (idx < m->tuned.size() && m->tuned[idx][0] >= 0 && m->tuned_batch == B) {
     const auto& t = m->tuned[idx];
     if (t[0] == CK_SPLITK) return splitk_plan(op, B, t[1], t[2]);
-    if (t[0] == CK_WIDE && m->ltab && m->ltab_off[idx] >= 0 && m->arena_bytes < 0x7fff0000ull &&
+    if (t[0] == CK_WIDE && m->ltab && m->ltab_off[idx] >= 0 && m->arena_bytes < kArenaMax &&
         wide_plan(op, esz, t[1], t[2] == 8 ? 8 : 4).ok) {
       ConvPlan p;
       p.kind = CK_WIDE;
@@ -4637,7 +4642,7 @@ int launch_nms(yk_model* m, int B, float iou, int max_det, float* dets, int32_t*
 hipError_t build_ktabs(yk_model* m, bool fast) {
   const int esz = esz_of(m->desc.act_dtype);
   const int epl = 16 / esz;  // K elements per lane per K step
-  if (m->arena_bytes >= 0x7fff0000ull || m->blob_bytes >= 0x7fff0000ull) fast = false;  // 32-bit offsets
+  if (m->arena_bytes >= kArenaMax || m->blob_bytes >= 0x7fff0000ull) fast = false;  // 32-bit offsets
   std::vector<int2> all;
   m->ktab_off.assign(m->ops.size(), -1);
   for (size_t i = 0; i < m->ops.size() && fast; ++i) {
@@ -4950,7 +4955,7 @@ int yk_model_create(yk_ctx* ctx, const yk_model_desc* desc, const void* host_blo
     for (size_t i = 0; i < m->ops.size(); ++i)
       if (m->ops[i].kind == YK_K_CONV && (m->ktab_off[i] < 0 || m->ops[i].src_ch[0] % 16 ||
                                           (m->ops[i].n_src > 1 && m->ops[i].src_ch[1] % 16))) {
-        yk::set_error("yk_model_create: FP8 needs every conv on the table kernel (16-channel sources, arena < 2 GiB)");
+        yk::set_error("yk_model_create: FP8 needs every conv on the table kernel (16-channel sources, arena < 4 GiB)");
         yk_model_destroy(m);
         return YK_ERR_ARG;
       }
@@ -5271,7 +5276,7 @@ int yk_model_autotune(yk_model* m, const uint8_t* frames, int batch, float conf,
         if (fp8 || (nnt > 1 && 4 * op.n_tiles < 3 * ((op.n_tiles + nnt - 1) / nnt) * nnt)) continue;
         cands.push_back({CK_SPLITK, nnt, npt});
       }
-    if (m->ltab && m->ltab_off[i] >= 0 && m->arena_bytes < 0x7fff0000ull && !m->no_wide)
+    if (m->ltab && m->ltab_off[i] >= 0 && m->arena_bytes < kArenaMax && !m->no_wide)
       for (int nnt : {2, 4}) {
         if (nnt == 4 && op.n_tiles <= 2) continue;
         for (int nw : {4, 8})
