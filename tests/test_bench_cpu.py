@@ -60,3 +60,30 @@ def test_kernel_peak_prices_split_kernels_on_bf16_rate():
     assert B.kernel_peak("conv_halo_kernel<1, 4, 1, 3>", "fp32")[0] == pk
     assert B.kernel_peak("conv_fast_kernel<yk::det::F32, 4, 2, false, 2>", "fp32")[0] == 157.3
     assert B.kernel_peak("conv_fastw_kernel<yk::det::BF16, 4, 2, 2>", "bf16")[0] == 2500.0
+
+
+@pytest.mark.parametrize("argv,want", [
+    ([], (2, 3)),                                    # config 3: two steps per batch-16 forward, 3 in flight
+    (["--dtype", "bf16"], (2, 3)),
+    (["--config", "4"], (4, 4)),                     # config 4: four steps of its one stream per forward
+    (["--config", "5"], (2, 3)),                     # config 5's fp8 leg: two steps per forward
+    (["--config", "5", "--dtype", "bf16"], (1, 4)),  # ... its bf16 leg (own process): one step
+    (["--config", "2"], (1, 4)),                     # config 2: BASELINE names batch 1
+    (["--config", "4", "--tbatch", "1", "--inflight", "2"], (1, 2)),
+    (["--no-pipeline"], (1, 1)),
+])
+def test_schedule_defaults_per_config_and_dtype(argv, want, monkeypatch):
+    """Frames per forward (temporal batching) and forwards in flight that bench.py runs by default:
+    per config, per dtype where the config says so (config 5), explicit flags win, and no
+    temporal batching without forwards in flight."""
+    B = _bench()
+    monkeypatch.setattr("sys.argv", ["bench.py"] + argv)
+    a = B.parse()
+    cfg = B.CONFIGS[a.config]
+    inflight = 1 if a.no_pipeline else a.inflight
+    assert (B.tbatch_of(a, cfg, a.dtype or cfg["dtype"]), inflight) == want
+    # the plan each temporal batch loads exists (the smaller batch's variants at the larger batch)
+    tb, S = want[0], cfg["S"]
+    if not a.no_pipeline and not any(x in argv for x in ("--tbatch", "--inflight")):
+        dtype = a.dtype or cfg["dtype"]
+        assert os.path.exists(B.plan_path(a, dtype, tb * S, cfg["W"], cfg["H"], cfg["imgsz"])), (argv, tb * S)
